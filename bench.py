@@ -1,0 +1,160 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node training samples/sec of the weather-MLP DDP job.
+
+BASELINE.json metric: "samples/sec (whole node) for weather-MLP DDP at 1/2/4/8 MI355X; epoch
+wall-clock".  Workload = the reference training step exactly (jobs/train_lightning_ddp.py):
+WeatherClassifier 5->64->2 (ReLU, Dropout 0.2), cross-entropy, Adam(lr=0.01), batch 4 PER RANK
+(weak scaling), DistributedSampler sharding, per-step gradient all-reduce across ranks plus
+the sync_dist train_loss.  ``--model weather-mlp-3x128`` runs BASELINE.json's 3-layer/128-h
+variant instead.  Data: synthetic weather rows (no network), random-init weights.
+
+Timed region: exactly K optimizer steps (each = fused gather/fwd/CE/bwd, RCCL all-reduce when
+N > 1, Adam), bracketed by barrier + device synchronize on both sides, max over ranks.
+
+    python bench.py --gpus 1 --steps 20000 --warmup 2000
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29511 bench.py --gpus 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+# BASELINE.md local probe (reference step shape, torch CPU, W=1): ~8,500 samples/s whole node.
+# The reference publishes no number (BASELINE.json "published": {}); this probe is the only one.
+BASELINE_SAMPLES_PER_SEC = {"weather": 8500.0}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20000)
+    p.add_argument("--warmup", type=int, default=2000)
+    p.add_argument("--model", default="weather", help="weather (reference 5-64-2) | weather-mlp-3x128")
+    p.add_argument("--batch", type=int, default=4, help="per-rank batch (reference: 4)")
+    p.add_argument("--rows", type=int, default=0, help="synthetic dataset rows (0 = sized to the run)")
+    p.add_argument("--epoch-rows", type=int, default=100000,
+                   help="dataset size used for the reported epoch wall-clock")
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    import dct_amd  # noqa: F401
+    from dct_amd.data.synthetic import weather_tensors
+    from dct_amd.models.mlp import build_mlp
+    from dct_amd.parallel.dist import init_distributed, shutdown
+    from dct_amd.trainer.engines import FusedMLPEngine, adam_hparams_from
+    from dct_amd.trainer.trainer import seed_everything
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        if a.gpus > 1 and world == 1:
+            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    ctx = init_distributed("gpu")
+    seed_everything(42)
+    total_steps = a.warmup + a.steps
+    rows = a.rows or int(math.ceil((total_steps + 8) * a.batch * ctx.world_size / 0.8)) + 1024
+    X, Y = weather_tensors(rows, seed=0, dim=5)
+    model = build_mlp(a.model, 5)
+    adam = adam_hparams_from(model.configure_optimizers())
+    if not FusedMLPEngine.applicable(model, ctx.device, a.batch):
+        raise SystemExit("model/batch not supported by the fused engine")
+    eng = FusedMLPEngine(model, ctx, a.batch, seed=42, adam=adam)
+    n_train = int(0.8 * rows)
+    perm = torch.randperm(rows, generator=torch.Generator().manual_seed(42))
+    eng.attach_data(X, Y, perm[:n_train], perm[n_train:])
+    n_items = eng.upload_epoch_indices(0, shuffle=True)
+    assert (total_steps - 1) * a.batch < n_items, "dataset too small for the requested steps"
+    loss = torch.zeros(total_steps, dtype=torch.float32, device=ctx.device)
+
+    # warmup (also captures the DDP step graph chunk outside the timed region)
+    eng.run_steps(n_items, a.warmup, loss if ctx.is_distributed else loss[: a.warmup], first_step=0)
+    if ctx.is_distributed and eng.use_graph:
+        C = min(eng.graph_chunk, a.steps)
+        eng._get_graph(n_items, C, loss)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    if ctx.is_distributed:
+        eng.run_steps(n_items, a.steps, loss, first_step=a.warmup)
+    else:
+        eng.run_steps(n_items, a.steps, loss[a.warmup:], first_step=a.warmup)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dt_t = torch.tensor([dt], dtype=torch.float64, device=ctx.device)
+    if ctx.is_distributed:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+
+    losses = loss.cpu()
+    finite = bool(torch.isfinite(losses).all())
+    first_l = float(losses[: max(1, a.warmup // 10)].mean())
+    last_l = float(losses[-max(1, a.steps // 10):].mean())
+    eng.global_step = total_steps
+    val_loss, val_acc = eng.validate()
+
+    samples = a.steps * a.batch * ctx.world_size
+    sps = samples / dt
+    ms_step = dt / a.steps * 1e3
+    # epoch wall-clock for an --epoch-rows dataset at the measured step rate (train part)
+    steps_per_epoch = math.ceil(math.ceil(int(0.8 * a.epoch_rows) / ctx.world_size) / a.batch)
+    base = BASELINE_SAMPLES_PER_SEC.get(a.model)
+    out = {
+        "metric": "samples/sec (whole node) for weather-MLP DDP",
+        "value": round(sps, 1),
+        "unit": "samples/s",
+        "n_gpus": ctx.world_size,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_step, 6),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (round(sps / base, 2) if base else None),
+        "dtype": "fp32",
+        "data": "synthetic",
+        "config": {
+            "model": ("WeatherClassifier 5-64-2 (reference jobs/train_lightning_ddp.py)" if a.model == "weather"
+                      else a.model),
+            "global_batch": a.batch * ctx.world_size,
+            "per_rank_batch": a.batch,
+            "seq_len": None,
+            "parallelism": f"dp{ctx.world_size}",
+            "optimizer": "adam lr=0.01",
+            "loss": eng.loss,
+            "engine": "fused-persistent" if not ctx.is_distributed else
+                      ("fused+rccl-allreduce+hipgraph" if eng.graph_used else "fused+rccl-allreduce"),
+            "baseline_ref": "BASELINE.md CPU probe, W=1, 8500 samples/s (reference publishes none)",
+        },
+        "extra": {
+            "us_per_step": round(ms_step * 1e3, 3),
+            "epoch_wall_clock_s_train": round(steps_per_epoch * ms_step / 1e3, 6),
+            "epoch_rows": a.epoch_rows,
+            "loss_first": round(first_l, 4),
+            "loss_last": round(last_l, 4),
+            "val_loss": round(val_loss, 4),
+            "val_acc": round(val_acc, 4),
+            "losses_finite": finite,
+            "device": torch.cuda.get_device_name(ctx.device),
+        },
+    }
+    if ctx.rank == 0:
+        print(json.dumps(out), flush=True)
+    shutdown(ctx)
+    return 0 if finite else 3
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,120 @@
+"""Build the native extension ``_dct_native`` in-tree with hipcc for gfx950.
+
+No hipify, no torch.utils.cpp_extension (which would run hipify over the sources): every
+``csrc/*.hip`` / ``csrc/*.cpp`` is compiled by ``hipcc --offload-arch=gfx950`` into
+``build/obj`` (incremental on source/header mtimes + flags) and linked into
+``<package>/_dct_native<EXT_SUFFIX>`` next to this file, so the built ``.so`` travels with
+the repository snapshot to the GPU box.  ``python -m dct_amd._build`` builds it by hand.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import sys
+import sysconfig
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+BUILD = os.path.join(os.path.dirname(PKG_DIR), "build", "obj")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("DCT_OFFLOAD_ARCH", "gfx950")
+MODULE = "_dct_native"
+
+
+def target_path() -> str:
+    return os.path.join(PKG_DIR, MODULE + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _sources():
+    return sorted(
+        os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp"))
+    )
+
+
+def _headers():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h"))
+
+
+def _flags(debug: bool = False):
+    import pybind11
+
+    f = [
+        f"--offload-arch={ARCH}",
+        "-O0" if debug else "-O3",
+        "-fPIC",
+        "-std=c++17",
+        "-Wno-unused-result",
+        "-Wno-unused-variable",
+        f"-I{CSRC}",
+        f"-I{pybind11.get_include()}",
+        f"-I{sysconfig.get_paths()['include']}",
+        f"-I{ROCM}/include",
+    ]
+    if debug:
+        f.append("-g")
+    return f
+
+
+def _stamp(src: str, flags) -> str:
+    h = hashlib.sha1()
+    h.update(" ".join(flags).encode())
+    for p in [src] + _headers():
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def _compile(src: str, flags, verbose: bool):
+    os.makedirs(BUILD, exist_ok=True)
+    base = os.path.basename(src)
+    stamp = _stamp(src, flags)
+    obj = os.path.join(BUILD, f"{base}.{stamp}.o")
+    if os.path.exists(obj):
+        return obj, False
+    lang = ["-x", "hip"] if src.endswith(".hip") else []
+    cmd = [os.path.join(ROCM, "bin", "hipcc")] + flags + lang + ["-c", src, "-o", obj + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {base}:\n{r.stdout}\n{r.stderr}")
+    os.replace(obj + ".tmp", obj)
+    return obj, True
+
+
+def build(force: bool = False, verbose: bool = False, jobs: int = 0, debug: bool = False) -> str:
+    flags = _flags(debug)
+    srcs = _sources()
+    jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 4)), 16)
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        results = list(ex.map(lambda s: _compile(s, flags, verbose), srcs))
+    objs = [o for o, _ in results]
+    rebuilt = any(b for _, b in results)
+    out = target_path()
+    if force or rebuilt or not os.path.exists(out):
+        cmd = (
+            [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"]
+            + objs
+            + [f"-L{ROCM}/lib", "-lrccl", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"]
+        )
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        os.replace(out + ".tmp", out)
+    return out
+
+
+def is_stale() -> bool:
+    out = target_path()
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(p) > t for p in _sources() + _headers())
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,285 @@
+// pybind11 module `_dct_native`: the Python face of the HIP kernels and the C++ runtime.
+// Tensors cross the boundary as raw device pointers (validated for shape/dtype/device by
+// the Python wrappers in ops/ before any launch) and streams as hipStream_t handles, so the
+// module has no libtorch dependency and builds in seconds with hipcc.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "mlp_fused.h"
+#include "runtime.h"
+
+namespace py = pybind11;
+
+static void check(int err, const char* what) {
+  if (err != 0) {
+    throw std::runtime_error(std::string(what) + " failed: " + hipGetErrorString((hipError_t)err));
+  }
+}
+
+template <class T>
+static T* P(uintptr_t x) {
+  return reinterpret_cast<T*>(x);
+}
+
+struct MlpPlan {
+  std::vector<char> shape;
+  int nt = 0, maxblk = 0, supported = 0;
+  int use_wave = 0;  // single-wave register-resident kernel (narrow MLPs), see mlp_wave.hip
+  MlpPlan(const std::vector<int>& dims, int bmax) {
+    if (dims.size() < 2 || dims.size() > 5) throw std::invalid_argument("MLP needs 1..4 linear layers");
+    for (int d : dims)
+      if (d < 1 || d > 4096) throw std::invalid_argument("MLP layer width out of range");
+    shape.resize(dct_mlp_shape_size());
+    if (dct_mlp_make_shape(shape.data(), dims.data(), (int)dims.size() - 1, bmax) != 0)
+      throw std::invalid_argument("bad MLP shape");
+    supported = dct_mlp_select(sh(), &nt, &maxblk);
+    const char* env = std::getenv("DCT_MLP_KERNEL");
+    const bool force_lds = env && std::string(env) == "lds";
+    use_wave = (!force_lds && dct_mlp_wave_supported(dims.data(), (int)dims.size() - 1, 1)) ? 1 : 0;
+    if (use_wave) supported = 1;
+  }
+  const dct::MlpShape* sh() const { return reinterpret_cast<const dct::MlpShape*>(shape.data()); }
+};
+
+PYBIND11_MODULE(_dct_native, m) {
+  m.doc() = "MI355X-native kernels and runtime for dct_amd";
+
+  // ------------------------------------------------------------------ device info
+  m.def("device_count", []() {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    return e == hipSuccess ? n : 0;
+  });
+  m.def("arch_name", [](int dev) {
+    hipDeviceProp_t p;
+    check((int)hipGetDeviceProperties(&p, dev), "hipGetDeviceProperties");
+    return std::string(p.gcnArchName);
+  });
+  m.def("synchronize", []() { check((int)hipDeviceSynchronize(), "hipDeviceSynchronize"); });
+
+  // ------------------------------------------------------------------ fused MLP
+  py::class_<MlpPlan>(m, "MlpPlan")
+      .def(py::init<const std::vector<int>&, int>(), py::arg("dims"), py::arg("bmax"))
+      .def_readonly("supported", &MlpPlan::supported)
+      .def_readonly("threads", &MlpPlan::nt)
+      .def_readonly("max_blocks_per_thread", &MlpPlan::maxblk)
+      .def_readonly("use_wave", &MlpPlan::use_wave)
+      .def_property_readonly("num_params", [](const MlpPlan& p) { return p.sh()->P; })
+      .def_property_readonly("lds_bytes", [](const MlpPlan& p) { return p.sh()->lds_floats * 4; })
+      .def_property_readonly("bmax", [](const MlpPlan& p) { return p.sh()->bmax; })
+      .def(
+          "train",
+          [](const MlpPlan& plan, uintptr_t p, uintptr_t mo, uintptr_t vo, uintptr_t grad_out, uintptr_t X, int ldx,
+             uintptr_t Y, uintptr_t idx, int n_items, int B, int steps, int t0, float lr, float b1, float b2,
+             float eps, float wd, float dropout, uint32_t seed, uint32_t step_base, uintptr_t loss_out, int mode,
+             int loss_kind, uintptr_t step_counter, uintptr_t cursor, uintptr_t prof, uintptr_t stream) {
+            if (!plan.supported) throw std::runtime_error("MLP too large for the fused kernel");
+            if (steps < 1 || n_items < 1 || B < 1) throw std::invalid_argument("empty launch");
+            if (!cursor && (int64_t)(steps - 1) * B >= n_items) throw std::invalid_argument("more steps than batches");
+            dct::MlpArgs a{};
+            a.p = P<float>(p);
+            a.m = P<float>(mo);
+            a.v = P<float>(vo);
+            a.grad_out = P<float>(grad_out);
+            a.X = P<const float>(X);
+            a.ldx = ldx;
+            a.Y = P<const int>(Y);
+            a.idx = P<const int>(idx);
+            a.n_items = n_items;
+            a.B = B;
+            a.steps = steps;
+            a.t0 = t0;
+            a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd;
+            a.dropout = dropout;
+            a.seed = seed;
+            a.step_base = step_base;
+            a.loss_out = P<float>(loss_out);
+            a.mode = mode;
+            a.loss_kind = loss_kind;
+            a.step_counter = P<int>(step_counter);
+            a.cursor = P<int>(cursor);
+            a.prof = P<unsigned long long>(prof);
+            if (cursor && mode != 1) throw std::invalid_argument("cursor is only valid in grad mode");
+            if (mode == 1 && !grad_out) throw std::invalid_argument("grad mode needs grad_out");
+            if (mode == 1 && steps != 1) throw std::invalid_argument("grad mode runs exactly one step");
+            const dct::MlpShape* sh = plan.sh();
+            if (plan.use_wave && dct_mlp_wave_supported(sh->dims, sh->L, B))
+              check(dct_mlp_wave_train(sh->dims, sh->L, &a, reinterpret_cast<void*>(stream)), "mlp_wave_train");
+            else
+              check(dct_mlp_train(plan.shape.data(), &a, reinterpret_cast<void*>(stream)), "mlp_train");
+          },
+          py::arg("p"), py::arg("m"), py::arg("v"), py::arg("grad_out"), py::arg("X"), py::arg("ldx"), py::arg("Y"),
+          py::arg("idx"), py::arg("n_items"), py::arg("B"), py::arg("steps"), py::arg("t0"), py::arg("lr"),
+          py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("dropout"), py::arg("seed"),
+          py::arg("step_base"), py::arg("loss_out"), py::arg("mode"), py::arg("loss_kind"), py::arg("step_counter"),
+          py::arg("cursor"), py::arg("prof") = 0, py::arg("stream") = 0)
+      .def(
+          "eval",
+          [](const MlpPlan& plan, uintptr_t p, uintptr_t X, int ldx, uintptr_t Y, uintptr_t idx, int n_items,
+             int loss_kind, uintptr_t acc_out, uintptr_t logits_out, int grid, uintptr_t stream) {
+            dct::MlpArgs a{};
+            a.p = P<float>(p);
+            a.X = P<const float>(X);
+            a.ldx = ldx;
+            a.Y = P<const int>(Y);
+            a.idx = P<const int>(idx);
+            a.n_items = n_items;
+            a.B = plan.sh()->bmax;
+            a.loss_kind = loss_kind;
+            a.eval_acc = P<float>(acc_out);
+            a.logits_out = P<float>(logits_out);
+            check(dct_mlp_eval(plan.shape.data(), &a, grid, reinterpret_cast<void*>(stream)), "mlp_eval");
+          },
+          py::arg("p"), py::arg("X"), py::arg("ldx"), py::arg("Y"), py::arg("idx"), py::arg("n_items"),
+          py::arg("loss_kind"), py::arg("acc_out"), py::arg("logits_out"), py::arg("grid"), py::arg("stream"));
+
+  // ------------------------------------------------------------------ optimizer
+  m.def(
+      "adam_flat",
+      [](uintptr_t p, uintptr_t g, uintptr_t mo, uintptr_t vo, uintptr_t p_bf16, int64_t n, float lr, float b1,
+         float b2, float eps, float wd, int64_t t, float grad_scale, int decoupled, uintptr_t step_counter,
+         uintptr_t stream) {
+        check(dct_adam_flat(P<float>(p), P<const float>(g), P<float>(mo), P<float>(vo), P<uint16_t>(p_bf16), n, lr,
+                            b1, b2, eps, wd, t, grad_scale, decoupled, P<const int>(step_counter),
+                            reinterpret_cast<void*>(stream)),
+              "adam_flat");
+      },
+      py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("p_bf16"), py::arg("n"), py::arg("lr"),
+      py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("t"), py::arg("grad_scale"),
+      py::arg("decoupled"), py::arg("step_counter"), py::arg("stream"));
+  m.def("f32_to_bf16", [](uintptr_t in, uintptr_t out, int64_t n, uintptr_t stream) {
+    check(dct_f32_to_bf16(P<const float>(in), P<uint16_t>(out), n, reinterpret_cast<void*>(stream)), "f32_to_bf16");
+  });
+
+  // ------------------------------------------------------------------ GEMM / NN ops
+  m.def(
+      "gemm_bf16",
+      [](uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias, int M, int N, int K, int lda, int ldb, int ldc,
+         int trans_a, int trans_b, int epilogue, int out_f32, int accumulate, uintptr_t aux, uintptr_t stream) {
+        check(dct_gemm_bf16(P<const uint16_t>(A), P<const uint16_t>(B), P<void>(C), P<const float>(bias), M, N, K,
+                            lda, ldb, ldc, trans_a, trans_b, epilogue, out_f32, accumulate, P<void>(aux),
+                            reinterpret_cast<void*>(stream)),
+              "gemm_bf16");
+      },
+      py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("M"), py::arg("N"), py::arg("K"),
+      py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("trans_a"), py::arg("trans_b"), py::arg("epilogue"),
+      py::arg("out_f32"), py::arg("accumulate"), py::arg("aux"), py::arg("stream"));
+  m.def(
+      "bias_act_bwd",
+      [](uintptr_t dY, uintptr_t act_aux, uintptr_t dZ_bf16, uintptr_t dbias, int M, int N, int ldy, int act,
+         int accumulate_bias, uintptr_t stream) {
+        check(dct_bias_act_bwd(P<const void>(dY), P<const void>(act_aux), P<uint16_t>(dZ_bf16), P<float>(dbias), M, N,
+                               ldy, act, accumulate_bias, reinterpret_cast<void*>(stream)),
+              "bias_act_bwd");
+      },
+      py::arg("dY"), py::arg("act_aux"), py::arg("dZ_bf16"), py::arg("dbias"), py::arg("M"), py::arg("N"),
+      py::arg("ldy"), py::arg("act"), py::arg("accumulate_bias"), py::arg("stream"));
+  m.def(
+      "cross_entropy_fwd_bwd",
+      [](uintptr_t logits, int logits_bf16, uintptr_t labels, uintptr_t dlogits, uintptr_t loss_sum,
+         uintptr_t correct_sum, int M, int C, float grad_scale, int loss_kind, uintptr_t stream) {
+        check(dct_loss_fwd_bwd(P<const void>(logits), logits_bf16, P<const int>(labels), P<void>(dlogits),
+                               P<float>(loss_sum), P<float>(correct_sum), M, C, grad_scale, loss_kind,
+                               reinterpret_cast<void*>(stream)),
+              "loss_fwd_bwd");
+      },
+      py::arg("logits"), py::arg("logits_bf16"), py::arg("labels"), py::arg("dlogits"), py::arg("loss_sum"),
+      py::arg("correct_sum"), py::arg("M"), py::arg("C"), py::arg("grad_scale"), py::arg("loss_kind"),
+      py::arg("stream"));
+  m.def(
+      "layernorm_fwd",
+      [](uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y, uintptr_t mean, uintptr_t rstd, int M, int N, float eps,
+         int in_bf16, int out_bf16, uintptr_t stream) {
+        check(dct_layernorm_fwd(P<const void>(x), P<const float>(w), P<const float>(b), P<void>(y), P<float>(mean),
+                                P<float>(rstd), M, N, eps, in_bf16, out_bf16, reinterpret_cast<void*>(stream)),
+              "layernorm_fwd");
+      });
+  m.def(
+      "layernorm_bwd",
+      [](uintptr_t dy, uintptr_t x, uintptr_t w, uintptr_t mean, uintptr_t rstd, uintptr_t dx, uintptr_t dw,
+         uintptr_t db, int M, int N, int bf16_io, uintptr_t stream) {
+        check(dct_layernorm_bwd(P<const void>(dy), P<const void>(x), P<const float>(w), P<const float>(mean),
+                                P<const float>(rstd), P<void>(dx), P<float>(dw), P<float>(db), M, N, bf16_io,
+                                reinterpret_cast<void*>(stream)),
+              "layernorm_bwd");
+      });
+  m.def(
+      "attention_fwd",
+      [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t lse, int Bsz, int H, int T, int D, int ldq,
+         int ldo, float scale, uintptr_t stream) {
+        check(dct_attention_fwd(P<const uint16_t>(q), P<const uint16_t>(k), P<const uint16_t>(v), P<uint16_t>(o),
+                                P<float>(lse), Bsz, H, T, D, ldq, ldo, scale, reinterpret_cast<void*>(stream)),
+              "attention_fwd");
+      });
+  m.def(
+      "attention_bwd",
+      [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t dout, uintptr_t lse, uintptr_t dq, uintptr_t dk,
+         uintptr_t dv, int Bsz, int H, int T, int D, int ldq, int ldo, float scale, uintptr_t stream) {
+        check(dct_attention_bwd(P<const uint16_t>(q), P<const uint16_t>(k), P<const uint16_t>(v), P<const uint16_t>(o),
+                                P<const uint16_t>(dout), P<const float>(lse), P<uint16_t>(dq), P<uint16_t>(dk),
+                                P<uint16_t>(dv), Bsz, H, T, D, ldq, ldo, scale, reinterpret_cast<void*>(stream)),
+              "attention_bwd");
+      });
+  m.def("gather_rows", [](uintptr_t src, uintptr_t idx, uintptr_t dst, int64_t n_rows, int row_bytes,
+                          uintptr_t stream) {
+    check(dct_gather_rows(P<const void>(src), P<const int>(idx), P<void>(dst), n_rows, row_bytes,
+                          reinterpret_cast<void*>(stream)),
+          "gather_rows");
+  });
+
+  // ------------------------------------------------------------------ runtime
+  m.def("comm_unique_id", []() { return py::bytes(dct::comm_unique_id()); });
+  py::class_<dct::Comm>(m, "Comm")
+      .def(py::init([](py::bytes uid, int world, int rank, int device) {
+             return new dct::Comm(std::string(uid), world, rank, device);
+           }),
+           py::arg("uid"), py::arg("world"), py::arg("rank"), py::arg("device"))
+      .def("allreduce", &dct::Comm::allreduce, py::arg("buf"), py::arg("count"), py::arg("dtype"), py::arg("op"),
+           py::arg("stream"))
+      .def("broadcast", &dct::Comm::broadcast, py::arg("buf"), py::arg("count"), py::arg("dtype"), py::arg("root"),
+           py::arg("stream"))
+      .def("reduce_scatter", &dct::Comm::reduce_scatter)
+      .def("all_gather", &dct::Comm::all_gather)
+      .def_property_readonly("rank", &dct::Comm::rank)
+      .def_property_readonly("world", &dct::Comm::world);
+  py::class_<dct::BucketReducer>(m, "BucketReducer")
+      .def(py::init([](dct::Comm* comm, uintptr_t flat, std::vector<int64_t> offs, std::vector<int64_t> counts,
+                       std::vector<int> pb, int dtype, int op) {
+             return new dct::BucketReducer(comm, flat, std::move(offs), std::move(counts), std::move(pb), dtype, op);
+           }),
+           py::arg("comm"), py::arg("flat_grad"), py::arg("bucket_offsets"), py::arg("bucket_counts"),
+           py::arg("param_bucket"), py::arg("dtype"), py::arg("op"), py::keep_alive<1, 2>())
+      .def("prepare", &dct::BucketReducer::prepare)
+      .def("mark_ready", &dct::BucketReducer::mark_ready)
+      .def("finalize", &dct::BucketReducer::finalize)
+      .def_property_readonly("num_buckets", &dct::BucketReducer::num_buckets)
+      .def_property_readonly("launched", &dct::BucketReducer::launched)
+      .def_property_readonly("comm_stream", &dct::BucketReducer::comm_stream);
+  py::class_<dct::StreamGraph>(m, "StreamGraph")
+      .def(py::init<>())
+      .def("begin", &dct::StreamGraph::begin)
+      .def("end", &dct::StreamGraph::end)
+      .def("replay", &dct::StreamGraph::replay)
+      .def("reset", &dct::StreamGraph::reset)
+      .def_property_readonly("num_nodes", &dct::StreamGraph::num_nodes);
+
+  m.attr("DT_F32") = (int)dct::DT_F32;
+  m.attr("DT_BF16") = (int)dct::DT_BF16;
+  m.attr("DT_F16") = (int)dct::DT_F16;
+  m.attr("DT_I32") = (int)dct::DT_I32;
+  m.attr("DT_I64") = (int)dct::DT_I64;
+  m.attr("DT_U8") = (int)dct::DT_U8;
+  m.attr("OP_SUM") = (int)dct::OP_SUM;
+  m.attr("OP_AVG") = (int)dct::OP_AVG;
+  m.attr("OP_MAX") = (int)dct::OP_MAX;
+  m.attr("OP_MIN") = (int)dct::OP_MIN;
+}

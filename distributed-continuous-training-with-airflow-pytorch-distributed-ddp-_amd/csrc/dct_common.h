@@ -1,0 +1,31 @@
+// Shared helpers for the dct HIP kernels (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define DCT_WAVE 64
+
+namespace dct {
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// bf16 <-> f32 on raw 16-bit storage (round-to-nearest-even; NaN kept NaN via the cast path)
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  return __bfloat16_as_ushort(__float2bfloat16(f));
+}
+
+}  // namespace dct

@@ -1,0 +1,236 @@
+// bf16 MFMA GEMM with fused bias/activation epilogue for gfx950.
+//
+//   C[M,N] (+)= op(A)[M,K] . op(B)[K,N]  (+ bias[N], act)      fp32 accumulate
+//   A: trans_a=0 -> stored [M][K] (lda), trans_a=1 -> stored [K][M]
+//   B: trans_b=1 -> stored [N][K] (ldb)  (torch Linear weight), trans_b=0 -> stored [K][N]
+//
+// The three products of a Linear layer map onto it as
+//   forward  Y  = X W^T + b  : A=X (0),   B=W (1)   epilogue bias(+relu/gelu), bf16 out (+aux)
+//   backward dX = dZ W       : A=dZ (0),  B=W (0)   bf16 out
+//   backward dW = dZ^T X     : A=dZ (1),  B=X (0)   fp32 out accumulated into the flat
+//                                                    gradient buffer (a DDP bucket view)
+//
+// Structure (CDNA4 guide §5 "standard MFMA GEMM main loop"): 128x128 block tile, BK=64,
+// 256 threads = 4 waves in 2x2, each wave 64x64 = 4x4 tiles of v_mfma_f32_16x16x32_bf16
+// (64 fp32 accumulators/lane); LDS images [rows][BK+8] with k contiguous so every A/B
+// fragment is one ds_read_b128 (row stride 144 B: the 16 rows of a fragment read land on
+// 16 distinct 16-B slots); global->LDS by register staging (16-B loads) double-buffered,
+// one barrier per K-step, next tile's loads issued before the current tile's MFMAs.
+// Transposed operands are transposed in the staging write (8 x ds_write_b16 per 16-B load).
+// Block index -> tile is remapped so blocks sharing an A row-panel run on one XCD (T1).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dct_common.h"
+#include "kernels.h"
+
+namespace dct {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int GBM = 128, GBN = 128, GBK = 64, GPAD = 8, GLD = GBK + GPAD, GNT = 256;
+
+__device__ __forceinline__ float gelu_f(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
+
+// Stage one BMxBK (or BNxBK) tile of an operand into registers.
+// Non-transposed: chunk c -> row c/8, k-chunk c%8 (8 bf16 each)  [storage [R][K]]
+// Transposed:     chunk c -> k c/16, row-chunk c%16               [storage [K][R]]
+template <bool TRANS>
+__device__ __forceinline__ void stage_load(const uint16_t* __restrict__ G, int ld, int R, int K, int r0, int k0,
+                                           bool vec, uint4 (&reg)[4]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = tid + q * GNT;
+    int row, kk;
+    if (!TRANS) {
+      row = r0 + (c >> 3);
+      kk = k0 + (c & 7) * 8;
+    } else {
+      kk = k0 + (c >> 4);
+      row = r0 + (c & 15) * 8;
+    }
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (!TRANS) {
+      if (row < R) {
+        const uint16_t* src = G + (size_t)row * ld + kk;
+        if (vec && kk + 8 <= K) {
+          v = *reinterpret_cast<const uint4*>(src);
+        } else {
+          uint16_t t[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) t[j] = (kk + j < K) ? src[j] : (uint16_t)0;
+          v.x = t[0] | ((uint32_t)t[1] << 16); v.y = t[2] | ((uint32_t)t[3] << 16);
+          v.z = t[4] | ((uint32_t)t[5] << 16); v.w = t[6] | ((uint32_t)t[7] << 16);
+        }
+      }
+    } else {
+      if (kk < K) {
+        const uint16_t* src = G + (size_t)kk * ld + row;
+        if (vec && row + 8 <= R) {
+          v = *reinterpret_cast<const uint4*>(src);
+        } else {
+          uint16_t t[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) t[j] = (row + j < R) ? src[j] : (uint16_t)0;
+          v.x = t[0] | ((uint32_t)t[1] << 16); v.y = t[2] | ((uint32_t)t[3] << 16);
+          v.z = t[4] | ((uint32_t)t[5] << 16); v.w = t[6] | ((uint32_t)t[7] << 16);
+        }
+      }
+    }
+    reg[q] = v;
+  }
+}
+
+template <bool TRANS>
+__device__ __forceinline__ void stage_store(uint16_t* S, const uint4 (&reg)[4]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = tid + q * GNT;
+    if (!TRANS) {
+      const int row = c >> 3, kc = (c & 7) * 8;
+      *reinterpret_cast<uint4*>(S + row * GLD + kc) = reg[q];
+    } else {
+      const int kk = c >> 4, r8 = (c & 15) * 8;
+      const uint32_t w[4] = {reg[q].x, reg[q].y, reg[q].z, reg[q].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        S[(r8 + 2 * j) * GLD + kk] = (uint16_t)(w[j] & 0xffff);
+        S[(r8 + 2 * j + 1) * GLD + kk] = (uint16_t)(w[j] >> 16);
+      }
+    }
+  }
+}
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(GNT, 2) void gemm_bf16_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  // LDS: A[2][GBM][GLD] then B[2][GBN][GLD]
+  uint16_t* const As0 = smem;
+  uint16_t* const Bs0 = smem + 2 * GBM * GLD;
+
+  // XCD-aware bijective remap: consecutive tiles (same A panel) onto one XCD group
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tiles_n = (g.N + GBN - 1) / GBN;
+  const int tm = wgid / tiles_n, tn = wgid % tiles_n;
+  const int m0 = tm * GBM, n0 = tn * GBN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (g.K + GBK - 1) / GBK;
+  uint4 ra[4], rb[4];
+  stage_load<TA>(g.A, g.lda, g.M, g.K, m0, 0, g.vec_a, ra);
+  stage_load<!TB>(g.B, g.ldb, g.N, g.K, n0, 0, g.vec_b, rb);
+  stage_store<TA>(As0, ra);
+  stage_store<!TB>(Bs0, rb);
+  __syncthreads();
+
+  const int frow = lane & 15;
+  const int fk = (lane >> 4) * 8;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool has_next = kt + 1 < nk;
+    if (has_next) {
+      stage_load<TA>(g.A, g.lda, g.M, g.K, m0, (kt + 1) * GBK, g.vec_a, ra);
+      stage_load<!TB>(g.B, g.ldb, g.N, g.K, n0, (kt + 1) * GBK, g.vec_b, rb);
+    }
+    const uint16_t* a_base = As0 + cur * GBM * GLD + (wr * 64 + frow) * GLD + fk;
+    const uint16_t* b_base = Bs0 + cur * GBN * GLD + (wc * 64 + frow) * GLD + fk;
+#pragma unroll
+    for (int ks = 0; ks < GBK / 32; ++ks) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(a_base + i * 16 * GLD + ks * 32);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(b_base + j * 16 * GLD + ks * 32);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (has_next) {
+      stage_store<TA>(As0 + (cur ^ 1) * GBM * GLD, ra);
+      stage_store<!TB>(Bs0 + (cur ^ 1) * GBN * GLD, rb);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: C layout col = lane&15, row = (lane>>4)*4 + r
+  const int ccol = lane & 15;
+  const int crow = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wc * 64 + j * 16 + ccol;
+      if (col >= g.N) continue;
+      const float bv = (g.bias && g.epilogue != EPI_NONE) ? g.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 64 + i * 16 + crow + r;
+        if (row >= g.M) continue;
+        float z = acc[i][j][r] * g.alpha + bv;
+        const size_t o = (size_t)row * g.ldc + col;
+        if (g.aux && g.epilogue == EPI_BIAS_GELU) reinterpret_cast<uint16_t*>(g.aux)[o] = f32_to_bf16(z);
+        if (g.epilogue == EPI_BIAS_RELU) z = fmaxf(z, 0.f);
+        else if (g.epilogue == EPI_BIAS_GELU) z = gelu_f(z);
+        if (g.out_f32) {
+          float* C = reinterpret_cast<float*>(g.C);
+          C[o] = g.accumulate ? C[o] + z : z;
+        } else {
+          uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
+          if (g.accumulate) z += bf16_to_f32(C[o]);
+          C[o] = f32_to_bf16(z);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace dct
+
+template <bool TA, bool TB>
+static hipError_t launch_gemm(const dct::GemmArgs& g, hipStream_t st) {
+  const size_t lds = (size_t)(2 * dct::GBM * dct::GLD + 2 * dct::GBN * dct::GLD) * sizeof(uint16_t);
+  auto fn = dct::gemm_bf16_kernel<TA, TB>;
+  hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  const int tiles = ((g.M + dct::GBM - 1) / dct::GBM) * ((g.N + dct::GBN - 1) / dct::GBN);
+  hipLaunchKernelGGL(fn, dim3(tiles), dim3(dct::GNT), lds, st, g);
+  return hipGetLastError();
+}
+
+extern "C" int dct_gemm_bf16(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K,
+                             int lda, int ldb, int ldc, int trans_a, int trans_b, int epilogue, int out_f32,
+                             int accumulate, void* aux, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  dct::GemmArgs g{};
+  g.A = A; g.B = B; g.C = C; g.bias = bias; g.aux = aux;
+  g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.epilogue = epilogue; g.out_f32 = out_f32; g.accumulate = accumulate; g.alpha = 1.0f;
+  // 16-B vector staging needs 16-B aligned rows along the contiguous dimension
+  g.vec_a = ((((uintptr_t)A) & 15) == 0) && (lda % 8 == 0);
+  g.vec_b = ((((uintptr_t)B) & 15) == 0) && (ldb % 8 == 0);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipError_t e;
+  if (!trans_a && trans_b) e = launch_gemm<false, true>(g, st);
+  else if (!trans_a && !trans_b) e = launch_gemm<false, false>(g, st);
+  else if (trans_a && !trans_b) e = launch_gemm<true, false>(g, st);
+  else e = launch_gemm<true, true>(g, st);
+  return (int)e;
+}

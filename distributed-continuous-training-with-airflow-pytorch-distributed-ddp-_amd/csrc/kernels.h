@@ -1,0 +1,48 @@
+// C API of the general NN kernels (GEMM, loss, norm, attention, gather).
+#pragma once
+#include <stdint.h>
+
+namespace dct {
+
+enum Epilogue { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_RELU = 2, EPI_BIAS_GELU = 3 };
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
+
+struct GemmArgs {
+  const uint16_t* A;
+  const uint16_t* B;
+  void* C;
+  const float* bias;
+  void* aux;
+  int M, N, K, lda, ldb, ldc;
+  int epilogue, out_f32, accumulate;
+  int vec_a, vec_b;
+  float alpha;
+};
+
+}  // namespace dct
+
+extern "C" {
+int dct_gemm_bf16(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K, int lda,
+                  int ldb, int ldc, int trans_a, int trans_b, int epilogue, int out_f32, int accumulate, void* aux,
+                  void* stream);
+// dZ = dY * act'(aux) (bf16 out); dbias[n] (+)= sum_m dZ[m][n]. dY is bf16. For RELU aux is
+// the activation OUTPUT (bf16), for GELU the pre-activation (bf16), for NONE unused.
+int dct_bias_act_bwd(const void* dY, const void* act_aux, uint16_t* dZ, float* dbias, int M, int N, int ldy, int act,
+                     int accumulate_bias, void* stream);
+// Row-wise CE (loss_kind 0) or MSE-vs-onehot (1): loss/correct sums (atomic fp32) and
+// dlogits = dL/dz * grad_scale (bf16 if logits_bf16 else fp32).
+int dct_loss_fwd_bwd(const void* logits, int logits_bf16, const int* labels, void* dlogits, float* loss_sum,
+                     float* correct_sum, int M, int C, float grad_scale, int loss_kind, void* stream);
+int dct_layernorm_fwd(const void* x, const float* w, const float* b, void* y, float* mean, float* rstd, int M, int N,
+                      float eps, int in_bf16, int out_bf16, void* stream);
+int dct_layernorm_bwd(const void* dy, const void* x, const float* w, const float* mean, const float* rstd, void* dx,
+                      float* dw, float* db, int M, int N, int bf16_io, void* stream);
+// q/k/v: element (b, t, h, d) at ptr[(b*T + t)*ldq + h*D + d] (a packed QKV projection
+// output); o/dout: at ptr[(b*T + t)*ldo + h*D + d]; lse fp32 [B*H*T].
+int dct_attention_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse, int Bsz, int H,
+                      int T, int D, int ldq, int ldo, float scale, void* stream);
+int dct_attention_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, const uint16_t* o,
+                      const uint16_t* dout, const float* lse, uint16_t* dq, uint16_t* dk, uint16_t* dv, int Bsz, int H,
+                      int T, int D, int ldq, int ldo, float scale, void* stream);
+int dct_gather_rows(const void* src, const int* idx, void* dst, int64_t n_rows, int row_bytes, void* stream);
+}

@@ -1,0 +1,104 @@
+// Host/device-shared descriptors of the fused MLP kernels (see mlp_fused_impl.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dct {
+
+constexpr int MLP_MAXL = 4;
+
+// Everything a launch needs about one MLP architecture, computed once on the host
+// (dct_mlp_make_shape): LDS layout, per-layer work split of the forward / dX phases and
+// the ownership of weight blocks for the dW + Adam phase.
+struct MlpShape {
+  int L;
+  int dims[MLP_MAXL + 1];
+  int rows4[MLP_MAXL];  // round4(out_l)
+  int cols4[MLP_MAXL];  // round4(in_l)
+  int ldw[MLP_MAXL];    // LDS row stride of W_l (floats)
+  int w_lds[MLP_MAXL];  // LDS offsets (floats)
+  int b_lds[MLP_MAXL];
+  int a_lds[MLP_MAXL + 1];  // activations A_l [BMAX][lda_l] for l >= 1; A_L = logits
+  int a0_lds[2];            // double-buffered input batch (next batch is written during a step)
+  int lab_lds[2];           // double-buffered labels (int)
+  int lda[MLP_MAXL + 1];
+  int dz_lds[MLP_MAXL];  // dZ_l [BMAX][rows4_l]
+  int woff[MLP_MAXL];    // torch flat offsets of W_l / b_l
+  int boff[MLP_MAXL];
+  // forward split: items = (rows4/4 output groups) << f_ksl k-splits, f_kc float4s per split
+  int f_ksl[MLP_MAXL], f_kc[MLP_MAXL], f_items[MLP_MAXL];
+  // dX split: items = (cols4/4 column groups) << d_osl o-splits, d_oc o-groups per split
+  int d_osl[MLP_MAXL], d_oc[MLP_MAXL], d_items[MLP_MAXL];
+  int br;                        // rows per owned weight block: 1 (small models) or 4
+  int blk_start[MLP_MAXL + 1];   // prefix count of weight blocks per layer
+  int blk_cols[MLP_MAXL];        // column blocks per row (cols4/4)
+  int bias_start[MLP_MAXL + 1];  // prefix count of biases
+  int nblk;
+  int nbias;
+  int P;
+  int red_lds;  // reduction scratch
+  int lds_floats;
+  int bmax;
+  int nt;        // threads per workgroup
+  int maxq;      // weight blocks per thread
+  int fuse_loss; // loss computed inside the last forward layer (classes <= 4)
+  int supported;
+};
+
+struct MlpArgs {
+  float* p;  // flat params (torch state_dict order): W0,b0,W1,b1,...
+  float* m;  // Adam exp_avg (same layout)
+  float* v;  // Adam exp_avg_sq
+  float* grad_out;  // GRAD mode: [P] grads + [P] = batch loss
+  const float* X;
+  int ldx;
+  const int* Y;
+  const int* idx;
+  int n_items;  // indices available to this launch
+  int B;        // batch size (<= BMAX)
+  int steps;
+  int t0;  // Adam steps already taken (bias correction uses t0+s+1)
+  float lr, b1, b2, eps, wd;
+  float dropout;
+  uint32_t seed;
+  uint32_t step_base;
+  float* loss_out;  // [steps]
+  int mode;         // 0 = train (Adam fused), 1 = grad only
+  int loss_kind;    // 0 = CE, 1 = MSE vs one-hot
+  // eval outputs
+  float* eval_acc;   // [2]: sum loss, sum correct (atomic)
+  float* logits_out; // optional [n_items][C]
+  // optional device step counter (Adam steps taken so far): when set it overrides t0 and
+  // step_base, and the kernel advances it by `steps` -> launches are graph-replayable.
+  int* step_counter;
+  // optional (GRAD mode): device batch cursor into idx. The kernel uses batch *cursor, first
+  // stores the previous step's (all-reduced) loss grad_out[P] into loss_out[*cursor - 1], and
+  // advances the cursor -> one captured step graph replays over a whole epoch.
+  int* cursor;
+  // diagnostic only: per-phase cycle sums (s_memtime deltas, thread 0) + [30]/[31] realtime
+  // start/end (100 MHz) when non-null; never set in production launches.
+  unsigned long long* prof;
+};
+
+hipError_t mlp_launch_train_L2(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
+hipError_t mlp_launch_train_L3(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
+hipError_t mlp_launch_train_L4(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
+hipError_t mlp_launch_eval_L2(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
+hipError_t mlp_launch_eval_L3(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
+hipError_t mlp_launch_eval_L4(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
+
+}  // namespace dct
+
+extern "C" {
+int dct_mlp_shape_size();
+int dct_mlp_make_shape(void* out, const int* dims, int L, int bmax);
+int dct_mlp_select(const dct::MlpShape* sh, int* nt, int* maxblk);
+int dct_mlp_train(const void* shape, const dct::MlpArgs* a, void* stream);
+int dct_mlp_eval(const void* shape, const dct::MlpArgs* a, int grid, void* stream);
+int dct_mlp_wave_supported(const int* dims, int L, int B);
+int dct_mlp_wave_train(const int* dims, int L, const dct::MlpArgs* a, void* stream);
+int dct_adam_flat(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, float lr,
+                  float b1, float b2, float eps, float wd, int64_t t, float grad_scale, int decoupled,
+                  const int* step_counter, void* stream);
+int dct_f32_to_bf16(const float* in, uint16_t* out, int64_t n, void* stream);
+}

@@ -1,0 +1,11 @@
+// Instantiation unit: fused MLP kernels with 4 linear layers (see mlp_fused_impl.h).
+#include "mlp_fused_impl.h"
+
+namespace dct {
+hipError_t mlp_launch_train_L4(const MlpShape& sh, const MlpArgs& a, hipStream_t st) {
+  return launch_train_L<4>(sh, a, st);
+}
+hipError_t mlp_launch_eval_L4(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st) {
+  return launch_eval_L<4>(sh, a, grid, st);
+}
+}  // namespace dct

@@ -1,0 +1,535 @@
+// Single-wave, register-resident MLP trainer for narrow MLPs (every hidden width <= 64).
+//
+// The reference model (WeatherClassifier 5-64-2, jobs/train_lightning_ddp.py:57-62) has 514
+// parameters and a batch of 4: one wave64 holds the whole training state in registers.
+// Lane j owns hidden unit j: its input-weight row W0[j][:], bias b0[j], its output-weight
+// column Wout[:, j] (and for 3 layers the middle row W1[j][:]), the Adam moments of all of
+// them, and its activations.  Per optimizer step:
+//   * the batch (x rows + labels, prefetched one step ahead into registers) is broadcast to
+//     every lane with v_readlane into SGPRs - no LDS, no barrier;
+//   * layer 0 is B x D0 FMAs per lane with SGPR operands; ReLU + inverted dropout
+//     (counter hash of (seed, step, row, unit));
+//   * hidden->hidden (3-layer nets): activations go through a 16 KB LDS tile read back as
+//     broadcast ds_read_b128; the backward uses a transposed copy of W1 kept in LDS;
+//   * the output layer is a cross-lane sum: DPP (quad_perm, row_ror) inside 16-lane rows,
+//     then v_readlane of the four row sums -> logits are wave-uniform;
+//   * CE/MSE and dlogits are computed redundantly by every lane (uniform values), so the
+//     backward needs no communication: dWout, dh, dW0 are lane-local FMAs;
+//   * Adam on the lane's own parameters (v_sqrt_f32 / v_rcp_f32).
+// A single wave needs no s_barrier: LDS instructions of one wave execute in order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dct_common.h"
+#include "mlp_fused.h"
+
+namespace dct {
+
+struct WaveShape {
+  int L;         // 2 or 3 linear layers
+  int d0, h1, h2, C;
+  int woff[3], boff[3];
+  int P;
+};
+
+__device__ __forceinline__ uint32_t wave_hash(uint32_t key) {
+  key ^= key >> 16;
+  key *= 0x7feb352du;
+  key ^= key >> 15;
+  key *= 0x846ca68bu;
+  key ^= key >> 16;
+  return key;
+}
+
+template <int CTRL>
+__device__ __forceinline__ float wdpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ float rl(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// sum over all 64 lanes of N values at once; results are wave-uniform
+template <int N>
+__device__ __forceinline__ void wave_sum_n(float (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += wdpp<0xB1>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += wdpp<0x4E>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += wdpp<0x124>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += wdpp<0x128>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = (rl(v[i], 0) + rl(v[i], 16)) + (rl(v[i], 32) + rl(v[i], 48));
+}
+
+__device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, float b1, float b2, float wd,
+                                      float step_size, float rbc2, float eps) {
+  g += wd * p;
+  m = b1 * m + (1.f - b1) * g;
+  v = b2 * v + (1.f - b2) * g * g;
+  p -= step_size * m * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(v) * rbc2 + eps);
+}
+
+template <int L, int BMAX, int D0, int CM>
+__global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
+  constexpr int HM = 64;
+  constexpr int NPF = (BMAX * D0 + BMAX + 63) / 64;  // prefetch dwords per lane
+  __shared__ __attribute__((aligned(16))) float hs[L == 3 ? BMAX * HM : 4];     // layer-0 activations
+  __shared__ __attribute__((aligned(16))) float ds[L == 3 ? BMAX * HM : 4];     // dh of the middle layer
+  __shared__ __attribute__((aligned(16))) float w1t[L == 3 ? HM * (HM + 4) : 4];  // W1^T (rows padded)
+  const int j = threadIdx.x;  // lane = hidden unit
+  const int d0 = sh.d0, H1 = sh.h1, H2 = (L == 3 ? sh.h2 : sh.h1), C = sh.C;
+  const bool adam = (a.mode == 0);
+  const bool own1 = j < H1;
+  const bool own2 = j < H2;  // unit of the last hidden layer
+
+  // ---------------------------------------------------------------- parameters -> registers
+  float w0[D0], mw0[D0], vw0[D0];
+  float b0 = 0.f, mb0 = 0.f, vb0 = 0.f;
+  float wo[CM], mwo[CM], vwo[CM];
+  float bo = 0.f, mbo = 0.f, vbo = 0.f;  // lane c < C owns bout[c]
+  float w1[L == 3 ? HM : 1], mw1[L == 3 ? HM : 1], vw1[L == 3 ? HM : 1];
+  float b1 = 0.f, mb1 = 0.f, vb1 = 0.f;
+  const int lo = L - 1;  // index of the output layer
+#pragma unroll
+  for (int k = 0; k < D0; ++k) {
+    const bool ok = own1 && k < d0;
+    const int f = sh.woff[0] + j * d0 + k;
+    w0[k] = ok ? a.p[f] : 0.f;
+    mw0[k] = (ok && adam) ? a.m[f] : 0.f;
+    vw0[k] = (ok && adam) ? a.v[f] : 0.f;
+  }
+  if (own1) {
+    b0 = a.p[sh.boff[0] + j];
+    if (adam) { mb0 = a.m[sh.boff[0] + j]; vb0 = a.v[sh.boff[0] + j]; }
+  }
+  if (L == 3) {
+#pragma unroll
+    for (int i = 0; i < (L == 3 ? HM : 1); ++i) {
+      const bool ok = own2 && i < H1;
+      const int f = sh.woff[1] + j * H1 + i;
+      w1[i] = ok ? a.p[f] : 0.f;
+      mw1[i] = (ok && adam) ? a.m[f] : 0.f;
+      vw1[i] = (ok && adam) ? a.v[f] : 0.f;
+    }
+    if (own2) {
+      b1 = a.p[sh.boff[1] + j];
+      if (adam) { mb1 = a.m[sh.boff[1] + j]; vb1 = a.v[sh.boff[1] + j]; }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < CM; ++c) {
+    const bool ok = own2 && c < C;
+    const int f = sh.woff[lo] + c * H2 + j;
+    wo[c] = ok ? a.p[f] : 0.f;
+    mwo[c] = (ok && adam) ? a.m[f] : 0.f;
+    vwo[c] = (ok && adam) ? a.v[f] : 0.f;
+  }
+  if (j < C) {
+    bo = a.p[sh.boff[lo] + j];
+    if (adam) { mbo = a.m[sh.boff[lo] + j]; vbo = a.v[sh.boff[lo] + j]; }
+  }
+  if (L == 3) {  // W1^T (row i = column i of W1) for the middle layer's backward
+#pragma unroll
+    for (int i = 0; i < (L == 3 ? HM : 1); ++i) w1t[i * (HM + 4) + j] = w1[i];
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  }
+
+  int cur0 = 0;
+  if (a.cursor) {
+    cur0 = __hip_atomic_load(a.cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (j == 0 && cur0 > 0 && a.loss_out) a.loss_out[cur0 - 1] = a.grad_out[sh.P];
+  }
+  int t0 = a.t0;
+  uint32_t step_base = a.step_base;
+  if (a.step_counter) {
+    t0 = __hip_atomic_load(a.step_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    step_base = (uint32_t)t0;
+  }
+  const int B = a.B;
+
+  // ---------------------------------------------------------------- batch prefetch
+  // slot r of lane j holds element e = j + 64 r: x[b][k] (e < BMAX*D0) or label b (next BMAX).
+  // Depth-2 pipeline: idx of batch s+2 and the x/label dwords of batch s+1 are issued at the
+  // top of step s; neither is consumed in step s, so no wait lands inside the step.
+  auto slot_of = [&](int r, int& b, int& k, bool& isx) {
+    const int e = j + 64 * r;
+    isx = e < BMAX * D0;
+    if (isx) { b = e / D0; k = e - b * D0; } else { b = e - BMAX * D0; k = 0; }
+  };
+  auto load_idx = [&](int sbatch, int (&ridx)[NPF]) {
+#pragma unroll
+    for (int r = 0; r < NPF; ++r) {
+      int b, k; bool isx;
+      slot_of(r, b, k, isx);
+      int qi = sbatch * B + (b < BMAX ? b : 0);
+      qi = (qi < a.n_items && qi >= 0) ? qi : 0;
+      ridx[r] = a.idx[qi];
+    }
+  };
+  auto load_vals = [&](int sbatch, const int (&ridx)[NPF], uint32_t (&raw)[NPF]) {
+    const int bsz = min(B, a.n_items - sbatch * B);
+#pragma unroll
+    for (int r = 0; r < NPF; ++r) {
+      int b, k; bool isx;
+      slot_of(r, b, k, isx);
+      const bool ok = (b < bsz) && (b < BMAX) && (!isx || k < d0);
+      const uint32_t* src = isx ? reinterpret_cast<const uint32_t*>(a.X) + (size_t)ridx[r] * a.ldx + (k < d0 ? k : 0)
+                                : reinterpret_cast<const uint32_t*>(a.Y) + ridx[r];
+      const uint32_t v = *src;
+      raw[r] = ok ? v : 0u;
+    }
+  };
+  uint32_t cur[NPF], nxt[NPF];
+  int ridx_a[NPF], ridx_b[NPF];
+  load_idx(cur0, ridx_a);
+  load_vals(cur0, ridx_a, cur);
+  load_idx(cur0 + 1, ridx_a);  // idx of batch cur0 + 1
+
+  const float keep_scale = (a.dropout > 0.f) ? 1.0f / (1.0f - a.dropout) : 1.0f;
+  const uint32_t drop_thr = (uint32_t)(a.dropout * 4294967296.0);
+  const bool prof = (a.prof != nullptr) && j == 0;
+  if (prof) a.prof[30] = __builtin_amdgcn_s_memrealtime();
+
+  for (int s = 0; s < a.steps; ++s) {
+    const int sb = s + cur0;
+    const int bs = min(B, a.n_items - sb * B);
+    const uint32_t gstep = step_base + (uint32_t)s;
+    // issue: values of batch sb+1 (idx already in registers) and idx of batch sb+2
+    load_vals(sb + 1, ridx_a, nxt);
+    load_idx(sb + 2, ridx_b);
+
+    // broadcast the current batch: x[b][k] and labels -> SGPR-uniform values
+    float x[BMAX][D0];
+    int y[BMAX];
+#pragma unroll
+    for (int b = 0; b < BMAX; ++b) {
+#pragma unroll
+      for (int k = 0; k < D0; ++k) {
+        const int e = b * D0 + k;
+        x[b][k] = __int_as_float(__builtin_amdgcn_readlane((int)cur[e / 64], e % 64));
+      }
+      const int e = BMAX * D0 + b;
+      y[b] = __builtin_amdgcn_readlane((int)cur[e / 64], e % 64);
+    }
+
+    // ---- layer 0: h[b] = dropout(relu(W0[j] . x[b] + b0))
+    const uint32_t hkey = (a.seed * 0x9E3779B1u) ^ (gstep * 0x85EBCA77u);
+    float h[BMAX];
+#pragma unroll
+    for (int b = 0; b < BMAX; ++b) {
+      float z = b0;
+#pragma unroll
+      for (int k = 0; k < D0; ++k) z += w0[k] * x[b][k];
+      z = fmaxf(z, 0.f);
+      if (drop_thr) {
+        const uint32_t r = wave_hash(hkey ^ ((uint32_t)(b * 64 + j) * 0xC2B2AE3Du));
+        z = (r < drop_thr) ? 0.f : z * keep_scale;
+      }
+      h[b] = own1 ? z : 0.f;
+    }
+    // ---- middle layer (3-layer nets): h2[b] = dropout(relu(W1[j] . h[b] + b1))
+    float h2[BMAX];
+    if (L == 3) {
+#pragma unroll
+      for (int b = 0; b < BMAX; ++b) hs[b * HM + j] = h[b];
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done (in-order DS)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+      for (int b = 0; b < BMAX; ++b) {
+        float z = b1;
+#pragma unroll
+        for (int i4 = 0; i4 < HM / 4; ++i4) {
+          const float4 hv = *reinterpret_cast<const float4*>(&hs[b * HM + i4 * 4]);
+          z += w1[i4 * 4 + 0] * hv.x + w1[i4 * 4 + 1] * hv.y + w1[i4 * 4 + 2] * hv.z + w1[i4 * 4 + 3] * hv.w;
+        }
+        z = fmaxf(z, 0.f);
+        if (drop_thr) {
+          const uint32_t r = wave_hash(hkey ^ ((uint32_t)(4096 + b * 64 + j) * 0xC2B2AE3Du));
+          z = (r < drop_thr) ? 0.f : z * keep_scale;
+        }
+        h2[b] = own2 ? z : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < BMAX; ++b) h2[b] = h[b];
+    }
+    // ---- output layer: logits[b][c] = sum_j Wout[c][j] h2_j[b] + bout[c]  (cross-lane)
+    float zc[BMAX * CM];
+#pragma unroll
+    for (int b = 0; b < BMAX; ++b)
+#pragma unroll
+      for (int c = 0; c < CM; ++c) zc[b * CM + c] = wo[c] * h2[b];
+    wave_sum_n(zc);
+    float boc[CM];
+#pragma unroll
+    for (int c = 0; c < CM; ++c) boc[c] = rl(bo, c);
+    // ---- loss + dlogits (wave-uniform, computed redundantly in every lane)
+    float dz[BMAX * CM];
+    float lsum = 0.f;
+    const float inv = 1.0f / (float)(bs > 0 ? bs : 1);
+#pragma unroll
+    for (int b = 0; b < BMAX; ++b) {
+      const bool live = b < bs;
+      float zz[CM];
+#pragma unroll
+      for (int c = 0; c < CM; ++c) zz[c] = zc[b * CM + c] + boc[c];
+      float lb = 0.f;
+      if (a.loss_kind == 0) {
+        float mx = -3.402823466e+38f;
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+          if (c < C) mx = fmaxf(mx, zz[c]);
+        float e[CM], se = 0.f, zy = 0.f;
+#pragma unroll
+        for (int c = 0; c < CM; ++c) {
+          e[c] = (c < C) ? __expf(zz[c] - mx) : 0.f;
+          se += e[c];
+          if (c == y[b]) zy = zz[c];
+        }
+        lb = mx + __logf(se) - zy;
+        const float rs = __builtin_amdgcn_rcpf(se);
+#pragma unroll
+        for (int c = 0; c < CM; ++c) dz[b * CM + c] = live ? (e[c] * rs - (c == y[b] ? 1.f : 0.f)) * inv : 0.f;
+      } else {
+        const float sc = 2.f / (float)C;
+#pragma unroll
+        for (int c = 0; c < CM; ++c) {
+          const float d = (c < C) ? zz[c] - (c == y[b] ? 1.f : 0.f) : 0.f;
+          lb += d * d;
+          dz[b * CM + c] = live ? d * sc * inv : 0.f;
+        }
+        lb /= (float)C;
+      }
+      lsum += live ? lb : 0.f;
+    }
+    if (j == 0) {
+      const float bl = bs > 0 ? lsum * inv : 0.f;
+      if (a.loss_out && !a.cursor) a.loss_out[s] = bl;
+      if (!adam) a.grad_out[sh.P] = bl;
+    }
+
+    // ---- backward (lane-local)
+    float gwo[CM], gbo = 0.f;
+#pragma unroll
+    for (int c = 0; c < CM; ++c) {
+      float g = 0.f;
+#pragma unroll
+      for (int b = 0; b < BMAX; ++b) g += dz[b * CM + c] * h2[b];
+      gwo[c] = g;
+    }
+#pragma unroll
+    for (int c = 0; c < CM; ++c) {
+      float g = 0.f;
+#pragma unroll
+      for (int b = 0; b < BMAX; ++b) g += dz[b * CM + c];
+      if (c == j) gbo = g;
+    }
+    float dh2[BMAX];  // dL/dpre-activation of the last hidden layer
+#pragma unroll
+    for (int b = 0; b < BMAX; ++b) {
+      float g = 0.f;
+#pragma unroll
+      for (int c = 0; c < CM; ++c) g += dz[b * CM + c] * wo[c];
+      dh2[b] = (h2[b] > 0.f) ? g * keep_scale : 0.f;
+    }
+    float dh[BMAX];
+    float gw1[L == 3 ? HM : 1], gb1 = 0.f;
+    if (L == 3) {
+      // dW1[j][i] = sum_b dh2_j[b] h_i[b]  (h_i from the LDS tile), db1 = sum_b dh2
+#pragma unroll
+      for (int i = 0; i < (L == 3 ? HM : 1); ++i) gw1[i] = 0.f;
+#pragma unroll
+      for (int b = 0; b < BMAX; ++b) {
+#pragma unroll
+        for (int i4 = 0; i4 < HM / 4; ++i4) {
+          const float4 hv = *reinterpret_cast<const float4*>(&hs[b * HM + i4 * 4]);
+          gw1[i4 * 4 + 0] += dh2[b] * hv.x;
+          gw1[i4 * 4 + 1] += dh2[b] * hv.y;
+          gw1[i4 * 4 + 2] += dh2[b] * hv.z;
+          gw1[i4 * 4 + 3] += dh2[b] * hv.w;
+        }
+        gb1 += dh2[b];
+      }
+      // dh_i[b] = sum_j W1[j][i] dh2_j[b]  via W1^T rows in LDS and dh2 broadcast
+#pragma unroll
+      for (int b = 0; b < BMAX; ++b) ds[b * HM + j] = dh2[b];
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+      for (int b = 0; b < BMAX; ++b) {
+        float g = 0.f;
+#pragma unroll
+        for (int i4 = 0; i4 < HM / 4; ++i4) {
+          const float4 wt = *reinterpret_cast<const float4*>(&w1t[j * (HM + 4) + i4 * 4]);
+          const float4 dv = *reinterpret_cast<const float4*>(&ds[b * HM + i4 * 4]);
+          g += wt.x * dv.x + wt.y * dv.y + wt.z * dv.z + wt.w * dv.w;
+        }
+        dh[b] = (h[b] > 0.f) ? g * keep_scale : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < BMAX; ++b) dh[b] = dh2[b];
+    }
+    float gw0[D0], gb0 = 0.f;
+#pragma unroll
+    for (int k = 0; k < D0; ++k) {
+      float g = 0.f;
+#pragma unroll
+      for (int b = 0; b < BMAX; ++b) g += dh[b] * x[b][k];
+      gw0[k] = g;
+    }
+#pragma unroll
+    for (int b = 0; b < BMAX; ++b) gb0 += dh[b];
+
+    if (adam) {
+      const int t = t0 + s + 1;
+      const float step_size = a.lr / (1.f - __powf(a.b1, (float)t));
+      const float rbc2 = __builtin_amdgcn_rsqf(1.f - __powf(a.b2, (float)t));
+      if (own1) {
+#pragma unroll
+        for (int k = 0; k < D0; ++k)
+          if (k < d0) adam1(w0[k], gw0[k], mw0[k], vw0[k], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+        adam1(b0, gb0, mb0, vb0, a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+      }
+      if (L == 3 && own2) {
+#pragma unroll
+        for (int i = 0; i < (L == 3 ? HM : 1); ++i)
+          if (i < H1) adam1(w1[i], gw1[i], mw1[i], vw1[i], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+        adam1(b1, gb1, mb1, vb1, a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+      }
+      if (own2) {
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+          if (c < C) adam1(wo[c], gwo[c], mwo[c], vwo[c], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+      }
+      if (j < C) adam1(bo, gbo, mbo, vbo, a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+      if (L == 3) {  // refresh W1^T for the next step's backward
+#pragma unroll
+        for (int i = 0; i < (L == 3 ? HM : 1); ++i) w1t[i * (HM + 4) + j] = w1[i];
+      }
+    } else {
+      if (own1) {
+#pragma unroll
+        for (int k = 0; k < D0; ++k)
+          if (k < d0) a.grad_out[sh.woff[0] + j * d0 + k] = gw0[k];
+        a.grad_out[sh.boff[0] + j] = gb0;
+      }
+      if (L == 3 && own2) {
+#pragma unroll
+        for (int i = 0; i < (L == 3 ? HM : 1); ++i)
+          if (i < H1) a.grad_out[sh.woff[1] + j * H1 + i] = gw1[i];
+        a.grad_out[sh.boff[1] + j] = gb1;
+      }
+      if (own2) {
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+          if (c < C) a.grad_out[sh.woff[lo] + c * H2 + j] = gwo[c];
+      }
+      if (j < C) a.grad_out[sh.boff[lo] + j] = gbo;
+    }
+#pragma unroll
+    for (int r = 0; r < NPF; ++r) {
+      cur[r] = nxt[r];
+      ridx_a[r] = ridx_b[r];
+    }
+  }
+  if (prof) a.prof[31] = __builtin_amdgcn_s_memrealtime();
+  if (a.cursor && j == 0) __hip_atomic_store(a.cursor, cur0 + a.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.step_counter && j == 0)
+    __hip_atomic_store(a.step_counter, t0 + a.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!adam) return;
+  // ---- write back params + moments
+#pragma unroll
+  for (int k = 0; k < D0; ++k) {
+    if (own1 && k < d0) {
+      const int f = sh.woff[0] + j * d0 + k;
+      a.p[f] = w0[k]; a.m[f] = mw0[k]; a.v[f] = vw0[k];
+    }
+  }
+  if (own1) {
+    const int f = sh.boff[0] + j;
+    a.p[f] = b0; a.m[f] = mb0; a.v[f] = vb0;
+  }
+  if (L == 3 && own2) {
+#pragma unroll
+    for (int i = 0; i < (L == 3 ? HM : 1); ++i) {
+      if (i < H1) {
+        const int f = sh.woff[1] + j * H1 + i;
+        a.p[f] = w1[i]; a.m[f] = mw1[i]; a.v[f] = vw1[i];
+      }
+    }
+    const int f = sh.boff[1] + j;
+    a.p[f] = b1; a.m[f] = mb1; a.v[f] = vb1;
+  }
+#pragma unroll
+  for (int c = 0; c < CM; ++c) {
+    if (own2 && c < C) {
+      const int f = sh.woff[lo] + c * H2 + j;
+      a.p[f] = wo[c]; a.m[f] = mwo[c]; a.v[f] = vwo[c];
+    }
+  }
+  if (j < C) {
+    const int f = sh.boff[lo] + j;
+    a.p[f] = bo; a.m[f] = mbo; a.v[f] = vbo;
+  }
+}
+
+}  // namespace dct
+
+namespace {
+using dct::MlpArgs;
+using dct::WaveShape;
+
+template <int L, int BMAX, int D0, int CM>
+hipError_t launch_wave(const WaveShape& sh, const MlpArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((dct::mlp_wave_kernel<L, BMAX, D0, CM>), dim3(1), dim3(64), 0, st, sh, a);
+  return hipGetLastError();
+}
+
+template <int L, int BMAX>
+hipError_t launch_wave_d0(const WaveShape& sh, const MlpArgs& a, hipStream_t st) {
+  if (sh.C > 4) return hipErrorInvalidValue;
+  if (sh.d0 <= 8) return launch_wave<L, BMAX, 8, 4>(sh, a, st);
+  if (sh.d0 <= 16) return launch_wave<L, BMAX, 16, 4>(sh, a, st);
+  return hipErrorInvalidValue;
+}
+}  // namespace
+
+extern "C" {
+
+// 1 if dims fit the single-wave kernel: 2 or 3 layers, hidden <= 64, d0 <= 16, classes <= 4
+int dct_mlp_wave_supported(const int* dims, int L, int B) {
+  if (L != 2 && L != 3) return 0;
+  if (dims[0] > 16 || dims[L] > 4 || B < 1 || B > 8) return 0;
+  for (int l = 1; l < L; ++l)
+    if (dims[l] > 64) return 0;
+  return 1;
+}
+
+int dct_mlp_wave_train(const int* dims, int L, const dct::MlpArgs* a, void* stream) {
+  if (!dct_mlp_wave_supported(dims, L, a->B)) return (int)hipErrorInvalidValue;
+  WaveShape sh{};
+  sh.L = L;
+  sh.d0 = dims[0];
+  sh.h1 = dims[1];
+  sh.h2 = L == 3 ? dims[2] : dims[1];
+  sh.C = dims[L];
+  int flat = 0;
+  for (int l = 0; l < L; ++l) {
+    sh.woff[l] = flat;
+    flat += dims[l] * dims[l + 1];
+    sh.boff[l] = flat;
+    flat += dims[l + 1];
+  }
+  sh.P = flat;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (L == 2) return (int)(a->B <= 4 ? launch_wave_d0<2, 4>(sh, *a, st) : launch_wave_d0<2, 8>(sh, *a, st));
+  return (int)(a->B <= 4 ? launch_wave_d0<3, 4>(sh, *a, st) : launch_wave_d0<3, 8>(sh, *a, st));
+}
+
+}  // extern "C"

@@ -1,0 +1,338 @@
+// Memory-bound NN kernels for gfx950: fused loss fwd+bwd, bias+activation backward with the
+// bias-gradient column reduction, LayerNorm fwd/bwd, and the on-device batch gather.
+// All of them vectorise bf16 I/O to 16-B per lane where the layout allows (CDNA guide G13)
+// and reduce per block before one atomic per (block, column) (G12).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dct_common.h"
+#include "kernels.h"
+
+namespace dct {
+
+__device__ __forceinline__ float gelu_grad(float z) {
+  const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * z * z);
+  return cdf + z * pdf;
+}
+
+__device__ __forceinline__ float ld_any(const void* p, size_t i, int bf16) {
+  return bf16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(p)[i]) : reinterpret_cast<const float*>(p)[i];
+}
+__device__ __forceinline__ void st_any(void* p, size_t i, float v, int bf16) {
+  if (bf16) reinterpret_cast<uint16_t*>(p)[i] = f32_to_bf16(v);
+  else reinterpret_cast<float*>(p)[i] = v;
+}
+
+// ------------------------------------------------------------------------------- loss
+__global__ __launch_bounds__(256) void loss_kernel(const void* logits, int lbf16, const int* labels, void* dlogits,
+                                                   float* loss_sum, float* correct_sum, int M, int C,
+                                                   float grad_scale, int loss_kind) {
+  __shared__ float red[2][4];
+  float l_acc = 0.f, c_acc = 0.f;
+  for (int row = blockIdx.x * blockDim.x + threadIdx.x; row < M; row += gridDim.x * blockDim.x) {
+    const size_t base = (size_t)row * C;
+    const int y = labels[row];
+    float mx = -3.402823466e+38f;
+    int am = 0;
+    for (int c = 0; c < C; ++c) {
+      const float z = ld_any(logits, base + c, lbf16);
+      if (z > mx) { mx = z; am = c; }
+    }
+    c_acc += (am == y) ? 1.f : 0.f;
+    if (loss_kind == 0) {
+      float s = 0.f;
+      for (int c = 0; c < C; ++c) s += __expf(ld_any(logits, base + c, lbf16) - mx);
+      const float lse = mx + __logf(s);
+      l_acc += lse - ld_any(logits, base + y, lbf16);
+      if (dlogits) {
+        const float rs = 1.f / s;
+        for (int c = 0; c < C; ++c) {
+          const float pr = __expf(ld_any(logits, base + c, lbf16) - mx) * rs;
+          st_any(dlogits, base + c, (pr - (c == y ? 1.f : 0.f)) * grad_scale, lbf16);
+        }
+      }
+    } else {
+      float acc = 0.f;
+      for (int c = 0; c < C; ++c) {
+        const float d = ld_any(logits, base + c, lbf16) - (c == y ? 1.f : 0.f);
+        acc += d * d;
+        if (dlogits) st_any(dlogits, base + c, 2.f * d * grad_scale / (float)C, lbf16);
+      }
+      l_acc += acc / (float)C;
+    }
+  }
+  l_acc = wave_sum(l_acc);
+  c_acc = wave_sum(c_acc);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][w] = l_acc; red[1][w] = c_acc; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { a += red[0][i]; b += red[1][i]; }
+    if (loss_sum) atomicAdd(loss_sum, a);
+    if (correct_sum) atomicAdd(correct_sum, b);
+  }
+}
+
+// ------------------------------------------------------------------------ bias+act bwd
+// block: 64 column-chunks (8 columns each) x 4 row lanes
+template <bool VEC>
+__global__ __launch_bounds__(256) void bias_act_bwd_kernel(const uint16_t* dY, const uint16_t* aux, uint16_t* dZ,
+                                                           float* dbias, int M, int N, int ldy, int act,
+                                                           int accumulate_bias) {
+  __shared__ float part[4][64 * 8];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int cc = blockIdx.x * 64 + tx;
+  const int c0 = cc * 8;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  if (c0 < N) {
+    for (int r = blockIdx.y * 4 + ty; r < M; r += gridDim.y * 4) {
+      const size_t o = (size_t)r * ldy + c0;
+      float dy[8], zz[8];
+      if (VEC && c0 + 8 <= N) {
+        const uint4 v = *reinterpret_cast<const uint4*>(dY + o);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { dy[2 * j] = bf16_to_f32(w[j] & 0xffff); dy[2 * j + 1] = bf16_to_f32(w[j] >> 16); }
+        if (act != ACT_NONE) {
+          const uint4 a = *reinterpret_cast<const uint4*>(aux + o);
+          const uint32_t u[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { zz[2 * j] = bf16_to_f32(u[j] & 0xffff); zz[2 * j + 1] = bf16_to_f32(u[j] >> 16); }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          dy[j] = (c0 + j < N) ? bf16_to_f32(dY[o + j]) : 0.f;
+          zz[j] = (act != ACT_NONE && c0 + j < N) ? bf16_to_f32(aux[o + j]) : 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float d = dy[j];
+        if (act == ACT_RELU) d = zz[j] > 0.f ? d : 0.f;
+        else if (act == ACT_GELU) d *= gelu_grad(zz[j]);
+        dy[j] = d;
+        acc[j] += d;
+      }
+      if (dZ) {
+        if (VEC && c0 + 8 <= N) {
+          uint4 v;
+          v.x = f32_to_bf16(dy[0]) | ((uint32_t)f32_to_bf16(dy[1]) << 16);
+          v.y = f32_to_bf16(dy[2]) | ((uint32_t)f32_to_bf16(dy[3]) << 16);
+          v.z = f32_to_bf16(dy[4]) | ((uint32_t)f32_to_bf16(dy[5]) << 16);
+          v.w = f32_to_bf16(dy[6]) | ((uint32_t)f32_to_bf16(dy[7]) << 16);
+          *reinterpret_cast<uint4*>(dZ + o) = v;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (c0 + j < N) dZ[o + j] = f32_to_bf16(dy[j]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[ty][tx * 8 + j] = acc[j];
+  __syncthreads();
+  if (ty == 0 && dbias && c0 < N) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (c0 + j < N) {
+        const float s = part[0][tx * 8 + j] + part[1][tx * 8 + j] + part[2][tx * 8 + j] + part[3][tx * 8 + j];
+        if (gridDim.y == 1 && !accumulate_bias) dbias[c0 + j] = s;
+        else atomicAdd(&dbias[c0 + j], s);
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------------------------- layernorm
+// one wave per row, N <= 64 * LN_MAX
+constexpr int LN_MAX = 32;
+
+__global__ __launch_bounds__(256) void layernorm_fwd_kernel(const void* x, const float* w, const float* b, void* y,
+                                                            float* mean_out, float* rstd_out, int M, int N, float eps,
+                                                            int in_bf16, int out_bf16) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const size_t base = (size_t)row * N;
+  float v[LN_MAX];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < LN_MAX; ++j) {
+    const int c = lane + j * 64;
+    v[j] = (c < N) ? ld_any(x, base + c, in_bf16) : 0.f;
+    s += v[j];
+  }
+  const float mean = wave_sum(s) / (float)N;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < LN_MAX; ++j) {
+    const int c = lane + j * 64;
+    const float d = (c < N) ? v[j] - mean : 0.f;
+    q += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)N + eps);
+#pragma unroll
+  for (int j = 0; j < LN_MAX; ++j) {
+    const int c = lane + j * 64;
+    if (c < N) st_any(y, base + c, (v[j] - mean) * rstd * (w ? w[c] : 1.f) + (b ? b[c] : 0.f), out_bf16);
+  }
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const void* dy, const void* x, const float* w,
+                                                            const float* mean, const float* rstd, void* dx, float* dw,
+                                                            float* db, int M, int N, int bf16_io) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nw = blockDim.x >> 6;
+  float dwa[LN_MAX], dba[LN_MAX];
+#pragma unroll
+  for (int j = 0; j < LN_MAX; ++j) { dwa[j] = 0.f; dba[j] = 0.f; }
+  for (int row = blockIdx.x * nw + wave; row < M; row += gridDim.x * nw) {
+    const size_t base = (size_t)row * N;
+    const float mu = mean[row], rs = rstd[row];
+    float g[LN_MAX], xh[LN_MAX];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < LN_MAX; ++j) {
+      const int c = lane + j * 64;
+      if (c < N) {
+        const float d = ld_any(dy, base + c, bf16_io);
+        xh[j] = (ld_any(x, base + c, bf16_io) - mu) * rs;
+        g[j] = d * (w ? w[c] : 1.f);
+        dwa[j] += d * xh[j];
+        dba[j] += d;
+      } else {
+        xh[j] = 0.f;
+        g[j] = 0.f;
+      }
+      s1 += g[j];
+      s2 += g[j] * xh[j];
+    }
+    s1 = wave_sum(s1) / (float)N;
+    s2 = wave_sum(s2) / (float)N;
+#pragma unroll
+    for (int j = 0; j < LN_MAX; ++j) {
+      const int c = lane + j * 64;
+      if (c < N) st_any(dx, base + c, rs * (g[j] - s1 - xh[j] * s2), bf16_io);
+    }
+  }
+  __shared__ float red[4][64 * 2];
+  // reduce dw/db across the block's waves, one atomic per column per block
+#pragma unroll
+  for (int j = 0; j < LN_MAX; ++j) {
+    const int c = lane + j * 64;
+    if (j * 64 >= N) break;
+    red[wave][lane] = dwa[j];
+    red[wave][64 + lane] = dba[j];
+    __syncthreads();
+    if (wave == 0 && c < N) {
+      float a = 0.f, bsum = 0.f;
+      for (int i = 0; i < nw; ++i) { a += red[i][lane]; bsum += red[i][64 + lane]; }
+      if (dw) atomicAdd(&dw[c], a);
+      if (db) atomicAdd(&db[c], bsum);
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------ gather
+__global__ __launch_bounds__(256) void gather_rows16_kernel(const uint4* src, const int* idx, uint4* dst,
+                                                            int64_t n_rows, int row_vec) {
+  const int64_t total = n_rows * row_vec;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / row_vec;
+    const int c = (int)(e - r * row_vec);
+    dst[e] = src[(int64_t)idx[r] * row_vec + c];
+  }
+}
+__global__ __launch_bounds__(256) void gather_rows4_kernel(const uint32_t* src, const int* idx, uint32_t* dst,
+                                                           int64_t n_rows, int row_words) {
+  const int64_t total = n_rows * row_words;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / row_words;
+    const int c = (int)(e - r * row_words);
+    dst[e] = src[(int64_t)idx[r] * row_words + c];
+  }
+}
+
+}  // namespace dct
+
+static inline int grid_cap(int64_t work, int block, int cap = 2048) {
+  int64_t g = (work + block - 1) / block;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+extern "C" {
+
+int dct_loss_fwd_bwd(const void* logits, int logits_bf16, const int* labels, void* dlogits, float* loss_sum,
+                     float* correct_sum, int M, int C, float grad_scale, int loss_kind, void* stream) {
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(dct::loss_kernel, dim3(grid_cap(M, 256, 1024)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     logits, logits_bf16, labels, dlogits, loss_sum, correct_sum, M, C, grad_scale, loss_kind);
+  return (int)hipGetLastError();
+}
+
+int dct_bias_act_bwd(const void* dY, const void* act_aux, uint16_t* dZ, float* dbias, int M, int N, int ldy, int act,
+                     int accumulate_bias, void* stream) {
+  if (M <= 0 || N <= 0) return 0;
+  const int ncc = (N + 7) / 8;
+  dim3 grid((ncc + 63) / 64, (unsigned)grid_cap((M + 3) / 4, 1, 512));
+  const bool vec = (N % 8 == 0) && (ldy % 8 == 0) && ((((uintptr_t)dY) | ((uintptr_t)act_aux) | ((uintptr_t)dZ)) & 15) == 0;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (vec)
+    hipLaunchKernelGGL(dct::bias_act_bwd_kernel<true>, grid, dim3(256), 0, st, (const uint16_t*)dY,
+                       (const uint16_t*)act_aux, dZ, dbias, M, N, ldy, act, accumulate_bias);
+  else
+    hipLaunchKernelGGL(dct::bias_act_bwd_kernel<false>, grid, dim3(256), 0, st, (const uint16_t*)dY,
+                       (const uint16_t*)act_aux, dZ, dbias, M, N, ldy, act, accumulate_bias);
+  return (int)hipGetLastError();
+}
+
+int dct_layernorm_fwd(const void* x, const float* w, const float* b, void* y, float* mean, float* rstd, int M, int N,
+                      float eps, int in_bf16, int out_bf16, void* stream) {
+  if (N > 64 * dct::LN_MAX) return (int)hipErrorInvalidValue;
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(dct::layernorm_fwd_kernel, dim3((M + 3) / 4), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     x, w, b, y, mean, rstd, M, N, eps, in_bf16, out_bf16);
+  return (int)hipGetLastError();
+}
+
+int dct_layernorm_bwd(const void* dy, const void* x, const float* w, const float* mean, const float* rstd, void* dx,
+                      float* dw, float* db, int M, int N, int bf16_io, void* stream) {
+  if (N > 64 * dct::LN_MAX) return (int)hipErrorInvalidValue;
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(dct::layernorm_bwd_kernel, dim3(grid_cap((M + 3) / 4, 1, 1024)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), dy, x, w, mean, rstd, dx, dw, db, M, N, bf16_io);
+  return (int)hipGetLastError();
+}
+
+int dct_gather_rows(const void* src, const int* idx, void* dst, int64_t n_rows, int row_bytes, void* stream) {
+  if (n_rows <= 0) return 0;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (row_bytes % 16 == 0 && ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) == 0) {
+    const int rv = row_bytes / 16;
+    hipLaunchKernelGGL(dct::gather_rows16_kernel, dim3(grid_cap(n_rows * rv, 256)), dim3(256), 0, st,
+                       (const uint4*)src, idx, (uint4*)dst, n_rows, rv);
+  } else if (row_bytes % 4 == 0) {
+    const int rw = row_bytes / 4;
+    hipLaunchKernelGGL(dct::gather_rows4_kernel, dim3(grid_cap(n_rows * rw, 256)), dim3(256), 0, st,
+                       (const uint32_t*)src, idx, (uint32_t*)dst, n_rows, rw);
+  } else {
+    return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

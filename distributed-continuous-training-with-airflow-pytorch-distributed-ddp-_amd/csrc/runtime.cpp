@@ -1,0 +1,218 @@
+// Native distributed runtime: RCCL communicator, gradient bucket reducer, HIP graph capture.
+//
+// Reference parity: the reference's collectives are all implicit inside
+// Lightning/torch DDP over gloo/TCP - Reducer buckets (X5, 2,056 B per step), the
+// sync_dist scalar all-reduces (X6/X7), broadcasts of the initial state (X3) and barriers
+// (X9).  This file is the MI355X replacement: one RCCL communicator per process (the torch
+// "nccl" backend on ROCm is RCCL too; owning the comm directly lets the C++ step executor
+// issue collectives with no Python on the path and capture them into hipGraphs), a
+// bucketed reducer whose buckets are views of ONE flat gradient buffer (no copy-in/out),
+// all-reduced with ncclAvg on a dedicated comm stream as soon as the backward kernels that
+// produce each bucket have been enqueued (event-ordered overlap with the rest of backward),
+// and a thin stream-capture wrapper used to collapse launch-bound step loops.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "runtime.h"
+
+namespace dct {
+
+static void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+static void nccl_check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+static ncclDataType_t to_nccl_dtype(int dt) {
+  switch (dt) {
+    case DT_F32: return ncclFloat32;
+    case DT_BF16: return ncclBfloat16;
+    case DT_F16: return ncclFloat16;
+    case DT_I32: return ncclInt32;
+    case DT_I64: return ncclInt64;
+    case DT_U8: return ncclUint8;
+    default: throw std::runtime_error("unsupported dtype for RCCL");
+  }
+}
+static ncclRedOp_t to_nccl_op(int op) {
+  switch (op) {
+    case OP_SUM: return ncclSum;
+    case OP_AVG: return ncclAvg;
+    case OP_MAX: return ncclMax;
+    case OP_MIN: return ncclMin;
+    default: throw std::runtime_error("unsupported reduce op");
+  }
+}
+
+std::string comm_unique_id() {
+  ncclUniqueId id;
+  nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  return std::string(id.internal, NCCL_UNIQUE_ID_BYTES);
+}
+
+Comm::Comm(const std::string& uid, int world, int rank, int device) : world_(world), rank_(rank), device_(device) {
+  if ((int)uid.size() != NCCL_UNIQUE_ID_BYTES) throw std::runtime_error("bad RCCL unique id size");
+  hip_check(hipSetDevice(device), "hipSetDevice");
+  ncclUniqueId id;
+  std::memcpy(id.internal, uid.data(), NCCL_UNIQUE_ID_BYTES);
+  ncclComm_t c;
+  nccl_check(ncclCommInitRank(&c, world, id, rank), "ncclCommInitRank");
+  comm_ = c;
+}
+
+Comm::~Comm() {
+  if (comm_) ncclCommDestroy(reinterpret_cast<ncclComm_t>(comm_));
+}
+
+void Comm::allreduce(uintptr_t buf, int64_t count, int dtype, int op, uintptr_t stream) {
+  if (count <= 0) return;
+  nccl_check(ncclAllReduce(reinterpret_cast<void*>(buf), reinterpret_cast<void*>(buf), (size_t)count,
+                           to_nccl_dtype(dtype), to_nccl_op(op), reinterpret_cast<ncclComm_t>(comm_),
+                           reinterpret_cast<hipStream_t>(stream)),
+             "ncclAllReduce");
+}
+
+void Comm::broadcast(uintptr_t buf, int64_t count, int dtype, int root, uintptr_t stream) {
+  if (count <= 0) return;
+  nccl_check(ncclBroadcast(reinterpret_cast<void*>(buf), reinterpret_cast<void*>(buf), (size_t)count,
+                           to_nccl_dtype(dtype), root, reinterpret_cast<ncclComm_t>(comm_),
+                           reinterpret_cast<hipStream_t>(stream)),
+             "ncclBroadcast");
+}
+
+void Comm::reduce_scatter(uintptr_t send, uintptr_t recv, int64_t recv_count, int dtype, int op, uintptr_t stream) {
+  nccl_check(ncclReduceScatter(reinterpret_cast<void*>(send), reinterpret_cast<void*>(recv), (size_t)recv_count,
+                               to_nccl_dtype(dtype), to_nccl_op(op), reinterpret_cast<ncclComm_t>(comm_),
+                               reinterpret_cast<hipStream_t>(stream)),
+             "ncclReduceScatter");
+}
+
+void Comm::all_gather(uintptr_t send, uintptr_t recv, int64_t send_count, int dtype, uintptr_t stream) {
+  nccl_check(ncclAllGather(reinterpret_cast<void*>(send), reinterpret_cast<void*>(recv), (size_t)send_count,
+                           to_nccl_dtype(dtype), reinterpret_cast<ncclComm_t>(comm_),
+                           reinterpret_cast<hipStream_t>(stream)),
+             "ncclAllGather");
+}
+
+// ------------------------------------------------------------------------- BucketReducer
+BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_t> bucket_offsets,
+                             std::vector<int64_t> bucket_counts, std::vector<int> param_bucket, int dtype,
+                             int op)
+    : comm_(comm),
+      flat_(flat_grad),
+      offsets_(std::move(bucket_offsets)),
+      counts_(std::move(bucket_counts)),
+      param_bucket_(std::move(param_bucket)),
+      dtype_(dtype),
+      op_(op) {
+  const size_t nb = offsets_.size();
+  if (counts_.size() != nb) throw std::runtime_error("bucket offsets/counts mismatch");
+  expected_.assign(nb, 0);
+  for (int b : param_bucket_) {
+    if (b < 0 || (size_t)b >= nb) throw std::runtime_error("param bucket index out of range");
+    expected_[b]++;
+  }
+  pending_.assign(nb, 0);
+  launched_.assign(nb, 0);
+  hip_check(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking), "hipStreamCreate");
+  ready_events_.resize(nb);
+  for (auto& e : ready_events_) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+  hip_check(hipEventCreateWithFlags(&done_event_, hipEventDisableTiming), "hipEventCreate");
+  dsize_ = (dtype == DT_BF16 || dtype == DT_F16) ? 2 : 4;
+}
+
+BucketReducer::~BucketReducer() {
+  for (auto& e : ready_events_) hipEventDestroy(e);
+  if (done_event_) hipEventDestroy(done_event_);
+  if (comm_stream_) hipStreamDestroy(comm_stream_);
+}
+
+void BucketReducer::prepare() {
+  std::fill(pending_.begin(), pending_.end(), 0);
+  std::fill(launched_.begin(), launched_.end(), 0);
+  next_to_launch_ = 0;
+  n_launched_ = 0;
+}
+
+void BucketReducer::launch_bucket(int b, uintptr_t compute_stream) {
+  hipStream_t cs = reinterpret_cast<hipStream_t>(compute_stream);
+  hip_check(hipEventRecord(ready_events_[b], cs), "hipEventRecord");
+  hip_check(hipStreamWaitEvent(comm_stream_, ready_events_[b], 0), "hipStreamWaitEvent");
+  if (comm_) {
+    comm_->allreduce(flat_ + (uintptr_t)(offsets_[b] * dsize_), counts_[b], dtype_, op_,
+                     reinterpret_cast<uintptr_t>(comm_stream_));
+  }
+  launched_[b] = 1;
+  n_launched_++;
+}
+
+// Buckets are launched strictly in index order (bucket 0 = last layers, filled first by
+// backward) so every rank issues the collectives in the same order even when hooks fire in
+// a different order on different ranks.
+int BucketReducer::mark_ready(int param_idx, uintptr_t compute_stream) {
+  if (param_idx < 0 || (size_t)param_idx >= param_bucket_.size()) throw std::runtime_error("param index out of range");
+  const int b = param_bucket_[param_idx];
+  pending_[b]++;
+  if (pending_[b] > expected_[b]) throw std::runtime_error("parameter marked ready twice in one step");
+  int launched_now = 0;
+  while (next_to_launch_ < (int)offsets_.size() && pending_[next_to_launch_] == expected_[next_to_launch_]) {
+    launch_bucket(next_to_launch_, compute_stream);
+    next_to_launch_++;
+    launched_now++;
+  }
+  return launched_now;
+}
+
+void BucketReducer::finalize(uintptr_t compute_stream) {
+  // buckets whose params did not all receive a gradient (unused params): reduce anyway so
+  // the collective sequence matches across ranks (find_unused_parameters=False semantics
+  // would error; we zero-fill instead, which is what DDP's static graph does).
+  while (next_to_launch_ < (int)offsets_.size()) {
+    launch_bucket(next_to_launch_, compute_stream);
+    next_to_launch_++;
+  }
+  hip_check(hipEventRecord(done_event_, comm_stream_), "hipEventRecord");
+  hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(compute_stream), done_event_, 0), "hipStreamWaitEvent");
+}
+
+// ---------------------------------------------------------------------------- StreamGraph
+StreamGraph::~StreamGraph() { reset(); }
+
+void StreamGraph::reset() {
+  if (exec_) hipGraphExecDestroy(exec_);
+  if (graph_) hipGraphDestroy(graph_);
+  exec_ = nullptr;
+  graph_ = nullptr;
+}
+
+void StreamGraph::begin(uintptr_t stream) {
+  reset();
+  hip_check(hipStreamBeginCapture(reinterpret_cast<hipStream_t>(stream), hipStreamCaptureModeThreadLocal),
+            "hipStreamBeginCapture");
+}
+
+void StreamGraph::end(uintptr_t stream) {
+  hip_check(hipStreamEndCapture(reinterpret_cast<hipStream_t>(stream), &graph_), "hipStreamEndCapture");
+  hip_check(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0), "hipGraphInstantiate");
+}
+
+void StreamGraph::replay(uintptr_t stream) {
+  if (!exec_) throw std::runtime_error("graph not captured");
+  hip_check(hipGraphLaunch(exec_, reinterpret_cast<hipStream_t>(stream)), "hipGraphLaunch");
+}
+
+size_t StreamGraph::num_nodes() const {
+  if (!graph_) return 0;
+  size_t n = 0;
+  hipGraphGetNodes(graph_, nullptr, &n);
+  return n;
+}
+
+}  // namespace dct

@@ -1,0 +1,157 @@
+"""Python face of the fused MLP training kernels (csrc/mlp_fused.hip).
+
+``FusedMLPKernel`` owns the launch plan of one MLP architecture and validates every operand
+on the host before a launch (shape, dtype, device, contiguity, index ranges): the kernel
+itself trusts its arguments.  Parameters, Adam moments and gradients are flat fp32 buffers
+in torch ``state_dict`` order (``net.0.weight, net.0.bias, net.3.weight, ...``), which is
+also the layout of the DDP gradient bucket and of the Lightning checkpoint.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+from ._native import native, ptr, stream_handle
+
+LOSS_KINDS = {"ce": 0, "mse": 1}
+
+
+def mlp_num_params(dims: Sequence[int]) -> int:
+    return sum(dims[i] * dims[i + 1] + dims[i + 1] for i in range(len(dims) - 1))
+
+
+class FusedMLPKernel:
+    def __init__(self, dims: Sequence[int], bmax: int):
+        if bmax not in (4, 16):
+            raise ValueError("fused MLP kernel is instantiated for batch <= 4 or <= 16")
+        self.dims = [int(d) for d in dims]
+        self.bmax = bmax
+        self._plan = None
+        self._eval_plan = None
+
+    @property
+    def plan(self):
+        if self._plan is None:
+            self._plan = native().MlpPlan(self.dims, self.bmax)
+        return self._plan
+
+    @property
+    def eval_plan(self):
+        if self._eval_plan is None:
+            self._eval_plan = native().MlpPlan(self.dims, 16)
+        return self._eval_plan
+
+    @staticmethod
+    def supported(dims: Sequence[int], batch: int) -> bool:
+        """Host-side mirror of dct::mlp_make_shape's plan (no GPU needed)."""
+        L = len(dims) - 1
+        if not (2 <= L <= 4) or batch > 16 or batch < 1:
+            return False
+        bmax = 4 if batch <= 4 else 16
+        r4 = lambda x: (x + 3) // 4 * 4  # noqa: E731
+        nblk4 = sum((r4(dims[i + 1]) // 4) * (r4(dims[i]) // 4) for i in range(L))
+        nblk1 = sum(dims[i + 1] * (r4(dims[i]) // 4) for i in range(L))
+        if nblk1 <= 512 or nblk4 <= 1024:
+            nt = 256
+        elif nblk4 <= 2048:
+            nt = 512
+        else:
+            return False
+        if sum(dims[1:]) > 2 * nt:
+            return False
+        lds = 0
+        for i in range(L):
+            ldw = r4(dims[i]) + (4 if r4(dims[i]) % 8 == 0 else 0)
+            lds += r4(dims[i + 1]) * ldw + r4(dims[i + 1])
+        lds += 2 * bmax * r4(dims[0]) + sum(bmax * r4(d) for d in dims[1:])
+        lds += sum(bmax * r4(d) for d in dims[1:]) + 2 * r4(bmax) + r4(2 * bmax)
+        return lds * 4 <= 160 * 1024
+
+    # ------------------------------------------------------------------ checks
+    def _check_params(self, *ts):
+        P = mlp_num_params(self.dims)
+        for t in ts:
+            if t is None:
+                continue
+            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == P):
+                raise ValueError(f"flat parameter buffer must be contiguous cuda fp32 [{P}], got "
+                                 f"{t.dtype} {tuple(t.shape)} on {t.device}")
+
+    def _check_data(self, X, Y, idx, n_items):
+        if not (X.is_cuda and X.dtype == torch.float32 and X.dim() == 2 and X.stride(1) == 1):
+            raise ValueError("X must be a cuda fp32 [N, D] row-major tensor")
+        if X.shape[1] < self.dims[0]:
+            raise ValueError(f"X has {X.shape[1]} features, model expects {self.dims[0]}")
+        if not (Y.is_cuda and Y.dtype == torch.int32 and Y.is_contiguous() and Y.numel() == X.shape[0]):
+            raise ValueError("Y must be cuda int32 [N]")
+        if not (idx.is_cuda and idx.dtype == torch.int32 and idx.is_contiguous() and idx.numel() >= n_items):
+            raise ValueError("idx must be cuda int32 with at least n_items entries")
+
+    # ------------------------------------------------------------------ launches
+    def train(self, p, m, v, X, Y, idx, n_items: int, batch: int, steps: int, t0: int, lr: float,
+              betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, dropout: float = 0.0,
+              seed: int = 0, step_base: int = 0, loss_out: Optional[torch.Tensor] = None,
+              loss: str = "ce", grad_out: Optional[torch.Tensor] = None, step_counter: Optional[torch.Tensor] = None,
+              cursor: Optional[torch.Tensor] = None, prof: Optional[torch.Tensor] = None,
+              stream: Optional[int] = None):
+        """Run ``steps`` fused optimizer steps (mode 0) or one gradient step (grad_out given)."""
+        mode = 1 if grad_out is not None else 0
+        self._check_params(p, m if mode == 0 else None, v if mode == 0 else None)
+        self._check_data(X, Y, idx, n_items)
+        if batch > self.bmax:
+            raise ValueError(f"batch {batch} > kernel bmax {self.bmax}")
+        if steps < 1 or (cursor is None and (steps - 1) * batch >= n_items):
+            raise ValueError("steps do not match the index list")
+        if cursor is not None and (mode != 1 or not (cursor.is_cuda and cursor.dtype == torch.int32)):
+            raise ValueError("cursor (cuda int32) is only valid with grad_out")
+        if mode == 1:
+            P = mlp_num_params(self.dims)
+            if not (grad_out.is_cuda and grad_out.dtype == torch.float32 and grad_out.numel() >= P + 1):
+                raise ValueError("grad_out must be cuda fp32 with P+1 entries (grads + loss)")
+        if step_counter is not None and not (step_counter.is_cuda and step_counter.dtype == torch.int32):
+            raise ValueError("step_counter must be a cuda int32 scalar tensor")
+        if loss_out is not None and not (loss_out.is_cuda and loss_out.dtype == torch.float32
+                                         and loss_out.numel() >= steps):
+            raise ValueError("loss_out must be cuda fp32 [steps]")
+        self.plan.train(
+            ptr(p), ptr(m) if mode == 0 else 0, ptr(v) if mode == 0 else 0, ptr(grad_out),
+            ptr(X), X.stride(0), ptr(Y), ptr(idx), int(n_items), int(batch), int(steps), int(t0),
+            float(lr), float(betas[0]), float(betas[1]), float(eps), float(weight_decay), float(dropout),
+            int(seed) & 0xFFFFFFFF, int(step_base) & 0xFFFFFFFF, ptr(loss_out), mode, LOSS_KINDS[loss],
+            ptr(step_counter), ptr(cursor), ptr(prof), stream if stream is not None else stream_handle(),
+        )
+
+    def evaluate(self, p, X, Y, idx, n_items: int, acc_out: torch.Tensor, loss: str = "ce",
+                 logits_out: Optional[torch.Tensor] = None, grid: Optional[int] = None,
+                 stream: Optional[int] = None):
+        """acc_out[0] += sum of per-row loss, acc_out[1] += #correct (no reset)."""
+        self._check_params(p)
+        self._check_data(X, Y, idx, n_items)
+        if not (acc_out.is_cuda and acc_out.dtype == torch.float32 and acc_out.numel() >= 2):
+            raise ValueError("acc_out must be cuda fp32 [2]")
+        if logits_out is not None and logits_out.numel() < n_items * self.dims[-1]:
+            raise ValueError("logits_out too small")
+        chunks = (n_items + 15) // 16
+        g = grid or max(1, min(chunks, 256))
+        self.eval_plan.eval(ptr(p), ptr(X), X.stride(0), ptr(Y), ptr(idx), int(n_items), LOSS_KINDS[loss],
+                            ptr(acc_out), ptr(logits_out), int(g),
+                            stream if stream is not None else stream_handle())
+
+
+# ---------------------------------------------------------------------------- reference
+def reference_mlp_forward(p: torch.Tensor, dims: Sequence[int], x: torch.Tensor) -> torch.Tensor:
+    """Plain-torch fp32 forward of the flat-parameter MLP (no dropout), for numerics tests."""
+    off = 0
+    h = x
+    L = len(dims) - 1
+    for l in range(L):
+        i, o = dims[l], dims[l + 1]
+        W = p[off: off + i * o].view(o, i)
+        off += i * o
+        b = p[off: off + o]
+        off += o
+        h = h @ W.t() + b
+        if l < L - 1:
+            h = torch.relu(h)
+    return h

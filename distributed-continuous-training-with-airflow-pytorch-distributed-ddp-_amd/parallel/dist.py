@@ -1,0 +1,159 @@
+"""Process-group bring-up and the distributed context.
+
+Reference topology (docker-compose.yml:115-151, jobs/train_lightning_ddp.py:129-140): two
+containers, each ONE process with ``NODE_RANK`` in {0,1}, ``WORLD_SIZE=2``,
+``MASTER_ADDR=pytorch-master``, ``MASTER_PORT=29500``; Lightning then runs
+``init_process_group("gloo", env://)``.  MI355X topology: one process per GPU launched by
+``torchrun`` (``RANK/LOCAL_RANK/WORLD_SIZE/LOCAL_WORLD_SIZE`` set), ``nccl`` (= RCCL) for device
+collectives with ``device_id`` bound, plus the native RCCL communicator of the C++ runtime for
+the fused step loop.  Both launch styles resolve through :func:`resolve_env`, so the
+reference's env contract keeps working (one process per "node" when only ``NODE_RANK`` is set).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import time
+from dataclasses import dataclass
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    world_size: int = 1
+    rank: int = 0
+    local_rank: int = 0
+    local_world_size: int = 1
+    node_rank: int = 0
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+    initialized_here: bool = False
+    native_comm: Any = None
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1
+
+    @property
+    def is_rank_zero(self) -> bool:
+        return self.rank == 0
+
+    # ------------------------------------------------------------------ collectives
+    def barrier(self):
+        if self.is_distributed and dist.is_initialized():
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def all_reduce_mean(self, t: torch.Tensor) -> torch.Tensor:
+        """Mean across ranks of a small tensor (returns a new tensor on t's device)."""
+        if not self.is_distributed:
+            return t
+        x = t.detach().clone()
+        if self.backend == "gloo" and x.is_cuda:
+            x = x.cpu()
+        elif self.backend == "nccl" and not x.is_cuda:
+            x = x.to(self.device)
+        dist.all_reduce(x, op=dist.ReduceOp.SUM)
+        x /= self.world_size
+        return x.to(t.device)
+
+    def all_reduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.is_distributed:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.is_distributed:
+            dist.broadcast(t, src=src)
+        return t
+
+    def broadcast_object(self, obj, src: int = 0):
+        if not self.is_distributed:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src, device=self.device if self.backend == "nccl" else None)
+        return lst[0]
+
+    def all_reduce_bool_and(self, flag: bool) -> bool:
+        if not self.is_distributed:
+            return flag
+        t = torch.tensor([0 if flag else 1], dtype=torch.int32,
+                         device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return int(t.item()) == 0
+
+
+def resolve_env(env=None) -> dict:
+    env = os.environ if env is None else env
+    world = int(env.get("WORLD_SIZE", "1"))
+    node_rank = int(env.get("NODE_RANK", env.get("GROUP_RANK", "0")))
+    if "RANK" in env:
+        rank = int(env["RANK"])
+    else:
+        # reference launch style: one process per node (devices=1, num_nodes=WORLD_SIZE)
+        rank = node_rank
+    local_rank = int(env.get("LOCAL_RANK", "0"))
+    local_world = int(env.get("LOCAL_WORLD_SIZE", "1"))
+    return dict(world_size=world, rank=rank, local_rank=local_rank, local_world_size=local_world,
+                node_rank=node_rank, master_addr=env.get("MASTER_ADDR", "127.0.0.1"),
+                master_port=int(env.get("MASTER_PORT", "29500")))
+
+
+def init_distributed(accelerator: str = "auto", backend: str = "auto", timeout_s: int = 1800,
+                     env=None) -> DistContext:
+    e = resolve_env(env)
+    use_gpu = accelerator in ("gpu", "cuda") or (accelerator == "auto" and torch.cuda.is_available())
+    if use_gpu and not torch.cuda.is_available():
+        raise RuntimeError("accelerator='gpu' requested but no HIP device is visible")
+    if use_gpu:
+        ndev = torch.cuda.device_count()
+        dev_index = e["local_rank"] % max(1, ndev)
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
+    else:
+        device = torch.device("cpu")
+    if backend == "auto":
+        backend = "nccl" if use_gpu else "gloo"
+    ctx = DistContext(world_size=e["world_size"], rank=e["rank"], local_rank=e["local_rank"],
+                      local_world_size=e["local_world_size"], node_rank=e["node_rank"], backend=backend,
+                      device=device)
+    if e["world_size"] > 1:
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", e["master_addr"])
+            os.environ.setdefault("MASTER_PORT", str(e["master_port"]))
+            kwargs = dict(backend=backend, init_method="env://", world_size=e["world_size"], rank=e["rank"],
+                          timeout=datetime.timedelta(seconds=timeout_s))
+            if backend == "nccl":
+                kwargs["device_id"] = device
+            dist.init_process_group(**kwargs)
+            ctx.initialized_here = True
+    else:
+        ctx.backend = "none"
+    return ctx
+
+
+def init_native_comm(ctx: DistContext):
+    """Create the C++ runtime's RCCL communicator (unique id shared over the c10d PG)."""
+    if ctx.native_comm is not None or not ctx.is_distributed or ctx.device.type != "cuda":
+        return ctx.native_comm
+    from ..ops._native import native
+
+    nat = native()
+    uid = nat.comm_unique_id() if ctx.rank == 0 else None
+    uid = ctx.broadcast_object(uid, src=0)
+    ctx.native_comm = nat.Comm(uid, ctx.world_size, ctx.rank, ctx.device.index)
+    return ctx.native_comm
+
+
+def shutdown(ctx: DistContext):
+    ctx.native_comm = None
+    if ctx.initialized_here and dist.is_initialized():
+        try:
+            dist.destroy_process_group()
+        except Exception:  # noqa: BLE001
+            pass

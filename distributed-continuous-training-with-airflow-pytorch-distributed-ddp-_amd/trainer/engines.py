@@ -1,0 +1,410 @@
+"""Step engines: how one training epoch / one optimizer step is executed.
+
+* ``FusedMLPEngine`` (GPU, MLP family with widths that fit one CU): the reference's whole
+  per-step hot loop (collate -> forward -> CE -> backward -> DDP all-reduce -> Adam,
+  jobs/train_lightning_ddp.py:66-71,88,136) runs in the fused HIP kernels of
+  csrc/mlp_fused.hip with the dataset resident in HBM and batches gathered on device.
+    - world size 1: ONE persistent launch runs every step of an epoch (weights in LDS, Adam
+      moments in VGPRs, nothing but the batch rows touches HBM per step).
+    - world size > 1: per step {fused fwd+bwd (grads + loss -> one flat buffer), RCCL
+      ncclAvg all-reduce of that buffer (gradients AND the sync_dist train_loss in ONE
+      collective: X5+X6 of SURVEY §2.6), fused flat Adam}; the epoch's step loop is captured
+      once into a HIP graph and replayed every epoch (the Adam step count and dropout stream
+      are read from a device counter, so replays are exact).
+* ``AutogradEngine`` (any TrainModule; CPU/gloo plumbing path and the large-model GPU path):
+  ``training_step`` + autograd, parameters/gradients as views of flat buffers, the bucketed
+  reducer hooked on ``post_accumulate_grad`` (overlap with backward), flat Adam.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..data.sampler import distributed_indices
+from ..ops.fused_mlp import FusedMLPKernel, mlp_num_params
+from ..ops.optim import FlatAdam, adam_flat_
+from ..parallel.dist import DistContext, init_native_comm
+from ..parallel.reducer import NativeBucketReducer, TorchBucketReducer, plan_buckets
+
+
+def adam_hparams_from(optimizer) -> Optional[Dict]:
+    """Extract Adam hyper-parameters from a configure_optimizers() result (None if not Adam)."""
+    opt = optimizer
+    if isinstance(opt, (list, tuple)):
+        if len(opt) != 1:
+            return None
+        opt = opt[0]
+    if isinstance(opt, dict):
+        opt = opt.get("optimizer")
+    if type(opt) is not torch.optim.Adam:
+        return None
+    g = opt.param_groups[0]
+    if g.get("amsgrad") or g.get("maximize"):
+        return None
+    return dict(lr=float(g["lr"]), betas=tuple(float(b) for b in g["betas"]), eps=float(g["eps"]),
+                weight_decay=float(g["weight_decay"]))
+
+
+class _EngineBase:
+    name = "base"
+
+    def __init__(self, model, ctx: DistContext, batch_size: int, seed: int):
+        self.model = model
+        self.ctx = ctx
+        self.B = int(batch_size)
+        self.seed = int(seed)
+        self.global_step = 0
+
+    def epoch_local_indices(self, n_train: int, epoch: int, shuffle: bool) -> torch.Tensor:
+        return distributed_indices(n_train, self.ctx.world_size, self.ctx.rank, shuffle=shuffle, seed=self.seed,
+                                   epoch=epoch)
+
+
+# ================================================================================ fused
+class FusedMLPEngine(_EngineBase):
+    name = "fused"
+
+    @staticmethod
+    def applicable(model, device: torch.device, batch_size: int) -> bool:
+        if device.type != "cuda" or not hasattr(model, "fused_spec"):
+            return False
+        spec = model.fused_spec()
+        return FusedMLPKernel.supported(spec["dims"], batch_size)
+
+    def __init__(self, model, ctx: DistContext, batch_size: int, seed: int, adam: Dict,
+                 steps_per_launch: int = 0, use_graph: Optional[bool] = None):
+        super().__init__(model, ctx, batch_size, seed)
+        spec = model.fused_spec()
+        self.dims = spec["dims"]
+        self.dropout = float(spec["dropout"])
+        self.loss = spec["loss"]
+        self.adam = adam
+        self.kernel = FusedMLPKernel(self.dims, bmax=4 if self.B <= 4 else 16)
+        self.P = mlp_num_params(self.dims)
+        dev = ctx.device
+        self.device = dev
+        self.p = self._flat_from_model().to(dev)
+        self.m = torch.zeros_like(self.p)
+        self.v = torch.zeros_like(self.p)
+        self.step_counter = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.steps_per_launch = int(steps_per_launch)
+        self.use_graph = (os.environ.get("DCT_GRAPH", "1") != "0") if use_graph is None else use_graph
+        self.rank_seed = (self.seed * 1000003 + ctx.rank * 7919 + 1) & 0xFFFFFFFF
+        self.comm = None
+        self.gbuf = None
+        self._graphs = {}
+        self.graph_chunk = int(os.environ.get("DCT_GRAPH_CHUNK", "256"))
+        self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.graph_used = False
+        if ctx.is_distributed:
+            self.comm = init_native_comm(ctx)
+            self.gbuf = torch.zeros(self.P + 1, dtype=torch.float32, device=dev)
+            self._broadcast_params()
+
+    # ------------------------------------------------------------------ params
+    def _linear_params(self):
+        out = []
+        for lin in self.model.linear_layers():
+            out += [lin.weight, lin.bias]
+        return out
+
+    def _flat_from_model(self) -> torch.Tensor:
+        return torch.cat([t.detach().float().reshape(-1).cpu() for t in self._linear_params()])
+
+    def _broadcast_params(self):
+        from ..ops._native import native
+
+        nat = native()
+        s = torch.cuda.current_stream().cuda_stream
+        self.comm.broadcast(self.p.data_ptr(), self.P, nat.DT_F32, 0, s)  # X3 (DDP _sync_module_states)
+
+    def sync_to_model(self):
+        """Copy the flat device parameters back into the nn.Module (for checkpoints/serving)."""
+        off = 0
+        flat = self.p.detach().cpu()
+        with torch.no_grad():
+            for t in self._linear_params():
+                n = t.numel()
+                t.copy_(flat[off: off + n].view_as(t))
+                off += n
+
+    def load_from_model(self):
+        self.p.copy_(self._flat_from_model().to(self.device))
+
+    def optimizer_state_dict(self) -> Dict:
+        shapes = [t.shape for t in self._linear_params()]
+        fa = FlatAdam(self.p, self.p, shapes, lr=self.adam["lr"], betas=self.adam["betas"], eps=self.adam["eps"],
+                      weight_decay=self.adam["weight_decay"])
+        fa.m, fa.v = self.m, self.v
+        fa.step_count = self.global_step
+        return fa.state_dict()
+
+    def load_optimizer_state(self, sd: Dict, global_step: int):
+        shapes = [t.shape for t in self._linear_params()]
+        fa = FlatAdam(self.p, self.p, shapes, **self.adam)
+        fa.m, fa.v = self.m, self.v
+        fa.load_state_dict(sd)
+        self.global_step = global_step
+        self.step_counter.fill_(int(fa.step_count))
+
+    # ------------------------------------------------------------------ data
+    def attach_data(self, X: torch.Tensor, Y: torch.Tensor, train_rows: torch.Tensor, val_rows: torch.Tensor):
+        dev = self.device
+        if X.shape[1] != self.dims[0]:
+            raise ValueError(f"dataset has {X.shape[1]} features, model expects {self.dims[0]}")
+        self.X = X.to(torch.float32).contiguous().pin_memory().to(dev, non_blocking=True)
+        self.Y = Y.to(torch.int32).contiguous().pin_memory().to(dev, non_blocking=True)
+        n = X.shape[0]
+        for rows in (train_rows, val_rows):
+            if rows.numel() and (int(rows.min()) < 0 or int(rows.max()) >= n):
+                raise ValueError("split indices out of range")
+        self.train_rows = train_rows.to(torch.int64)
+        self.val_rows = val_rows.to(torch.int64)
+        n_local = math.ceil(len(self.train_rows) / self.ctx.world_size)
+        self.idx = torch.zeros(max(1, n_local), dtype=torch.int32, device=dev)
+        vl = math.ceil(max(1, len(self.val_rows)) / self.ctx.world_size)
+        self.val_idx = torch.zeros(max(1, vl), dtype=torch.int32, device=dev)
+        self.eval_acc = torch.zeros(2, dtype=torch.float32, device=dev)
+
+    def steps_per_epoch(self) -> int:
+        n_local = math.ceil(len(self.train_rows) / self.ctx.world_size)
+        return math.ceil(n_local / self.B)
+
+    def upload_epoch_indices(self, epoch: int, shuffle: bool = True) -> int:
+        local = self.epoch_local_indices(len(self.train_rows), epoch, shuffle)
+        rows = self.train_rows[local].to(torch.int32)
+        self.idx[: rows.numel()].copy_(rows.pin_memory(), non_blocking=True)
+        return rows.numel()
+
+    # ------------------------------------------------------------------ train
+    def _launch_persistent(self, n_items: int, steps: int, loss_out: torch.Tensor, idx_off: int = 0):
+        a = self.adam
+        self.kernel.train(self.p, self.m, self.v, self.X, self.Y, self.idx[idx_off:], n_items=n_items,
+                          batch=self.B, steps=steps, t0=0, lr=a["lr"], betas=a["betas"], eps=a["eps"],
+                          weight_decay=a["weight_decay"], dropout=self.dropout, seed=self.rank_seed,
+                          loss_out=loss_out, loss=self.loss, step_counter=self.step_counter)
+
+    def run_steps(self, n_items: int, steps: int, loss_out: torch.Tensor, first_step: int = 0):
+        """Enqueue ``steps`` optimizer steps over batches [first_step, first_step+steps) of self.idx.
+
+        Single rank: persistent launches write loss_out[0:steps].  DDP: loss_out is indexed by the
+        absolute batch index (loss_out[first_step + s]) and must hold first_step + steps entries.
+        No host synchronisation either way."""
+        if steps <= 0:
+            return
+        if not self.ctx.is_distributed:
+            chunk = self.steps_per_launch or steps
+            s = 0
+            while s < steps:
+                k = min(chunk, steps - s)
+                off = (first_step + s) * self.B
+                self._launch_persistent(n_items - off, k, loss_out[s: s + k], idx_off=off)
+                s += k
+            return
+        if (first_step + steps - 1) * self.B >= n_items or loss_out.numel() < first_step + steps:
+            raise ValueError("DDP step range exceeds the epoch's batches / loss buffer")
+        self.cursor.fill_(first_step)
+        C = min(self.graph_chunk, steps)
+        full, rem = divmod(steps, C)
+        done = 0
+        if self.use_graph:
+            g = self._get_graph(n_items, C, loss_out)
+            if g is not None:
+                for _ in range(full):
+                    g.replay()
+                done = full * C
+                self.graph_used = True
+        for _ in range(steps - done):
+            self._ddp_step(n_items, loss_out)
+        # the last step's reduced loss is flushed by the next kernel; flush it here instead
+        last = first_step + steps - 1
+        loss_out[last: last + 1].copy_(self.gbuf[self.P: self.P + 1])
+
+    def _ddp_step(self, n_items: int, loss_out: torch.Tensor):
+        """One DDP step at the device cursor: fused fwd/bwd (grads + local loss -> gbuf) ->
+        RCCL ncclAvg all-reduce of gbuf (X5 + X6 in one collective) -> fused flat Adam."""
+        from ..ops._native import native
+
+        a = self.adam
+        self.kernel.train(self.p, None, None, self.X, self.Y, self.idx, n_items=n_items, batch=self.B, steps=1,
+                          t0=0, lr=a["lr"], dropout=self.dropout, seed=self.rank_seed, loss=self.loss,
+                          grad_out=self.gbuf, step_counter=self.step_counter, cursor=self.cursor,
+                          loss_out=loss_out)
+        nat = native()
+        stream = torch.cuda.current_stream().cuda_stream
+        self.comm.allreduce(self.gbuf.data_ptr(), self.P + 1, nat.DT_F32, nat.OP_AVG, stream)
+        adam_flat_(self.p, self.gbuf[: self.P], self.m, self.v, 1, a["lr"], a["betas"], a["eps"],
+                   a["weight_decay"], step_counter=self.step_counter)
+
+    def _get_graph(self, n_items: int, C: int, loss_out: torch.Tensor):
+        key = (n_items, C, loss_out.data_ptr())
+        if key in self._graphs:
+            return self._graphs[key]
+        from ..ops._native import native
+
+        nat = native()
+        # RCCL lazy init and kernel attribute setup must happen outside the capture
+        scratch = torch.zeros(64, dtype=torch.float32, device=self.device)
+        self.comm.allreduce(scratch.data_ptr(), 64, nat.DT_F32, nat.OP_SUM, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize(self.device)
+        state = (self.p, self.m, self.v, self.step_counter, self.cursor, self.gbuf, loss_out)
+        saved = [t.clone() for t in state]
+        # one eager step first (kernel attributes, RCCL channels), then roll the state back
+        self._ddp_step(n_items, loss_out)
+        torch.cuda.synchronize(self.device)
+        for t, sv in zip(state, saved):
+            t.copy_(sv)
+        g = torch.cuda.CUDAGraph()
+        try:
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                    for _ in range(C):
+                        self._ddp_step(n_items, loss_out)
+            torch.cuda.current_stream().wait_stream(s)
+        except Exception as e:  # noqa: BLE001 - eager fallback keeps training correct
+            print(f"[dct] HIP graph capture failed ({e!r}); DDP steps run eagerly", flush=True)
+            g = None
+        torch.cuda.synchronize(self.device)
+        for t, sv in zip(state, saved):
+            t.copy_(sv)
+        self._graphs[key] = g
+        return g
+
+    def train_epoch(self, epoch: int, shuffle: bool = True) -> torch.Tensor:
+        n_items = self.upload_epoch_indices(epoch, shuffle)
+        steps = math.ceil(n_items / self.B)
+        loss_out = getattr(self, "_loss_buf", None)
+        if loss_out is None or loss_out.numel() < steps:
+            self._loss_buf = loss_out = torch.zeros(max(1, steps), dtype=torch.float32, device=self.device)
+        self.run_steps(n_items, steps, loss_out[:steps])
+        self.global_step += steps
+        return loss_out[:steps]
+
+    # ------------------------------------------------------------------ eval
+    def validate(self, rows: Optional[torch.Tensor] = None, limit: Optional[int] = None) -> Tuple[float, float]:
+        rows = self.val_rows if rows is None else rows
+        local = distributed_indices(len(rows), self.ctx.world_size, self.ctx.rank, shuffle=False)
+        if limit is not None:
+            local = local[:limit]
+        r = rows[local].to(torch.int32)
+        if r.numel() == 0:
+            return float("nan"), float("nan")
+        if r.numel() > self.val_idx.numel():
+            self.val_idx = torch.zeros(r.numel(), dtype=torch.int32, device=self.device)
+        self.val_idx[: r.numel()].copy_(r)
+        self.eval_acc.zero_()
+        self.kernel.evaluate(self.p, self.X, self.Y, self.val_idx, r.numel(), self.eval_acc, loss=self.loss)
+        stats = self.eval_acc / float(r.numel())
+        stats = self.ctx.all_reduce_mean(stats)
+        vals = stats.cpu().tolist()
+        return vals[0], vals[1]
+
+
+# ============================================================================= autograd
+class AutogradEngine(_EngineBase):
+    name = "autograd"
+
+    def __init__(self, model, ctx: DistContext, batch_size: int, seed: int, bucket_cap_bytes: int = 8 << 20,
+                 first_bucket_bytes: int = 1 << 20):
+        super().__init__(model, ctx, batch_size, seed)
+        dev = ctx.device
+        self.device = dev
+        model.to(dev)
+        params = [p for p in model.parameters() if p.requires_grad]
+        self.params = params
+        numels = [p.numel() for p in params]
+        total = sum(numels)
+        self.flat_p = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.flat_g = torch.zeros(total, dtype=torch.float32, device=dev)
+        off = 0
+        with torch.no_grad():
+            for p in params:
+                n = p.numel()
+                self.flat_p[off: off + n].copy_(p.detach().reshape(-1).float())
+                p.data = self.flat_p[off: off + n].view_as(p)
+                p.grad = self.flat_g[off: off + n].view_as(p)
+                off += n
+        if ctx.is_distributed:
+            ctx.broadcast_(self.flat_p, 0) if ctx.backend != "nccl" else self._bcast_nccl()
+        self.plan = plan_buckets(numels, 4, bucket_cap_bytes, first_bucket_bytes)
+        self.reducer = None
+        if ctx.is_distributed:
+            if dev.type == "cuda":
+                comm = init_native_comm(ctx)
+                self.reducer = NativeBucketReducer(comm, self.flat_g, self.plan)
+            else:
+                self.reducer = TorchBucketReducer(self.flat_g, self.plan, ctx.world_size)
+            self._hooks = []
+            for i, p in enumerate(params):
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+        opt = model.configure_optimizers()
+        hp = adam_hparams_from(opt)
+        if hp is not None:
+            self.optimizer = FlatAdam(self.flat_p, self.flat_g, [p.shape for p in params], **hp)
+            self.torch_optimizer = None
+        else:
+            self.optimizer = None
+            self.torch_optimizer = opt[0] if isinstance(opt, (list, tuple)) else opt
+
+    def _bcast_nccl(self):
+        self.ctx.broadcast_(self.flat_p, 0)
+
+    def _make_hook(self, i):
+        def hook(_p):
+            self.reducer.mark_ready(i)
+        return hook
+
+    def attach_data(self, X: torch.Tensor, Y: torch.Tensor, train_rows: torch.Tensor, val_rows: torch.Tensor):
+        self.X = X.to(self.device, torch.float32)
+        self.Y = Y.to(self.device, torch.int64)
+        self.train_rows = train_rows.to(torch.int64)
+        self.val_rows = val_rows.to(torch.int64)
+
+    def steps_per_epoch(self) -> int:
+        return math.ceil(math.ceil(len(self.train_rows) / self.ctx.world_size) / self.B)
+
+    def train_step(self, rows: torch.Tensor, batch_idx: int):
+        x = self.X[rows.to(self.device)]
+        y = self.Y[rows.to(self.device)]
+        self.flat_g.zero_()
+        if self.reducer is not None:
+            self.reducer.prepare()
+        self.model.train()
+        loss = self.model.training_step((x, y), batch_idx)
+        if isinstance(loss, dict):
+            loss = loss["loss"]
+        loss.backward()
+        if self.reducer is not None:
+            self.reducer.finalize()
+        if self.optimizer is not None:
+            self.optimizer.step()
+        else:
+            if self.ctx.is_distributed and self.reducer is None:
+                pass
+            self.torch_optimizer.step()
+        self.global_step += 1
+        return loss.detach()
+
+    def optimizer_state_dict(self) -> Dict:
+        if self.optimizer is not None:
+            return self.optimizer.state_dict()
+        return self.torch_optimizer.state_dict()
+
+    def load_optimizer_state(self, sd: Dict, global_step: int):
+        if self.optimizer is not None:
+            self.optimizer.load_state_dict(sd)
+        else:
+            self.torch_optimizer.load_state_dict(sd)
+        self.global_step = global_step
+
+    def sync_to_model(self):
+        pass  # parameters ARE views of the flat buffer
+
+    def load_from_model(self):
+        pass

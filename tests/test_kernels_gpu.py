@@ -1,0 +1,352 @@
+"""Numerics of the HIP kernels against plain-torch fp32 references (run on a real MI355X)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import dct_amd  # noqa: F401
+from dct_amd.ops._native import native
+from dct_amd.ops.fused_mlp import FusedMLPKernel, mlp_num_params, reference_mlp_forward
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_net(dims):
+    layers = []
+    for i in range(len(dims) - 1):
+        layers.append(torch.nn.Linear(dims[i], dims[i + 1]))
+        if i < len(dims) - 2:
+            layers.append(torch.nn.ReLU())
+    return torch.nn.Sequential(*layers)
+
+
+def _flat(net):
+    return torch.cat([t.detach().reshape(-1) for t in net.state_dict().values()])
+
+
+def _ref_loss(logits, y, kind):
+    if kind == "ce":
+        return F.cross_entropy(logits, y)
+    return F.mse_loss(logits, F.one_hot(y, logits.shape[1]).float())
+
+
+def test_native_loaded_and_arch():
+    nat = native()
+    assert nat.device_count() >= 1
+    assert "gfx950" in nat.arch_name(0)
+
+
+@pytest.mark.parametrize("kernel", ["auto", "lds"])
+@pytest.mark.parametrize("loss", ["ce", "mse"])
+@pytest.mark.parametrize("dims,B", [([5, 64, 2], 4), ([5, 128, 128, 2], 4), ([5, 64, 2], 3), ([9, 48, 64, 3], 4),
+                                    ([16, 32, 48, 32, 3], 16), ([5, 128, 128, 2], 16), ([7, 20, 2], 9),
+                                    ([7, 20, 2], 8)])
+def test_fused_train_matches_torch_adam(dims, B, loss, kernel, cuda, monkeypatch):
+    monkeypatch.setenv("DCT_MLP_KERNEL", kernel)
+    torch.manual_seed(1)
+    N, n_items = 301, 50
+    X = torch.randn(N, dims[0])
+    Y = torch.randint(0, dims[-1], (N,))
+    idx = torch.randperm(N)[:n_items]
+    net = _ref_net(dims)
+    p = _flat(net).to(cuda)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    steps = math.ceil(n_items / B)
+    losses = torch.zeros(steps, device=cuda)
+    k = FusedMLPKernel(dims, bmax=4 if B <= 4 else 16)
+    k.train(p, m, v, X.to(cuda), Y.to(cuda, torch.int32), idx.to(cuda, torch.int32), n_items=n_items, batch=B,
+            steps=steps, t0=0, lr=0.01, loss=loss, loss_out=losses)
+    opt = torch.optim.Adam(net.parameters(), lr=0.01)
+    ref_losses = []
+    for s in range(steps):
+        rows = idx[s * B:(s + 1) * B]
+        opt.zero_grad()
+        l = _ref_loss(net(X[rows]), Y[rows], loss)
+        l.backward()
+        opt.step()
+        ref_losses.append(l.item())
+    got = p.cpu()
+    want = _flat(net)
+    err = (got - want).abs()
+    assert err.median() < 1e-5, err.median()
+    assert err.max() < 2e-3, err.max()
+    assert torch.allclose(losses.cpu(), torch.tensor(ref_losses), atol=2e-4, rtol=1e-3)
+    # moments written back in torch flat order
+    st = opt.state_dict()["state"]
+    ref_m = torch.cat([st[i]["exp_avg"].reshape(-1) for i in range(len(st))])
+    assert torch.allclose(m.cpu(), ref_m, atol=1e-4, rtol=1e-2)
+
+
+@pytest.mark.parametrize("kernel", ["auto", "lds"])
+@pytest.mark.parametrize("dims,B", [([5, 64, 2], 4), ([5, 128, 128, 2], 4), ([12, 40, 40, 5], 13),
+                                    ([9, 48, 64, 3], 4)])
+def test_fused_grad_mode_matches_autograd(dims, B, kernel, cuda, monkeypatch):
+    monkeypatch.setenv("DCT_MLP_KERNEL", kernel)
+    torch.manual_seed(2)
+    N = 64
+    X = torch.randn(N, dims[0])
+    Y = torch.randint(0, dims[-1], (N,))
+    idx = torch.arange(B, dtype=torch.int32)
+    net = _ref_net(dims)
+    p = _flat(net).to(cuda)
+    P = mlp_num_params(dims)
+    g = torch.zeros(P + 1, device=cuda)
+    k = FusedMLPKernel(dims, bmax=4 if B <= 4 else 16)
+    k.train(p, None, None, X.to(cuda), Y.to(cuda, torch.int32), idx.to(cuda), n_items=B, batch=B, steps=1, t0=0,
+            lr=0.01, grad_out=g)
+    l = F.cross_entropy(net(X[:B]), Y[:B])
+    l.backward()
+    want = torch.cat([q.grad.reshape(-1) for q in net.parameters()])
+    assert torch.allclose(g[:P].cpu(), want, atol=1e-6, rtol=1e-4)
+    assert abs(g[P].item() - l.item()) < 1e-5
+
+
+@pytest.mark.parametrize("kernel", ["auto", "lds"])
+def test_fused_dropout_keep_rate(kernel, cuda, monkeypatch):
+    monkeypatch.setenv("DCT_MLP_KERNEL", kernel)
+    # With dropout p the expected hidden activation is preserved (inverted scaling) and the
+    # per-step masks differ; compare mean loss-gradient magnitude across many steps vs p=0.
+    torch.manual_seed(3)
+    dims = [8, 128, 2]
+    N = 4096
+    X = torch.randn(N, 8).abs()
+    Y = torch.randint(0, 2, (N,))
+    net = _ref_net(dims)
+    with torch.no_grad():
+        net[0].bias.fill_(1.0)
+        net[0].weight.abs_()
+    P = mlp_num_params(dims)
+    k = FusedMLPKernel(dims, bmax=4)
+    outs = []
+    for pdrop in (0.0, 0.5):
+        p = _flat(net).to(cuda)
+        gsum = torch.zeros(P + 1, device=cuda)
+        nz = 0
+        for s in range(200):
+            g = torch.zeros(P + 1, device=cuda)
+            idx = torch.arange(s, s + 1, dtype=torch.int32, device=cuda)
+            # batch of ONE row: a W2 gradient entry is zero exactly when its hidden unit was dropped
+            k.train(p, None, None, X.to(cuda), Y.to(cuda, torch.int32), idx, n_items=1, batch=1, steps=1, t0=0,
+                    lr=0.0, dropout=pdrop, seed=7, step_base=s, grad_out=g)
+            w2 = g[8 * 128 + 128: 8 * 128 + 128 + 2 * 128].view(2, 128)
+            nz += (w2.abs() > 0).float().mean().item()
+            gsum += g
+        outs.append(nz / 200)
+    keep0, keep5 = outs
+    assert keep0 > 0.99
+    assert 0.40 < keep5 / keep0 < 0.60
+
+
+def test_fused_eval_matches_torch(cuda):
+    torch.manual_seed(4)
+    dims = [5, 128, 128, 2]
+    net = _ref_net(dims)
+    N = 1000
+    X = torch.randn(N, 5)
+    Y = torch.randint(0, 2, (N,))
+    idx = torch.randperm(N)[:777].to(torch.int32)
+    k = FusedMLPKernel(dims, bmax=4)
+    acc = torch.zeros(2, device=cuda)
+    logits = torch.zeros(777 * 2, device=cuda)
+    p = _flat(net).to(cuda)
+    k.evaluate(p, X.to(cuda), Y.to(cuda, torch.int32), idx.to(cuda), 777, acc, logits_out=logits)
+    z = net(X[idx.long()])
+    assert torch.allclose(logits.view(777, 2).cpu(), z, atol=1e-4, rtol=1e-4)
+    ls = F.cross_entropy(z, Y[idx.long()], reduction="sum").item()
+    corr = (z.argmax(1) == Y[idx.long()]).sum().item()
+    assert abs(acc[0].item() - ls) < 1e-2
+    assert acc[1].item() == corr
+    ref = reference_mlp_forward(p.cpu(), dims, X[:3])
+    assert torch.allclose(ref, net(X[:3]), atol=1e-5)
+
+
+def test_adam_flat_matches_torch(cuda):
+    from dct_amd.ops.optim import adam_flat_
+
+    torch.manual_seed(5)
+    n = 1037
+    w = torch.randn(n)
+    net_p = torch.nn.Parameter(w.clone())
+    opt = torch.optim.Adam([net_p], lr=0.01, weight_decay=0.1)
+    p = w.clone().to(cuda)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    counter = torch.zeros(1, dtype=torch.int32, device=cuda)
+    for t in range(1, 6):
+        g = torch.randn(n)
+        net_p.grad = g.clone()
+        opt.step()
+        if t % 2:
+            adam_flat_(p, g.to(cuda), m, v, t, 0.01, weight_decay=0.1)
+        else:  # device-counter path
+            counter.fill_(t)
+            adam_flat_(p, g.to(cuda), m, v, 1, 0.01, weight_decay=0.1, step_counter=counter)
+    assert torch.allclose(p.cpu(), net_p.detach(), atol=1e-6, rtol=1e-5)
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 200, 72), (1, 17, 8), (257, 1024, 256), (64, 3, 1024)])
+@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
+def test_gemm_bf16(M, N, K, ta, tb, cuda):
+    torch.manual_seed(6)
+    A = torch.randn(M, K, device=cuda)
+    B = torch.randn(K, N, device=cuda)
+    As = A.t().contiguous() if ta else A.contiguous()
+    Bs = B.t().contiguous() if tb else B.contiguous()
+    As, Bs = _bf(As), _bf(Bs)
+    C = torch.zeros(M, N, device=cuda)
+    nat = native()
+    nat.gemm_bf16(As.data_ptr(), Bs.data_ptr(), C.data_ptr(), 0, M, N, K, As.stride(0), Bs.stride(0), N, ta, tb, 0, 1,
+                  0, 0, torch.cuda.current_stream().cuda_stream)
+    ref = (As.float().t() if ta else As.float()) @ (Bs.float().t() if tb else Bs.float())
+    torch.cuda.synchronize()
+    assert torch.allclose(C, ref, atol=2e-3 * math.sqrt(K), rtol=1e-3)
+
+
+@pytest.mark.parametrize("epi", [1, 2, 3])
+def test_gemm_epilogues_and_accumulate(epi, cuda):
+    torch.manual_seed(7)
+    M, N, K = 200, 96, 128
+    X = _bf(torch.randn(M, K, device=cuda))
+    W = _bf(torch.randn(N, K, device=cuda) * 0.1)
+    b = torch.randn(N, device=cuda)
+    Y = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    aux = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    nat = native()
+    nat.gemm_bf16(X.data_ptr(), W.data_ptr(), Y.data_ptr(), b.data_ptr(), M, N, K, K, K, N, 0, 1, epi, 0, 0,
+                  aux.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    z = X.float() @ W.float().t() + b
+    ref = {1: z, 2: torch.relu(z), 3: F.gelu(z)}[epi]
+    torch.cuda.synchronize()
+    assert torch.allclose(Y.float(), ref, atol=3e-2, rtol=2e-2)
+    if epi == 3:
+        assert torch.allclose(aux.float(), z, atol=3e-2, rtol=2e-2)
+    # fp32 accumulate
+    C = torch.ones(M, N, device=cuda)
+    nat.gemm_bf16(X.data_ptr(), W.data_ptr(), C.data_ptr(), 0, M, N, K, K, K, N, 0, 1, 0, 1, 1, 0,
+                  torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.allclose(C, 1 + X.float() @ W.float().t(), atol=1e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_bias_act_bwd(act, cuda):
+    torch.manual_seed(8)
+    M, N = 333, 136
+    dY = _bf(torch.randn(M, N, device=cuda))
+    z = _bf(torch.randn(M, N, device=cuda))
+    aux = z if act != 1 else _bf(torch.relu(z.float()))
+    dZ = torch.empty_like(dY)
+    db = torch.zeros(N, device=cuda)
+    native().bias_act_bwd(dY.data_ptr(), aux.data_ptr(), dZ.data_ptr(), db.data_ptr(), M, N, N, act, 0,
+                          torch.cuda.current_stream().cuda_stream)
+    zz = z.float().requires_grad_(True)
+    if act == 0:
+        ref = dY.float()
+    elif act == 1:
+        ref = dY.float() * (aux.float() > 0)
+    else:
+        F.gelu(zz).backward(dY.float())
+        ref = zz.grad
+    torch.cuda.synchronize()
+    assert torch.allclose(dZ.float(), ref, atol=2e-2, rtol=2e-2)
+    assert torch.allclose(db, ref.sum(0), atol=0.3, rtol=2e-2)
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_loss_kernel(kind, cuda):
+    torch.manual_seed(9)
+    M, C = 1000, 3
+    z = torch.randn(M, C, device=cuda)
+    y = torch.randint(0, C, (M,), device=cuda)
+    dz = torch.empty_like(z)
+    ls = torch.zeros(1, device=cuda)
+    cs = torch.zeros(1, device=cuda)
+    native().cross_entropy_fwd_bwd(z.data_ptr(), 0, y.to(torch.int32).data_ptr(), dz.data_ptr(), ls.data_ptr(),
+                                   cs.data_ptr(), M, C, 1.0 / M, kind, torch.cuda.current_stream().cuda_stream)
+    zz = z.clone().requires_grad_(True)
+    l = F.cross_entropy(zz, y) if kind == 0 else F.mse_loss(zz, F.one_hot(y, C).float())
+    l.backward()
+    torch.cuda.synchronize()
+    assert abs(ls.item() / M - l.item()) < 1e-4
+    assert torch.allclose(dz, zz.grad, atol=1e-6, rtol=1e-4)
+    assert cs.item() == (z.argmax(1) == y).sum().item()
+
+
+def test_layernorm_fwd_bwd(cuda):
+    torch.manual_seed(10)
+    M, N = 513, 192
+    x = torch.randn(M, N, device=cuda)
+    w = torch.randn(N, device=cuda)
+    b = torch.randn(N, device=cuda)
+    y = torch.empty_like(x)
+    mean = torch.empty(M, device=cuda)
+    rstd = torch.empty(M, device=cuda)
+    nat = native()
+    st = torch.cuda.current_stream().cuda_stream
+    nat.layernorm_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), M, N,
+                      1e-5, 0, 0, st)
+    xx = x.clone().requires_grad_(True)
+    ww = w.clone().requires_grad_(True)
+    bb = b.clone().requires_grad_(True)
+    ref = F.layer_norm(xx, (N,), ww, bb, 1e-5)
+    dy = torch.randn_like(ref)
+    ref.backward(dy)
+    dx = torch.empty_like(x)
+    dw = torch.zeros(N, device=cuda)
+    db = torch.zeros(N, device=cuda)
+    nat.layernorm_bwd(dy.data_ptr(), x.data_ptr(), w.data_ptr(), mean.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
+                      dw.data_ptr(), db.data_ptr(), M, N, 0, st)
+    torch.cuda.synchronize()
+    assert torch.allclose(y, ref.detach(), atol=1e-4, rtol=1e-4)
+    assert torch.allclose(dx, xx.grad, atol=1e-4, rtol=1e-3)
+    assert torch.allclose(dw, ww.grad, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(db, bb.grad, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("Bsz,H,T,D", [(2, 4, 6, 16), (3, 2, 33, 32), (1, 1, 256, 64)])
+def test_attention_fwd_bwd(Bsz, H, T, D, cuda):
+    torch.manual_seed(11)
+    dm = H * D
+    qkv = _bf(torch.randn(Bsz * T, 3 * dm, device=cuda))
+    o = torch.empty(Bsz * T, dm, device=cuda, dtype=torch.bfloat16)
+    lse = torch.empty(Bsz * H * T, device=cuda)
+    nat = native()
+    st = torch.cuda.current_stream().cuda_stream
+    scale = 1.0 / math.sqrt(D)
+    q, k, v = (qkv[:, i * dm:(i + 1) * dm] for i in range(3))
+    nat.attention_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr(), Bsz, H, T, D, 3 * dm,
+                      dm, scale, st)
+
+    def split(t):
+        return t.float().reshape(Bsz, T, H, D).permute(0, 2, 1, 3)
+
+    qq, kk, vv = (split(t).requires_grad_(True) for t in (q, k, v))
+    ref = F.scaled_dot_product_attention(qq, kk, vv)
+    torch.cuda.synchronize()
+    got = o.float().reshape(Bsz, T, H, D).permute(0, 2, 1, 3)
+    assert torch.allclose(got, ref.detach(), atol=2e-2, rtol=2e-2)
+    do = _bf(torch.randn(Bsz * T, dm, device=cuda))
+    ref.backward(split(do))
+    dqkv = torch.zeros_like(qkv)
+    dq, dk, dv = (dqkv[:, i * dm:(i + 1) * dm] for i in range(3))
+    nat.attention_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), do.data_ptr(), lse.data_ptr(),
+                      dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), Bsz, H, T, D, 3 * dm, dm, scale, st)
+    torch.cuda.synchronize()
+    for g, r in ((dq, qq.grad), (dk, kk.grad), (dv, vv.grad)):
+        gg = g.float().reshape(Bsz, T, H, D).permute(0, 2, 1, 3)
+        assert torch.allclose(gg, r, atol=5e-2, rtol=5e-2), (gg - r).abs().max()
+
+
+def test_gather_rows(cuda):
+    src = torch.randn(1000, 12, device=cuda)
+    idx = torch.randint(0, 1000, (333,), device=cuda, dtype=torch.int32)
+    dst = torch.empty(333, 12, device=cuda)
+    native().gather_rows(src.data_ptr(), idx.data_ptr(), dst.data_ptr(), 333, 48, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(dst, src[idx.long()])

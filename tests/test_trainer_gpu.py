@@ -1,0 +1,77 @@
+"""End-to-end training on the GPU engines."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+from torch.utils.data import DataLoader, random_split
+
+import dct_amd  # noqa: F401
+from dct_amd.ckpt import ModelCheckpoint, load_checkpoint
+from dct_amd.data.dataset import TensorPairDataset
+from dct_amd.data.synthetic import weather_tensors
+from dct_amd.models.mlp import MLPClassifier, WeatherClassifier
+from dct_amd.tracking import InMemoryLogger
+from dct_amd.trainer import Trainer, seed_everything
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _loaders(n=2000, bs=4):
+    seed_everything(42)
+    x, y = weather_tensors(n, seed=0)
+    ds = TensorPairDataset(x, y)
+    tr, va = random_split(ds, [int(0.8 * n), n - int(0.8 * n)])
+    return DataLoader(tr, batch_size=bs, shuffle=True), DataLoader(va, batch_size=bs)
+
+
+def test_fit_fused_engine_writes_lightning_checkpoints(tmp_path):
+    tl, vl = _loaders()
+    model = WeatherClassifier(5)
+    ck = ModelCheckpoint(dirpath=str(tmp_path), filename="weather-best-{epoch:02d}-{val_loss:.2f}", monitor="val_loss",
+                         mode="min", save_top_k=1, save_last=True)
+    logger = InMemoryLogger()
+    tr = Trainer(max_epochs=3, accelerator="gpu", logger=logger, callbacks=[ck], log_every_n_steps=5)
+    tr.fit(model, tl, vl)
+    assert tr.engine.name == "fused"
+    assert os.path.exists(ck.best_model_path) and os.path.exists(tmp_path / "last.ckpt")
+    ckpt = load_checkpoint(ck.best_model_path)
+    assert set(ckpt["state_dict"]) == {"net.0.weight", "net.0.bias", "net.3.weight", "net.3.bias"}
+    assert ckpt["hyper_parameters"] == {"input_dim": 5}
+    m2 = WeatherClassifier.load_from_checkpoint(ck.best_model_path, input_dim=5)
+    assert all(t.device.type == "cpu" for t in m2.state_dict().values())
+    vals = [v for _, v in logger.history("val_loss")]
+    assert len(vals) == 3 and vals[-1] < vals[0] + 0.05
+    assert tr.callback_metrics["val_acc"] > 0.6
+    # train_loss logged every 5 steps with step = k-1
+    steps = [s for s, _ in logger.history("train_loss")]
+    assert steps[:2] == [4, 9]
+
+
+def test_fused_matches_autograd_engine_without_dropout():
+    def run(engine, acc):
+        tl, vl = _loaders(800)
+        torch.manual_seed(0)
+        model = MLPClassifier(5, hidden=(64,), dropout=0.0)
+        tr = Trainer(max_epochs=2, accelerator=acc, engine=engine, num_sanity_val_steps=0, verbose=False)
+        tr.fit(model, tl, vl)
+        return tr.callback_metrics["val_loss"], model
+    l_f, m_f = run("fused", "gpu")
+    l_a, m_a = run("autograd", "cpu")
+    assert abs(l_f - l_a) < 5e-3
+
+
+def test_bench_contract_single_gpu():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "400", "--warmup", "40"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    out = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in out
+    assert out["n_gpus"] == 1 and out["steps"] == 400 and out["value"] > 0
+    assert out["extra"]["losses_finite"]
