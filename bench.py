@@ -78,15 +78,15 @@ def main():
     loss = torch.zeros(total_steps, dtype=torch.float32, device=ctx.device)
 
     # warmup (also captures the DDP step graph chunk outside the timed region)
-    eng.run_steps(n_items, a.warmup, loss if ctx.is_distributed else loss[: a.warmup], first_step=0)
-    if ctx.is_distributed and eng.use_graph:
+    eng.run_steps(n_items, a.warmup, loss if eng.ddp else loss[: a.warmup], first_step=0)
+    if eng.ddp and eng.use_graph:
         C = min(eng.graph_chunk, a.steps)
         eng._get_graph(n_items, C, loss)
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if ctx.is_distributed:
+    if eng.ddp:
         eng.run_steps(n_items, a.steps, loss, first_step=a.warmup)
     else:
         eng.run_steps(n_items, a.steps, loss[a.warmup:], first_step=a.warmup)
@@ -134,8 +134,9 @@ def main():
             "parallelism": f"dp{ctx.world_size}",
             "optimizer": "adam lr=0.01",
             "loss": eng.loss,
-            "engine": "fused-persistent" if not ctx.is_distributed else
-                      ("fused+rccl-allreduce+hipgraph" if eng.graph_used else "fused+rccl-allreduce"),
+            "engine": "fused-persistent" if not eng.ddp else
+                      ("fused+rccl-allreduce" + ("+update-then-grad" if eng.fused_update else "+adam")
+                       + ("+hipgraph" if eng.graph_used else "")),
             "baseline_ref": "BASELINE.md CPU probe, W=1, 8500 samples/s (reference publishes none)",
         },
         "extra": {

@@ -81,7 +81,8 @@ PYBIND11_MODULE(_dct_native, m) {
           [](const MlpPlan& plan, uintptr_t p, uintptr_t mo, uintptr_t vo, uintptr_t grad_out, uintptr_t X, int ldx,
              uintptr_t Y, uintptr_t idx, int n_items, int B, int steps, int t0, float lr, float b1, float b2,
              float eps, float wd, float dropout, uint32_t seed, uint32_t step_base, uintptr_t loss_out, int mode,
-             int loss_kind, uintptr_t step_counter, uintptr_t cursor, uintptr_t prof, uintptr_t stream) {
+             int loss_kind, uintptr_t step_counter, uintptr_t cursor, uintptr_t prof, uintptr_t pending,
+             uintptr_t stage, uintptr_t stream) {
             if (!plan.supported) throw std::runtime_error("MLP too large for the fused kernel");
             if (steps < 1 || n_items < 1 || B < 1) throw std::invalid_argument("empty launch");
             if (!cursor && (int64_t)(steps - 1) * B >= n_items) throw std::invalid_argument("more steps than batches");
@@ -108,6 +109,10 @@ PYBIND11_MODULE(_dct_native, m) {
             a.step_counter = P<int>(step_counter);
             a.cursor = P<int>(cursor);
             a.prof = P<unsigned long long>(prof);
+            a.pending = P<int>(pending);
+            a.stage = P<uint32_t>(stage);
+            if (pending && (mode != 1 || !plan.use_wave || !mo || !vo))
+              throw std::invalid_argument("update-then-grad needs grad mode, m/v and the single-wave kernel");
             if (cursor && mode != 1) throw std::invalid_argument("cursor is only valid in grad mode");
             if (mode == 1 && !grad_out) throw std::invalid_argument("grad mode needs grad_out");
             if (mode == 1 && steps != 1) throw std::invalid_argument("grad mode runs exactly one step");
@@ -121,7 +126,8 @@ PYBIND11_MODULE(_dct_native, m) {
           py::arg("idx"), py::arg("n_items"), py::arg("B"), py::arg("steps"), py::arg("t0"), py::arg("lr"),
           py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("dropout"), py::arg("seed"),
           py::arg("step_base"), py::arg("loss_out"), py::arg("mode"), py::arg("loss_kind"), py::arg("step_counter"),
-          py::arg("cursor"), py::arg("prof") = 0, py::arg("stream") = 0)
+          py::arg("cursor"), py::arg("prof") = 0, py::arg("pending") = 0, py::arg("stage") = 0,
+          py::arg("stream") = 0)
       .def(
           "eval",
           [](const MlpPlan& plan, uintptr_t p, uintptr_t X, int ldx, uintptr_t Y, uintptr_t idx, int n_items,

@@ -78,6 +78,15 @@ struct MlpArgs {
   // diagnostic only: per-phase cycle sums (s_memtime deltas, thread 0) + [30]/[31] realtime
   // start/end (100 MHz) when non-null; never set in production launches.
   unsigned long long* prof;
+  // optional (GRAD mode, single-wave kernel): "update-then-grad". If *pending != 0 the
+  // kernel first applies Adam with the (all-reduced) gradients still in grad_out, then
+  // computes the new gradients; p/m/v are written back and *pending is set to 1.
+  int* pending;
+  // optional (single-wave kernel): tagged staging buffer for the next launch's batch,
+  // [0] = batch index of the staged data, [64..) = one dword per lane per prefetch slot.
+  // A launch whose cursor equals the tag reads its batch from here (one round trip, issued
+  // with the parameter loads) instead of the dependent idx -> x gather.
+  uint32_t* stage;
 };
 
 hipError_t mlp_launch_train_L2(const MlpShape& sh, const MlpArgs& a, hipStream_t st);

@@ -83,6 +83,8 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
   const int j = threadIdx.x;  // lane = hidden unit
   const int d0 = sh.d0, H1 = sh.h1, H2 = (L == 3 ? sh.h2 : sh.h1), C = sh.C;
   const bool adam = (a.mode == 0);
+  const bool fuse_upd = (!adam) && (a.pending != nullptr);  // apply pending Adam, then grad
+  const bool need_mv = adam || fuse_upd;
   const bool own1 = j < H1;
   const bool own2 = j < H2;  // unit of the last hidden layer
 
@@ -99,12 +101,12 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
     const bool ok = own1 && k < d0;
     const int f = sh.woff[0] + j * d0 + k;
     w0[k] = ok ? a.p[f] : 0.f;
-    mw0[k] = (ok && adam) ? a.m[f] : 0.f;
-    vw0[k] = (ok && adam) ? a.v[f] : 0.f;
+    mw0[k] = (ok && need_mv) ? a.m[f] : 0.f;
+    vw0[k] = (ok && need_mv) ? a.v[f] : 0.f;
   }
   if (own1) {
     b0 = a.p[sh.boff[0] + j];
-    if (adam) { mb0 = a.m[sh.boff[0] + j]; vb0 = a.v[sh.boff[0] + j]; }
+    if (need_mv) { mb0 = a.m[sh.boff[0] + j]; vb0 = a.v[sh.boff[0] + j]; }
   }
   if (L == 3) {
 #pragma unroll
@@ -112,12 +114,12 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
       const bool ok = own2 && i < H1;
       const int f = sh.woff[1] + j * H1 + i;
       w1[i] = ok ? a.p[f] : 0.f;
-      mw1[i] = (ok && adam) ? a.m[f] : 0.f;
-      vw1[i] = (ok && adam) ? a.v[f] : 0.f;
+      mw1[i] = (ok && need_mv) ? a.m[f] : 0.f;
+      vw1[i] = (ok && need_mv) ? a.v[f] : 0.f;
     }
     if (own2) {
       b1 = a.p[sh.boff[1] + j];
-      if (adam) { mb1 = a.m[sh.boff[1] + j]; vb1 = a.v[sh.boff[1] + j]; }
+      if (need_mv) { mb1 = a.m[sh.boff[1] + j]; vb1 = a.v[sh.boff[1] + j]; }
     }
   }
 #pragma unroll
@@ -125,12 +127,42 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
     const bool ok = own2 && c < C;
     const int f = sh.woff[lo] + c * H2 + j;
     wo[c] = ok ? a.p[f] : 0.f;
-    mwo[c] = (ok && adam) ? a.m[f] : 0.f;
-    vwo[c] = (ok && adam) ? a.v[f] : 0.f;
+    mwo[c] = (ok && need_mv) ? a.m[f] : 0.f;
+    vwo[c] = (ok && need_mv) ? a.v[f] : 0.f;
   }
   if (j < C) {
     bo = a.p[sh.boff[lo] + j];
-    if (adam) { mbo = a.m[sh.boff[lo] + j]; vbo = a.v[sh.boff[lo] + j]; }
+    if (need_mv) { mbo = a.m[sh.boff[lo] + j]; vbo = a.v[sh.boff[lo] + j]; }
+  }
+  int t0 = a.t0;
+  uint32_t step_base = a.step_base;
+  if (a.step_counter) {
+    t0 = __hip_atomic_load(a.step_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    step_base = (uint32_t)t0;
+  }
+  if (fuse_upd && __hip_atomic_load(a.pending, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+    // previous step's all-reduced gradients are in grad_out: apply its Adam update first
+    const float tt = (float)t0;
+    const float step_size = a.lr / (1.f - __powf(a.b1, tt));
+    const float rbc2 = __builtin_amdgcn_rsqf(1.f - __powf(a.b2, tt));
+    if (own1) {
+#pragma unroll
+      for (int k = 0; k < D0; ++k)
+        if (k < d0) adam1(w0[k], a.grad_out[sh.woff[0] + j * d0 + k], mw0[k], vw0[k], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+      adam1(b0, a.grad_out[sh.boff[0] + j], mb0, vb0, a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+    }
+    if (L == 3 && own2) {
+#pragma unroll
+      for (int i = 0; i < (L == 3 ? HM : 1); ++i)
+        if (i < H1) adam1(w1[i], a.grad_out[sh.woff[1] + j * H1 + i], mw1[i], vw1[i], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+      adam1(b1, a.grad_out[sh.boff[1] + j], mb1, vb1, a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+    }
+    if (own2) {
+#pragma unroll
+      for (int c = 0; c < CM; ++c)
+        if (c < C) adam1(wo[c], a.grad_out[sh.woff[lo] + c * H2 + j], mwo[c], vwo[c], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+    }
+    if (j < C) adam1(bo, a.grad_out[sh.boff[lo] + j], mbo, vbo, a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
   }
   if (L == 3) {  // W1^T (row i = column i of W1) for the middle layer's backward
 #pragma unroll
@@ -143,12 +175,6 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
   if (a.cursor) {
     cur0 = __hip_atomic_load(a.cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (j == 0 && cur0 > 0 && a.loss_out) a.loss_out[cur0 - 1] = a.grad_out[sh.P];
-  }
-  int t0 = a.t0;
-  uint32_t step_base = a.step_base;
-  if (a.step_counter) {
-    t0 = __hip_atomic_load(a.step_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    step_base = (uint32_t)t0;
   }
   const int B = a.B;
 
@@ -186,8 +212,17 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
   };
   uint32_t cur[NPF], nxt[NPF];
   int ridx_a[NPF], ridx_b[NPF];
-  load_idx(cur0, ridx_a);
-  load_vals(cur0, ridx_a, cur);
+  bool staged = false;
+  if (a.stage) {
+    const int tag = (int)__hip_atomic_load(&a.stage[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int r = 0; r < NPF; ++r) cur[r] = a.stage[64 + r * 64 + j];
+    staged = (tag == cur0 + 1);  // tag stores batch index + 1 (0 = empty)
+  }
+  if (!staged) {
+    load_idx(cur0, ridx_a);
+    load_vals(cur0, ridx_a, cur);
+  }
   load_idx(cur0 + 1, ridx_a);  // idx of batch cur0 + 1
 
   const float keep_scale = (a.dropout > 0.f) ? 1.0f / (1.0f - a.dropout) : 1.0f;
@@ -439,10 +474,21 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
     }
   }
   if (prof) a.prof[31] = __builtin_amdgcn_s_memrealtime();
+  if (a.stage) {  // hand the already-fetched next batch to the next launch
+    const int nb = cur0 + a.steps;
+    const bool ok = nb * B < a.n_items;
+    if (ok) {
+#pragma unroll
+      for (int r = 0; r < NPF; ++r) a.stage[64 + r * 64 + j] = cur[r];
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // every lane's stage stores complete before the tag
+    if (j == 0) __hip_atomic_store(&a.stage[0], ok ? (uint32_t)(nb + 1) : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (a.cursor && j == 0) __hip_atomic_store(a.cursor, cur0 + a.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (a.step_counter && j == 0)
     __hip_atomic_store(a.step_counter, t0 + a.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (!adam) return;
+  if (fuse_upd && j == 0) __hip_atomic_store(a.pending, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!need_mv) return;
   // ---- write back params + moments
 #pragma unroll
   for (int k = 0; k < D0; ++k) {

@@ -36,6 +36,10 @@ class FusedMLPKernel:
             self._plan = native().MlpPlan(self.dims, self.bmax)
         return self._plan
 
+    def fused_update_supported(self, batch: int) -> bool:
+        """True if the update-then-grad DDP step (one kernel per step) is available."""
+        return bool(self.plan.use_wave) and batch <= 8
+
     @property
     def eval_plan(self):
         if self._eval_plan is None:
@@ -94,10 +98,14 @@ class FusedMLPKernel:
               seed: int = 0, step_base: int = 0, loss_out: Optional[torch.Tensor] = None,
               loss: str = "ce", grad_out: Optional[torch.Tensor] = None, step_counter: Optional[torch.Tensor] = None,
               cursor: Optional[torch.Tensor] = None, prof: Optional[torch.Tensor] = None,
+              pending: Optional[torch.Tensor] = None, stage: Optional[torch.Tensor] = None,
               stream: Optional[int] = None):
         """Run ``steps`` fused optimizer steps (mode 0) or one gradient step (grad_out given)."""
         mode = 1 if grad_out is not None else 0
-        self._check_params(p, m if mode == 0 else None, v if mode == 0 else None)
+        need_mv = mode == 0 or pending is not None
+        self._check_params(p, m if need_mv else None, v if need_mv else None)
+        if pending is not None and not (pending.is_cuda and pending.dtype == torch.int32):
+            raise ValueError("pending must be a cuda int32 flag")
         self._check_data(X, Y, idx, n_items)
         if batch > self.bmax:
             raise ValueError(f"batch {batch} > kernel bmax {self.bmax}")
@@ -109,17 +117,21 @@ class FusedMLPKernel:
             P = mlp_num_params(self.dims)
             if not (grad_out.is_cuda and grad_out.dtype == torch.float32 and grad_out.numel() >= P + 1):
                 raise ValueError("grad_out must be cuda fp32 with P+1 entries (grads + loss)")
+        if stage is not None and not (stage.is_cuda and stage.dtype == torch.int32 and stage.numel() >= 64 * 3):
+            raise ValueError("stage must be a cuda int32 buffer of >= 192 entries")
         if step_counter is not None and not (step_counter.is_cuda and step_counter.dtype == torch.int32):
             raise ValueError("step_counter must be a cuda int32 scalar tensor")
         if loss_out is not None and not (loss_out.is_cuda and loss_out.dtype == torch.float32
                                          and loss_out.numel() >= steps):
             raise ValueError("loss_out must be cuda fp32 [steps]")
         self.plan.train(
-            ptr(p), ptr(m) if mode == 0 else 0, ptr(v) if mode == 0 else 0, ptr(grad_out),
+            ptr(p), ptr(m) if need_mv else 0, ptr(v) if need_mv else 0, ptr(grad_out),
             ptr(X), X.stride(0), ptr(Y), ptr(idx), int(n_items), int(batch), int(steps), int(t0),
             float(lr), float(betas[0]), float(betas[1]), float(eps), float(weight_decay), float(dropout),
             int(seed) & 0xFFFFFFFF, int(step_base) & 0xFFFFFFFF, ptr(loss_out), mode, LOSS_KINDS[loss],
-            ptr(step_counter), ptr(cursor), ptr(prof), stream if stream is not None else stream_handle(),
+            ptr(step_counter), ptr(cursor), ptr(prof), ptr(pending),
+            ptr(stage) if (stage is not None and self.plan.use_wave) else 0,
+            stream if stream is not None else stream_handle(),
         )
 
     def evaluate(self, p, X, Y, idx, n_items: int, acc_out: torch.Tensor, loss: str = "ce",

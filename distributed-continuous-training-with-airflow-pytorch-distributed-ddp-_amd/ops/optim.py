@@ -50,6 +50,18 @@ def adam_flat_(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tenso
         p_bf16.copy_(p)
 
 
+def _torch_adam_group_defaults() -> Dict:
+    """The param-group keys the installed ``torch.optim.Adam`` writes (they vary by torch
+    version, e.g. ``decoupled_weight_decay`` since 2.6), so our optimizer state dicts stay
+    loadable by ``torch.optim.Adam.load_state_dict`` and by Lightning."""
+    try:
+        d = dict(torch.optim.Adam([torch.zeros(1, requires_grad=True)]).defaults)
+    except Exception:  # noqa: BLE001
+        d = dict(lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False, maximize=False,
+                 foreach=None, capturable=False, differentiable=False, fused=None)
+    return d
+
+
 class FlatAdam:
     """Adam over a flat parameter buffer, torch.optim.Adam-compatible state_dict."""
 
@@ -63,9 +75,10 @@ class FlatAdam:
         self.m = torch.zeros_like(flat_param)
         self.v = torch.zeros_like(flat_param)
         self.shapes = [torch.Size(s) for s in param_shapes]
-        self.param_groups = [dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=False,
-                                  maximize=False, foreach=None, capturable=False, differentiable=False,
-                                  fused=None, params=list(range(len(self.shapes))))]
+        group = _torch_adam_group_defaults()
+        group.update(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay,
+                     params=list(range(len(self.shapes))))
+        self.param_groups = [group]
         self.step_count = 0
         self.p_bf16: Optional[torch.Tensor] = None
 

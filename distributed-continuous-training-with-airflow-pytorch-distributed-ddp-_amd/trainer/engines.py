@@ -96,12 +96,24 @@ class FusedMLPEngine(_EngineBase):
         self.rank_seed = (self.seed * 1000003 + ctx.rank * 7919 + 1) & 0xFFFFFFFF
         self.comm = None
         self.gbuf = None
+        # DDP step path; DCT_FORCE_DDP=1 drives it at world size 1 (single-GPU test of the
+        # RCCL communicator + graph capture + device cursors)
+        self.ddp = ctx.is_distributed or os.environ.get("DCT_FORCE_DDP", "0") == "1"
+        self.fused_update = self.kernel.fused_update_supported(self.B) and os.environ.get("DCT_FUSED_UPDATE", "1") != "0"
+        self.pending = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.stage = torch.zeros(64 * 4, dtype=torch.int32, device=dev)  # next-batch hand-off
         self._graphs = {}
         self.graph_chunk = int(os.environ.get("DCT_GRAPH_CHUNK", "256"))
         self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
         self.graph_used = False
         if ctx.is_distributed:
             self.comm = init_native_comm(ctx)
+        elif self.ddp:
+            from ..ops._native import native
+
+            nat = native()
+            self.comm = nat.Comm(nat.comm_unique_id(), 1, 0, dev.index or 0)
+        if self.ddp:
             self.gbuf = torch.zeros(self.P + 1, dtype=torch.float32, device=dev)
             self._broadcast_params()
 
@@ -175,6 +187,7 @@ class FusedMLPEngine(_EngineBase):
         return math.ceil(n_local / self.B)
 
     def upload_epoch_indices(self, epoch: int, shuffle: bool = True) -> int:
+        self.stage.zero_()  # staged batches refer to the previous index list
         local = self.epoch_local_indices(len(self.train_rows), epoch, shuffle)
         rows = self.train_rows[local].to(torch.int32)
         self.idx[: rows.numel()].copy_(rows.pin_memory(), non_blocking=True)
@@ -196,7 +209,7 @@ class FusedMLPEngine(_EngineBase):
         No host synchronisation either way."""
         if steps <= 0:
             return
-        if not self.ctx.is_distributed:
+        if not self.ddp:
             chunk = self.steps_per_launch or steps
             s = 0
             while s < steps:
@@ -220,6 +233,11 @@ class FusedMLPEngine(_EngineBase):
                 self.graph_used = True
         for _ in range(steps - done):
             self._ddp_step(n_items, loss_out)
+        if self.fused_update:  # the last step's update is still pending: apply it
+            a = self.adam
+            adam_flat_(self.p, self.gbuf[: self.P], self.m, self.v, 1, a["lr"], a["betas"], a["eps"],
+                       a["weight_decay"], step_counter=self.step_counter)
+            self.pending.zero_()
         # the last step's reduced loss is flushed by the next kernel; flush it here instead
         last = first_step + steps - 1
         loss_out[last: last + 1].copy_(self.gbuf[self.P: self.P + 1])
@@ -230,12 +248,21 @@ class FusedMLPEngine(_EngineBase):
         from ..ops._native import native
 
         a = self.adam
+        nat = native()
+        stream = torch.cuda.current_stream().cuda_stream
+        if self.fused_update:
+            # one kernel: apply the previous step's (reduced) Adam update, then fwd/bwd
+            self.kernel.train(self.p, self.m, self.v, self.X, self.Y, self.idx, n_items=n_items, batch=self.B,
+                              steps=1, t0=0, lr=a["lr"], betas=a["betas"], eps=a["eps"],
+                              weight_decay=a["weight_decay"], dropout=self.dropout, seed=self.rank_seed,
+                              loss=self.loss, grad_out=self.gbuf, step_counter=self.step_counter,
+                              cursor=self.cursor, loss_out=loss_out, pending=self.pending, stage=self.stage)
+            self.comm.allreduce(self.gbuf.data_ptr(), self.P + 1, nat.DT_F32, nat.OP_AVG, stream)
+            return
         self.kernel.train(self.p, None, None, self.X, self.Y, self.idx, n_items=n_items, batch=self.B, steps=1,
                           t0=0, lr=a["lr"], dropout=self.dropout, seed=self.rank_seed, loss=self.loss,
                           grad_out=self.gbuf, step_counter=self.step_counter, cursor=self.cursor,
                           loss_out=loss_out)
-        nat = native()
-        stream = torch.cuda.current_stream().cuda_stream
         self.comm.allreduce(self.gbuf.data_ptr(), self.P + 1, nat.DT_F32, nat.OP_AVG, stream)
         adam_flat_(self.p, self.gbuf[: self.P], self.m, self.v, 1, a["lr"], a["betas"], a["eps"],
                    a["weight_decay"], step_counter=self.step_counter)
@@ -251,7 +278,8 @@ class FusedMLPEngine(_EngineBase):
         scratch = torch.zeros(64, dtype=torch.float32, device=self.device)
         self.comm.allreduce(scratch.data_ptr(), 64, nat.DT_F32, nat.OP_SUM, torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize(self.device)
-        state = (self.p, self.m, self.v, self.step_counter, self.cursor, self.gbuf, loss_out)
+        state = (self.p, self.m, self.v, self.step_counter, self.cursor, self.gbuf, loss_out, self.pending,
+                 self.stage)
         saved = [t.clone() for t in state]
         # one eager step first (kernel attributes, RCCL channels), then roll the state back
         self._ddp_step(n_items, loss_out)

@@ -75,3 +75,45 @@ def test_bench_contract_single_gpu():
         assert k in out
     assert out["n_gpus"] == 1 and out["steps"] == 400 and out["value"] > 0
     assert out["extra"]["losses_finite"]
+
+
+@pytest.mark.parametrize("fused_update", ["1", "0"])
+@pytest.mark.parametrize("graph", ["1", "0"])
+def test_ddp_step_path_world1_matches_persistent(fused_update, graph, monkeypatch):
+    """The DDP step loop (native RCCL comm, graph chunks, device cursor/step counter,
+    update-then-grad) at world size 1 must reproduce the persistent single-launch path."""
+    from dct_amd.parallel.dist import init_distributed
+    from dct_amd.trainer.engines import FusedMLPEngine, adam_hparams_from
+
+    x, y = weather_tensors(3000, seed=1)
+    rows = torch.randperm(3000, generator=torch.Generator().manual_seed(0))
+
+    def run(force):
+        monkeypatch.setenv("DCT_FORCE_DDP", force)
+        monkeypatch.setenv("DCT_GRAPH", graph)
+        monkeypatch.setenv("DCT_GRAPH_CHUNK", "7")
+        monkeypatch.setenv("DCT_FUSED_UPDATE", fused_update)
+        torch.manual_seed(0)
+        model = MLPClassifier(5, hidden=(64,), dropout=0.0)
+        ctx = init_distributed("gpu")
+        eng = FusedMLPEngine(model, ctx, 4, seed=42, adam=adam_hparams_from(model.configure_optimizers()))
+        eng.attach_data(x, y, rows[:2400], rows[2400:])
+        n = eng.upload_epoch_indices(0)
+        loss = torch.zeros(64, device=ctx.device)
+        if eng.ddp:
+            eng.run_steps(n, 30, loss, first_step=0)
+            eng.run_steps(n, 23, loss, first_step=30)
+        else:
+            eng.run_steps(n, 30, loss[:30], first_step=0)
+            eng.run_steps(n, 23, loss[30:53], first_step=30)
+        torch.cuda.synchronize()
+        assert int(eng.step_counter.item()) == 53
+        return eng.p.cpu(), eng.m.cpu(), loss[:53].cpu(), eng
+
+    p0, m0, l0, _ = run("0")
+    p1, m1, l1, e1 = run("1")
+    assert e1.ddp and e1.comm is not None
+    assert e1.graph_used == (graph == "1")
+    assert torch.allclose(l0, l1, atol=1e-5), (l0 - l1).abs().max()
+    assert (p0 - p1).abs().max() < 1e-3 and (p0 - p1).abs().median() < 1e-6
+    assert torch.allclose(m0, m1, atol=1e-5)
