@@ -78,27 +78,41 @@ def main():
     loss = torch.zeros(total_steps, dtype=torch.float32, device=ctx.device)
 
     # warmup (also captures the DDP step graph chunk outside the timed region)
-    eng.run_steps(n_items, a.warmup, loss if eng.ddp else loss[: a.warmup], first_step=0)
-    if eng.ddp and eng.use_graph:
+    eng.run_steps(n_items, a.warmup, loss, first_step=0)
+    if eng.xg is not None and not eng.xg_verify(fallback=True):
+        eng.run_steps(n_items, a.warmup, loss, first_step=0)  # re-warm on the RCCL path
+    if eng.ddp and eng.xg is None and eng.use_graph:
         C = min(eng.graph_chunk, a.steps)
         eng._get_graph(n_items, C, loss)
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if eng.ddp:
-        eng.run_steps(n_items, a.steps, loss, first_step=a.warmup)
-    else:
-        eng.run_steps(n_items, a.steps, loss[a.warmup:], first_step=a.warmup)
+    eng.run_steps(n_items, a.steps, loss, first_step=a.warmup)
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    dt_t = torch.tensor([dt], dtype=torch.float64, device=ctx.device)
+    dt_t = torch.tensor([dt], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
     if ctx.is_distributed:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
 
+    xg_ok = eng.xg_verify(fallback=True) if eng.xg is not None else None
+    if eng.xg is not None or eng.ddp:
+        engine_desc = eng.step_mode if eng.xg is not None else (
+            "fused+rccl-allreduce" + ("+update-then-grad" if eng.fused_update else "+adam")
+            + ("+hipgraph" if eng.graph_used else ""))
+    else:
+        engine_desc = "fused-persistent"
+    # DDP invariant: every rank holds the same parameters after the timed steps
+    in_sync = True
+    if ctx.is_distributed:
+        ref = eng.p.clone()
+        ctx.broadcast_(ref, src=0)
+        diff = torch.tensor([float((eng.p - ref).abs().max())], device=ctx.device if ctx.backend == "nccl" else "cpu")
+        dist.all_reduce(diff, op=dist.ReduceOp.MAX)
+        in_sync = float(diff.item()) == 0.0
     losses = loss.cpu()
     finite = bool(torch.isfinite(losses).all())
     first_l = float(losses[: max(1, a.warmup // 10)].mean())
@@ -134,9 +148,7 @@ def main():
             "parallelism": f"dp{ctx.world_size}",
             "optimizer": "adam lr=0.01",
             "loss": eng.loss,
-            "engine": "fused-persistent" if not eng.ddp else
-                      ("fused+rccl-allreduce" + ("+update-then-grad" if eng.fused_update else "+adam")
-                       + ("+hipgraph" if eng.graph_used else "")),
+            "engine": engine_desc,
             "baseline_ref": "BASELINE.md CPU probe, W=1, 8500 samples/s (reference publishes none)",
         },
         "extra": {
@@ -148,13 +160,15 @@ def main():
             "val_loss": round(val_loss, 4),
             "val_acc": round(val_acc, 4),
             "losses_finite": finite,
+            "params_in_sync": in_sync,
+            "xgmi_exchange_ok": xg_ok,
             "device": torch.cuda.get_device_name(ctx.device),
         },
     }
     if ctx.rank == 0:
         print(json.dumps(out), flush=True)
     shutdown(ctx)
-    return 0 if finite else 3
+    return 0 if (finite and in_sync) else 3
 
 
 if __name__ == "__main__":

@@ -82,7 +82,8 @@ PYBIND11_MODULE(_dct_native, m) {
              uintptr_t Y, uintptr_t idx, int n_items, int B, int steps, int t0, float lr, float b1, float b2,
              float eps, float wd, float dropout, uint32_t seed, uint32_t step_base, uintptr_t loss_out, int mode,
              int loss_kind, uintptr_t step_counter, uintptr_t cursor, uintptr_t prof, uintptr_t pending,
-             uintptr_t stage, uintptr_t stream) {
+             uintptr_t stage, uintptr_t stream, uintptr_t xg_recv, uintptr_t xg_peers, int xg_world, int xg_rank,
+             uintptr_t xg_status, int64_t xg_timeout) {
             if (!plan.supported) throw std::runtime_error("MLP too large for the fused kernel");
             if (steps < 1 || n_items < 1 || B < 1) throw std::invalid_argument("empty launch");
             if (!cursor && (int64_t)(steps - 1) * B >= n_items) throw std::invalid_argument("more steps than batches");
@@ -111,6 +112,14 @@ PYBIND11_MODULE(_dct_native, m) {
             a.prof = P<unsigned long long>(prof);
             a.pending = P<int>(pending);
             a.stage = P<uint32_t>(stage);
+            a.xg_recv = P<unsigned long long>(xg_recv);
+            a.xg_peers = P<unsigned long long* const>(xg_peers);
+            a.xg_world = xg_world;
+            a.xg_rank = xg_rank;
+            a.xg_status = P<unsigned int>(xg_status);
+            a.xg_timeout = xg_timeout;
+            if (xg_world > 1 && !(plan.use_wave && dct_mlp_wave_supported(plan.sh()->dims, plan.sh()->L, B)))
+              throw std::invalid_argument("in-kernel all-reduce needs the single-wave kernel");
             if (pending && (mode != 1 || !plan.use_wave || !mo || !vo))
               throw std::invalid_argument("update-then-grad needs grad mode, m/v and the single-wave kernel");
             if (cursor && mode != 1) throw std::invalid_argument("cursor is only valid in grad mode");
@@ -127,7 +136,8 @@ PYBIND11_MODULE(_dct_native, m) {
           py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("dropout"), py::arg("seed"),
           py::arg("step_base"), py::arg("loss_out"), py::arg("mode"), py::arg("loss_kind"), py::arg("step_counter"),
           py::arg("cursor"), py::arg("prof") = 0, py::arg("pending") = 0, py::arg("stage") = 0,
-          py::arg("stream") = 0)
+          py::arg("stream") = 0, py::arg("xg_recv") = 0, py::arg("xg_peers") = 0, py::arg("xg_world") = 0,
+          py::arg("xg_rank") = 0, py::arg("xg_status") = 0, py::arg("xg_timeout") = 200000000LL)
       .def(
           "eval",
           [](const MlpPlan& plan, uintptr_t p, uintptr_t X, int ldx, uintptr_t Y, uintptr_t idx, int n_items,
@@ -270,6 +280,27 @@ PYBIND11_MODULE(_dct_native, m) {
       .def_property_readonly("num_buckets", &dct::BucketReducer::num_buckets)
       .def_property_readonly("launched", &dct::BucketReducer::launched)
       .def_property_readonly("comm_stream", &dct::BucketReducer::comm_stream);
+  py::class_<dct::PeerExchange>(m, "PeerExchange")
+      .def(py::init<int, int, int64_t>(), py::arg("world"), py::arg("rank"), py::arg("bytes"))
+      .def("ipc_handle", [](const dct::PeerExchange& x) { return py::bytes(x.ipc_handle()); })
+      .def("open_peers",
+           [](dct::PeerExchange& x, const std::vector<py::bytes>& hs) {
+             std::vector<std::string> v;
+             for (const auto& h : hs) v.emplace_back(std::string(h));
+             x.open_peers(v);
+           })
+      .def("set_peers", &dct::PeerExchange::set_peers)
+      .def("reset", &dct::PeerExchange::reset, py::arg("stream") = 0)
+      .def("read_status", &dct::PeerExchange::read_status)
+      .def_property_readonly("recv", &dct::PeerExchange::recv)
+      .def_property_readonly("peers", &dct::PeerExchange::peers)
+      .def_property_readonly("status", &dct::PeerExchange::status)
+      .def_property_readonly("bytes", &dct::PeerExchange::bytes)
+      .def_property_readonly("world", &dct::PeerExchange::world)
+      .def_property_readonly("rank", &dct::PeerExchange::rank);
+  m.def("mlp_xg_slab_granules", [](const std::vector<int>& dims) {
+    return (int64_t)dct_mlp_xg_slab_granules(dims.data(), (int)dims.size() - 1);
+  });
   py::class_<dct::StreamGraph>(m, "StreamGraph")
       .def(py::init<>())
       .def("begin", &dct::StreamGraph::begin)

@@ -87,7 +87,20 @@ struct MlpArgs {
   // A launch whose cursor equals the tag reads its batch from here (one round trip, issued
   // with the parameter loads) instead of the dependent idx -> x gather.
   uint32_t* stage;
+  // optional (single-wave kernel, train mode): in-kernel data-parallel gradient averaging
+  // across GPUs.  Every rank pushes its step gradients as 8-byte {tag, value} granules
+  // straight into each peer's receive buffer (peer-mapped over xGMI via IPC) and sums the
+  // peers' granules in rank order, so all ranks apply bit-identical Adam updates with no
+  // host round trip, no RCCL launch and no kernel boundary per step.  See mlp_wave.hip.
+  unsigned long long* xg_recv;              // own receive buffer, [2][W][KX][64] granules
+  unsigned long long* const* xg_peers;      // device array [W]: every rank's receive buffer
+  int xg_world;                             // 0/1 = off
+  int xg_rank;
+  unsigned int* xg_status;                  // [0]: 0 ok, else (global step + 1) of a timeout
+  long long xg_timeout;                     // spin limit in s_memrealtime ticks (100 MHz)
 };
+
+constexpr int XG_MAXW = 8;  // ranks of the in-kernel exchange (one node)
 
 hipError_t mlp_launch_train_L2(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
 hipError_t mlp_launch_train_L3(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
@@ -106,6 +119,7 @@ int dct_mlp_train(const void* shape, const dct::MlpArgs* a, void* stream);
 int dct_mlp_eval(const void* shape, const dct::MlpArgs* a, int grid, void* stream);
 int dct_mlp_wave_supported(const int* dims, int L, int B);
 int dct_mlp_wave_train(const int* dims, int L, const dct::MlpArgs* a, void* stream);
+size_t dct_mlp_xg_slab_granules(const int* dims, int L);
 int dct_adam_flat(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, float lr,
                   float b1, float b2, float eps, float wd, int64_t t, float grad_scale, int decoupled,
                   const int* step_counter, void* stream);

@@ -17,6 +17,18 @@
 //     backward needs no communication: dWout, dh, dW0 are lane-local FMAs;
 //   * Adam on the lane's own parameters (v_sqrt_f32 / v_rcp_f32).
 // A single wave needs no s_barrier: LDS instructions of one wave execute in order.
+//
+// Data parallelism inside the kernel (XG): with W ranks (one process per GPU), every step
+// each rank pushes its lane-local gradients as 8-byte {tag = global step + 1, fp32 value}
+// granules, system-scope (write-through), straight into every peer's receive buffer - the
+// peers' buffers are mapped into this process over xGMI with IPC handles.  The receiver
+// polls its own (uncached) buffer until every granule of every peer carries the step's tag
+// (the data IS the flag: no release fence, no separate flag round trip), then sums the W
+// contributions in rank order, so all ranks hold bit-identical averaged gradients and apply
+// identical Adam updates.  Two parity slabs make reuse safe: a rank can only write step s+2
+// into a slab after receiving everyone's step s+1, i.e. after every peer finished reading
+// step s.  Spins are bounded (xg_timeout); a timeout records the step in xg_status and ends
+// the launch on every rank instead of hanging the GPU.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -73,7 +85,71 @@ __device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, flo
   p -= step_size * m * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(v) * rbc2 + eps);
 }
 
-template <int L, int BMAX, int D0, int CM>
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+// One step's gradient exchange; g (KX values per lane) is replaced by the rank average.
+template <int KX>
+__device__ __forceinline__ bool xg_allreduce(float (&g)[KX], const MlpArgs& a, gu64* const (&peer)[XG_MAXW],
+                                             uint32_t gstep, int j) {
+  const int W = a.xg_world, rank = a.xg_rank;
+  const uint32_t tag = gstep + 1u;
+  const size_t slab = (size_t)KX * 64;
+  const size_t par = (size_t)(gstep & 1u) * W;
+  const unsigned long long hi = (unsigned long long)tag << 32;
+#pragma unroll
+  for (int q = 0; q < XG_MAXW; ++q) {
+    if (q < W && q != rank) {
+      gu64* dst = peer[q] + (par + rank) * slab + j;
+#pragma unroll
+      for (int k = 0; k < KX; ++k)
+        __hip_atomic_store(dst + k * 64, hi | __float_as_uint(g[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  float acc[KX];
+#pragma unroll
+  for (int k = 0; k < KX; ++k) acc[k] = 0.f;
+  const gu64* recv = (const gu64*)(a.xg_recv);
+#pragma unroll
+  for (int q = 0; q < XG_MAXW; ++q) {
+    if (q >= W) break;
+    float v[KX];
+    if (q == rank) {
+#pragma unroll
+      for (int k = 0; k < KX; ++k) v[k] = g[k];
+    } else {
+      const gu64* src = recv + (par + q) * slab + j;
+      unsigned long long t_start = 0;
+      for (int spin = 0;; ++spin) {
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < KX; ++k) {
+          const unsigned long long x = __hip_atomic_load(src + k * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          v[k] = __uint_as_float((uint32_t)x);
+          ok &= (uint32_t)(x >> 32) == tag;
+        }
+        if (__all(ok)) break;
+        if (spin == 0) {
+          t_start = __builtin_amdgcn_s_memrealtime();
+        } else if ((spin & 31) == 0 &&
+                   (long long)(__builtin_amdgcn_s_memrealtime() - t_start) > a.xg_timeout) {
+          if (j == 0) __hip_atomic_store(a.xg_status, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KX; ++k) acc[k] += v[k];
+  }
+  const float invw = 1.0f / (float)W;
+#pragma unroll
+  for (int k = 0; k < KX; ++k) g[k] = acc[k] * invw;
+  return true;
+}
+
+// EX: the shape equals the template bounds (d0 == D0, C == CM) -> every guard folds away.
+// XG: in-kernel gradient all-reduce across ranks (train mode, 2 layers).
+template <int L, int BMAX, int D0, int CM, bool EX, bool XG>
 __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
   constexpr int HM = 64;
   constexpr int NPF = (BMAX * D0 + BMAX + 63) / 64;  // prefetch dwords per lane
@@ -81,7 +157,7 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
   __shared__ __attribute__((aligned(16))) float ds[L == 3 ? BMAX * HM : 4];     // dh of the middle layer
   __shared__ __attribute__((aligned(16))) float w1t[L == 3 ? HM * (HM + 4) : 4];  // W1^T (rows padded)
   const int j = threadIdx.x;  // lane = hidden unit
-  const int d0 = sh.d0, H1 = sh.h1, H2 = (L == 3 ? sh.h2 : sh.h1), C = sh.C;
+  const int d0 = EX ? D0 : sh.d0, H1 = sh.h1, H2 = (L == 3 ? sh.h2 : sh.h1), C = EX ? CM : sh.C;
   const bool adam = (a.mode == 0);
   const bool fuse_upd = (!adam) && (a.pending != nullptr);  // apply pending Adam, then grad
   const bool need_mv = adam || fuse_upd;
@@ -229,6 +305,12 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
   const uint32_t drop_thr = (uint32_t)(a.dropout * 4294967296.0);
   const bool prof = (a.prof != nullptr) && j == 0;
   if (prof) a.prof[30] = __builtin_amdgcn_s_memrealtime();
+  gu64* peer[XG_MAXW];
+  if (XG) {
+#pragma unroll
+    for (int q = 0; q < XG_MAXW; ++q) peer[q] = (gu64*)(q < a.xg_world ? a.xg_peers[q] : nullptr);
+  }
+  int done = a.steps;
 
   for (int s = 0; s < a.steps; ++s) {
     const int sb = s + cur0;
@@ -344,7 +426,7 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
     }
     if (j == 0) {
       const float bl = bs > 0 ? lsum * inv : 0.f;
-      if (a.loss_out && !a.cursor) a.loss_out[s] = bl;
+      if (a.loss_out && !a.cursor && !XG) a.loss_out[s] = bl;
       if (!adam) a.grad_out[sh.P] = bl;
     }
 
@@ -421,6 +503,32 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
 #pragma unroll
     for (int b = 0; b < BMAX; ++b) gb0 += dh[b];
 
+    if (XG) {  // average the gradients (and the batch loss) across ranks in-kernel
+      static_assert(!XG || L == 2, "in-kernel all-reduce is implemented for 2-layer nets");
+      constexpr int KX = D0 + CM + 2;
+      float gv[KX];
+#pragma unroll
+      for (int k = 0; k < D0; ++k) gv[k] = gw0[k];
+      gv[D0] = gb0;
+#pragma unroll
+      for (int c = 0; c < CM; ++c) gv[D0 + 1 + c] = gwo[c];
+      const float bl = bs > 0 ? lsum * inv : 0.f;
+      gv[D0 + 1 + CM] = (j < C) ? gbo : (j == 63 ? bl : 0.f);
+      const unsigned long long tx = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+      if (!xg_allreduce<KX>(gv, a, peer, gstep, j)) {
+        done = s;
+        break;
+      }
+      if (prof) a.prof[29] += __builtin_amdgcn_s_memrealtime() - tx;
+#pragma unroll
+      for (int k = 0; k < D0; ++k) gw0[k] = gv[k];
+      gb0 = gv[D0];
+#pragma unroll
+      for (int c = 0; c < CM; ++c) gwo[c] = gv[D0 + 1 + c];
+      gbo = gv[D0 + 1 + CM];
+      const float lavg = rl(gv[D0 + 1 + CM], 63);
+      if (j == 0 && a.loss_out && !a.cursor) a.loss_out[s] = lavg;
+    }
     if (adam) {
       const int t = t0 + s + 1;
       const float step_size = a.lr / (1.f - __powf(a.b1, (float)t));
@@ -475,7 +583,7 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
   }
   if (prof) a.prof[31] = __builtin_amdgcn_s_memrealtime();
   if (a.stage) {  // hand the already-fetched next batch to the next launch
-    const int nb = cur0 + a.steps;
+    const int nb = cur0 + done;
     const bool ok = nb * B < a.n_items;
     if (ok) {
 #pragma unroll
@@ -484,9 +592,9 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
     __builtin_amdgcn_s_waitcnt(0);  // every lane's stage stores complete before the tag
     if (j == 0) __hip_atomic_store(&a.stage[0], ok ? (uint32_t)(nb + 1) : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (a.cursor && j == 0) __hip_atomic_store(a.cursor, cur0 + a.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.cursor && j == 0) __hip_atomic_store(a.cursor, cur0 + done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (a.step_counter && j == 0)
-    __hip_atomic_store(a.step_counter, t0 + a.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.step_counter, t0 + done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (fuse_upd && j == 0) __hip_atomic_store(a.pending, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (!need_mv) return;
   // ---- write back params + moments
@@ -531,17 +639,19 @@ namespace {
 using dct::MlpArgs;
 using dct::WaveShape;
 
-template <int L, int BMAX, int D0, int CM>
+template <int L, int BMAX, int D0, int CM, bool EX, bool XG>
 hipError_t launch_wave(const WaveShape& sh, const MlpArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((dct::mlp_wave_kernel<L, BMAX, D0, CM>), dim3(1), dim3(64), 0, st, sh, a);
+  hipLaunchKernelGGL((dct::mlp_wave_kernel<L, BMAX, D0, CM, EX, XG>), dim3(1), dim3(64), 0, st, sh, a);
   return hipGetLastError();
 }
 
-template <int L, int BMAX>
+template <int L, int BMAX, bool XG>
 hipError_t launch_wave_d0(const WaveShape& sh, const MlpArgs& a, hipStream_t st) {
   if (sh.C > 4) return hipErrorInvalidValue;
-  if (sh.d0 <= 8) return launch_wave<L, BMAX, 8, 4>(sh, a, st);
-  if (sh.d0 <= 16) return launch_wave<L, BMAX, 16, 4>(sh, a, st);
+  if constexpr (L == 2)
+    if (sh.d0 == 5 && sh.C == 2) return launch_wave<L, BMAX, 5, 2, true, XG>(sh, a, st);  // WeatherClassifier
+  if (sh.d0 <= 8) return launch_wave<L, BMAX, 8, 4, false, XG>(sh, a, st);
+  if (sh.d0 <= 16) return launch_wave<L, BMAX, 16, 4, false, XG>(sh, a, st);
   return hipErrorInvalidValue;
 }
 }  // namespace
@@ -555,6 +665,14 @@ int dct_mlp_wave_supported(const int* dims, int L, int B) {
   for (int l = 1; l < L; ++l)
     if (dims[l] > 64) return 0;
   return 1;
+}
+
+// receive-buffer granules per rank per parity for the in-kernel all-reduce (0 = unsupported)
+size_t dct_mlp_xg_slab_granules(const int* dims, int L) {
+  if (L != 2 || !dct_mlp_wave_supported(dims, L, 1)) return 0;
+  const int D0 = (dims[0] == 5 && dims[2] == 2) ? 5 : (dims[0] <= 8 ? 8 : 16);
+  const int CM = (dims[0] == 5 && dims[2] == 2) ? 2 : 4;
+  return (size_t)(D0 + CM + 2) * 64;
 }
 
 int dct_mlp_wave_train(const int* dims, int L, const dct::MlpArgs* a, void* stream) {
@@ -574,8 +692,15 @@ int dct_mlp_wave_train(const int* dims, int L, const dct::MlpArgs* a, void* stre
   }
   sh.P = flat;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (L == 2) return (int)(a->B <= 4 ? launch_wave_d0<2, 4>(sh, *a, st) : launch_wave_d0<2, 8>(sh, *a, st));
-  return (int)(a->B <= 4 ? launch_wave_d0<3, 4>(sh, *a, st) : launch_wave_d0<3, 8>(sh, *a, st));
+  const bool xg = a->xg_world > 1;
+  if (xg) {
+    if (L != 2 || a->mode != 0 || !a->xg_recv || !a->xg_peers || !a->xg_status || a->xg_world > dct::XG_MAXW ||
+        a->xg_rank < 0 || a->xg_rank >= a->xg_world || a->cursor || a->pending)
+      return (int)hipErrorInvalidValue;
+    return (int)(a->B <= 4 ? launch_wave_d0<2, 4, true>(sh, *a, st) : launch_wave_d0<2, 8, true>(sh, *a, st));
+  }
+  if (L == 2) return (int)(a->B <= 4 ? launch_wave_d0<2, 4, false>(sh, *a, st) : launch_wave_d0<2, 8, false>(sh, *a, st));
+  return (int)(a->B <= 4 ? launch_wave_d0<3, 4, false>(sh, *a, st) : launch_wave_d0<3, 8, false>(sh, *a, st));
 }
 
 }  // extern "C"

@@ -215,4 +215,73 @@ size_t StreamGraph::num_nodes() const {
   return n;
 }
 
+// ------------------------------------------------------------------------ PeerExchange
+PeerExchange::PeerExchange(int world, int rank, int64_t bytes) : world_(world), rank_(rank), bytes_(bytes) {
+  if (world < 1 || rank < 0 || rank >= world || bytes <= 0) throw std::invalid_argument("PeerExchange: bad arguments");
+  hip_check(hipExtMallocWithFlags(&recv_, (size_t)bytes, hipDeviceMallocUncached), "hipExtMallocWithFlags(uncached)");
+  hip_check(hipMalloc(reinterpret_cast<void**>(&d_peers_), sizeof(void*) * world), "hipMalloc(peers)");
+  hip_check(hipMalloc(reinterpret_cast<void**>(&status_), 64), "hipMalloc(status)");
+  hip_check(hipMemset(recv_, 0, (size_t)bytes), "hipMemset(recv)");
+  hip_check(hipMemset(status_, 0, 64), "hipMemset(status)");
+  std::vector<void*> self(world, nullptr);
+  self[rank] = recv_;
+  upload(self);
+}
+
+PeerExchange::~PeerExchange() {
+  hipDeviceSynchronize();
+  for (void* p : opened_) hipIpcCloseMemHandle(p);
+  if (recv_) hipFree(recv_);
+  if (d_peers_) hipFree(d_peers_);
+  if (status_) hipFree(status_);
+}
+
+void PeerExchange::upload(const std::vector<void*>& ptrs) {
+  hip_check(hipMemcpy(d_peers_, ptrs.data(), sizeof(void*) * world_, hipMemcpyHostToDevice), "hipMemcpy(peers)");
+}
+
+std::string PeerExchange::ipc_handle() const {
+  hipIpcMemHandle_t h;
+  hip_check(hipIpcGetMemHandle(&h, recv_), "hipIpcGetMemHandle");
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void PeerExchange::open_peers(const std::vector<std::string>& handles) {
+  if ((int)handles.size() != world_) throw std::invalid_argument("PeerExchange: need one handle per rank");
+  std::vector<void*> ptrs(world_, nullptr);
+  for (int q = 0; q < world_; ++q) {
+    if (q == rank_) {
+      ptrs[q] = recv_;
+      continue;
+    }
+    if (handles[q].size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("PeerExchange: bad handle");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handles[q].data(), sizeof(h));
+    void* p = nullptr;
+    hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    opened_.push_back(p);
+    ptrs[q] = p;
+  }
+  upload(ptrs);
+}
+
+void PeerExchange::set_peers(const std::vector<uintptr_t>& addrs) {
+  if ((int)addrs.size() != world_) throw std::invalid_argument("PeerExchange: need one address per rank");
+  std::vector<void*> ptrs(world_);
+  for (int q = 0; q < world_; ++q) ptrs[q] = reinterpret_cast<void*>(addrs[q]);
+  upload(ptrs);
+}
+
+unsigned int PeerExchange::read_status() const {
+  unsigned int v = 0;
+  hip_check(hipMemcpy(&v, status_, sizeof(v), hipMemcpyDeviceToHost), "hipMemcpy(status)");
+  return v;
+}
+
+void PeerExchange::reset(uintptr_t stream) {
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hip_check(hipMemsetAsync(recv_, 0, (size_t)bytes_, st), "hipMemsetAsync(recv)");
+  hip_check(hipMemsetAsync(status_, 0, 64, st), "hipMemsetAsync(status)");
+}
+
 }  // namespace dct

@@ -56,6 +56,38 @@ class BucketReducer {
   hipEvent_t done_event_ = nullptr;
 };
 
+// Receive buffers of the in-kernel (xGMI) gradient exchange.  Each rank allocates an
+// UNCACHED device buffer (remote xGMI writes land in HBM, the local poll must not hit a stale
+// L2 line), exports it as an IPC handle, and maps every peer's buffer into its own address
+// space; `peers()` is a device array of the W buffer addresses, indexed by rank.
+class PeerExchange {
+ public:
+  PeerExchange(int world, int rank, int64_t bytes);
+  ~PeerExchange();
+  PeerExchange(const PeerExchange&) = delete;
+  PeerExchange& operator=(const PeerExchange&) = delete;
+  std::string ipc_handle() const;                          // this rank's buffer
+  void open_peers(const std::vector<std::string>& handles);  // all ranks' handles, rank order
+  void set_peers(const std::vector<uintptr_t>& ptrs);        // same process (tests): raw addresses
+  void reset(uintptr_t stream);                              // zero receive buffer + status
+  unsigned int read_status() const;                          // synchronous D2H of status[0]
+  uintptr_t recv() const { return reinterpret_cast<uintptr_t>(recv_); }
+  uintptr_t peers() const { return reinterpret_cast<uintptr_t>(d_peers_); }
+  uintptr_t status() const { return reinterpret_cast<uintptr_t>(status_); }
+  int64_t bytes() const { return bytes_; }
+  int world() const { return world_; }
+  int rank() const { return rank_; }
+
+ private:
+  void upload(const std::vector<void*>& ptrs);
+  int world_, rank_;
+  int64_t bytes_;
+  void* recv_ = nullptr;
+  void** d_peers_ = nullptr;
+  unsigned int* status_ = nullptr;
+  std::vector<void*> opened_;
+};
+
 class StreamGraph {
  public:
   StreamGraph() = default;

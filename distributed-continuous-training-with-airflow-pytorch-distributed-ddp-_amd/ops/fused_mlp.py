@@ -99,8 +99,11 @@ class FusedMLPKernel:
               loss: str = "ce", grad_out: Optional[torch.Tensor] = None, step_counter: Optional[torch.Tensor] = None,
               cursor: Optional[torch.Tensor] = None, prof: Optional[torch.Tensor] = None,
               pending: Optional[torch.Tensor] = None, stage: Optional[torch.Tensor] = None,
-              stream: Optional[int] = None):
-        """Run ``steps`` fused optimizer steps (mode 0) or one gradient step (grad_out given)."""
+              stream: Optional[int] = None, xg=None, xg_timeout_s: float = 2.0):
+        """Run ``steps`` fused optimizer steps (mode 0) or one gradient step (grad_out given).
+
+        ``xg``: a native ``PeerExchange`` -> data-parallel steps with the gradient all-reduce done
+        inside the kernel over peer-mapped receive buffers (see ``parallel.xgmi``)."""
         mode = 1 if grad_out is not None else 0
         need_mv = mode == 0 or pending is not None
         self._check_params(p, m if need_mv else None, v if need_mv else None)
@@ -124,6 +127,15 @@ class FusedMLPKernel:
         if loss_out is not None and not (loss_out.is_cuda and loss_out.dtype == torch.float32
                                          and loss_out.numel() >= steps):
             raise ValueError("loss_out must be cuda fp32 [steps]")
+        xg_args = {}
+        if xg is not None and xg.world > 1:
+            if mode != 0 or cursor is not None or pending is not None or not self.xg_supported(batch):
+                raise ValueError("in-kernel all-reduce needs train mode on the single-wave 2-layer kernel")
+            need = 2 * xg.world * self.xg_slab_granules() * 8
+            if xg.bytes < need:
+                raise ValueError(f"exchange buffer too small ({xg.bytes} < {need} bytes)")
+            xg_args = dict(xg_recv=xg.recv, xg_peers=xg.peers, xg_world=xg.world, xg_rank=xg.rank,
+                           xg_status=xg.status, xg_timeout=int(xg_timeout_s * 1e8))
         self.plan.train(
             ptr(p), ptr(m) if need_mv else 0, ptr(v) if need_mv else 0, ptr(grad_out),
             ptr(X), X.stride(0), ptr(Y), ptr(idx), int(n_items), int(batch), int(steps), int(t0),
@@ -132,7 +144,20 @@ class FusedMLPKernel:
             ptr(step_counter), ptr(cursor), ptr(prof), ptr(pending),
             ptr(stage) if (stage is not None and self.plan.use_wave) else 0,
             stream if stream is not None else stream_handle(),
+            **xg_args,
         )
+
+    # ------------------------------------------------------------ in-kernel all-reduce
+    def xg_slab_granules(self) -> int:
+        """8-byte granules per (parity, source rank) slab of the exchange buffer (0 = unsupported)."""
+        return int(native().mlp_xg_slab_granules(list(self.dims)))
+
+    def xg_supported(self, batch: int) -> bool:
+        return (len(self.dims) == 3 and self.plan.use_wave and self.xg_slab_granules() > 0
+                and 1 <= batch <= min(self.bmax, 8))
+
+    def xg_buffer_bytes(self, world: int) -> int:
+        return 2 * world * self.xg_slab_granules() * 8
 
     def evaluate(self, p, X, Y, idx, n_items: int, acc_out: torch.Tensor, loss: str = "ce",
                  logits_out: Optional[torch.Tensor] = None, grid: Optional[int] = None,

@@ -64,12 +64,22 @@ class DistContext:
 
     def all_reduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
         if self.is_distributed:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            if self.backend == "gloo" and t.is_cuda:  # gloo control plane: stage through host memory
+                x = t.cpu()
+                dist.all_reduce(x, op=dist.ReduceOp.SUM)
+                t.copy_(x)
+            else:
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return t
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.is_distributed:
-            dist.broadcast(t, src=src)
+            if self.backend == "gloo" and t.is_cuda:
+                x = t.cpu()
+                dist.broadcast(x, src=src)
+                t.copy_(x)
+            else:
+                dist.broadcast(t, src=src)
         return t
 
     def broadcast_object(self, obj, src: int = 0):
@@ -78,6 +88,20 @@ class DistContext:
         lst = [obj]
         dist.broadcast_object_list(lst, src=src, device=self.device if self.backend == "nccl" else None)
         return lst[0]
+
+    def all_gather_object(self, obj) -> list:
+        if not self.is_distributed:
+            return [obj]
+        out = [None] * self.world_size
+        dist.all_gather_object(out, obj)
+        return out
+
+    def all_reduce_max_int(self, value: int) -> int:
+        if not self.is_distributed:
+            return int(value)
+        t = torch.tensor([int(value)], dtype=torch.int64, device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return int(t.item())
 
     def all_reduce_bool_and(self, flag: bool) -> bool:
         if not self.is_distributed:
@@ -119,6 +143,11 @@ def init_distributed(accelerator: str = "auto", backend: str = "auto", timeout_s
         device = torch.device("cpu")
     if backend == "auto":
         backend = "nccl" if use_gpu else "gloo"
+        if use_gpu and e["world_size"] > 1 and e["local_world_size"] > torch.cuda.device_count():
+            # more ranks than devices on this node (rehearsals on a 1-GPU box): RCCL refuses two
+            # ranks on one device, so the control plane runs on gloo and data-parallel gradient
+            # exchange must go through the in-kernel xGMI/IPC path (parallel/xgmi.py)
+            backend = "gloo"
     ctx = DistContext(world_size=e["world_size"], rank=e["rank"], local_rank=e["local_rank"],
                       local_world_size=e["local_world_size"], node_rank=e["node_rank"], backend=backend,
                       device=device)

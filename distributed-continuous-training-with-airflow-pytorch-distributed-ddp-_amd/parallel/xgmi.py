@@ -1,0 +1,88 @@
+"""In-kernel data-parallel gradient all-reduce over xGMI peer mappings.
+
+Why: the reference's DDP step (jobs/train_lightning_ddp.py:136 -> torch Reducer -> one 2,056-byte
+bucket all-reduce + the 4-byte ``sync_dist`` loss all-reduce per step) is pure
+latency.  On MI355X a per-step RCCL collective costs more than the whole fused step itself (two
+kernel boundaries + the collective's own launch and protocol), so for the models the single-wave
+kernel trains (2-layer MLPs, widths <= 64) the gradient exchange moves INTO the persistent kernel:
+
+* every rank allocates an uncached receive buffer ``[2 parity][W src][KX][64 lanes]`` of 8-byte
+  granules and exports it with ``hipIpcGetMemHandle`` (dmabuf); the W handles are exchanged over
+  the c10d process group and each rank maps its peers' buffers (``hipIpcOpenMemHandle``, xGMI
+  peer access) - one node, up to 8 GPUs, fully connected by xGMI;
+* per step each rank writes {tag = step + 1, fp32 gradient} granules straight into every peer's
+  buffer (write-through system-scope stores), then polls its own buffer until all peers' tags
+  match and sums the contributions in rank order (bit-identical on all ranks; the loss rides in
+  the same granules, so the logged ``train_loss`` is the cross-rank mean like ``sync_dist``);
+* no kernel boundary, no host round trip, no RCCL launch per step; RCCL remains the path for
+  everything else (initial broadcast, validation metrics, the autograd engine's bucketed reducer).
+
+Selection: ``DCT_ALLREDUCE=auto`` (default: use it when the model/batch qualify, all ranks are on
+one node and every rank could map every peer), ``xgmi`` (required: raise if unavailable) or
+``rccl`` (never).  Failures are detected collectively: a bounded spin records a timeout in the
+status word; :func:`check` max-reduces it over ranks so every rank takes the same decision.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+from .dist import DistContext
+
+
+def mode() -> str:
+    m = os.environ.get("DCT_ALLREDUCE", "auto").lower()
+    if m not in ("auto", "xgmi", "rccl"):
+        raise ValueError(f"DCT_ALLREDUCE must be auto|xgmi|rccl, got {m!r}")
+    return m
+
+
+def timeout_s() -> float:
+    return float(os.environ.get("DCT_XG_TIMEOUT_S", "20"))
+
+
+def setup_peer_exchange(kernel, ctx: DistContext, batch: int):
+    """Collective: returns a native PeerExchange on every rank, or None on every rank."""
+    m = mode()
+    W = ctx.world_size
+    single_node = ctx.local_world_size == W
+    eligible = (m != "rccl" and ctx.device.type == "cuda" and 2 <= W <= 8 and single_node
+                and kernel.xg_supported(batch))
+    # every rank must take the same decision before any collective below diverges
+    if not ctx.all_reduce_bool_and(eligible):
+        if m == "xgmi":
+            raise RuntimeError("DCT_ALLREDUCE=xgmi but the in-kernel all-reduce is not applicable "
+                               f"(world {W}, single node {single_node}, dims {kernel.dims}, batch {batch})")
+        return None
+    from ..ops._native import native
+
+    xg, handle, err = None, b"", None
+    try:
+        xg = native().PeerExchange(W, ctx.rank, kernel.xg_buffer_bytes(W))
+        handle = xg.ipc_handle()
+    except Exception as e:  # noqa: BLE001
+        err = e
+    handles = ctx.all_gather_object(handle)
+    if err is None and all(handles):
+        try:
+            xg.open_peers(handles)
+        except Exception as e:  # noqa: BLE001
+            err = e
+    ok = ctx.all_reduce_bool_and(err is None)
+    if not ok:
+        if m == "xgmi":
+            raise RuntimeError(f"in-kernel all-reduce setup failed on some rank (this rank: {err!r})")
+        if ctx.rank == 0:
+            print(f"[dct] xGMI peer exchange unavailable ({err!r}); using RCCL per step", flush=True)
+        return None
+    return xg
+
+
+def status(xg) -> int:
+    """This rank's exchange status word (0 = ok, else the step + 1 that timed out); syncs."""
+    return int(xg.read_status())
+
+
+def check(xg, ctx: DistContext) -> int:
+    """Collective: max over ranks of the status word (0 = every exchange completed)."""
+    return ctx.all_reduce_max_int(status(xg))

@@ -6,7 +6,10 @@
   csrc/mlp_fused.hip with the dataset resident in HBM and batches gathered on device.
     - world size 1: ONE persistent launch runs every step of an epoch (weights in LDS, Adam
       moments in VGPRs, nothing but the batch rows touches HBM per step).
-    - world size > 1: per step {fused fwd+bwd (grads + loss -> one flat buffer), RCCL
+    - world size > 1, 2-layer nets of the single-wave kernel (the reference model): the same
+      persistent launch, with the DDP gradient average done INSIDE the kernel over xGMI peer
+      mappings (parallel/xgmi.py) - one launch per rank per epoch, no per-step collective.
+    - other world size > 1 cases: per step {fused fwd+bwd (grads + loss -> one flat buffer), RCCL
       ncclAvg all-reduce of that buffer (gradients AND the sync_dist train_loss in ONE
       collective: X5+X6 of SURVEY §2.6), fused flat Adam}; the epoch's step loop is captured
       once into a HIP graph and replayed every epoch (the Adam step count and dropout stream
@@ -107,7 +110,7 @@ class FusedMLPEngine(_EngineBase):
         self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
         self.graph_used = False
         if ctx.is_distributed:
-            self.comm = init_native_comm(ctx)
+            self.comm = init_native_comm(ctx) if ctx.backend == "nccl" else None
         elif self.ddp:
             from ..ops._native import native
 
@@ -116,6 +119,15 @@ class FusedMLPEngine(_EngineBase):
         if self.ddp:
             self.gbuf = torch.zeros(self.P + 1, dtype=torch.float32, device=dev)
             self._broadcast_params()
+        self.xg = None  # in-kernel xGMI all-reduce (parallel/xgmi.py)
+        if ctx.is_distributed:
+            from ..parallel.xgmi import setup_peer_exchange, timeout_s
+
+            self.xg = setup_peer_exchange(self.kernel, ctx, self.B)
+            self.xg_timeout_s = timeout_s()
+            if self.xg is None and self.comm is None:
+                raise RuntimeError("distributed fused engine needs RCCL (backend nccl) or the in-kernel "
+                                   "xGMI exchange; neither is available")
 
     # ------------------------------------------------------------------ params
     def _linear_params(self):
@@ -128,6 +140,9 @@ class FusedMLPEngine(_EngineBase):
         return torch.cat([t.detach().float().reshape(-1).cpu() for t in self._linear_params()])
 
     def _broadcast_params(self):
+        if self.comm is None:  # gloo control plane (ranks sharing a device)
+            self.ctx.broadcast_(self.p, src=0)
+            return
         from ..ops._native import native
 
         nat = native()
@@ -162,6 +177,12 @@ class FusedMLPEngine(_EngineBase):
         fa.load_state_dict(sd)
         self.global_step = global_step
         self.step_counter.fill_(int(fa.step_count))
+        if self.xg is not None:  # exchange tags derive from the step counter: drop stale granules
+            torch.cuda.synchronize(self.device)
+            self.ctx.barrier()
+            self.xg.reset(torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize(self.device)
+            self.ctx.barrier()
 
     # ------------------------------------------------------------------ data
     def attach_data(self, X: torch.Tensor, Y: torch.Tensor, train_rows: torch.Tensor, val_rows: torch.Tensor):
@@ -199,27 +220,36 @@ class FusedMLPEngine(_EngineBase):
         self.kernel.train(self.p, self.m, self.v, self.X, self.Y, self.idx[idx_off:], n_items=n_items,
                           batch=self.B, steps=steps, t0=0, lr=a["lr"], betas=a["betas"], eps=a["eps"],
                           weight_decay=a["weight_decay"], dropout=self.dropout, seed=self.rank_seed,
-                          loss_out=loss_out, loss=self.loss, step_counter=self.step_counter)
+                          loss_out=loss_out, loss=self.loss, step_counter=self.step_counter,
+                          xg=self.xg, xg_timeout_s=getattr(self, "xg_timeout_s", 20.0))
+
+    @property
+    def step_mode(self) -> str:
+        if self.xg is not None:
+            return "fused-persistent+xgmi-inkernel-allreduce"
+        if not self.ddp:
+            return "fused-persistent"
+        return "fused-step+rccl" + ("+graph" if self.use_graph else "")
 
     def run_steps(self, n_items: int, steps: int, loss_out: torch.Tensor, first_step: int = 0):
         """Enqueue ``steps`` optimizer steps over batches [first_step, first_step+steps) of self.idx.
 
-        Single rank: persistent launches write loss_out[0:steps].  DDP: loss_out is indexed by the
-        absolute batch index (loss_out[first_step + s]) and must hold first_step + steps entries.
-        No host synchronisation either way."""
+        loss_out is indexed by the absolute batch index (loss_out[first_step + s]) and must hold
+        first_step + steps entries (with DDP: the cross-rank mean loss).  No host synchronisation."""
         if steps <= 0:
             return
-        if not self.ddp:
+        if (first_step + steps - 1) * self.B >= n_items or loss_out.numel() < first_step + steps:
+            raise ValueError("step range exceeds the epoch's batches / loss buffer")
+        if not self.ddp or self.xg is not None:
             chunk = self.steps_per_launch or steps
             s = 0
             while s < steps:
                 k = min(chunk, steps - s)
-                off = (first_step + s) * self.B
-                self._launch_persistent(n_items - off, k, loss_out[s: s + k], idx_off=off)
+                b = first_step + s
+                off = b * self.B
+                self._launch_persistent(n_items - off, k, loss_out[b: b + k], idx_off=off)
                 s += k
             return
-        if (first_step + steps - 1) * self.B >= n_items or loss_out.numel() < first_step + steps:
-            raise ValueError("DDP step range exceeds the epoch's batches / loss buffer")
         self.cursor.fill_(first_step)
         C = min(self.graph_chunk, steps)
         full, rem = divmod(steps, C)
@@ -310,9 +340,38 @@ class FusedMLPEngine(_EngineBase):
         loss_out = getattr(self, "_loss_buf", None)
         if loss_out is None or loss_out.numel() < steps:
             self._loss_buf = loss_out = torch.zeros(max(1, steps), dtype=torch.float32, device=self.device)
+        if self.xg is not None:
+            torch.cuda.synchronize(self.device)
+            self.ctx.barrier()  # start the epoch's kernels together (the exchange spins are bounded)
         self.run_steps(n_items, steps, loss_out[:steps])
+        if self.xg is not None:
+            self.xg_verify(fallback=False)
         self.global_step += steps
         return loss_out[:steps]
+
+    def xg_verify(self, fallback: bool) -> bool:
+        """Collective check of the in-kernel exchange.  On a timeout either raise (training: the
+        steps of that launch are incomplete) or, with ``fallback``, re-sync every rank from rank 0
+        and continue on the RCCL step path (benchmarks)."""
+        if self.xg is None:
+            return True
+        from ..parallel.xgmi import check
+
+        st = check(self.xg, self.ctx)
+        if st == 0:
+            return True
+        msg = f"in-kernel xGMI all-reduce timed out (step tag {st})"
+        if not fallback:
+            raise RuntimeError(msg)
+        if self.ctx.rank == 0:
+            print(f"[dct] {msg}; re-syncing from rank 0 and falling back to RCCL", flush=True)
+        self.xg = None
+        if self.comm is None:
+            raise RuntimeError(msg + " and no RCCL communicator is available to fall back to")
+        for t in (self.p, self.m, self.v, self.step_counter):
+            self.ctx.broadcast_(t, src=0)
+        torch.cuda.synchronize(self.device)
+        return False
 
     # ------------------------------------------------------------------ eval
     def validate(self, rows: Optional[torch.Tensor] = None, limit: Optional[int] = None) -> Tuple[float, float]:

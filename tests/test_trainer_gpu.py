@@ -100,12 +100,8 @@ def test_ddp_step_path_world1_matches_persistent(fused_update, graph, monkeypatc
         eng.attach_data(x, y, rows[:2400], rows[2400:])
         n = eng.upload_epoch_indices(0)
         loss = torch.zeros(64, device=ctx.device)
-        if eng.ddp:
-            eng.run_steps(n, 30, loss, first_step=0)
-            eng.run_steps(n, 23, loss, first_step=30)
-        else:
-            eng.run_steps(n, 30, loss[:30], first_step=0)
-            eng.run_steps(n, 23, loss[30:53], first_step=30)
+        eng.run_steps(n, 30, loss, first_step=0)
+        eng.run_steps(n, 23, loss, first_step=30)
         torch.cuda.synchronize()
         assert int(eng.step_counter.item()) == 53
         return eng.p.cpu(), eng.m.cpu(), loss[:53].cpu(), eng

@@ -1,0 +1,139 @@
+"""In-kernel data-parallel all-reduce (parallel/xgmi.py, csrc/mlp_wave.hip XG path).
+
+Reference semantics: DDP averages every rank's gradients before an identical Adam step on each
+rank (jobs/train_lightning_ddp.py:136), and ``sync_dist`` logs the mean loss.
+Checked against a plain-torch fp32 emulation of W ranks (sum of per-rank grads in rank order / W,
+then torch Adam)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import dct_amd  # noqa: F401
+from dct_amd.data.sampler import distributed_indices
+from dct_amd.data.synthetic import weather_tensors
+from dct_amd.ops._native import native
+from dct_amd.ops.fused_mlp import FusedMLPKernel
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _net(seed=0):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Linear(5, 64), torch.nn.ReLU(), torch.nn.Linear(64, 2))
+
+
+def _flat(net):
+    return torch.cat([t.detach().reshape(-1) for t in net.state_dict().values()])
+
+
+def ddp_reference(net, X, Y, shards, B, steps, lr=0.01):
+    """W-rank DDP emulation: per-rank CE grads, rank-ordered sum / W, one torch Adam step."""
+    opt = torch.optim.Adam(net.parameters(), lr=lr)
+    params = list(net.parameters())
+    losses = []
+    for s in range(steps):
+        gsum = [torch.zeros_like(p) for p in params]
+        lsum = 0.0
+        for r, sh in enumerate(shards):
+            rows = sh[s * B:(s + 1) * B]
+            loss = F.cross_entropy(net(X[rows]), Y[rows])
+            gs = torch.autograd.grad(loss, params)
+            for a, g in zip(gsum, gs):
+                a += g
+            lsum += loss.item()
+        for p, g in zip(params, gsum):
+            p.grad = g / len(shards)
+        opt.step()
+        losses.append(lsum / len(shards))
+    return _flat(net), torch.tensor(losses)
+
+
+@pytest.mark.parametrize("W", [2])
+def test_in_process_exchange_matches_ddp_reference(W, cuda):
+    """W 'ranks' as concurrent single-wave kernels on W streams of one GPU, peers = raw pointers.
+    (W = 2 only: streams of one process share GPU_MAX_HW_QUEUES hardware queues, so more
+    in-process ranks may be serialised behind each other; W > 2 runs as processes below.)"""
+    nat = native()
+    B, steps = 4, 120
+    kern = FusedMLPKernel([5, 64, 2], bmax=4)
+    assert kern.xg_supported(B)
+    xs = [nat.PeerExchange(W, r, kern.xg_buffer_bytes(W)) for r in range(W)]
+    for x in xs:
+        x.set_peers([y.recv for y in xs])
+    X, Y = weather_tensors(3000, seed=5)
+    shards = [distributed_indices(3000, W, r, shuffle=True, seed=42, epoch=0) for r in range(W)]
+    net = _net(1)
+    p0 = _flat(net)
+    ps = [p0.clone().to(cuda) for _ in range(W)]
+    ms = [torch.zeros_like(ps[0]) for _ in range(W)]
+    vs = [torch.zeros_like(ps[0]) for _ in range(W)]
+    losses = [torch.zeros(steps, device=cuda) for _ in range(W)]
+    scs = [torch.zeros(1, dtype=torch.int32, device=cuda) for _ in range(W)]
+    Xd, Yd = X.to(cuda), Y.to(cuda, torch.int32)
+    idx = [s.to(cuda, torch.int32) for s in shards]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(cuda) for _ in range(W)]
+    for r in range(W):
+        kern.train(ps[r], ms[r], vs[r], Xd, Yd, idx[r], n_items=idx[r].numel(), batch=B, steps=steps, t0=0,
+                   lr=0.01, loss_out=losses[r], step_counter=scs[r], xg=xs[r], xg_timeout_s=5.0,
+                   stream=streams[r].cuda_stream)
+    torch.cuda.synchronize()
+    assert [x.read_status() for x in xs] == [0] * W
+    assert all(int(sc.item()) == steps for sc in scs)
+    for r in range(1, W):  # bit-identical replicas, identical synced losses
+        assert torch.equal(ps[r], ps[0])
+        assert torch.equal(losses[r], losses[0])
+    want, want_l = ddp_reference(net, X, Y, shards, B, steps)
+    err = (ps[0].cpu() - want).abs()
+    assert err.median() < 1e-5 and err.max() < 2e-3, (err.median(), err.max())
+    assert torch.allclose(losses[0].cpu(), want_l, atol=2e-4, rtol=1e-3)
+
+
+def test_exchange_timeout_is_bounded_and_reported(cuda):
+    """A rank whose peer never runs must give up after the timeout, flag it, and exit."""
+    nat = native()
+    kern = FusedMLPKernel([5, 64, 2], bmax=4)
+    xs = [nat.PeerExchange(2, r, kern.xg_buffer_bytes(2)) for r in range(2)]
+    for x in xs:
+        x.set_peers([y.recv for y in xs])
+    X, Y = weather_tensors(500, seed=0)
+    p = _flat(_net()).to(cuda)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    sc = torch.zeros(1, dtype=torch.int32, device=cuda)
+    idx = torch.arange(400, dtype=torch.int32, device=cuda)
+    kern.train(p, m, v, X.to(cuda), Y.to(cuda, torch.int32), idx, n_items=400, batch=4, steps=50, t0=0, lr=0.01,
+               step_counter=sc, xg=xs[0], xg_timeout_s=0.2)
+    torch.cuda.synchronize()
+    assert xs[0].read_status() == 1  # tag of step 0
+    assert int(sc.item()) == 0  # no step was applied
+    assert torch.equal(p.cpu(), _flat(_net()))
+
+
+@pytest.mark.parametrize("W", [2, 4])
+def test_multi_process_ipc_exchange(W, tmp_path, cuda):
+    """Real IPC path: W processes, receive buffers exported/imported with hipIpc handles."""
+    out = tmp_path / "xg.json"
+    steps, B = 80, 4
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={W}",
+                        "--master-addr=127.0.0.1", f"--master-port={29561 + W}",
+                        os.path.join(ROOT, "tests", "xg_worker.py"), str(out), str(steps), str(B)],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    assert res["status"] == 0 and res["step_counter"] == steps
+    ps = [torch.tensor(p) for p in res["params"]]
+    p0 = ps[0]
+    assert all(torch.equal(p, p0) for p in ps)
+    X, Y = weather_tensors(4000, seed=3)
+    shards = [distributed_indices(4000, W, r, shuffle=True, seed=42, epoch=0) for r in range(W)]
+    want, want_l = ddp_reference(_net(0), X, Y, shards, B, steps)
+    err = (p0 - want).abs()
+    assert err.median() < 1e-5 and err.max() < 2e-3, (err.median(), err.max())
+    assert torch.allclose(torch.tensor(res["losses"][0]), want_l, atol=2e-4, rtol=1e-3)

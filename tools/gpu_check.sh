@@ -21,6 +21,11 @@ for s in $STEPS; do
     pytest) run pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ;;
     bench) run bench_weather 300 python bench.py
            run bench_3x128 300 python bench.py --model weather-mlp-3x128 ;;
+    xgtest) run pytest_xgmi 600 python -m pytest tests/test_xgmi_gpu.py -q -rf -x ;;
+    xgbench2) run bench_dp2_shared 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 \
+                  --master-addr=127.0.0.1 --master-port=29571 bench.py --gpus 2 --steps 20000 --warmup 2000 ;;
+    xgbench4) run bench_dp4_shared 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=4 \
+                  --master-addr=127.0.0.1 --master-port=29572 bench.py --gpus 4 --steps 20000 --warmup 2000 ;;
     prof) export TMPDIR=/tmp
           run prof_weather 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_weather -o run --output-format csv -- python3 bench.py --steps 5000 --warmup 500 ;;
     *) run "$s" 900 bash -c "$s" ;;
