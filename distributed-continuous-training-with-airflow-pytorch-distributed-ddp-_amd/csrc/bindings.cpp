@@ -83,7 +83,7 @@ PYBIND11_MODULE(_dct_native, m) {
              float eps, float wd, float dropout, uint32_t seed, uint32_t step_base, uintptr_t loss_out, int mode,
              int loss_kind, uintptr_t step_counter, uintptr_t cursor, uintptr_t prof, uintptr_t pending,
              uintptr_t stage, uintptr_t stream, uintptr_t xg_recv, uintptr_t xg_peers, int xg_world, int xg_rank,
-             uintptr_t xg_status, int64_t xg_timeout) {
+             uintptr_t xg_status, int64_t xg_timeout, int xg_poll) {
             if (!plan.supported) throw std::runtime_error("MLP too large for the fused kernel");
             if (steps < 1 || n_items < 1 || B < 1) throw std::invalid_argument("empty launch");
             if (!cursor && (int64_t)(steps - 1) * B >= n_items) throw std::invalid_argument("more steps than batches");
@@ -118,6 +118,7 @@ PYBIND11_MODULE(_dct_native, m) {
             a.xg_rank = xg_rank;
             a.xg_status = P<unsigned int>(xg_status);
             a.xg_timeout = xg_timeout;
+            a.xg_poll = xg_poll;
             if (xg_world > 1 && !(plan.use_wave && dct_mlp_wave_supported(plan.sh()->dims, plan.sh()->L, B)))
               throw std::invalid_argument("in-kernel all-reduce needs the single-wave kernel");
             if (pending && (mode != 1 || !plan.use_wave || !mo || !vo))
@@ -137,7 +138,7 @@ PYBIND11_MODULE(_dct_native, m) {
           py::arg("step_base"), py::arg("loss_out"), py::arg("mode"), py::arg("loss_kind"), py::arg("step_counter"),
           py::arg("cursor"), py::arg("prof") = 0, py::arg("pending") = 0, py::arg("stage") = 0,
           py::arg("stream") = 0, py::arg("xg_recv") = 0, py::arg("xg_peers") = 0, py::arg("xg_world") = 0,
-          py::arg("xg_rank") = 0, py::arg("xg_status") = 0, py::arg("xg_timeout") = 200000000LL)
+          py::arg("xg_rank") = 0, py::arg("xg_status") = 0, py::arg("xg_timeout") = 200000000LL, py::arg("xg_poll") = 0)
       .def(
           "eval",
           [](const MlpPlan& plan, uintptr_t p, uintptr_t X, int ldx, uintptr_t Y, uintptr_t idx, int n_items,

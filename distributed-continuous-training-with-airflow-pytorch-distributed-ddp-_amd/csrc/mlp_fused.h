@@ -98,6 +98,7 @@ struct MlpArgs {
   int xg_rank;
   unsigned int* xg_status;                  // [0]: 0 ok, else (global step + 1) of a timeout
   long long xg_timeout;                     // spin limit in s_memrealtime ticks (100 MHz)
+  int xg_poll;                              // 0 full sweeps, 1 probe-then-sweep, 2 sequential
 };
 
 constexpr int XG_MAXW = 8;  // ranks of the in-kernel exchange (one node)

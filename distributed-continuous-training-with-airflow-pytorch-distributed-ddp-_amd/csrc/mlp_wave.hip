@@ -85,61 +85,103 @@ __device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, flo
   p -= step_size * m * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(v) * rbc2 + eps);
 }
 
-typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef unsigned int xg_v4u __attribute__((ext_vector_type(4)));
+constexpr int XG_SYS = 17;  // buffer aux bits: sc0 | sc1 = system scope (write-through, no stale L2 hit)
 
-// One step's gradient exchange; g (KX values per lane) is replaced by the rank average.
-template <int KX>
-__device__ __forceinline__ bool xg_allreduce(float (&g)[KX], const MlpArgs& a, gu64* const (&peer)[XG_MAXW],
+// One step's gradient exchange; g (KX values per lane, KX even) is replaced by the rank average.
+// Granule layout per (parity, source): [KX/2][64 lanes] x 16 B = two {value, tag} granules, so
+// every store / load instruction moves one contiguous KB.  Pushes are 16-B system-scope stores;
+// each 8-B half is tag-checked on its own, so a split 16-B write can never be mistaken for a
+// complete one.  The poll sweeps ALL sources per pass (one round trip per pass, not per peer).
+template <int KX, int XW>
+__device__ __forceinline__ bool xg_allreduce(float (&g)[KX], const MlpArgs& a,
+                                             const __amdgpu_buffer_rsrc_t (&prs)[XW], __amdgpu_buffer_rsrc_t rrs,
                                              uint32_t gstep, int j) {
+  static_assert(KX % 2 == 0, "granule pairs");
+  constexpr int K2 = KX / 2;
   const int W = a.xg_world, rank = a.xg_rank;
   const uint32_t tag = gstep + 1u;
-  const size_t slab = (size_t)KX * 64;
-  const size_t par = (size_t)(gstep & 1u) * W;
-  const unsigned long long hi = (unsigned long long)tag << 32;
+  const int par = (int)(gstep & 1u) * W;
 #pragma unroll
-  for (int q = 0; q < XG_MAXW; ++q) {
+  for (int q = 0; q < XW; ++q) {
     if (q < W && q != rank) {
-      gu64* dst = peer[q] + (par + rank) * slab + j;
+      const int base = ((par + rank) * K2 * 64 + j) * 16;
 #pragma unroll
-      for (int k = 0; k < KX; ++k)
-        __hip_atomic_store(dst + k * 64, hi | __float_as_uint(g[k]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      for (int k2 = 0; k2 < K2; ++k2) {
+        xg_v4u d;
+        d.x = __float_as_uint(g[2 * k2]);
+        d.y = tag;
+        d.z = __float_as_uint(g[2 * k2 + 1]);
+        d.w = tag;
+        __builtin_amdgcn_raw_buffer_store_b128(d, prs[q], base + k2 * 64 * 16, 0, XG_SYS);
+      }
+    }
+  }
+  float v[XW][KX];
+  unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  int spin = 0;
+  auto timed_out = [&]() -> bool {
+    if ((++spin & 15) == 0 && (long long)(__builtin_amdgcn_s_memrealtime() - t_start) > a.xg_timeout) {
+      if (j == 0) __hip_atomic_store(a.xg_status, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return true;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    return false;
+  };
+  // load every granule pair of source q into v[q]; true when all carry this step's tag
+  auto load_src = [&](int q, float (&vq)[KX]) -> bool {
+    const int qq = q < W ? q : 0;
+    const int base = ((par + qq) * K2 * 64 + j) * 16;
+    bool okq = true;
+#pragma unroll
+    for (int k2 = 0; k2 < K2; ++k2) {
+      const xg_v4u d = __builtin_amdgcn_raw_buffer_load_b128(rrs, base + k2 * 64 * 16, 0, XG_SYS);
+      vq[2 * k2] = __uint_as_float(d.x);
+      vq[2 * k2 + 1] = __uint_as_float(d.z);
+      okq &= (d.y == tag) & (d.w == tag);
+    }
+    return okq;
+  };
+  if (a.xg_poll == 2) {  // sequential: one source at a time
+#pragma unroll
+    for (int q = 0; q < XW; ++q) {
+      if (q < W && q != rank) {
+        while (!__all(load_src(q, v[q])))
+          if (timed_out()) return false;
+      }
+    }
+  } else {
+    if (a.xg_poll == 1) {  // cheap probe: the last granule pair of every source, then one sweep
+      for (;;) {
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < XW; ++q) {
+          const int qq = q < W ? q : 0;
+          const int off = (((par + qq) * K2 + (K2 - 1)) * 64 + j) * 16;
+          const xg_v4u d = __builtin_amdgcn_raw_buffer_load_b128(rrs, off, 0, XG_SYS);
+          ok &= ((d.y == tag) & (d.w == tag)) | (q >= W) | (q == rank);
+        }
+        if (__all(ok)) break;
+        if (timed_out()) return false;
+      }
+    }
+    for (;;) {  // full sweep of all sources per pass
+      bool ok = true;
+#pragma unroll
+      for (int q = 0; q < XW; ++q) ok &= load_src(q, v[q]) | (q >= W) | (q == rank);
+      if (__all(ok)) break;
+      if (timed_out()) return false;
     }
   }
   float acc[KX];
 #pragma unroll
   for (int k = 0; k < KX; ++k) acc[k] = 0.f;
-  const gu64* recv = (const gu64*)(a.xg_recv);
 #pragma unroll
-  for (int q = 0; q < XG_MAXW; ++q) {
-    if (q >= W) break;
-    float v[KX];
-    if (q == rank) {
+  for (int q = 0; q < XW; ++q) {
+    if (q < W) {
 #pragma unroll
-      for (int k = 0; k < KX; ++k) v[k] = g[k];
-    } else {
-      const gu64* src = recv + (par + q) * slab + j;
-      unsigned long long t_start = 0;
-      for (int spin = 0;; ++spin) {
-        bool ok = true;
-#pragma unroll
-        for (int k = 0; k < KX; ++k) {
-          const unsigned long long x = __hip_atomic_load(src + k * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          v[k] = __uint_as_float((uint32_t)x);
-          ok &= (uint32_t)(x >> 32) == tag;
-        }
-        if (__all(ok)) break;
-        if (spin == 0) {
-          t_start = __builtin_amdgcn_s_memrealtime();
-        } else if ((spin & 31) == 0 &&
-                   (long long)(__builtin_amdgcn_s_memrealtime() - t_start) > a.xg_timeout) {
-          if (j == 0) __hip_atomic_store(a.xg_status, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          return false;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
+      for (int k = 0; k < KX; ++k) acc[k] += (q == rank) ? g[k] : v[q][k];
     }
-#pragma unroll
-    for (int k = 0; k < KX; ++k) acc[k] += v[k];
   }
   const float invw = 1.0f / (float)W;
 #pragma unroll
@@ -148,8 +190,8 @@ __device__ __forceinline__ bool xg_allreduce(float (&g)[KX], const MlpArgs& a, g
 }
 
 // EX: the shape equals the template bounds (d0 == D0, C == CM) -> every guard folds away.
-// XG: in-kernel gradient all-reduce across ranks (train mode, 2 layers).
-template <int L, int BMAX, int D0, int CM, bool EX, bool XG>
+// XW > 0: in-kernel gradient all-reduce across up to XW ranks (train mode, 2 layers).
+template <int L, int BMAX, int D0, int CM, bool EX, int XW>
 __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
   constexpr int HM = 64;
   constexpr int NPF = (BMAX * D0 + BMAX + 63) / 64;  // prefetch dwords per lane
@@ -305,10 +347,18 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
   const uint32_t drop_thr = (uint32_t)(a.dropout * 4294967296.0);
   const bool prof = (a.prof != nullptr) && j == 0;
   if (prof) a.prof[30] = __builtin_amdgcn_s_memrealtime();
-  gu64* peer[XG_MAXW];
+  constexpr bool XG = XW > 0;
+  constexpr int XWN = XW > 0 ? XW : 1;
+  __amdgpu_buffer_rsrc_t prs[XWN];
+  __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(a.xg_recv, 0, 0, 0x00020000);
   if (XG) {
+    const int nbytes = 2 * a.xg_world * (D0 + CM + 2 + ((D0 + CM) & 1)) * 64 * 8;
+    rrs = __builtin_amdgcn_make_buffer_rsrc(a.xg_recv, 0, nbytes, 0x00020000);
 #pragma unroll
-    for (int q = 0; q < XG_MAXW; ++q) peer[q] = (gu64*)(q < a.xg_world ? a.xg_peers[q] : nullptr);
+    for (int q = 0; q < XWN; ++q) {
+      void* pq = (q < a.xg_world) ? (void*)a.xg_peers[q] : (void*)a.xg_recv;
+      prs[q] = __builtin_amdgcn_make_buffer_rsrc(pq, 0, nbytes, 0x00020000);
+    }
   }
   int done = a.steps;
 
@@ -505,17 +555,19 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
 
     if (XG) {  // average the gradients (and the batch loss) across ranks in-kernel
       static_assert(!XG || L == 2, "in-kernel all-reduce is implemented for 2-layer nets");
-      constexpr int KX = D0 + CM + 2;
+      constexpr int KX = D0 + CM + 2 + ((D0 + CM) & 1);  // even: 16-B granule pairs
       float gv[KX];
+#pragma unroll
+      for (int k = 0; k < KX; ++k) gv[k] = 0.f;
 #pragma unroll
       for (int k = 0; k < D0; ++k) gv[k] = gw0[k];
       gv[D0] = gb0;
 #pragma unroll
       for (int c = 0; c < CM; ++c) gv[D0 + 1 + c] = gwo[c];
       const float bl = bs > 0 ? lsum * inv : 0.f;
-      gv[D0 + 1 + CM] = (j < C) ? gbo : (j == 63 ? bl : 0.f);
+      gv[D0 + 1 + CM] = (j < C) ? gbo : (j == 63 ? bl : 0.f);  // bias grads + the batch loss
       const unsigned long long tx = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
-      if (!xg_allreduce<KX>(gv, a, peer, gstep, j)) {
+      if (!xg_allreduce<KX, XWN>(gv, a, prs, rrs, gstep, j)) {
         done = s;
         break;
       }
@@ -639,20 +691,27 @@ namespace {
 using dct::MlpArgs;
 using dct::WaveShape;
 
-template <int L, int BMAX, int D0, int CM, bool EX, bool XG>
+template <int L, int BMAX, int D0, int CM, bool EX, int XW>
 hipError_t launch_wave(const WaveShape& sh, const MlpArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((dct::mlp_wave_kernel<L, BMAX, D0, CM, EX, XG>), dim3(1), dim3(64), 0, st, sh, a);
+  hipLaunchKernelGGL((dct::mlp_wave_kernel<L, BMAX, D0, CM, EX, XW>), dim3(1), dim3(64), 0, st, sh, a);
   return hipGetLastError();
 }
 
-template <int L, int BMAX, bool XG>
+template <int L, int BMAX, int XW>
 hipError_t launch_wave_d0(const WaveShape& sh, const MlpArgs& a, hipStream_t st) {
   if (sh.C > 4) return hipErrorInvalidValue;
   if constexpr (L == 2)
-    if (sh.d0 == 5 && sh.C == 2) return launch_wave<L, BMAX, 5, 2, true, XG>(sh, a, st);  // WeatherClassifier
-  if (sh.d0 <= 8) return launch_wave<L, BMAX, 8, 4, false, XG>(sh, a, st);
-  if (sh.d0 <= 16) return launch_wave<L, BMAX, 16, 4, false, XG>(sh, a, st);
+    if (sh.d0 == 5 && sh.C == 2) return launch_wave<L, BMAX, 5, 2, true, XW>(sh, a, st);  // WeatherClassifier
+  if (sh.d0 <= 8) return launch_wave<L, BMAX, 8, 4, false, XW>(sh, a, st);
+  if (sh.d0 <= 16) return launch_wave<L, BMAX, 16, 4, false, XW>(sh, a, st);
   return hipErrorInvalidValue;
+}
+
+template <int BMAX>
+hipError_t launch_wave_xg(const WaveShape& sh, const MlpArgs& a, hipStream_t st) {
+  if (a.xg_world <= 2) return launch_wave_d0<2, BMAX, 2>(sh, a, st);
+  if (a.xg_world <= 4) return launch_wave_d0<2, BMAX, 4>(sh, a, st);
+  return launch_wave_d0<2, BMAX, 8>(sh, a, st);
 }
 }  // namespace
 
@@ -672,7 +731,7 @@ size_t dct_mlp_xg_slab_granules(const int* dims, int L) {
   if (L != 2 || !dct_mlp_wave_supported(dims, L, 1)) return 0;
   const int D0 = (dims[0] == 5 && dims[2] == 2) ? 5 : (dims[0] <= 8 ? 8 : 16);
   const int CM = (dims[0] == 5 && dims[2] == 2) ? 2 : 4;
-  return (size_t)(D0 + CM + 2) * 64;
+  return (size_t)(D0 + CM + 2 + ((D0 + CM) & 1)) * 64;
 }
 
 int dct_mlp_wave_train(const int* dims, int L, const dct::MlpArgs* a, void* stream) {
@@ -697,10 +756,10 @@ int dct_mlp_wave_train(const int* dims, int L, const dct::MlpArgs* a, void* stre
     if (L != 2 || a->mode != 0 || !a->xg_recv || !a->xg_peers || !a->xg_status || a->xg_world > dct::XG_MAXW ||
         a->xg_rank < 0 || a->xg_rank >= a->xg_world || a->cursor || a->pending)
       return (int)hipErrorInvalidValue;
-    return (int)(a->B <= 4 ? launch_wave_d0<2, 4, true>(sh, *a, st) : launch_wave_d0<2, 8, true>(sh, *a, st));
+    return (int)(a->B <= 4 ? launch_wave_xg<4>(sh, *a, st) : launch_wave_xg<8>(sh, *a, st));
   }
-  if (L == 2) return (int)(a->B <= 4 ? launch_wave_d0<2, 4, false>(sh, *a, st) : launch_wave_d0<2, 8, false>(sh, *a, st));
-  return (int)(a->B <= 4 ? launch_wave_d0<3, 4, false>(sh, *a, st) : launch_wave_d0<3, 8, false>(sh, *a, st));
+  if (L == 2) return (int)(a->B <= 4 ? launch_wave_d0<2, 4, 0>(sh, *a, st) : launch_wave_d0<2, 8, 0>(sh, *a, st));
+  return (int)(a->B <= 4 ? launch_wave_d0<3, 4, 0>(sh, *a, st) : launch_wave_d0<3, 8, 0>(sh, *a, st));
 }
 
 }  // extern "C"

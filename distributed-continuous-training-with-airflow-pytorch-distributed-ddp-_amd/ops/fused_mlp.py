@@ -8,6 +8,7 @@ also the layout of the DDP gradient bucket and of the Lightning checkpoint.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Sequence
 
 import torch
@@ -135,7 +136,8 @@ class FusedMLPKernel:
             if xg.bytes < need:
                 raise ValueError(f"exchange buffer too small ({xg.bytes} < {need} bytes)")
             xg_args = dict(xg_recv=xg.recv, xg_peers=xg.peers, xg_world=xg.world, xg_rank=xg.rank,
-                           xg_status=xg.status, xg_timeout=int(xg_timeout_s * 1e8))
+                           xg_status=xg.status, xg_timeout=int(xg_timeout_s * 1e8),
+                           xg_poll=int(os.environ.get("DCT_XG_POLL", "0")))
         self.plan.train(
             ptr(p), ptr(m) if need_mv else 0, ptr(v) if need_mv else 0, ptr(grad_out),
             ptr(X), X.stride(0), ptr(Y), ptr(idx), int(n_items), int(batch), int(steps), int(t0),
