@@ -2,14 +2,17 @@
 """Headline benchmark: whole-node training samples/sec of the weather-MLP DDP job.
 
 BASELINE.json metric: "samples/sec (whole node) for weather-MLP DDP at 1/2/4/8 MI355X; epoch
-wall-clock".  Workload = the reference training step exactly (jobs/train_lightning_ddp.py):
+wall-clock".  Default workload = the reference training step exactly (jobs/train_lightning_ddp.py):
 WeatherClassifier 5->64->2 (ReLU, Dropout 0.2), cross-entropy, Adam(lr=0.01), batch 4 PER RANK
 (weak scaling), DistributedSampler sharding, per-step gradient all-reduce across ranks plus
-the sync_dist train_loss.  ``--model weather-mlp-3x128`` runs BASELINE.json's 3-layer/128-h
-variant instead.  Data: synthetic weather rows (no network), random-init weights.
+the sync_dist train_loss.  Other BASELINE.json configs:
+  --model weather-mlp-3x128    3-layer / 128-h weather MLP (fused single-CU kernel)
+  --model tabular-mlp-4x1024   100M x 256 synthetic rows (bf16, HBM-resident), 256-1024-1024-1024-2
+                               MLP, MSE, Adam(1e-3), batch 4096 per rank, graph-captured MFMA step
+Data: synthetic rows (no network), random-init weights.
 
-Timed region: exactly K optimizer steps (each = fused gather/fwd/CE/bwd, RCCL all-reduce when
-N > 1, Adam), bracketed by barrier + device synchronize on both sides, max over ranks.
+Timed region: exactly K optimizer steps, bracketed by barrier + device synchronize on both
+sides, max over ranks.
 
     python bench.py --gpus 1 --steps 20000 --warmup 2000
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
@@ -29,39 +32,69 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 # BASELINE.md local probe (reference step shape, torch CPU, W=1): ~8,500 samples/s whole node.
 # The reference publishes no number (BASELINE.json "published": {}); this probe is the only one.
 BASELINE_SAMPLES_PER_SEC = {"weather": 8500.0}
+TABULAR = ("tabular-mlp-4x1024",)
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20000)
-    p.add_argument("--warmup", type=int, default=2000)
-    p.add_argument("--model", default="weather", help="weather (reference 5-64-2) | weather-mlp-3x128")
-    p.add_argument("--batch", type=int, default=4, help="per-rank batch (reference: 4)")
-    p.add_argument("--rows", type=int, default=0, help="synthetic dataset rows (0 = sized to the run)")
-    p.add_argument("--epoch-rows", type=int, default=100000,
-                   help="dataset size used for the reported epoch wall-clock")
-    return p.parse_args()
+    p.add_argument("--steps", type=int, default=None, help="timed steps (default 20000; tabular 200)")
+    p.add_argument("--warmup", type=int, default=None, help="untimed steps (default 2000; tabular 20)")
+    p.add_argument("--model", default="weather", help="weather | weather-mlp-3x128 | tabular-mlp-4x1024")
+    p.add_argument("--batch", type=int, default=None, help="per-rank batch (reference: 4; tabular: 4096)")
+    p.add_argument("--rows", type=int, default=0,
+                   help="synthetic dataset rows (0 = sized to the run; tabular: 100M per BASELINE config 4)")
+    p.add_argument("--epoch-rows", type=int, default=None,
+                   help="dataset size used for the reported epoch wall-clock (weather 100k, tabular 100M)")
+    a = p.parse_args()
+    tab = a.model in TABULAR
+    a.steps = a.steps if a.steps is not None else (200 if tab else 20000)
+    a.warmup = a.warmup if a.warmup is not None else (20 if tab else 2000)
+    a.batch = a.batch if a.batch is not None else (4096 if tab else 4)
+    a.epoch_rows = a.epoch_rows if a.epoch_rows is not None else (100_000_000 if tab else 100_000)
+    return a
 
 
-def main():
-    a = parse()
+def _timed(ctx, fn):
     import torch
     import torch.distributed as dist
 
-    import dct_amd  # noqa: F401
+    torch.cuda.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dt_t = torch.tensor([dt], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
+    if ctx.is_distributed:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    return float(dt_t.item())
+
+
+def _params_in_sync(ctx, p):
+    """DDP invariant: every rank holds the same parameters after the timed steps."""
+    import torch
+    import torch.distributed as dist
+
+    if not ctx.is_distributed:
+        return True
+    ref = p.clone()
+    ctx.broadcast_(ref, src=0)
+    diff = torch.tensor([float((p - ref).abs().max())], device=ctx.device if ctx.backend == "nccl" else "cpu")
+    dist.all_reduce(diff, op=dist.ReduceOp.MAX)
+    return float(diff.item()) == 0.0
+
+
+def setup_weather(a, ctx):
+    import torch
+
     from dct_amd.data.synthetic import weather_tensors
     from dct_amd.models.mlp import build_mlp
-    from dct_amd.parallel.dist import init_distributed, shutdown
     from dct_amd.trainer.engines import FusedMLPEngine, adam_hparams_from
-    from dct_amd.trainer.trainer import seed_everything
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != a.gpus:
-        if a.gpus > 1 and world == 1:
-            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    ctx = init_distributed("gpu")
-    seed_everything(42)
     total_steps = a.warmup + a.steps
     rows = a.rows or int(math.ceil((total_steps + 8) * a.batch * ctx.world_size / 0.8)) + 1024
     X, Y = weather_tensors(rows, seed=0, dim=5)
@@ -73,52 +106,75 @@ def main():
     n_train = int(0.8 * rows)
     perm = torch.randperm(rows, generator=torch.Generator().manual_seed(42))
     eng.attach_data(X, Y, perm[:n_train], perm[n_train:])
+    return eng, 5
+
+
+def setup_tabular(a, ctx):
+    import torch
+
+    from dct_amd.data.synthetic import make_tabular_device
+    from dct_amd.models.mlp import build_mlp
+    from dct_amd.trainer.engines import adam_hparams_from
+    from dct_amd.trainer.graph_engine import GraphMLPEngine
+
+    feats = 256
+    rows = a.rows or 100_000_000
+    X, Y = make_tabular_device(rows, feats, num_classes=2, device=ctx.device, dtype=torch.bfloat16, seed=0)
+    model = build_mlp(a.model, feats)
+    adam = adam_hparams_from(model.configure_optimizers())
+    eng = GraphMLPEngine(model, ctx, a.batch, seed=42, adam=adam)
+    n_train = int(0.8 * rows)
+    perm = torch.randperm(rows, generator=torch.Generator().manual_seed(42))  # reference random_split
+    eng.attach_data(X, Y, perm[:n_train], perm[n_train:])
+    return eng, feats
+
+
+def main():
+    a = parse()
+    import torch
+
+    import dct_amd  # noqa: F401
+    from dct_amd.parallel.dist import init_distributed, shutdown
+    from dct_amd.trainer.trainer import seed_everything
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus and a.gpus > 1 and world == 1:
+        raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    ctx = init_distributed("gpu")
+    seed_everything(42)
+    tab = a.model in TABULAR
+    eng, feats = (setup_tabular if tab else setup_weather)(a, ctx)
+    total_steps = a.warmup + a.steps
     n_items = eng.upload_epoch_indices(0, shuffle=True)
-    assert (total_steps - 1) * a.batch < n_items, "dataset too small for the requested steps"
+    if total_steps * a.batch > n_items:
+        raise SystemExit(f"dataset too small: {total_steps} steps x {a.batch} > {n_items} rows per rank")
     loss = torch.zeros(total_steps, dtype=torch.float32, device=ctx.device)
 
-    # warmup (also captures the DDP step graph chunk outside the timed region)
+    # warmup (also builds / captures the step graphs outside the timed region)
     eng.run_steps(n_items, a.warmup, loss, first_step=0)
-    if eng.xg is not None and not eng.xg_verify(fallback=True):
+    if getattr(eng, "xg", None) is not None and not eng.xg_verify(fallback=True):
         eng.run_steps(n_items, a.warmup, loss, first_step=0)  # re-warm on the RCCL path
-    if eng.ddp and eng.xg is None and eng.use_graph:
-        C = min(eng.graph_chunk, a.steps)
-        eng._get_graph(n_items, C, loss)
-    torch.cuda.synchronize()
-    ctx.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    eng.run_steps(n_items, a.steps, loss, first_step=a.warmup)
-    torch.cuda.synchronize()
-    ctx.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    dt_t = torch.tensor([dt], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
-    if ctx.is_distributed:
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-    dt = float(dt_t.item())
+    if not tab and eng.ddp and eng.xg is None and eng.use_graph:
+        eng._get_graph(n_items, min(eng.graph_chunk, a.steps), loss)
+    dt = _timed(ctx, lambda: eng.run_steps(n_items, a.steps, loss, first_step=a.warmup))
 
-    xg_ok = eng.xg_verify(fallback=True) if eng.xg is not None else None
-    if eng.xg is not None or eng.ddp:
+    xg_ok = eng.xg_verify(fallback=True) if getattr(eng, "xg", None) is not None else None
+    if tab:
+        engine_desc = ("graph-mlp-executor(bf16 mfma gemm)" + ("+rccl-bucket-allreduce" if ctx.is_distributed else "")
+                       + ("+hipgraph" if eng.graph_used else ""))
+    elif eng.xg is not None or eng.ddp:
         engine_desc = eng.step_mode if eng.xg is not None else (
             "fused+rccl-allreduce" + ("+update-then-grad" if eng.fused_update else "+adam")
             + ("+hipgraph" if eng.graph_used else ""))
     else:
         engine_desc = "fused-persistent"
-    # DDP invariant: every rank holds the same parameters after the timed steps
-    in_sync = True
-    if ctx.is_distributed:
-        ref = eng.p.clone()
-        ctx.broadcast_(ref, src=0)
-        diff = torch.tensor([float((eng.p - ref).abs().max())], device=ctx.device if ctx.backend == "nccl" else "cpu")
-        dist.all_reduce(diff, op=dist.ReduceOp.MAX)
-        in_sync = float(diff.item()) == 0.0
+    in_sync = _params_in_sync(ctx, eng.p)
     losses = loss.cpu()
     finite = bool(torch.isfinite(losses).all())
     first_l = float(losses[: max(1, a.warmup // 10)].mean())
     last_l = float(losses[-max(1, a.steps // 10):].mean())
     eng.global_step = total_steps
-    val_loss, val_acc = eng.validate()
+    val_loss, val_acc = eng.validate(limit=(64 * a.batch) if tab else None)
 
     samples = a.steps * a.batch * ctx.world_size
     sps = samples / dt
@@ -126,6 +182,8 @@ def main():
     # epoch wall-clock for an --epoch-rows dataset at the measured step rate (train part)
     steps_per_epoch = math.ceil(math.ceil(int(0.8 * a.epoch_rows) / ctx.world_size) / a.batch)
     base = BASELINE_SAMPLES_PER_SEC.get(a.model)
+    models = {"weather": "WeatherClassifier 5-64-2 (reference jobs/train_lightning_ddp.py)",
+              "tabular-mlp-4x1024": "tabular MLP 256-1024-1024-1024-2 (BASELINE config 4)"}
     out = {
         "metric": "samples/sec (whole node) for weather-MLP DDP",
         "value": round(sps, 1),
@@ -137,18 +195,19 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": (round(sps / base, 2) if base else None),
-        "dtype": "fp32",
+        "dtype": "bf16" if tab else "fp32",
         "data": "synthetic",
         "config": {
-            "model": ("WeatherClassifier 5-64-2 (reference jobs/train_lightning_ddp.py)" if a.model == "weather"
-                      else a.model),
+            "model": models.get(a.model, a.model),
             "global_batch": a.batch * ctx.world_size,
             "per_rank_batch": a.batch,
             "seq_len": None,
             "parallelism": f"dp{ctx.world_size}",
-            "optimizer": "adam lr=0.01",
+            "optimizer": f"adam lr={eng.adam['lr']:g}",
             "loss": eng.loss,
             "engine": engine_desc,
+            "dataset_rows": int(eng.X.shape[0]),
+            "features": feats,
             "baseline_ref": "BASELINE.md CPU probe, W=1, 8500 samples/s (reference publishes none)",
         },
         "extra": {
@@ -165,6 +224,9 @@ def main():
             "device": torch.cuda.get_device_name(ctx.device),
         },
     }
+    if tab:
+        flops = 6.0 * sum(eng.dims[i] * eng.dims[i + 1] for i in range(len(eng.dims) - 1)) * a.batch
+        out["extra"]["model_tflops_per_gpu"] = round(flops / (ms_step * 1e-3) / 1e12, 1)
     if ctx.rank == 0:
         print(json.dumps(out), flush=True)
     shutdown(ctx)

@@ -16,6 +16,7 @@
 #include "kernels.h"
 #include "mlp_fused.h"
 #include "runtime.h"
+#include "mlp_executor.h"
 
 namespace py = pybind11;
 
@@ -191,6 +192,36 @@ PYBIND11_MODULE(_dct_native, m) {
       py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("trans_a"), py::arg("trans_b"), py::arg("epilogue"),
       py::arg("out_f32"), py::arg("accumulate"), py::arg("aux"), py::arg("stream"));
   m.def(
+      "gemm_bf16_ex",
+      [](uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias, int M, int N, int K, int lda, int ldb, int ldc,
+         int trans_a, int trans_b, int epilogue, int out_f32, int accumulate, uintptr_t aux, uintptr_t colsum,
+         uintptr_t stream) {
+        check(dct_gemm_bf16_ex(P<const uint16_t>(A), P<const uint16_t>(B), P<void>(C), P<const float>(bias), M, N, K,
+                               lda, ldb, ldc, trans_a, trans_b, epilogue, out_f32, accumulate, P<void>(aux),
+                               P<float>(colsum), reinterpret_cast<void*>(stream)),
+              "gemm_bf16_ex");
+      },
+      py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("M"), py::arg("N"), py::arg("K"),
+      py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("trans_a"), py::arg("trans_b"), py::arg("epilogue"),
+      py::arg("out_f32"), py::arg("accumulate"), py::arg("aux"), py::arg("colsum"), py::arg("stream"));
+  m.def("skinny_fwd", [](uintptr_t X, uintptr_t W, uintptr_t bias, uintptr_t Y, int B, int K, int C, uintptr_t stream) {
+    check(dct_skinny_fwd(P<const uint16_t>(X), P<const uint16_t>(W), P<const float>(bias), P<uint16_t>(Y), B, K, C,
+                         reinterpret_cast<void*>(stream)),
+          "skinny_fwd");
+  });
+  m.def("skinny_dx", [](uintptr_t dZ, uintptr_t W, uintptr_t aux, uintptr_t dX, int B, int K, int C, uintptr_t stream) {
+    check(dct_skinny_dx(P<const uint16_t>(dZ), P<const uint16_t>(W), P<const uint16_t>(aux), P<uint16_t>(dX), B, K, C,
+                        reinterpret_cast<void*>(stream)),
+          "skinny_dx");
+  });
+  m.def("skinny_dw", [](uintptr_t dZ, uintptr_t X, uintptr_t dW, uintptr_t db, int B, int K, int C, uintptr_t stream) {
+    check(dct_skinny_dw(P<const uint16_t>(dZ), P<const uint16_t>(X), P<float>(dW), P<float>(db), B, K, C,
+                        reinterpret_cast<void*>(stream)),
+          "skinny_dw");
+  });
+  m.attr("EPI_RELU_MASK") = 4;
+  m.attr("EPI_GELU_GRAD") = 5;
+  m.def(
       "bias_act_bwd",
       [](uintptr_t dY, uintptr_t act_aux, uintptr_t dZ_bf16, uintptr_t dbias, int M, int N, int ldy, int act,
          int accumulate_bias, uintptr_t stream) {
@@ -302,6 +333,22 @@ PYBIND11_MODULE(_dct_native, m) {
   m.def("mlp_xg_slab_granules", [](const std::vector<int>& dims) {
     return (int64_t)dct_mlp_xg_slab_granules(dims.data(), (int)dims.size() - 1);
   });
+  py::class_<dct::MlpStepExecutor>(m, "MlpStepExecutor")
+      .def(py::init<const std::vector<int>&, int, int, int, uintptr_t, uintptr_t, uintptr_t, uintptr_t, uintptr_t,
+                    const std::vector<uintptr_t>&, const std::vector<uintptr_t>&, uintptr_t, uintptr_t, uintptr_t,
+                    uintptr_t, dct::BucketReducer*>(),
+           py::arg("dims"), py::arg("batch"), py::arg("act"), py::arg("loss_kind"), py::arg("p"), py::arg("p_bf16"),
+           py::arg("g"), py::arg("m"), py::arg("v"), py::arg("acts"), py::arg("pre"), py::arg("dz0"), py::arg("dz1"),
+           py::arg("ybuf"), py::arg("stats"), py::arg("reducer") = nullptr, py::keep_alive<1, 17>())
+      .def("set_adam", &dct::MlpStepExecutor::set_adam, py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"),
+           py::arg("wd"), py::arg("decoupled") = 0)
+      .def("step", &dct::MlpStepExecutor::step, py::arg("X"), py::arg("row_bytes"), py::arg("Y"), py::arg("idx"),
+           py::arg("n_items"), py::arg("cursor"), py::arg("step_counter"), py::arg("loss_out"), py::arg("loss_cap"),
+           py::arg("rows"), py::arg("stream"))
+      .def("eval_batch", &dct::MlpStepExecutor::eval_batch, py::arg("X"), py::arg("row_bytes"), py::arg("Y"),
+           py::arg("idx"), py::arg("n_items"), py::arg("cursor"), py::arg("rows"), py::arg("stats"),
+           py::arg("stream"))
+      .def_property_readonly("num_params", &dct::MlpStepExecutor::num_params);
   py::class_<dct::StreamGraph>(m, "StreamGraph")
       .def(py::init<>())
       .def("begin", &dct::StreamGraph::begin)

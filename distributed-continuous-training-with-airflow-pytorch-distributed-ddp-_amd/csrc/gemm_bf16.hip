@@ -19,6 +19,9 @@
 // Transposed operands are transposed in the staging write (8 x ds_write_b16 per 16-B load).
 // Block index -> tile is remapped so blocks sharing an A row-panel run on one XCD (T1).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "dct_common.h"
@@ -32,6 +35,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int GBM = 128, GBN = 128, GBK = 64, GPAD = 8, GLD = GBK + GPAD, GNT = 256;
 
 __device__ __forceinline__ float gelu_f(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad_f(float z) {
+  const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
+  return cdf + z * 0.3989422804014327f * __expf(-0.5f * z * z);
+}
 
 // Stage one BMxBK (or BNxBK) tile of an operand into registers.
 // Non-transposed: chunk c -> row c/8, k-chunk c%8 (8 bf16 each)  [storage [R][K]]
@@ -179,7 +186,7 @@ __global__ __launch_bounds__(GNT, 2) void gemm_bf16_kernel(GemmArgs g) {
     for (int j = 0; j < 4; ++j) {
       const int col = n0 + wc * 64 + j * 16 + ccol;
       if (col >= g.N) continue;
-      const float bv = (g.bias && g.epilogue != EPI_NONE) ? g.bias[col] : 0.f;
+      const float bv = (g.bias && g.epilogue >= EPI_BIAS && g.epilogue <= EPI_BIAS_GELU) ? g.bias[col] : 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wr * 64 + i * 16 + crow + r;
@@ -189,6 +196,205 @@ __global__ __launch_bounds__(GNT, 2) void gemm_bf16_kernel(GemmArgs g) {
         if (g.aux && g.epilogue == EPI_BIAS_GELU) reinterpret_cast<uint16_t*>(g.aux)[o] = f32_to_bf16(z);
         if (g.epilogue == EPI_BIAS_RELU) z = fmaxf(z, 0.f);
         else if (g.epilogue == EPI_BIAS_GELU) z = gelu_f(z);
+        else if (g.epilogue == EPI_RELU_MASK) z = bf16_to_f32(reinterpret_cast<const uint16_t*>(g.aux)[o]) > 0.f ? z : 0.f;
+        else if (g.epilogue == EPI_GELU_GRAD) z *= gelu_grad_f(bf16_to_f32(reinterpret_cast<const uint16_t*>(g.aux)[o]));
+        if (g.out_f32) {
+          float* C = reinterpret_cast<float*>(g.C);
+          C[o] = g.accumulate ? C[o] + z : z;
+        } else {
+          uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
+          if (g.accumulate) z += bf16_to_f32(C[o]);
+          C[o] = f32_to_bf16(z);
+        }
+      }
+    }
+  }
+}
+
+
+// ================================================================== fast path (v2)
+// Same tile geometry, but the operands reach LDS by global_load_lds (16-B LDS-DMA, no VGPR
+// staging) as verbatim copies of global memory, and transposed operands are transposed by
+// the hardware on the way OUT of LDS (ds_read_b64_tr_b16) instead of by 8 ds_write_b16 per
+// 16-B chunk on the way in.  Two LDS images:
+//   KC ("k contiguous", A row-major / B = W[N][K]): [128 rows][64 k], 16-B chunk c of row r at
+//      physical chunk c ^ (r & 7); fragments by ds_read_b128.
+//   MC ("rows contiguous", A stored [K][M] / B stored [K][N]): [64 k][128 rows], chunk c of
+//      k-row k at c ^ f(k), f(k) = ((k & 3) | ((k >> 1) & 4)) << 1, which spreads the 8 k-rows a
+//      32-lane half reads per ds_read_b64_tr_b16 over all 64 banks.
+// Split-K (fp32 output, few tiles, e.g. dW = dZ^T X with K = batch): slices accumulate with
+// float atomics into C (zeroed by the launcher unless accumulating).
+constexpr int G2_BYTES = GBM * GBK * 2;  // one operand image (16 KB)
+
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ int mc_swz(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
+
+// one 128 x 64 operand tile -> LDS image (4 glds per thread)
+template <bool MC>
+__device__ __forceinline__ void g2_fill(const uint16_t* __restrict__ G, int ld, int R, int r0, int k0, char* img) {
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int L = q * 256 + wave * 64 + lane;  // linear 16-B chunk of the image
+    const uint16_t* src;
+    if (!MC) {
+      const int r = L >> 3, pc = L & 7;
+      const int c = pc ^ (r & 7);
+      int row = r0 + r;
+      row = row < R ? row : R - 1;
+      src = G + (size_t)row * ld + k0 + c * 8;
+    } else {
+      const int k = L >> 4, pc = L & 15;
+      const int c = pc ^ mc_swz(k);
+      int col = r0 + c * 8;
+      col = col + 8 <= R ? col : R - 8;
+      src = G + (size_t)(k0 + k) * ld + col;
+    }
+    // LDS-DMA in inline asm: hipcc would otherwise wait vmcnt(0) before every later ds_read
+    // (it cannot prove the DMA does not alias them), serialising the prefetch with the MFMAs.
+    // Completion is counted by hand: the k-loop's "s_waitcnt vmcnt(0)" before its barrier.
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(lds_void*)(img + (q * 256 + wave * 64) * 16));
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(dst)
+        : "memory");
+  }
+}
+
+// 16 x 32 operand fragment (rows rb..rb+15, k-slice ks) in the MFMA A/B layout
+template <bool MC>
+__device__ __forceinline__ bf16x8 g2_frag(const char* img, int rb, int ks, int lane) {
+  if (!MC) {
+    const int row = rb + (lane & 15);
+    const int c = ks * 4 + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(img + row * 128 + ((c ^ (row & 7)) << 4));
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int k = ks * 32 + 8 * g + q;
+    const int c = (rb >> 3) + (p >> 1);
+    const int k2 = k + 4;
+    const char* a0 = img + k * 256 + ((c ^ mc_swz(k)) << 4) + (p & 1) * 8;
+    const char* a1 = img + k2 * 256 + ((c ^ mc_swz(k2)) << 4) + (p & 1) * 8;
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)(a0));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)(a1));
+    bf16x8 r;
+    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+    return r;
+  }
+}
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(GNT, 2) void gemm2_kernel(GemmArgs g, int splits) {
+  extern __shared__ __attribute__((aligned(16))) char smem2[];
+  // [buf][A,B] images of 16 KB each
+  constexpr bool AMC = TA, BMC = !TB;
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tile = wgid / splits, split = wgid - tile * splits;
+  const int tiles_n = (g.N + GBN - 1) / GBN;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int nk_all = g.K / GBK;
+  const int per = (nk_all + splits - 1) / splits;
+  const int kt0 = split * per;
+  const int kt1 = min(nk_all, kt0 + per);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // colsum: one wave column (wc == 0) of the first N tile sums its A rows
+  const bool do_cs = g.colsum != nullptr && tn == 0 && wc == 0;
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  auto img = [&](int buf, int op) -> char* { return smem2 + (buf * 2 + op) * G2_BYTES; };
+  auto fill = [&](int buf, int kt) {
+    const int k0 = kt * GBK;
+    if (!TA) g2_fill<false>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
+    else g2_fill<true>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
+    if (TB) g2_fill<false>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
+    else g2_fill<true>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
+  };
+  if (kt0 < kt1) {
+    fill(0, kt0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int cur = (kt - kt0) & 1;
+      if (kt + 1 < kt1) fill(cur ^ 1, kt + 1);
+      const char* ai = img(cur, 0);
+      const char* bi = img(cur, 1);
+#pragma unroll
+      for (int ks = 0; ks < GBK / 32; ++ks) {
+        bf16x8 af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = g2_frag<AMC>(ai, wr * 64 + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = g2_frag<BMC>(bi, wc * 64 + j * 16, ks, lane);
+        if (do_cs) {  // fused bias gradient: row sums of the A fragments (lane: 8 k of row l&15)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cs[i] += bf16_to_f32((uint16_t)af[i][e]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+  if (do_cs) {  // lanes l, l+16, l+32, l+48 hold partial sums of the same row
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = cs[i];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      const int row = m0 + wr * 64 + i * 16 + (lane & 15);
+      if (lane < 16 && row < g.M) atomicAdd(g.colsum + row, v);
+    }
+  }
+  // ---- epilogue: C layout col = lane&15, row = (lane>>4)*4 + r
+  const int ccol = lane & 15;
+  const int crow = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wc * 64 + j * 16 + ccol;
+      if (col >= g.N) continue;
+      const float bv = (g.bias && g.epilogue >= EPI_BIAS && g.epilogue <= EPI_BIAS_GELU) ? g.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 64 + i * 16 + crow + r;
+        if (row >= g.M) continue;
+        float z = acc[i][j][r] * g.alpha + bv;
+        const size_t o = (size_t)row * g.ldc + col;
+        if (splits > 1) {
+          atomicAdd(reinterpret_cast<float*>(g.C) + o, z);
+          continue;
+        }
+        if (g.aux && g.epilogue == EPI_BIAS_GELU) reinterpret_cast<uint16_t*>(g.aux)[o] = f32_to_bf16(z);
+        if (g.epilogue == EPI_BIAS_RELU) z = fmaxf(z, 0.f);
+        else if (g.epilogue == EPI_BIAS_GELU) z = gelu_f(z);
+        else if (g.epilogue == EPI_RELU_MASK) z = bf16_to_f32(reinterpret_cast<const uint16_t*>(g.aux)[o]) > 0.f ? z : 0.f;
+        else if (g.epilogue == EPI_GELU_GRAD) z *= gelu_grad_f(bf16_to_f32(reinterpret_cast<const uint16_t*>(g.aux)[o]));
         if (g.out_f32) {
           float* C = reinterpret_cast<float*>(g.C);
           C[o] = g.accumulate ? C[o] + z : z;
@@ -215,6 +421,67 @@ static hipError_t launch_gemm(const dct::GemmArgs& g, hipStream_t st) {
   return hipGetLastError();
 }
 
+static bool gemm_v2_ok(const dct::GemmArgs& g, int ta, int tb) {
+  if (getenv("DCT_GEMM_V1")) return false;
+  if (g.K % dct::GBK) return false;
+  auto aligned = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
+  if (!aligned(g.A) || !aligned(g.B) || g.lda % 8 || g.ldb % 8) return false;
+  if (ta && g.M % 8) return false;    // MC image of A: 8-row chunks inside [0, M)
+  if (!tb && g.N % 8) return false;   // MC image of B
+  return true;
+}
+
+template <bool TA, bool TB>
+static hipError_t launch_gemm2(const dct::GemmArgs& g, hipStream_t st) {
+  const size_t lds = 4 * (size_t)dct::G2_BYTES;
+  auto fn = dct::gemm2_kernel<TA, TB>;
+  hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  const int tiles = ((g.M + dct::GBM - 1) / dct::GBM) * ((g.N + dct::GBN - 1) / dct::GBN);
+  const int nk = g.K / dct::GBK;
+  int splits = 1;
+  if (g.out_f32 && g.epilogue == dct::EPI_NONE && g.alpha == 1.0f && tiles < 256 && nk >= 8) {
+    splits = std::min(nk / 4, (512 + tiles - 1) / tiles);
+    if (splits < 1) splits = 1;
+  }
+  if (splits > 1 && !g.accumulate) {  // slices accumulate atomically into a zeroed C
+    e = hipMemset2DAsync(g.C, (size_t)g.ldc * 4, 0, (size_t)g.N * 4, (size_t)g.M, st);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(fn, dim3(tiles * splits), dim3(dct::GNT), lds, st, g, splits);
+  return hipGetLastError();
+}
+
+extern "C" int dct_bias_act_bwd(const void* dY, const void* act_aux, uint16_t* dZ, float* dbias, int M, int N,
+                                int ldy, int act, int accumulate_bias, void* stream);
+
+extern "C" int dct_gemm_bf16_ex(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K,
+                                int lda, int ldb, int ldc, int trans_a, int trans_b, int epilogue, int out_f32,
+                                int accumulate, void* aux, float* colsum, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  dct::GemmArgs g{};
+  g.A = A; g.B = B; g.C = C; g.bias = bias; g.aux = aux;
+  g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.epilogue = epilogue; g.out_f32 = out_f32; g.accumulate = accumulate; g.alpha = 1.0f;
+  g.vec_a = ((((uintptr_t)A) & 15) == 0) && (lda % 8 == 0);
+  g.vec_b = ((((uintptr_t)B) & 15) == 0) && (ldb % 8 == 0);
+  g.colsum = colsum;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (gemm_v2_ok(g, trans_a, trans_b)) {
+    if (!trans_a && trans_b) return (int)launch_gemm2<false, true>(g, st);
+    if (!trans_a && !trans_b) return (int)launch_gemm2<false, false>(g, st);
+    if (trans_a && !trans_b) return (int)launch_gemm2<true, false>(g, st);
+    return (int)launch_gemm2<true, true>(g, st);
+  }
+  g.colsum = nullptr;
+  int e = dct_gemm_bf16(A, B, C, bias, M, N, K, lda, ldb, ldc, trans_a, trans_b, epilogue, out_f32, accumulate, aux,
+                        stream);
+  if (e || !colsum) return e;
+  // generic path: the A rows' sums by the column-sum kernel (op(A) = A^T when trans_a: A is [K][M])
+  if (trans_a) return dct_bias_act_bwd(A, nullptr, nullptr, colsum, K, M, lda, 0, 1, stream);
+  return (int)hipErrorNotSupported;
+}
+
 extern "C" int dct_gemm_bf16(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K,
                              int lda, int ldb, int ldc, int trans_a, int trans_b, int epilogue, int out_f32,
                              int accumulate, void* aux, void* stream) {
@@ -228,6 +495,12 @@ extern "C" int dct_gemm_bf16(const uint16_t* A, const uint16_t* B, void* C, cons
   g.vec_b = ((((uintptr_t)B) & 15) == 0) && (ldb % 8 == 0);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipError_t e;
+  if (gemm_v2_ok(g, trans_a, trans_b)) {
+    if (!trans_a && trans_b) return (int)launch_gemm2<false, true>(g, st);
+    if (!trans_a && !trans_b) return (int)launch_gemm2<false, false>(g, st);
+    if (trans_a && !trans_b) return (int)launch_gemm2<true, false>(g, st);
+    return (int)launch_gemm2<true, true>(g, st);
+  }
   if (!trans_a && trans_b) e = launch_gemm<false, true>(g, st);
   else if (!trans_a && !trans_b) e = launch_gemm<false, false>(g, st);
   else if (trans_a && !trans_b) e = launch_gemm<true, false>(g, st);

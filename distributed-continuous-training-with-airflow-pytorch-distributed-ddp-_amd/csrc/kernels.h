@@ -4,7 +4,10 @@
 
 namespace dct {
 
-enum Epilogue { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_RELU = 2, EPI_BIAS_GELU = 3 };
+// EPI_RELU_MASK: z = aux[o] > 0 ? z : 0 with aux the layer's bf16 ReLU OUTPUT (backward dX GEMM
+// producing the previous layer's dZ directly); EPI_GELU_GRAD: z *= gelu'(aux[o]), aux = the
+// bf16 pre-activation.
+enum Epilogue { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_RELU = 2, EPI_BIAS_GELU = 3, EPI_RELU_MASK = 4, EPI_GELU_GRAD = 5 };
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
 
 struct GemmArgs {
@@ -17,6 +20,7 @@ struct GemmArgs {
   int epilogue, out_f32, accumulate;
   int vec_a, vec_b;
   float alpha;
+  float* colsum;  // optional: colsum[m] += sum_k op(A)[m][k] (the bias gradient of a dW GEMM)
 };
 
 }  // namespace dct
@@ -25,6 +29,19 @@ extern "C" {
 int dct_gemm_bf16(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K, int lda,
                   int ldb, int ldc, int trans_a, int trans_b, int epilogue, int out_f32, int accumulate, void* aux,
                   void* stream);
+// same, plus colsum[m] += sum over k of op(A)[m][k] (fused bias gradient; colsum accumulates)
+int dct_gemm_bf16_ex(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K, int lda,
+                     int ldb, int ldc, int trans_a, int trans_b, int epilogue, int out_f32, int accumulate, void* aux,
+                     float* colsum, void* stream);
+// Skinny layers (C <= 8 outputs, e.g. the classifier head) as bandwidth kernels:
+//   fwd: Y[b][c] = sum_k X[b][k] W[c][k] + bias[c]            (bf16 X/W/Y)
+//   dx : dX[b][k] = sum_c dZ[b][c] W[c][k], masked by aux[b][k] > 0 when aux (ReLU output)
+//   dw : dW[c][k] += sum_b dZ[b][c] X[b][k] ; db[c] += sum_b dZ[b][c]   (fp32, accumulate)
+int dct_skinny_fwd(const uint16_t* X, const uint16_t* W, const float* bias, uint16_t* Y, int B, int K, int C,
+                   void* stream);
+int dct_skinny_dx(const uint16_t* dZ, const uint16_t* W, const uint16_t* aux, uint16_t* dX, int B, int K, int C,
+                  void* stream);
+int dct_skinny_dw(const uint16_t* dZ, const uint16_t* X, float* dW, float* db, int B, int K, int C, void* stream);
 // dZ = dY * act'(aux) (bf16 out); dbias[n] (+)= sum_m dZ[m][n]. dY is bf16. For RELU aux is
 // the activation OUTPUT (bf16), for GELU the pre-activation (bf16), for NONE unused.
 int dct_bias_act_bwd(const void* dY, const void* act_aux, uint16_t* dZ, float* dbias, int M, int N, int ldy, int act,

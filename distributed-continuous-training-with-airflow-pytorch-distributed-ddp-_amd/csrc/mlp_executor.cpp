@@ -1,0 +1,185 @@
+// Native step executor for wide MLPs (the BASELINE "100M x 256, 4-layer MLP-1024h" family):
+// one data-parallel training step issued from C++ with no Python and no autograd on the path,
+// designed to be captured ONCE into a hipGraph and replayed for every step of an epoch.
+//
+// Reference step (jobs/train_lightning_ddp.py:66-71,88,136 through Lightning/torch DDP):
+//   collate -> forward (Linear/ReLU) -> loss -> autograd backward -> DDP bucket all-reduce -> Adam.
+// MI355X step (all on one compute stream, the all-reduce on the reducer's comm stream):
+//   step_begin (Adam t += 1, zero loss stats; memset grads)
+//   gather_batch          HBM-resident bf16 dataset rows idx[cursor*B + r] -> X_b (16-B copies)
+//   L x gemm_bf16         A_{l+1} = act(A_l W_l^T + b_l): MFMA GEMM, bias+ReLU/GELU epilogue, bf16 out
+//   loss_fwd_bwd          CE / MSE + dlogits (scaled 1/rows), loss & accuracy sums
+//   loss_to_slot          batch-mean loss -> g[P] (all-reduced with the grads: sync_dist for free)
+//   for l = L-1 .. 0:     bias_act_bwd (dZ = dA * act', db = colsum) ; dW_l = dZ^T A_l (fp32 straight
+//                         into the flat gradient buffer = the DDP bucket views) ; mark params ready
+//                         (the reducer launches each full bucket's ncclAvg on its comm stream while
+//                         the earlier layers' backward GEMMs keep running) ; dA_l = dZ W_l
+//   finalize              compute stream waits for the last bucket
+//   adam_flat             fp32 master update + bf16 shadow weights for the next forward's GEMMs
+//   step_end              loss_out[cursor] = reduced loss ; cursor += 1
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "mlp_executor.h"
+#include "mlp_fused.h"
+#include "runtime.h"
+
+extern "C" {
+int dct_gather_batch(const void* X, int row_bytes, const int* Y, const int* idx, const int* cursor, int stride,
+                     int B, int n_items, void* xdst, int* ydst, void* stream);
+int dct_step_begin(int* step_counter, float* stats, void* stream);
+int dct_loss_to_slot(const float* stats, float* slot, float inv_rows, void* stream);
+int dct_step_end(int* cursor, const float* slot, float* loss_out, int loss_cap, void* stream);
+}
+
+namespace dct {
+
+static void ck(int e, const char* what) {
+  if (e != 0) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString((hipError_t)e));
+}
+
+MlpStepExecutor::MlpStepExecutor(const std::vector<int>& dims, int batch, int act, int loss_kind, uintptr_t p,
+                                 uintptr_t p_bf16, uintptr_t g, uintptr_t m, uintptr_t v,
+                                 const std::vector<uintptr_t>& acts, const std::vector<uintptr_t>& pre,
+                                 uintptr_t dz0, uintptr_t dz1, uintptr_t ybuf, uintptr_t stats,
+                                 BucketReducer* reducer)
+    : dims_(dims), B_(batch), act_(act), loss_kind_(loss_kind), reducer_(reducer) {
+  L_ = (int)dims.size() - 1;
+  if (L_ < 1) throw std::invalid_argument("MlpStepExecutor: need at least one layer");
+  if ((int)acts.size() != L_ + 1) throw std::invalid_argument("MlpStepExecutor: need L+1 activation buffers");
+  if (act_ == ACT_GELU && (int)pre.size() != L_ + 1)
+    throw std::invalid_argument("MlpStepExecutor: GELU needs L+1 pre-activation buffers");
+  if (dims[0] % 8) throw std::invalid_argument("MlpStepExecutor: input width must be a multiple of 8");
+  p_ = reinterpret_cast<float*>(p);
+  pb_ = reinterpret_cast<uint16_t*>(p_bf16);
+  g_ = reinterpret_cast<float*>(g);
+  m_ = reinterpret_cast<float*>(m);
+  v_ = reinterpret_cast<float*>(v);
+  for (auto a : acts) acts_.push_back(reinterpret_cast<uint16_t*>(a));
+  for (auto a : pre) pre_.push_back(reinterpret_cast<uint16_t*>(a));
+  dz_[0] = reinterpret_cast<uint16_t*>(dz0);
+  dz_[1] = reinterpret_cast<uint16_t*>(dz1);
+  y_ = reinterpret_cast<int*>(ybuf);
+  stats_ = reinterpret_cast<float*>(stats);
+  int64_t off = 0;
+  for (int l = 0; l < L_; ++l) {
+    woff_.push_back(off);
+    off += (int64_t)dims[l] * dims[l + 1];
+    boff_.push_back(off);
+    off += dims[l + 1];
+  }
+  P_ = off;
+}
+
+void MlpStepExecutor::set_adam(float lr, float b1, float b2, float eps, float wd, int decoupled) {
+  lr_ = lr; b1_ = b1; b2_ = b2; eps_ = eps; wd_ = wd; decoupled_ = decoupled;
+}
+
+void MlpStepExecutor::forward(int rows, hipStream_t st) {
+  for (int l = 0; l < L_; ++l) {
+    const int din = dims_[l], dout = dims_[l + 1];
+    const bool last = l == L_ - 1;
+    int epi = EPI_BIAS;
+    void* aux = nullptr;
+    if (!last) {
+      if (act_ == ACT_RELU) epi = EPI_BIAS_RELU;
+      else if (act_ == ACT_GELU) { epi = EPI_BIAS_GELU; aux = pre_[l + 1]; }
+    }
+    if (last && skinny(l)) {  // classifier head: a bandwidth kernel, not a 2-of-128-column MFMA tile
+      ck(dct_skinny_fwd(acts_[l], pb_ + woff_[l], p_ + boff_[l], acts_[l + 1], rows, din, dout, st), "skinny fwd");
+      continue;
+    }
+    ck(dct_gemm_bf16(acts_[l], pb_ + woff_[l], acts_[l + 1], p_ + boff_[l], rows, dout, din, din, din, dout,
+                     /*trans_a*/ 0, /*trans_b*/ 1, epi, /*out_f32*/ 0, /*accumulate*/ 0, aux, st),
+       "forward gemm");
+  }
+}
+
+void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t idx, int n_items, uintptr_t cursor,
+                           uintptr_t step_counter, uintptr_t loss_out, int loss_cap, int rows, uintptr_t stream) {
+  if (rows < 1 || rows > B_) throw std::invalid_argument("rows must be in [1, batch]");
+  if (row_bytes != dims_[0] * 2) throw std::invalid_argument("dataset row width does not match the model input");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int* cur = reinterpret_cast<int*>(cursor);
+  int* sc = reinterpret_cast<int*>(step_counter);
+  if (reducer_) reducer_->prepare();
+  ck(dct_step_begin(sc, stats_, st), "step_begin");
+  ck((int)hipMemsetAsync(g_, 0, (size_t)(P_ + 1) * sizeof(float), st), "memset grads");
+  ck(dct_gather_batch(reinterpret_cast<const void*>(X), row_bytes, reinterpret_cast<const int*>(Y),
+                      reinterpret_cast<const int*>(idx), cur, B_, rows, n_items, acts_[0], y_, st),
+     "gather_batch");
+  forward(rows, st);
+  const int C = dims_[L_];
+  int ci = 0;  // dz_[ci] holds dL/d(output of the current layer)
+  ck(dct_loss_fwd_bwd(acts_[L_], 1, y_, dz_[ci], stats_, stats_ + 1, rows, C, 1.0f / (float)rows, loss_kind_, st),
+     "loss");
+  ck(dct_loss_to_slot(stats_, g_ + P_, 1.0f / (float)rows, st), "loss_to_slot");
+  if (reducer_) reducer_->mark_ready(2 * L_, stream);  // the loss slot rides in the last-layer bucket
+  // dz_[ci] = dL/dZ_l (pre-activation gradient of layer l): the loss kernel's dlogits for the
+  // head, then each dX GEMM's activation-derivative epilogue (ReLU mask / GELU') for the layer below.
+  for (int l = L_ - 1; l >= 0; --l) {
+    const int din = dims_[l], dout = dims_[l + 1];
+    const int mask_epi = act_ == ACT_GELU ? EPI_GELU_GRAD : EPI_RELU_MASK;
+    const void* mask_aux = act_ == ACT_GELU ? (const void*)(l > 0 ? pre_[l] : nullptr) : (const void*)acts_[l];
+    if (skinny(l)) {
+      // dW (+ fused db) and dX of a <= 8-output layer as bandwidth kernels
+      ck(dct_skinny_dw(dz_[ci], acts_[l], g_ + woff_[l], g_ + boff_[l], rows, din, dout, st), "skinny dW");
+      if (reducer_) {
+        reducer_->mark_ready(2 * l + 1, stream);
+        reducer_->mark_ready(2 * l, stream);
+      }
+      if (l > 0) {
+        if (act_ == ACT_GELU) {  // GELU' needs the pre-activation: generic GEMM path
+          ck(dct_gemm_bf16(dz_[ci], pb_ + woff_[l], dz_[ci ^ 1], nullptr, rows, din, dout, dout, din, din, 0, 0,
+                           mask_epi, 0, 0, const_cast<void*>(mask_aux), st),
+             "dX gemm");
+        } else {
+          ck(dct_skinny_dx(dz_[ci], pb_ + woff_[l], acts_[l], dz_[ci ^ 1], rows, din, dout, st), "skinny dX");
+        }
+        ci ^= 1;
+      }
+      continue;
+    }
+    // dW = dZ^T A_l (fp32 into the zeroed flat gradient buffer = a DDP bucket view), with the
+    // bias gradient db = colsum(dZ) fused into the same GEMM
+    ck(dct_gemm_bf16_ex(dz_[ci], acts_[l], g_ + woff_[l], nullptr, dout, din, rows, dout, din, din,
+                        /*trans_a*/ 1, /*trans_b*/ 0, EPI_NONE, /*out_f32*/ 1, /*accumulate*/ 1, nullptr,
+                        g_ + boff_[l], st),
+       "dW gemm");
+    if (reducer_) {
+      reducer_->mark_ready(2 * l + 1, stream);
+      reducer_->mark_ready(2 * l, stream);
+    }
+    if (l > 0) {  // dZ_{l-1} = (dZ_l W_l) * act'(.)  in the epilogue
+      ck(dct_gemm_bf16(dz_[ci], pb_ + woff_[l], dz_[ci ^ 1], nullptr, rows, din, dout, dout, din, din,
+                       /*trans_a*/ 0, /*trans_b*/ 0, mask_epi, /*out_f32*/ 0, /*accumulate*/ 0,
+                       const_cast<void*>(mask_aux), st),
+         "dX gemm");
+      ci ^= 1;
+    }
+  }
+  if (reducer_) reducer_->finalize(stream);
+  ck(dct_adam_flat(p_, g_, m_, v_, pb_, P_, lr_, b1_, b2_, eps_, wd_, 1, 1.0f, decoupled_, sc, st), "adam");
+  ck(dct_step_end(cur, g_ + P_, reinterpret_cast<float*>(loss_out), loss_cap, st), "step_end");
+}
+
+void MlpStepExecutor::eval_batch(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t idx, int n_items,
+                                 uintptr_t cursor, int rows, uintptr_t stats, uintptr_t stream) {
+  if (rows < 1 || rows > B_) throw std::invalid_argument("rows must be in [1, batch]");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int* cur = reinterpret_cast<int*>(cursor);
+  ck(dct_gather_batch(reinterpret_cast<const void*>(X), row_bytes, reinterpret_cast<const int*>(Y),
+                      reinterpret_cast<const int*>(idx), cur, B_, rows, n_items, acts_[0], y_, st),
+     "gather_batch");
+  forward(rows, st);
+  float* s = reinterpret_cast<float*>(stats);
+  ck(dct_loss_fwd_bwd(acts_[L_], 1, y_, nullptr, s, s + 1, rows, dims_[L_], 1.0f, loss_kind_, st), "eval loss");
+  ck(dct_step_end(cur, s, nullptr, 0, st), "advance cursor");
+}
+
+}  // namespace dct

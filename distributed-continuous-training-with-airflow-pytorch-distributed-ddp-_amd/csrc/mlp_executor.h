@@ -1,0 +1,54 @@
+// Native graph-capturable training step for wide MLPs (see mlp_executor.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+namespace dct {
+
+class BucketReducer;
+
+class MlpStepExecutor {
+ public:
+  // dims: [d0, d1, ..., dL]; buffers are device pointers owned by the caller:
+  //   p/g/m/v fp32 flat (g has P+1 entries: grads + the loss slot), p_bf16 bf16 flat shadow,
+  //   acts[l] bf16 [batch][d_l] (acts[0] = gathered input, acts[L] = logits),
+  //   pre[l] bf16 [batch][d_l] pre-activations (GELU only), dz0/dz1 bf16 [batch][max d],
+  //   ybuf int32 [batch], stats fp32 [2].
+  MlpStepExecutor(const std::vector<int>& dims, int batch, int act, int loss_kind, uintptr_t p, uintptr_t p_bf16,
+                  uintptr_t g, uintptr_t m, uintptr_t v, const std::vector<uintptr_t>& acts,
+                  const std::vector<uintptr_t>& pre, uintptr_t dz0, uintptr_t dz1, uintptr_t ybuf, uintptr_t stats,
+                  BucketReducer* reducer);
+  void set_adam(float lr, float b1, float b2, float eps, float wd, int decoupled);
+  // One optimizer step on batch *cursor of idx (rows <= batch); advances *cursor and *step_counter.
+  void step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t idx, int n_items, uintptr_t cursor,
+            uintptr_t step_counter, uintptr_t loss_out, int loss_cap, int rows, uintptr_t stream);
+  // Forward + loss/accuracy sums (added into stats[0..1]) on batch *cursor; advances *cursor.
+  void eval_batch(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t idx, int n_items, uintptr_t cursor, int rows,
+                  uintptr_t stats, uintptr_t stream);
+  int64_t num_params() const { return P_; }
+
+ private:
+  void forward(int rows, hipStream_t st);
+  // layers with <= 8 outputs run as bandwidth kernels (csrc/skinny.hip)
+  bool skinny(int l) const { return dims_[l + 1] <= 8 && dims_[l] % 8 == 0 && woff_[l] % 8 == 0; }
+  std::vector<int> dims_;
+  int L_ = 0, B_ = 0, act_ = 1, loss_kind_ = 0;
+  float* p_ = nullptr;
+  uint16_t* pb_ = nullptr;
+  float* g_ = nullptr;
+  float* m_ = nullptr;
+  float* v_ = nullptr;
+  std::vector<uint16_t*> acts_, pre_;
+  uint16_t* dz_[2] = {nullptr, nullptr};
+  int* y_ = nullptr;
+  float* stats_ = nullptr;
+  std::vector<int64_t> woff_, boff_;
+  int64_t P_ = 0;
+  BucketReducer* reducer_ = nullptr;
+  float lr_ = 1e-3f, b1_ = 0.9f, b2_ = 0.999f, eps_ = 1e-8f, wd_ = 0.f;
+  int decoupled_ = 0;
+};
+
+}  // namespace dct

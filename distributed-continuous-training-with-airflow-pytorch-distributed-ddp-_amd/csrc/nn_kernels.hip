@@ -288,7 +288,9 @@ int dct_bias_act_bwd(const void* dY, const void* act_aux, uint16_t* dZ, float* d
                      int accumulate_bias, void* stream) {
   if (M <= 0 || N <= 0) return 0;
   const int ncc = (N + 7) / 8;
-  dim3 grid((ncc + 63) / 64, (unsigned)grid_cap((M + 3) / 4, 1, 512));
+  // row blocks of >= 64 rows: few float atomics per column (a 512-way atomicAdd fan-in on the
+  // same 1024 addresses serialised this kernel to ~100 us at M = 4096)
+  dim3 grid((ncc + 63) / 64, (unsigned)grid_cap((M + 63) / 64, 1, 64));
   const bool vec = (N % 8 == 0) && (ldy % 8 == 0) && ((((uintptr_t)dY) | ((uintptr_t)act_aux) | ((uintptr_t)dZ)) & 15) == 0;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (vec)

@@ -1,0 +1,199 @@
+// Skinny layers: C <= 8 outputs (the classifier head of the tabular / TabTransformer models).
+//
+// A 128x128 MFMA tile would compute 2 useful columns out of 128, and the dW of such a layer
+// (2 x 1024 with K = batch) has too few rows for any tile shape.  These layers are HBM
+// streams, so they are written as bandwidth kernels: 16-byte loads, fp32 accumulation, the
+// tiny weight panel read through the cache, wave reductions by shuffles.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dct_common.h"
+
+namespace dct {
+
+constexpr int SK_CMAX = 8;
+
+__device__ __forceinline__ void unpack8(const uint4& v, float (&f)[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[2 * j] = bf16_to_f32(w[j] & 0xffff);
+    f[2 * j + 1] = bf16_to_f32(w[j] >> 16);
+  }
+}
+
+// Y[b][c] = X[b] . W[c] + bias[c]: one wave per row, each lane 8 k per 512-k chunk
+__global__ __launch_bounds__(256) void skinny_fwd_kernel(const uint16_t* __restrict__ X,
+                                                         const uint16_t* __restrict__ W,
+                                                         const float* __restrict__ bias, uint16_t* __restrict__ Y,
+                                                         int B, int K, int C) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  float acc[SK_CMAX];
+#pragma unroll
+  for (int c = 0; c < SK_CMAX; ++c) acc[c] = 0.f;
+  for (int k = lane * 8; k < K; k += 512) {
+    float x[8];
+    unpack8(*reinterpret_cast<const uint4*>(X + (size_t)b * K + k), x);
+#pragma unroll
+    for (int c = 0; c < SK_CMAX; ++c) {
+      if (c < C) {
+        float w[8];
+        unpack8(*reinterpret_cast<const uint4*>(W + (size_t)c * K + k), w);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[c] += x[e] * w[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < SK_CMAX; ++c) {
+    if (c < C) {
+      float v = wave_sum(acc[c]);
+      if (lane == 0) Y[(size_t)b * C + c] = f32_to_bf16(v + (bias ? bias[c] : 0.f));
+    }
+  }
+}
+
+// dX[b][k..k+8) = sum_c dZ[b][c] W[c][k..k+8)  (masked by the ReLU output aux > 0)
+__global__ __launch_bounds__(256) void skinny_dx_kernel(const uint16_t* __restrict__ dZ,
+                                                        const uint16_t* __restrict__ W,
+                                                        const uint16_t* __restrict__ aux, uint16_t* __restrict__ dX,
+                                                        int B, int K, int C) {
+  const int kv = K / 8;
+  const int64_t total = (int64_t)B * kv;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(e / kv);
+    const int k = (int)(e - (int64_t)b * kv) * 8;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = 0.f;
+#pragma unroll
+    for (int c = 0; c < SK_CMAX; ++c) {
+      if (c < C) {
+        const float dz = bf16_to_f32(dZ[(size_t)b * C + c]);
+        float w[8];
+        unpack8(*reinterpret_cast<const uint4*>(W + (size_t)c * K + k), w);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += dz * w[j];
+      }
+    }
+    const size_t off = (size_t)b * K + k;
+    if (aux) {
+      float a[8];
+      unpack8(*reinterpret_cast<const uint4*>(aux + off), a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = a[j] > 0.f ? o[j] : 0.f;
+    }
+    uint4 v;
+    v.x = f32_to_bf16(o[0]) | ((uint32_t)f32_to_bf16(o[1]) << 16);
+    v.y = f32_to_bf16(o[2]) | ((uint32_t)f32_to_bf16(o[3]) << 16);
+    v.z = f32_to_bf16(o[4]) | ((uint32_t)f32_to_bf16(o[5]) << 16);
+    v.w = f32_to_bf16(o[6]) | ((uint32_t)f32_to_bf16(o[7]) << 16);
+    *reinterpret_cast<uint4*>(dX + off) = v;
+  }
+}
+
+// dW[c][k] += sum_b dZ[b][c] X[b][k], db[c] += sum_b dZ[b][c].
+// Block: 64 lanes x 8 k = 512 columns, 4 row lanes; blockIdx.y splits the rows.
+__global__ __launch_bounds__(256) void skinny_dw_kernel(const uint16_t* __restrict__ dZ,
+                                                        const uint16_t* __restrict__ X, float* __restrict__ dW,
+                                                        float* __restrict__ db, int B, int K, int C, int rows_per) {
+  __shared__ float red[4][SK_CMAX][64 * 8 + 1];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int k = (blockIdx.x * 64 + tx) * 8;
+  const int r0 = blockIdx.y * rows_per;
+  const int r1 = min(B, r0 + rows_per);
+  float acc[SK_CMAX][8];
+  float dbs[SK_CMAX];
+#pragma unroll
+  for (int c = 0; c < SK_CMAX; ++c) {
+    dbs[c] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
+  }
+  if (k < K) {
+    for (int b = r0 + ty; b < r1; b += 4) {
+      float x[8];
+      unpack8(*reinterpret_cast<const uint4*>(X + (size_t)b * K + k), x);
+#pragma unroll
+      for (int c = 0; c < SK_CMAX; ++c) {
+        if (c < C) {
+          const float dz = bf16_to_f32(dZ[(size_t)b * C + c]);
+          dbs[c] += dz;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[c][j] += dz * x[j];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < SK_CMAX; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[ty][c][tx * 8 + j] = acc[c][j];
+  __syncthreads();
+  if (ty == 0 && k < K) {
+#pragma unroll
+    for (int c = 0; c < SK_CMAX; ++c) {
+      if (c < C) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = red[0][c][tx * 8 + j] + red[1][c][tx * 8 + j] + red[2][c][tx * 8 + j] + red[3][c][tx * 8 + j];
+          atomicAdd(dW + (size_t)c * K + k + j, v);
+        }
+      }
+    }
+  }
+  if (db && blockIdx.x == 0) {  // bias grads: lane 0 of each row lane saw every row of its stride
+    __syncthreads();
+    if (tx == 0) {
+#pragma unroll
+      for (int c = 0; c < SK_CMAX; ++c) red[ty][c][0] = dbs[c];
+    }
+    __syncthreads();
+    if (threadIdx.x < C) {
+      const int c = threadIdx.x;
+      atomicAdd(db + c, red[0][c][0] + red[1][c][0] + red[2][c][0] + red[3][c][0]);
+    }
+  }
+}
+
+}  // namespace dct
+
+extern "C" {
+
+int dct_skinny_fwd(const uint16_t* X, const uint16_t* W, const float* bias, uint16_t* Y, int B, int K, int C,
+                   void* stream) {
+  if (C > dct::SK_CMAX || K % 8 || (((uintptr_t)X | (uintptr_t)W) & 15)) return (int)hipErrorInvalidValue;
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(dct::skinny_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), X,
+                     W, bias, Y, B, K, C);
+  return (int)hipGetLastError();
+}
+
+int dct_skinny_dx(const uint16_t* dZ, const uint16_t* W, const uint16_t* aux, uint16_t* dX, int B, int K, int C,
+                  void* stream) {
+  if (C > dct::SK_CMAX || K % 8 || (((uintptr_t)W | (uintptr_t)dX | (uintptr_t)aux) & 15))
+    return (int)hipErrorInvalidValue;
+  if (B <= 0) return 0;
+  const int64_t total = (int64_t)B * (K / 8);
+  int grid = (int)((total + 255) / 256);
+  grid = grid > 4096 ? 4096 : grid;
+  hipLaunchKernelGGL(dct::skinny_dx_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), dZ, W,
+                     aux, dX, B, K, C);
+  return (int)hipGetLastError();
+}
+
+int dct_skinny_dw(const uint16_t* dZ, const uint16_t* X, float* dW, float* db, int B, int K, int C, void* stream) {
+  if (C > dct::SK_CMAX || K % 8 || (((uintptr_t)X) & 15)) return (int)hipErrorInvalidValue;
+  if (B <= 0) return 0;
+  const int kb = (K + 511) / 512;
+  int splits = (B + 63) / 64;  // >= 64 rows per block
+  splits = splits > 128 ? 128 : splits;
+  const int rows_per = (B + splits - 1) / splits;
+  hipLaunchKernelGGL(dct::skinny_dw_kernel, dim3(kb, splits), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), dZ,
+                     X, dW, db, B, K, C, rows_per);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -77,8 +77,10 @@ def weather_tensors(n: int, seed: int = 0, dim: int = 5):
 
 
 def make_tabular_device(rows: int, feats: int, num_classes: int = 2, device="cuda", dtype=None,
-                        seed: int = 0, chunk: int = 1 << 24):
-    """Large synthetic tabular set generated in place on the device (chunked, no host copy)."""
+                        seed: int = 0, chunk: int = 1 << 22):
+    """Large synthetic tabular set generated in place on the device (chunked, no host copy).
+
+    Chunks stay below 2^31 fp32 elements per GEMV (hipBLAS fails on larger operands)."""
     import torch
 
     dtype = dtype or torch.bfloat16

@@ -89,10 +89,11 @@ def build_mlp(name: str, input_dim: int, hidden: Optional[Sequence[int]] = None,
               dropout: float = 0.2, loss: str = "ce", lr: float = 0.01) -> MLPClassifier:
     if name == "weather":
         return WeatherClassifier(input_dim)
+    # name -> (hidden widths, dropout, loss, lr); BASELINE.json configs 1-4
     presets = {
-        "weather-mlp-3x128": ((128, 128), 0.2),
-        "tabular-mlp-4x1024": ((1024, 1024, 1024), 0.0),
+        "weather-mlp-3x128": ((128, 128), 0.2, "ce", 0.01),
+        "tabular-mlp-4x1024": ((1024, 1024, 1024), 0.0, "mse", 1e-3),
     }
     if name in presets and hidden is None:
-        hidden, dropout = presets[name]
+        hidden, dropout, loss, lr = presets[name]
     return MLPClassifier(input_dim, hidden=hidden or (64,), num_classes=num_classes, dropout=dropout, loss=loss, lr=lr)

@@ -70,6 +70,7 @@ class _EngineBase:
 # ================================================================================ fused
 class FusedMLPEngine(_EngineBase):
     name = "fused"
+    epoch_engine = True  # runs whole epochs on device; the Trainer reads back per-step losses
 
     @staticmethod
     def applicable(model, device: torch.device, batch_size: int) -> bool:

@@ -31,6 +31,7 @@ from ..data.dataset import dataset_tensors
 from ..data.sampler import distributed_indices
 from ..parallel.dist import DistContext, init_distributed, shutdown
 from .engines import AutogradEngine, FusedMLPEngine, adam_hparams_from
+from .graph_engine import GraphMLPEngine
 
 
 def seed_everything(seed: int = 42) -> int:
@@ -213,6 +214,11 @@ class Trainer:
             return FusedMLPEngine(model, ctx, batch_size, seed, adam, steps_per_launch=self.steps_per_launch)
         if choice == "fused":
             raise RuntimeError("engine='fused' requested but the model/device/batch is not supported by it")
+        if choice in ("auto", "graph") and adam is not None and GraphMLPEngine.applicable(model, ctx.device, batch_size):
+            return GraphMLPEngine(model, ctx, batch_size, seed, adam, self.strategy.bucket_cap_bytes,
+                                  self.strategy.first_bucket_bytes)
+        if choice == "graph":
+            raise RuntimeError("engine='graph' requested but the model/device is not supported by it")
         model.to(ctx.device)
         return AutogradEngine(model, ctx, batch_size, seed, self.strategy.bucket_cap_bytes,
                               self.strategy.first_bucket_bytes)
@@ -334,7 +340,7 @@ class Trainer:
     def _train_epoch(self, epoch: int, B: int, shuffle: bool) -> int:
         self._stage = "train"
         eng = self.engine
-        if isinstance(eng, FusedMLPEngine):
+        if getattr(eng, "epoch_engine", False):
             losses = eng.train_epoch(epoch, shuffle)
             n = losses.numel()
             first = self.global_step
@@ -377,7 +383,7 @@ class Trainer:
         self._stage = "sanity" if sanity else "val"
         eng = self.engine
         try:
-            if isinstance(eng, FusedMLPEngine):
+            if getattr(eng, "epoch_engine", False):
                 limit = None if limit_batches is None else limit_batches * VB
                 vl, va = eng.validate(limit=limit)
                 return {} if sanity else {"val_loss": vl, "val_acc": va}

@@ -1,0 +1,121 @@
+"""Wide-MLP graph-captured step (csrc/mlp_executor.cpp + trainer/graph_engine.py) against a
+plain-torch fp32 reference of the same step (bf16 operands -> bf16-level tolerances)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import dct_amd  # noqa: F401
+from dct_amd.models.mlp import MLPClassifier
+from dct_amd.parallel.dist import init_distributed
+from dct_amd.trainer.engines import adam_hparams_from
+from dct_amd.trainer.graph_engine import GraphMLPEngine
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, d, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(n, d, generator=g)
+    w = torch.randn(d, generator=g)
+    Y = ((X @ w) > 0).long()
+    return X, Y
+
+
+def _engine(dims, B, loss="mse", lr=1e-3, use_graph=True):
+    torch.manual_seed(0)
+    model = MLPClassifier(dims[0], hidden=tuple(dims[1:-1]), num_classes=dims[-1], dropout=0.0, loss=loss, lr=lr)
+    ctx = init_distributed("gpu")
+    eng = GraphMLPEngine(model, ctx, B, seed=42, adam=adam_hparams_from(model.configure_optimizers()),
+                         use_graph=use_graph)
+    return model, eng
+
+
+@pytest.mark.parametrize("loss", ["mse", "ce"])
+@pytest.mark.parametrize("dims,B", [([64, 256, 256, 2], 64), ([256, 1024, 1024, 1024, 2], 256), ([32, 96, 3], 50)])
+def test_one_step_gradients_match_torch(dims, B, loss, cuda):
+    """lr = 0: one executor step leaves the weights and exposes g = dL/dp; compare with autograd
+    on the same bf16-rounded inputs and weights."""
+    model, eng = _engine(dims, B, loss=loss, lr=0.0)
+    X, Y = _data(4 * B, dims[0])
+    Y = Y % dims[-1]
+    rows = torch.arange(4 * B)
+    eng.attach_data(X, Y, rows, rows[:B])
+    eng.idx[:B].copy_(torch.arange(B, dtype=torch.int32))
+    loss_out = torch.zeros(1, device=cuda)
+    eng.cursor.zero_()
+    eng._step(B, loss_out, B)
+    torch.cuda.synchronize()
+    # reference: fp32 autograd on bf16-rounded data/weights
+    ref = MLPClassifier(dims[0], hidden=tuple(dims[1:-1]), num_classes=dims[-1], dropout=0.0, loss=loss)
+    with torch.no_grad():
+        for (n, t), (_, t0) in zip(ref.state_dict().items(), model.state_dict().items()):
+            t.copy_(t0.to(torch.bfloat16).float() if "weight" in n else t0)
+    xb = X[:B].to(torch.bfloat16).float()
+    # forward values rounded to bf16 after every layer like the kernels' bf16 activations
+    # (straight-through: the rounding does not enter the gradient)
+    h = xb
+    for mod in ref.net:
+        h = mod(h)
+        if isinstance(mod, torch.nn.Linear):
+            h = h + (h.to(torch.bfloat16).float() - h).detach()
+    logits = h
+    if loss == "ce":
+        lref = F.cross_entropy(logits, Y[:B])
+    else:
+        lref = F.mse_loss(logits, F.one_hot(Y[:B], dims[-1]).float())
+    lref.backward()
+    want = torch.cat([p.grad.reshape(-1) for p in ref.parameters()])
+    got = eng.g[: eng.P].cpu()
+    rel = (got - want).norm() / want.norm()
+    assert rel < 4e-2, rel
+    assert abs(float(loss_out.item()) - lref.item()) < 2e-2 * max(1.0, abs(lref.item()))
+    assert int(eng.cursor.item()) == 1 and int(eng.step_counter.item()) == 1
+
+
+def test_graph_replay_equals_eager_and_learns(cuda):
+    dims, B = [64, 256, 256, 2], 128
+    X, Y = _data(40 * B + 37, dims[0], seed=3)
+    n = X.shape[0]
+    res = []
+    for use_graph in (True, False):
+        model, eng = _engine(dims, B, lr=1e-3, use_graph=use_graph)
+        rows = torch.arange(n)
+        eng.attach_data(X, Y, rows[: 40 * B + 37], rows[:512])
+        losses = []
+        for ep in range(3):
+            losses.append(eng.train_epoch(ep).cpu())
+        torch.cuda.synchronize()
+        assert eng.graph_used == use_graph
+        res.append((torch.cat(losses), eng.p.cpu(), eng))
+    (l_g, p_g, eg), (l_e, p_e, _) = res
+    assert l_g.numel() == 3 * math.ceil((40 * B + 37) / B)
+    # bias grads and split-K dW use float atomics: runs agree to rounding, not bit for bit (and
+    # Adam turns rounding noise on ~0 gradients into +-lr steps), so compare in norm
+    assert torch.allclose(l_g, l_e, atol=1e-3), (l_g - l_e).abs().max()
+    assert (p_g - p_e).norm() / p_e.norm() < 1e-2
+    assert l_g[-10:].mean() < l_g[:10].mean()
+    vl, va = eg.validate()
+    assert va > 0.7
+
+
+def test_trainer_fit_graph_engine_writes_checkpoint(tmp_path, cuda):
+    from torch.utils.data import DataLoader, TensorDataset
+
+    from dct_amd.ckpt import ModelCheckpoint, load_checkpoint
+    from dct_amd.trainer import Trainer
+
+    X, Y = _data(3000, 64, seed=1)
+    ds = TensorDataset(X, Y)
+    tl = DataLoader(torch.utils.data.Subset(ds, range(2400)), batch_size=256, shuffle=True)
+    vl = DataLoader(torch.utils.data.Subset(ds, range(2400, 3000)), batch_size=256)
+    model = MLPClassifier(64, hidden=(128, 128), dropout=0.0, loss="mse", lr=1e-3)
+    ck = ModelCheckpoint(dirpath=str(tmp_path), filename="best-{epoch:02d}", monitor="val_loss", mode="min",
+                         save_top_k=1, save_last=True)
+    tr = Trainer(max_epochs=2, accelerator="gpu", callbacks=[ck], engine="graph", verbose=False)
+    tr.fit(model, tl, vl)
+    assert tr.engine.name == "graph"
+    sd = load_checkpoint(str(tmp_path / "last.ckpt"))["state_dict"]
+    assert set(sd) == set(model.state_dict())
+    assert tr.callback_metrics["val_loss"] < 0.5

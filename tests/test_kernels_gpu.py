@@ -190,9 +190,12 @@ def _bf(x):
     return x.to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 200, 72), (1, 17, 8), (257, 1024, 256), (64, 3, 1024)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 200, 72), (1, 17, 8), (257, 1024, 256), (64, 3, 1024),
+                                   (136, 264, 128), (512, 256, 2048), (1024, 1024, 4096), (2, 1024, 512)])
 @pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
 def test_gemm_bf16(M, N, K, ta, tb, cuda):
+    """fp32 out; covers the LDS-DMA/transpose-read fast path (K % 64 == 0), its split-K form
+    (few tiles, long K) and the generic fallback (odd K / unaligned shapes)."""
     torch.manual_seed(6)
     A = torch.randn(M, K, device=cuda)
     B = torch.randn(K, N, device=cuda)
@@ -206,6 +209,33 @@ def test_gemm_bf16(M, N, K, ta, tb, cuda):
     ref = (As.float().t() if ta else As.float()) @ (Bs.float().t() if tb else Bs.float())
     torch.cuda.synchronize()
     assert torch.allclose(C, ref, atol=2e-3 * math.sqrt(K), rtol=1e-3)
+    # accumulate=1 adds onto C (split-K slices add atomically onto the existing values)
+    nat.gemm_bf16(As.data_ptr(), Bs.data_ptr(), C.data_ptr(), 0, M, N, K, As.stride(0), Bs.stride(0), N, ta, tb, 0, 1,
+                  1, 0, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.allclose(C, 2 * ref, atol=4e-3 * math.sqrt(K), rtol=2e-3)
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0)])
+def test_gemm_bf16_out_and_fast_path_match_generic(ta, tb, cuda, monkeypatch):
+    """bf16 output; the fast path and the generic kernel agree."""
+    torch.manual_seed(9)
+    M, N, K = 384, 512, 640
+    A = _bf(torch.randn(K, M, device=cuda) if ta else torch.randn(M, K, device=cuda))
+    B = _bf(torch.randn(N, K, device=cuda) if tb else torch.randn(K, N, device=cuda))
+    nat = native()
+    outs = []
+    for v1 in ("0", "1"):
+        if v1 == "1":
+            monkeypatch.setenv("DCT_GEMM_V1", "1")
+        C = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+        nat.gemm_bf16(A.data_ptr(), B.data_ptr(), C.data_ptr(), 0, M, N, K, A.stride(0), B.stride(0), N, ta, tb, 0, 0,
+                      0, 0, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append(C.float())
+    ref = (A.float().t() if ta else A.float()) @ (B.float().t() if tb else B.float())
+    assert torch.allclose(outs[0], ref, atol=0.3, rtol=2e-2)
+    assert torch.allclose(outs[0], outs[1], atol=0.25, rtol=1e-2)
 
 
 @pytest.mark.parametrize("epi", [1, 2, 3])
@@ -350,3 +380,68 @@ def test_gather_rows(cuda):
     native().gather_rows(src.data_ptr(), idx.data_ptr(), dst.data_ptr(), 333, 48, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert torch.equal(dst, src[idx.long()])
+
+
+def test_gemm_fused_bias_grad_and_mask_epilogues(cuda):
+    """dW GEMM with the bias gradient fused (colsum) and the dX GEMM's ReLU-mask / GELU' epilogues."""
+    torch.manual_seed(10)
+    nat = native()
+    st = torch.cuda.current_stream().cuda_stream
+    Bt, Dout, Din = 512, 256, 128
+    dZ = _bf(torch.randn(Bt, Dout, device=cuda))
+    A = _bf(torch.randn(Bt, Din, device=cuda))
+    for v1 in (False, True):
+        dW = torch.zeros(Dout, Din, device=cuda)
+        db = torch.zeros(Dout, device=cuda)
+        if v1:
+            import os
+            os.environ["DCT_GEMM_V1"] = "1"
+        try:
+            nat.gemm_bf16_ex(dZ.data_ptr(), A.data_ptr(), dW.data_ptr(), 0, Dout, Din, Bt, Dout, Din, Din, 1, 0, 0, 1,
+                             1, 0, db.data_ptr(), st)
+        finally:
+            import os
+            os.environ.pop("DCT_GEMM_V1", None)
+        torch.cuda.synchronize()
+        assert torch.allclose(dW, dZ.float().t() @ A.float(), atol=0.1, rtol=1e-2)
+        assert torch.allclose(db, dZ.float().sum(0), atol=0.05, rtol=1e-3)
+    W = _bf(torch.randn(Dout, Din, device=cuda) * 0.1)
+    act = _bf(torch.relu(torch.randn(Bt, Din, device=cuda)))
+    out = torch.empty(Bt, Din, device=cuda, dtype=torch.bfloat16)
+    nat.gemm_bf16(dZ.data_ptr(), W.data_ptr(), out.data_ptr(), 0, Bt, Din, Dout, Dout, Din, Din, 0, 0,
+                  nat.EPI_RELU_MASK, 0, 0, act.data_ptr(), st)
+    torch.cuda.synchronize()
+    ref = (dZ.float() @ W.float()) * (act.float() > 0)
+    assert torch.allclose(out.float(), ref, atol=5e-2, rtol=2e-2)
+    pre = _bf(torch.randn(Bt, Din, device=cuda))
+    nat.gemm_bf16(dZ.data_ptr(), W.data_ptr(), out.data_ptr(), 0, Bt, Din, Dout, Dout, Din, Din, 0, 0,
+                  nat.EPI_GELU_GRAD, 0, 0, pre.data_ptr(), st)
+    torch.cuda.synchronize()
+    z = pre.float().requires_grad_(True)
+    F.gelu(z).backward(dZ.float() @ W.float())
+    assert torch.allclose(out.float(), z.grad, atol=5e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("C", [1, 2, 3, 8])
+def test_skinny_head_kernels(C, cuda):
+    torch.manual_seed(11)
+    nat = native()
+    st = torch.cuda.current_stream().cuda_stream
+    Bt, K = 777, 1024
+    X = _bf(torch.randn(Bt, K, device=cuda))
+    W = _bf(torch.randn(C, K, device=cuda) * 0.05)
+    b = torch.randn(C, device=cuda)
+    Y = torch.empty(Bt, C, device=cuda, dtype=torch.bfloat16)
+    nat.skinny_fwd(X.data_ptr(), W.data_ptr(), b.data_ptr(), Y.data_ptr(), Bt, K, C, st)
+    dZ = _bf(torch.randn(Bt, C, device=cuda))
+    act = _bf(torch.relu(torch.randn(Bt, K, device=cuda)))
+    dX = torch.empty(Bt, K, device=cuda, dtype=torch.bfloat16)
+    nat.skinny_dx(dZ.data_ptr(), W.data_ptr(), act.data_ptr(), dX.data_ptr(), Bt, K, C, st)
+    dW = torch.zeros(C, K, device=cuda)
+    db = torch.zeros(C, device=cuda)
+    nat.skinny_dw(dZ.data_ptr(), X.data_ptr(), dW.data_ptr(), db.data_ptr(), Bt, K, C, st)
+    torch.cuda.synchronize()
+    assert torch.allclose(Y.float(), X.float() @ W.float().t() + b, atol=3e-2, rtol=2e-2)
+    assert torch.allclose(dX.float(), (dZ.float() @ W.float()) * (act.float() > 0), atol=2e-2, rtol=2e-2)
+    assert torch.allclose(dW, dZ.float().t() @ X.float(), atol=5e-2, rtol=1e-3)
+    assert torch.allclose(db, dZ.float().sum(0), atol=1e-2, rtol=1e-3)
