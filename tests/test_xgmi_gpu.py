@@ -54,13 +54,10 @@ def ddp_reference(net, X, Y, shards, B, steps, lr=0.01):
     return _flat(net), torch.tensor(losses)
 
 
-@pytest.mark.parametrize("W", [2])
-def test_in_process_exchange_matches_ddp_reference(W, cuda):
-    """W 'ranks' as concurrent single-wave kernels on W streams of one GPU, peers = raw pointers.
-    (W = 2 only: streams of one process share GPU_MAX_HW_QUEUES hardware queues, so more
-    in-process ranks may be serialised behind each other; W > 2 runs as processes below.)"""
+def _in_process_run(W, steps, B, out_path):
+    """W 'ranks' as concurrent single-wave kernels on W streams of one GPU, peers = raw pointers."""
     nat = native()
-    B, steps = 4, 120
+    cuda = torch.device("cuda", 0)
     kern = FusedMLPKernel([5, 64, 2], bmax=4)
     assert kern.xg_supported(B)
     xs = [nat.PeerExchange(W, r, kern.xg_buffer_bytes(W)) for r in range(W)]
@@ -68,8 +65,7 @@ def test_in_process_exchange_matches_ddp_reference(W, cuda):
         x.set_peers([y.recv for y in xs])
     X, Y = weather_tensors(3000, seed=5)
     shards = [distributed_indices(3000, W, r, shuffle=True, seed=42, epoch=0) for r in range(W)]
-    net = _net(1)
-    p0 = _flat(net)
+    p0 = _flat(_net(1))
     ps = [p0.clone().to(cuda) for _ in range(W)]
     ms = [torch.zeros_like(ps[0]) for _ in range(W)]
     vs = [torch.zeros_like(ps[0]) for _ in range(W)]
@@ -84,15 +80,33 @@ def test_in_process_exchange_matches_ddp_reference(W, cuda):
                    lr=0.01, loss_out=losses[r], step_counter=scs[r], xg=xs[r], xg_timeout_s=5.0,
                    stream=streams[r].cuda_stream)
     torch.cuda.synchronize()
-    assert [x.read_status() for x in xs] == [0] * W
-    assert all(int(sc.item()) == steps for sc in scs)
-    for r in range(1, W):  # bit-identical replicas, identical synced losses
-        assert torch.equal(ps[r], ps[0])
-        assert torch.equal(losses[r], losses[0])
-    want, want_l = ddp_reference(net, X, Y, shards, B, steps)
-    err = (ps[0].cpu() - want).abs()
+    json.dump({"status": [x.read_status() for x in xs], "steps": [int(sc.item()) for sc in scs],
+               "params": [p.cpu().tolist() for p in ps], "losses": [l.cpu().tolist() for l in losses]},
+              open(out_path, "w"))
+
+
+def test_in_process_exchange_matches_ddp_reference(tmp_path, cuda):
+    """Runs in a fresh process: streams of one process share GPU_MAX_HW_QUEUES hardware queues
+    round-robin, so after other tests created streams the two 'ranks' could land on one queue
+    and serialise (W > 2 runs as separate processes below)."""
+    W, B, steps = 2, 4, 120
+    out = tmp_path / "inproc.json"
+    code = (f"import sys; sys.path.insert(0, {ROOT!r}); sys.path.insert(0, {os.path.join(ROOT, 'tests')!r}); "
+            f"import test_xgmi_gpu as t; t._in_process_run({W}, {steps}, {B}, {str(out)!r})")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    res = json.loads(out.read_text())
+    assert res["status"] == [0] * W and res["steps"] == [steps] * W
+    ps = [torch.tensor(p) for p in res["params"]]
+    ls = [torch.tensor(l) for l in res["losses"]]
+    for r_ in range(1, W):  # bit-identical replicas, identical synced losses
+        assert torch.equal(ps[r_], ps[0]) and torch.equal(ls[r_], ls[0])
+    X, Y = weather_tensors(3000, seed=5)
+    shards = [distributed_indices(3000, W, r_, shuffle=True, seed=42, epoch=0) for r_ in range(W)]
+    want, want_l = ddp_reference(_net(1), X, Y, shards, B, steps)
+    err = (ps[0] - want).abs()
     assert err.median() < 1e-5 and err.max() < 2e-3, (err.median(), err.max())
-    assert torch.allclose(losses[0].cpu(), want_l, atol=2e-4, rtol=1e-3)
+    assert torch.allclose(ls[0], want_l, atol=2e-4, rtol=1e-3)
 
 
 def test_exchange_timeout_is_bounded_and_reported(cuda):
