@@ -9,6 +9,9 @@ the sync_dist train_loss.  Other BASELINE.json configs:
   --model weather-mlp-3x128    3-layer / 128-h weather MLP (fused single-CU kernel)
   --model tabular-mlp-4x1024   100M x 256 synthetic rows (bf16, HBM-resident), 256-1024-1024-1024-2
                                MLP, MSE, Adam(1e-3), batch 4096 per rank, graph-captured MFMA step
+  --model tabtransformer       4-layer TabTransformer over 64 feature tokens (d 64, 4 heads), CE,
+                               Adam(1e-3), batch 512 per rank, HIP GEMM/LayerNorm/attention kernels,
+                               autograd step captured in a HIP graph
 Data: synthetic rows (no network), random-init weights.
 
 Timed region: exactly K optimizer steps, bracketed by barrier + device synchronize on both
@@ -33,6 +36,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 # The reference publishes no number (BASELINE.json "published": {}); this probe is the only one.
 BASELINE_SAMPLES_PER_SEC = {"weather": 8500.0}
 TABULAR = ("tabular-mlp-4x1024",)
+TRANSFORMER = ("tabtransformer",)
 
 
 def parse():
@@ -48,10 +52,12 @@ def parse():
                    help="dataset size used for the reported epoch wall-clock (weather 100k, tabular 100M)")
     a = p.parse_args()
     tab = a.model in TABULAR
-    a.steps = a.steps if a.steps is not None else (200 if tab else 20000)
-    a.warmup = a.warmup if a.warmup is not None else (20 if tab else 2000)
-    a.batch = a.batch if a.batch is not None else (4096 if tab else 4)
-    a.epoch_rows = a.epoch_rows if a.epoch_rows is not None else (100_000_000 if tab else 100_000)
+    tt = a.model in TRANSFORMER
+    a.steps = a.steps if a.steps is not None else (200 if (tab or tt) else 20000)
+    a.warmup = a.warmup if a.warmup is not None else (20 if (tab or tt) else 2000)
+    a.batch = a.batch if a.batch is not None else (4096 if tab else (512 if tt else 4))
+    a.epoch_rows = a.epoch_rows if a.epoch_rows is not None else (
+        100_000_000 if tab else (10_000_000 if tt else 100_000))
     return a
 
 
@@ -129,6 +135,54 @@ def setup_tabular(a, ctx):
     return eng, feats
 
 
+class _StepLoop:
+    """run_steps() over an AutogradEngine (one train_step per batch of the local shard)."""
+
+    def __init__(self, eng, ctx):
+        self.eng, self.ctx = eng, ctx
+
+    def upload_epoch_indices(self, epoch, shuffle=True):
+        local = self.eng.epoch_local_indices(len(self.eng.train_rows), epoch, shuffle)
+        self.rows = self.eng.train_rows[local].to(self.eng.device)
+        return self.rows.numel()
+
+    def run_steps(self, n_items, steps, loss_out, first_step=0):
+        B = self.eng.B
+        for s in range(first_step, first_step + steps):
+            loss_out[s] = self.eng.train_step(self.rows[s * B:(s + 1) * B], s)
+
+    def validate(self, limit=None):
+        import torch
+
+        eng = self.eng
+        rows = eng.val_rows[: (limit or len(eng.val_rows))].to(eng.device)
+        with torch.no_grad():
+            eng.model.eval()
+            logits = eng.model(eng.X[rows])
+            loss = torch.nn.functional.cross_entropy(logits, eng.Y[rows])
+            acc = (logits.argmax(1) == eng.Y[rows]).float().mean()
+            eng.model.train()
+        return float(loss), float(acc)
+
+
+def setup_transformer(a, ctx):
+    import torch
+
+    from dct_amd.data.synthetic import make_tabular_device
+    from dct_amd.models import build_model
+    from dct_amd.trainer.engines import AutogradEngine
+
+    feats = 64
+    rows = a.rows or 10_000_000
+    X, Y = make_tabular_device(rows, feats, num_classes=2, device=ctx.device, dtype=torch.float32, seed=0)
+    model = build_model("tabtransformer", feats, d_model=64, heads=4, layers=4, lr=1e-3)
+    eng = AutogradEngine(model, ctx, a.batch, seed=42)
+    n_train = int(0.8 * rows)
+    perm = torch.randperm(rows, generator=torch.Generator().manual_seed(42))
+    eng.attach_data(X, Y, perm[:n_train], perm[n_train:])
+    return eng, feats
+
+
 def main():
     a = parse()
     import torch
@@ -143,23 +197,32 @@ def main():
     ctx = init_distributed("gpu")
     seed_everything(42)
     tab = a.model in TABULAR
-    eng, feats = (setup_tabular if tab else setup_weather)(a, ctx)
+    tt = a.model in TRANSFORMER
+    if tt:
+        eng, feats = setup_transformer(a, ctx)
+        loop = _StepLoop(eng, ctx)
+    else:
+        eng, feats = (setup_tabular if tab else setup_weather)(a, ctx)
+        loop = eng
     total_steps = a.warmup + a.steps
-    n_items = eng.upload_epoch_indices(0, shuffle=True)
+    n_items = loop.upload_epoch_indices(0, shuffle=True)
     if total_steps * a.batch > n_items:
         raise SystemExit(f"dataset too small: {total_steps} steps x {a.batch} > {n_items} rows per rank")
     loss = torch.zeros(total_steps, dtype=torch.float32, device=ctx.device)
 
     # warmup (also builds / captures the step graphs outside the timed region)
-    eng.run_steps(n_items, a.warmup, loss, first_step=0)
+    loop.run_steps(n_items, a.warmup, loss, first_step=0)
     if getattr(eng, "xg", None) is not None and not eng.xg_verify(fallback=True):
         eng.run_steps(n_items, a.warmup, loss, first_step=0)  # re-warm on the RCCL path
-    if not tab and eng.ddp and eng.xg is None and eng.use_graph:
+    if not (tab or tt) and eng.ddp and eng.xg is None and eng.use_graph:
         eng._get_graph(n_items, min(eng.graph_chunk, a.steps), loss)
-    dt = _timed(ctx, lambda: eng.run_steps(n_items, a.steps, loss, first_step=a.warmup))
+    dt = _timed(ctx, lambda: loop.run_steps(n_items, a.steps, loss, first_step=a.warmup))
 
     xg_ok = eng.xg_verify(fallback=True) if getattr(eng, "xg", None) is not None else None
-    if tab:
+    if tt:
+        engine_desc = ("autograd(hip gemm/layernorm/attention)" + ("+rccl-bucket-allreduce" if ctx.is_distributed
+                                                                    else "") + ("+hipgraph" if eng.graph_used else ""))
+    elif tab:
         engine_desc = ("graph-mlp-executor(bf16 mfma gemm)" + ("+rccl-bucket-allreduce" if ctx.is_distributed else "")
                        + ("+hipgraph" if eng.graph_used else ""))
     elif eng.xg is not None or eng.ddp:
@@ -168,13 +231,13 @@ def main():
             + ("+hipgraph" if eng.graph_used else ""))
     else:
         engine_desc = "fused-persistent"
-    in_sync = _params_in_sync(ctx, eng.p)
+    in_sync = _params_in_sync(ctx, eng.flat_p if tt else eng.p)
     losses = loss.cpu()
     finite = bool(torch.isfinite(losses).all())
     first_l = float(losses[: max(1, a.warmup // 10)].mean())
     last_l = float(losses[-max(1, a.steps // 10):].mean())
     eng.global_step = total_steps
-    val_loss, val_acc = eng.validate(limit=(64 * a.batch) if tab else None)
+    val_loss, val_acc = loop.validate(limit=(64 * a.batch) if (tab or tt) else None)
 
     samples = a.steps * a.batch * ctx.world_size
     sps = samples / dt
@@ -183,7 +246,8 @@ def main():
     steps_per_epoch = math.ceil(math.ceil(int(0.8 * a.epoch_rows) / ctx.world_size) / a.batch)
     base = BASELINE_SAMPLES_PER_SEC.get(a.model)
     models = {"weather": "WeatherClassifier 5-64-2 (reference jobs/train_lightning_ddp.py)",
-              "tabular-mlp-4x1024": "tabular MLP 256-1024-1024-1024-2 (BASELINE config 4)"}
+              "tabular-mlp-4x1024": "tabular MLP 256-1024-1024-1024-2 (BASELINE config 4)",
+              "tabtransformer": "TabTransformer 4 layers, 64 feature tokens, d 64, 4 heads (BASELINE config 5)"}
     out = {
         "metric": "samples/sec (whole node) for weather-MLP DDP",
         "value": round(sps, 1),
@@ -195,7 +259,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": (round(sps / base, 2) if base else None),
-        "dtype": "bf16" if tab else "fp32",
+        "dtype": "bf16" if (tab or tt) else "fp32",
         "data": "synthetic",
         "config": {
             "model": models.get(a.model, a.model),
@@ -203,10 +267,11 @@ def main():
             "per_rank_batch": a.batch,
             "seq_len": None,
             "parallelism": f"dp{ctx.world_size}",
-            "optimizer": f"adam lr={eng.adam['lr']:g}",
-            "loss": eng.loss,
+            "optimizer": f"adam lr={(eng.optimizer.lr if tt else eng.adam['lr']):g}",
+            "loss": "ce" if tt else eng.loss,
             "engine": engine_desc,
             "dataset_rows": int(eng.X.shape[0]),
+            "seq_len_tokens": feats if tt else None,
             "features": feats,
             "baseline_ref": "BASELINE.md CPU probe, W=1, 8500 samples/s (reference publishes none)",
         },

@@ -1,0 +1,84 @@
+"""TabTransformer-style model over feature tokens (BASELINE.json config 5).
+
+Each numeric feature f of a row becomes a token ``x_f * E_f + c_f`` (d_model wide); L pre-norm
+transformer blocks (LayerNorm -> packed QKV -> feature-token attention -> out projection ->
+residual; LayerNorm -> GELU MLP -> residual) mix the tokens; the mean token goes through a
+final LayerNorm and a linear head.  On MI355X every GEMM / LayerNorm / attention is a native
+HIP kernel (ops/nn.py) with bf16 activations on an fp32 residual stream; on CPU the same module
+runs plain torch ops.  Training contract = the reference LightningModule's (training_step logs
+``train_loss``; validation_step logs ``val_loss`` / ``val_acc``; Adam).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.nn import ACT_GELU, attention, layer_norm, linear
+from ..trainer.module import TrainModule
+
+
+class _Block(nn.Module):
+    def __init__(self, d: int, heads: int, ffn_mult: int):
+        super().__init__()
+        self.heads = heads
+        self.ln1_w, self.ln1_b = nn.Parameter(torch.ones(d)), nn.Parameter(torch.zeros(d))
+        self.qkv = nn.Linear(d, 3 * d)
+        self.proj = nn.Linear(d, d)
+        self.ln2_w, self.ln2_b = nn.Parameter(torch.ones(d)), nn.Parameter(torch.zeros(d))
+        self.fc1 = nn.Linear(d, ffn_mult * d)
+        self.fc2 = nn.Linear(ffn_mult * d, d)
+
+    def forward(self, h: torch.Tensor, B: int, T: int) -> torch.Tensor:
+        d = h.shape[1]
+        a = layer_norm(h, self.ln1_w, self.ln1_b)
+        qkv = linear(a, self.qkv.weight, self.qkv.bias)
+        o = attention(qkv, B, self.heads, T, d // self.heads)
+        h = h + linear(o, self.proj.weight, self.proj.bias).float()
+        a = layer_norm(h, self.ln2_w, self.ln2_b)
+        f = linear(a, self.fc1.weight, self.fc1.bias, ACT_GELU)
+        return h + linear(f, self.fc2.weight, self.fc2.bias).float()
+
+
+class TabTransformer(TrainModule):
+    def __init__(self, num_features: int = 64, d_model: int = 64, heads: int = 4, layers: int = 4, ffn_mult: int = 4,
+                 num_classes: int = 2, lr: float = 1e-3):
+        super().__init__()
+        self.save_hyperparameters()
+        if d_model % heads:
+            raise ValueError("d_model must be divisible by heads")
+        self.F, self.d, self.lr = num_features, d_model, lr
+        self.feat_w = nn.Parameter(torch.randn(num_features, d_model) / math.sqrt(d_model))
+        self.feat_b = nn.Parameter(torch.zeros(num_features, d_model))
+        self.blocks = nn.ModuleList([_Block(d_model, heads, ffn_mult) for _ in range(layers)])
+        self.ln_w, self.ln_b = nn.Parameter(torch.ones(d_model)), nn.Parameter(torch.zeros(d_model))
+        self.head = nn.Linear(d_model, num_classes)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B = x.shape[0]
+        h = (x.float()[:, :, None] * self.feat_w + self.feat_b).reshape(B * self.F, self.d)
+        for blk in self.blocks:
+            h = blk(h, B, self.F)
+        pooled = h.reshape(B, self.F, self.d).mean(1)
+        z = layer_norm(pooled, self.ln_w, self.ln_b)
+        return linear(z, self.head.weight, self.head.bias).float()
+
+    def training_step(self, batch, batch_idx):
+        x, y = batch
+        loss = F.cross_entropy(self(x), y)
+        self.log("train_loss", loss, sync_dist=True)
+        return loss
+
+    def validation_step(self, batch, batch_idx):
+        x, y = batch
+        logits = self(x)
+        loss = F.cross_entropy(logits, y)
+        acc = (logits.argmax(1) == y).float().mean()
+        self.log("val_loss", loss, sync_dist=True, prog_bar=True)
+        self.log("val_acc", acc, sync_dist=True, prog_bar=True)
+        return loss
+
+    def configure_optimizers(self):
+        return torch.optim.Adam(self.parameters(), lr=self.lr)

@@ -89,8 +89,25 @@ class FlatAdam:
     def step(self, grad_scale: float = 1.0):
         self.step_count += 1
         g = self.param_groups[0]
+        counter = None
+        if self.p.is_cuda:
+            # the Adam step count lives on the device (advanced by a kernel, read by the Adam
+            # kernel), so a captured step graph replays with the right bias correction
+            counter = self._device_counter()
+            counter.add_(1)
         adam_flat_(self.p, self.g, self.m, self.v, self.step_count, g["lr"], g["betas"], g["eps"],
-                   g["weight_decay"], grad_scale=grad_scale, p_bf16=self.p_bf16)
+                   g["weight_decay"], grad_scale=grad_scale, p_bf16=self.p_bf16, step_counter=counter)
+
+    def _device_counter(self) -> torch.Tensor:
+        c = getattr(self, "_counter", None)
+        if c is None or c.device != self.p.device:
+            self._counter = c = torch.full((1,), self.step_count - 1, dtype=torch.int32, device=self.p.device)
+        return c
+
+    def sync_device_counter(self):
+        """Re-seed the device step counter from the host count (after a state load)."""
+        if self.p.is_cuda:
+            self._device_counter().fill_(self.step_count)
 
     def zero_grad(self):
         self.g.zero_()
@@ -138,3 +155,5 @@ class FlatAdam:
             self.step_count = max(steps)
         else:
             self.step_count = 0
+        if getattr(self, "_counter", None) is not None:
+            self._counter.fill_(self.step_count)

@@ -431,6 +431,7 @@ class AutogradEngine(_EngineBase):
             self._hooks = []
             for i, p in enumerate(params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+        self.graph_used = False
         opt = model.configure_optimizers()
         hp = adam_hparams_from(opt)
         if hp is not None:
@@ -457,9 +458,7 @@ class AutogradEngine(_EngineBase):
     def steps_per_epoch(self) -> int:
         return math.ceil(math.ceil(len(self.train_rows) / self.ctx.world_size) / self.B)
 
-    def train_step(self, rows: torch.Tensor, batch_idx: int):
-        x = self.X[rows.to(self.device)]
-        y = self.Y[rows.to(self.device)]
+    def _step_body(self, x, y, batch_idx: int):
         self.flat_g.zero_()
         if self.reducer is not None:
             self.reducer.prepare()
@@ -473,11 +472,79 @@ class AutogradEngine(_EngineBase):
         if self.optimizer is not None:
             self.optimizer.step()
         else:
-            if self.ctx.is_distributed and self.reducer is None:
-                pass
             self.torch_optimizer.step()
+        return loss
+
+    def train_step(self, rows: torch.Tensor, batch_idx: int):
+        rows_d = rows.to(self.device)
+        if self._graph_ok(rows_d.numel()):
+            loss = self._graph_step(rows_d, batch_idx)
+        elif getattr(self, "_warming", False):
+            # graph warmup steps run on the capture stream (torch's capture recipe): autograd's
+            # AccumulateGrad nodes then already live on that stream when the step is captured
+            s = self._capture_stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                loss = self._step_body(self.X[rows_d], self.Y[rows_d], batch_idx).detach()
+            torch.cuda.current_stream().wait_stream(s)
+        else:
+            loss = self._step_body(self.X[rows_d], self.Y[rows_d], batch_idx)
         self.global_step += 1
         return loss.detach()
+
+    def _capture_stream(self):
+        s = getattr(self, "_cap_stream", None)
+        if s is None:
+            self._cap_stream = s = torch.cuda.Stream(self.device)
+        return s
+
+    # ------------------------------------------------------------------ HIP graph of the step
+    # GPU + flat Adam: after GRAPH_WARMUP eager steps the whole step (zero grads, forward,
+    # backward with the bucket all-reduces issued from the grad hooks on the reducer's comm
+    # stream, finalize, Adam with the device step counter) is captured once and replayed; the
+    # batch is gathered into static input buffers by index_select on the device.
+    GRAPH_WARMUP = 3
+
+    def _graph_ok(self, n_rows: int) -> bool:
+        self._warming = False
+        if self.device.type != "cuda" or self.optimizer is None or n_rows != self.B:
+            return False
+        if os.environ.get("DCT_GRAPH", "1") == "0" or getattr(self, "_graph_failed", False):
+            return False
+        self._eager_full = getattr(self, "_eager_full", 0)
+        if getattr(self, "_graph", None) is None and self._eager_full < self.GRAPH_WARMUP:
+            self._eager_full += 1
+            self._warming = True
+            return False
+        return True
+
+    def _graph_step(self, rows_d: torch.Tensor, batch_idx: int):
+        if getattr(self, "_graph", None) is None:
+            self._x_static = self.X[rows_d].clone()
+            self._y_static = self.Y[rows_d].clone()
+            g = torch.cuda.CUDAGraph()
+            try:
+                s = self._capture_stream()
+                s.wait_stream(torch.cuda.current_stream())
+                torch.cuda.synchronize(self.device)
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                        self._loss_static = self._step_body(self._x_static, self._y_static, batch_idx).detach()
+                torch.cuda.current_stream().wait_stream(s)
+            except Exception as e:  # noqa: BLE001 - eager steps stay correct
+                print(f"[dct] HIP graph capture of the autograd step failed ({e!r}); running eagerly", flush=True)
+                self._graph_failed = True
+                torch.cuda.synchronize(self.device)
+                return self._step_body(self.X[rows_d], self.Y[rows_d], batch_idx)
+            self._graph = g
+            self.graph_used = True
+            # capture records without executing: Adam's host count moved, the device one did not
+            self.optimizer.step_count -= 1
+        torch.index_select(self.X, 0, rows_d, out=self._x_static)
+        torch.index_select(self.Y, 0, rows_d, out=self._y_static)
+        self._graph.replay()
+        self.optimizer.step_count += 1
+        return self._loss_static
 
     def optimizer_state_dict(self) -> Dict:
         if self.optimizer is not None:

@@ -86,8 +86,8 @@ class TrainModule(nn.Module):
         if self._trainer is not None:
             self._trainer._log_from_module(name, value, sync_dist=sync_dist, prog_bar=prog_bar, on_step=on_step,
                                            on_epoch=on_epoch, batch_size=batch_size)
-        else:
-            self._logged[name] = value
+        else:  # detached: a stored loss must not keep the autograd graph (and its streams) alive
+            self._logged[name] = value.detach() if isinstance(value, torch.Tensor) else value
 
     def training_step(self, batch, batch_idx):  # pragma: no cover - abstract
         raise NotImplementedError

@@ -23,7 +23,7 @@ import dct_amd  # noqa: E402
 from dct_amd.ckpt import ModelCheckpoint  # noqa: E402
 from dct_amd.config import default_config  # noqa: E402
 from dct_amd.data.dataset import TensorPairDataset, WeatherDataset  # noqa: E402
-from dct_amd.models.mlp import build_mlp  # noqa: E402
+from dct_amd.models import build_model  # noqa: E402
 from dct_amd.tracking import MLFlowLogger  # noqa: E402
 from dct_amd.trainer import DDPStrategy, Trainer, seed_everything  # noqa: E402
 
@@ -79,7 +79,7 @@ def main(argv=None) -> int:
     val_loader = DataLoader(val_set, batch_size=a.batch_size, shuffle=False, num_workers=0)
 
     input_dim = full_dataset.features.shape[1]
-    model = build_mlp(a.model, input_dim, lr=a.lr)
+    model = build_model(a.model, input_dim, lr=a.lr)
 
     world_size = int(os.environ.get("WORLD_SIZE", 1))
     trainer = Trainer(
