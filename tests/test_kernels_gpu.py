@@ -339,8 +339,13 @@ def test_layernorm_fwd_bwd(cuda):
     assert torch.allclose(db, bb.grad, atol=1e-3, rtol=1e-3)
 
 
-@pytest.mark.parametrize("Bsz,H,T,D", [(2, 4, 6, 16), (3, 2, 33, 32), (1, 1, 256, 64)])
-def test_attention_fwd_bwd(Bsz, H, T, D, cuda):
+@pytest.mark.parametrize("scalar", [False, True])
+@pytest.mark.parametrize("Bsz,H,T,D", [(2, 4, 6, 16), (3, 2, 33, 32), (1, 1, 256, 64), (5, 4, 64, 16), (3, 2, 32, 32),
+                                       (2, 3, 48, 64), (7, 1, 16, 16)])
+def test_attention_fwd_bwd(Bsz, H, T, D, scalar, cuda, monkeypatch):
+    """MFMA path (T, D multiples of 16, T <= 64) and the scalar LDS path against torch SDPA."""
+    if scalar:
+        monkeypatch.setenv("DCT_ATTN_SCALAR", "1")
     torch.manual_seed(11)
     dm = H * D
     qkv = _bf(torch.randn(Bsz * T, 3 * dm, device=cuda))
