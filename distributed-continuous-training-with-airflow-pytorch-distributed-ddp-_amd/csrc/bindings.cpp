@@ -204,6 +204,12 @@ PYBIND11_MODULE(_dct_native, m) {
       py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("M"), py::arg("N"), py::arg("K"),
       py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("trans_a"), py::arg("trans_b"), py::arg("epilogue"),
       py::arg("out_f32"), py::arg("accumulate"), py::arg("aux"), py::arg("colsum"), py::arg("stream"));
+  m.def("gemm_bf16_residual", [](uintptr_t A, uintptr_t W, uintptr_t C, uintptr_t bias, uintptr_t residual, int M, int N,
+                                  int K, uintptr_t stream) {
+    check(dct_gemm_bf16_residual(P<const uint16_t>(A), P<const uint16_t>(W), P<float>(C), P<const float>(bias),
+                                 P<const float>(residual), M, N, K, reinterpret_cast<void*>(stream)),
+          "gemm_bf16_residual");
+  });
   m.def("skinny_fwd", [](uintptr_t X, uintptr_t W, uintptr_t bias, uintptr_t Y, int B, int K, int C, uintptr_t stream) {
     check(dct_skinny_fwd(P<const uint16_t>(X), P<const uint16_t>(W), P<const float>(bias), P<uint16_t>(Y), B, K, C,
                          reinterpret_cast<void*>(stream)),

@@ -193,6 +193,7 @@ __global__ __launch_bounds__(GNT, 2) void gemm_bf16_kernel(GemmArgs g) {
         if (row >= g.M) continue;
         float z = acc[i][j][r] * g.alpha + bv;
         const size_t o = (size_t)row * g.ldc + col;
+        if (g.residual) z += g.residual[o];
         if (g.aux && g.epilogue == EPI_BIAS_GELU) reinterpret_cast<uint16_t*>(g.aux)[o] = f32_to_bf16(z);
         if (g.epilogue == EPI_BIAS_RELU) z = fmaxf(z, 0.f);
         else if (g.epilogue == EPI_BIAS_GELU) z = gelu_f(z);
@@ -290,7 +291,11 @@ __device__ __forceinline__ bf16x8 g2_frag(const char* img, int rb, int ks, int l
   }
 }
 
-template <bool TA, bool TB>
+// SPLIT: split-K slices reduce with float atomics.  Those keep the MFMA's natural C layout
+// (lane = column) so every atomic instruction covers 16 consecutive columns of 4 rows; the
+// plain-store kernels swap the MFMA operands instead (lane = row, 4 consecutive columns per
+// lane -> 8/16-byte row stores).
+template <bool TA, bool TB, bool SPLIT>
 __global__ __launch_bounds__(GNT, 2) void gemm2_kernel(GemmArgs g, int splits) {
   extern __shared__ __attribute__((aligned(16))) char smem2[];
   // [buf][A,B] images of 16 KB each
@@ -354,7 +359,8 @@ __global__ __launch_bounds__(GNT, 2) void gemm2_kernel(GemmArgs g, int splits) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = SPLIT ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0)
+                              : __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -370,38 +376,126 @@ __global__ __launch_bounds__(GNT, 2) void gemm2_kernel(GemmArgs g, int splits) {
       if (lane < 16 && row < g.M) atomicAdd(g.colsum + row, v);
     }
   }
-  // ---- epilogue: C layout col = lane&15, row = (lane>>4)*4 + r
-  const int ccol = lane & 15;
-  const int crow = (lane >> 4) * 4;
+  // ---- epilogue.  The MFMAs ran with swapped operands (B fragment first), so each 16x16
+  // accumulator is the TRANSPOSED tile: lane (c = lane&15, g = lane>>4) holds row 16i + c and the
+  // 4 CONSECUTIVE columns 16j + 4g .. +3 -> 8-byte bf16 / 16-byte fp32 row stores instead of
+  // 2-byte scattered ones (and 4-wide bias / aux loads).
+  if (SPLIT) {  // natural layout: col = lane&15, rows 4*(lane>>4) + r
+    const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wc * 64 + j * 16 + col_l;
+        if (col >= g.N) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wr * 64 + i * 16 + row_l + r;
+          if (row < g.M) atomicAdd(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col, acc[i][j][r] * g.alpha);
+        }
+      }
+    return;
+  }
+  const int c16 = lane & 15;
+  const int g4 = (lane >> 4) * 4;
+  const bool bias_epi = g.bias && g.epilogue >= EPI_BIAS && g.epilogue <= EPI_BIAS_GELU;
+  const bool vec_ok = (g.ldc % 4 == 0) && ((((uintptr_t)g.C) & 15) == 0) &&
+                      (!g.aux || (((uintptr_t)g.aux) & 7) == 0);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
+    const int row = m0 + wr * 64 + i * 16 + c16;
+    if (row >= g.M) continue;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wc * 64 + j * 16 + ccol;
-      if (col >= g.N) continue;
-      const float bv = (g.bias && g.epilogue >= EPI_BIAS && g.epilogue <= EPI_BIAS_GELU) ? g.bias[col] : 0.f;
+      const int col0 = n0 + wc * 64 + j * 16 + g4;
+      if (col0 >= g.N) continue;
+      const size_t o0 = (size_t)row * g.ldc + col0;
+      const bool full = vec_ok && col0 + 4 <= g.N;
+      float z[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wr * 64 + i * 16 + crow + r;
-        if (row >= g.M) continue;
-        float z = acc[i][j][r] * g.alpha + bv;
-        const size_t o = (size_t)row * g.ldc + col;
-        if (splits > 1) {
-          atomicAdd(reinterpret_cast<float*>(g.C) + o, z);
-          continue;
-        }
-        if (g.aux && g.epilogue == EPI_BIAS_GELU) reinterpret_cast<uint16_t*>(g.aux)[o] = f32_to_bf16(z);
-        if (g.epilogue == EPI_BIAS_RELU) z = fmaxf(z, 0.f);
-        else if (g.epilogue == EPI_BIAS_GELU) z = gelu_f(z);
-        else if (g.epilogue == EPI_RELU_MASK) z = bf16_to_f32(reinterpret_cast<const uint16_t*>(g.aux)[o]) > 0.f ? z : 0.f;
-        else if (g.epilogue == EPI_GELU_GRAD) z *= gelu_grad_f(bf16_to_f32(reinterpret_cast<const uint16_t*>(g.aux)[o]));
-        if (g.out_f32) {
-          float* C = reinterpret_cast<float*>(g.C);
-          C[o] = g.accumulate ? C[o] + z : z;
+      for (int r = 0; r < 4; ++r) z[r] = acc[i][j][r] * g.alpha;
+      if (bias_epi) {
+        if (full) {
+          const float4 bv = *reinterpret_cast<const float4*>(g.bias + col0);
+          z[0] += bv.x; z[1] += bv.y; z[2] += bv.z; z[3] += bv.w;
         } else {
-          uint16_t* C = reinterpret_cast<uint16_t*>(g.C);
-          if (g.accumulate) z += bf16_to_f32(C[o]);
-          C[o] = f32_to_bf16(z);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) z[r] += (col0 + r < g.N) ? g.bias[col0 + r] : 0.f;
+        }
+      }
+      if (g.residual) {
+        const float* R = g.residual + o0;
+        if (full) {
+          const float4 rv = *reinterpret_cast<const float4*>(R);
+          z[0] += rv.x; z[1] += rv.y; z[2] += rv.z; z[3] += rv.w;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) z[r] += (col0 + r < g.N) ? R[r] : 0.f;
+        }
+      }
+      uint16_t* aux16 = reinterpret_cast<uint16_t*>(g.aux);
+      if (g.epilogue == EPI_BIAS_GELU && aux16) {  // keep the pre-activation for GELU'
+        if (full) {
+          uint2 pk;
+          pk.x = f32_to_bf16(z[0]) | ((uint32_t)f32_to_bf16(z[1]) << 16);
+          pk.y = f32_to_bf16(z[2]) | ((uint32_t)f32_to_bf16(z[3]) << 16);
+          *reinterpret_cast<uint2*>(aux16 + o0) = pk;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (col0 + r < g.N) aux16[o0 + r] = f32_to_bf16(z[r]);
+        }
+      }
+      if (g.epilogue == EPI_RELU_MASK || g.epilogue == EPI_GELU_GRAD) {
+        float a[4];
+        if (full) {
+          const uint2 pk = *reinterpret_cast<const uint2*>(aux16 + o0);
+          a[0] = bf16_to_f32(pk.x & 0xffff); a[1] = bf16_to_f32(pk.x >> 16);
+          a[2] = bf16_to_f32(pk.y & 0xffff); a[3] = bf16_to_f32(pk.y >> 16);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) a[r] = (col0 + r < g.N) ? bf16_to_f32(aux16[o0 + r]) : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          z[r] = g.epilogue == EPI_RELU_MASK ? (a[r] > 0.f ? z[r] : 0.f) : z[r] * gelu_grad_f(a[r]);
+      } else if (g.epilogue == EPI_BIAS_RELU) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z[r] = fmaxf(z[r], 0.f);
+      } else if (g.epilogue == EPI_BIAS_GELU) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z[r] = gelu_f(z[r]);
+      }
+      if (g.out_f32) {
+        float* C = reinterpret_cast<float*>(g.C) + o0;
+        if (full) {
+          float4 v = make_float4(z[0], z[1], z[2], z[3]);
+          if (g.accumulate) {
+            const float4 c0 = *reinterpret_cast<const float4*>(C);
+            v.x += c0.x; v.y += c0.y; v.z += c0.z; v.w += c0.w;
+          }
+          *reinterpret_cast<float4*>(C) = v;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (col0 + r < g.N) C[r] = g.accumulate ? C[r] + z[r] : z[r];
+        }
+      } else {
+        uint16_t* C = reinterpret_cast<uint16_t*>(g.C) + o0;
+        if (full) {
+          if (g.accumulate) {
+            const uint2 c0 = *reinterpret_cast<const uint2*>(C);
+            z[0] += bf16_to_f32(c0.x & 0xffff); z[1] += bf16_to_f32(c0.x >> 16);
+            z[2] += bf16_to_f32(c0.y & 0xffff); z[3] += bf16_to_f32(c0.y >> 16);
+          }
+          uint2 pk;
+          pk.x = f32_to_bf16(z[0]) | ((uint32_t)f32_to_bf16(z[1]) << 16);
+          pk.y = f32_to_bf16(z[2]) | ((uint32_t)f32_to_bf16(z[3]) << 16);
+          *reinterpret_cast<uint2*>(C) = pk;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (col0 + r < g.N) C[r] = f32_to_bf16((g.accumulate ? bf16_to_f32(C[r]) : 0.f) + z[r]);
         }
       }
     }
@@ -434,9 +528,7 @@ static bool gemm_v2_ok(const dct::GemmArgs& g, int ta, int tb) {
 template <bool TA, bool TB>
 static hipError_t launch_gemm2(const dct::GemmArgs& g, hipStream_t st) {
   const size_t lds = 4 * (size_t)dct::G2_BYTES;
-  auto fn = dct::gemm2_kernel<TA, TB>;
-  hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return e;
+  hipError_t e;
   const int tiles = ((g.M + dct::GBM - 1) / dct::GBM) * ((g.N + dct::GBN - 1) / dct::GBN);
   const int nk = g.K / dct::GBK;
   int splits = 1;
@@ -448,6 +540,9 @@ static hipError_t launch_gemm2(const dct::GemmArgs& g, hipStream_t st) {
     e = hipMemset2DAsync(g.C, (size_t)g.ldc * 4, 0, (size_t)g.N * 4, (size_t)g.M, st);
     if (e != hipSuccess) return e;
   }
+  auto fn = splits > 1 ? dct::gemm2_kernel<TA, TB, true> : dct::gemm2_kernel<TA, TB, false>;
+  e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(fn, dim3(tiles * splits), dim3(dct::GNT), lds, st, g, splits);
   return hipGetLastError();
 }
@@ -480,6 +575,29 @@ extern "C" int dct_gemm_bf16_ex(const uint16_t* A, const uint16_t* B, void* C, c
   // generic path: the A rows' sums by the column-sum kernel (op(A) = A^T when trans_a: A is [K][M])
   if (trans_a) return dct_bias_act_bwd(A, nullptr, nullptr, colsum, K, M, lda, 0, 1, stream);
   return (int)hipErrorNotSupported;
+}
+
+extern "C" int dct_gemm_bf16_residual(const uint16_t* A, const uint16_t* W, float* C, const float* bias,
+                                      const float* residual, int M, int N, int K, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  dct::GemmArgs g{};
+  g.A = A; g.B = W; g.C = C; g.bias = bias; g.residual = residual;
+  g.M = M; g.N = N; g.K = K; g.lda = K; g.ldb = K; g.ldc = N;
+  g.epilogue = bias ? dct::EPI_BIAS : dct::EPI_NONE; g.out_f32 = 1; g.accumulate = 0; g.alpha = 1.0f;
+  g.vec_a = ((((uintptr_t)A) & 15) == 0) && (K % 8 == 0);
+  g.vec_b = ((((uintptr_t)W) & 15) == 0) && (K % 8 == 0);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (gemm_v2_ok(g, 0, 1)) {
+    // no split-K here: the residual is folded into the (single) writer of each element
+    const int tiles = ((M + dct::GBM - 1) / dct::GBM) * ((N + dct::GBN - 1) / dct::GBN);
+    const size_t lds = 4 * (size_t)dct::G2_BYTES;
+    auto fn = dct::gemm2_kernel<false, true, false>;
+    hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(fn, dim3(tiles), dim3(dct::GNT), lds, st, g, 1);
+    return (int)hipGetLastError();
+  }
+  return (int)launch_gemm<false, true>(g, st);
 }
 
 extern "C" int dct_gemm_bf16(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K,

@@ -21,6 +21,7 @@ struct GemmArgs {
   int vec_a, vec_b;
   float alpha;
   float* colsum;  // optional: colsum[m] += sum_k op(A)[m][k] (the bias gradient of a dW GEMM)
+  const float* residual;  // optional (fp32 out): C = residual + op(A) op(B) + bias, ld = ldc
 };
 
 }  // namespace dct
@@ -33,6 +34,9 @@ int dct_gemm_bf16(const uint16_t* A, const uint16_t* B, void* C, const float* bi
 int dct_gemm_bf16_ex(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K, int lda,
                      int ldb, int ldc, int trans_a, int trans_b, int epilogue, int out_f32, int accumulate, void* aux,
                      float* colsum, void* stream);
+// fp32 C = residual + A W^T + bias (the residual-stream update of a transformer block)
+int dct_gemm_bf16_residual(const uint16_t* A, const uint16_t* W, float* C, const float* bias, const float* residual,
+                           int M, int N, int K, void* stream);
 // Skinny layers (C <= 8 outputs, e.g. the classifier head) as bandwidth kernels:
 //   fwd: Y[b][c] = sum_k X[b][k] W[c][k] + bias[c]            (bf16 X/W/Y)
 //   dx : dX[b][k] = sum_c dZ[b][c] W[c][k], masked by aux[b][k] > 0 when aux (ReLU output)

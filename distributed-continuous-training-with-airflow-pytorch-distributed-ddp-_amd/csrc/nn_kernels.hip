@@ -3,6 +3,8 @@
 // All of them vectorise bf16 I/O to 16-B per lane where the layout allows (CDNA guide G13)
 // and reduce per block before one atomic per (block, column) (G12).
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "dct_common.h"
@@ -89,6 +91,7 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const uint16_t* dY, c
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
   if (c0 < N) {
+#pragma unroll 4
     for (int r = blockIdx.y * 4 + ty; r < M; r += gridDim.y * 4) {
       const size_t o = (size_t)r * ldy + c0;
       float dy[8], zz[8];
@@ -245,6 +248,123 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const void* dy, cons
   }
 }
 
+// ----------------------------------------------------------- narrow LayerNorm (N <= 256)
+// Transformer widths (d_model 32..256): one lane owns 4 consecutive columns of a row, a row
+// takes LPR = pow2(N/4) lanes, a wave holds 64/LPR rows; statistics by xor-shuffles inside
+// the lane group.  (The one-wave-per-row kernel above leaves 63/64 lanes idle at N = 64.)
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < LPR; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ void ld4any(const void* p, size_t i, int bf16, float (&v)[4]) {
+  if (bf16) {
+    const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(p) + i);
+    v[0] = bf16_to_f32(u.x & 0xffff); v[1] = bf16_to_f32(u.x >> 16);
+    v[2] = bf16_to_f32(u.y & 0xffff); v[3] = bf16_to_f32(u.y >> 16);
+  } else {
+    const float4 f = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + i);
+    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+  }
+}
+__device__ __forceinline__ void st4any(void* p, size_t i, int bf16, const float (&v)[4]) {
+  if (bf16) {
+    uint2 u;
+    u.x = f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
+    u.y = f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p) + i) = u;
+  } else {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + i) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void layernorm_fwd_small(const void* x, const float* w, const float* b, void* y,
+                                                           float* mean_out, float* rstd_out, int M, int N, float eps,
+                                                           int in_bf16, int out_bf16) {
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, sub = lane / LPR, li = lane % LPR;
+  const int c0 = li * 4;
+  const bool act = c0 < N;
+  float wv[4] = {1.f, 1.f, 1.f, 1.f}, bv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (act && w) { const float4 t = *reinterpret_cast<const float4*>(w + c0); wv[0] = t.x; wv[1] = t.y; wv[2] = t.z; wv[3] = t.w; }
+  if (act && b) { const float4 t = *reinterpret_cast<const float4*>(b + c0); bv[0] = t.x; bv[1] = t.y; bv[2] = t.z; bv[3] = t.w; }
+  const int wave_g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  for (int row = wave_g * RPW + sub; row < M; row += gridDim.x * 4 * RPW) {
+    const size_t base = (size_t)row * N + c0;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (act) ld4any(x, base, in_bf16, v);
+    const float mean = group_sum<LPR>(v[0] + v[1] + v[2] + v[3]) / (float)N;
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { const float d = act ? v[e] - mean : 0.f; q += d * d; }
+    const float rstd = rsqrtf(group_sum<LPR>(q) / (float)N + eps);
+    if (act) {
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (v[e] - mean) * rstd * wv[e] + bv[e];
+      st4any(y, base, out_bf16, o);
+    }
+    if (li == 0) {
+      if (mean_out) mean_out[row] = mean;
+      if (rstd_out) rstd_out[row] = rstd;
+    }
+  }
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void layernorm_bwd_small(const void* dy, const void* x, const float* w,
+                                                           const float* mean_in, const float* rstd_in, void* dx,
+                                                           float* dw, float* db, int M, int N, int bf16_io) {
+  constexpr int RPW = 64 / LPR;
+  __shared__ float red[2][256 * 4];
+  const int lane = threadIdx.x & 63, sub = lane / LPR, li = lane % LPR;
+  const int c0 = li * 4;
+  const bool act = c0 < N;
+  float wv[4] = {1.f, 1.f, 1.f, 1.f};
+  if (act && w) { const float4 t = *reinterpret_cast<const float4*>(w + c0); wv[0] = t.x; wv[1] = t.y; wv[2] = t.z; wv[3] = t.w; }
+  float aw[4] = {0.f, 0.f, 0.f, 0.f}, ab[4] = {0.f, 0.f, 0.f, 0.f};
+  const int wave_g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  for (int row = wave_g * RPW + sub; row < M; row += gridDim.x * 4 * RPW) {
+    const size_t base = (size_t)row * N + c0;
+    float xv[4] = {0.f, 0.f, 0.f, 0.f}, gv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (act) { ld4any(x, base, bf16_io, xv); ld4any(dy, base, bf16_io, gv); }
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[4], gw[4], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      xh[e] = act ? (xv[e] - mean) * rstd : 0.f;
+      gw[e] = gv[e] * wv[e];
+      s1 += gw[e];
+      s2 += gw[e] * xh[e];
+      aw[e] += gv[e] * xh[e];
+      ab[e] += gv[e];
+    }
+    s1 = group_sum<LPR>(s1) / (float)N;
+    s2 = group_sum<LPR>(s2) / (float)N;
+    if (act) {
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = rstd * (gw[e] - s1 - xh[e] * s2);
+      st4any(dx, base, bf16_io, o);
+    }
+  }
+  // column partials: threads with the same li own the same 4 columns
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { red[0][threadIdx.x * 4 + e] = aw[e]; red[1][threadIdx.x * 4 + e] = ab[e]; }
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < LPR * 4; cc += blockDim.x) {
+    const int l = cc / 4, e = cc % 4;
+    if (l * 4 >= N) continue;
+    float sw = 0.f, sb = 0.f;
+    for (int t = l; t < 256; t += LPR) { sw += red[0][t * 4 + e]; sb += red[1][t * 4 + e]; }
+    if (dw) atomicAdd(&dw[l * 4 + e], sw);
+    if (db) atomicAdd(&db[l * 4 + e], sb);
+  }
+}
+
 // ------------------------------------------------------------------------------ gather
 __global__ __launch_bounds__(256) void gather_rows16_kernel(const uint4* src, const int* idx, uint4* dst,
                                                             int64_t n_rows, int row_vec) {
@@ -289,8 +409,9 @@ int dct_bias_act_bwd(const void* dY, const void* act_aux, uint16_t* dZ, float* d
   if (M <= 0 || N <= 0) return 0;
   const int ncc = (N + 7) / 8;
   // row blocks of >= 64 rows: few float atomics per column (a 512-way atomicAdd fan-in on the
-  // same 1024 addresses serialised this kernel to ~100 us at M = 4096)
-  dim3 grid((ncc + 63) / 64, (unsigned)grid_cap((M + 63) / 64, 1, 64));
+  // same 1024 addresses serialised this kernel to ~100 us at M = 4096), enough blocks to fill
+  // the chip (the row loop keeps 4 rows of loads in flight per thread)
+  dim3 grid((ncc + 63) / 64, (unsigned)grid_cap((M + 63) / 64, 1, std::max(64, 512 / std::max(1, (ncc + 63) / 64))));
   const bool vec = (N % 8 == 0) && (ldy % 8 == 0) && ((((uintptr_t)dY) | ((uintptr_t)act_aux) | ((uintptr_t)dZ)) & 15) == 0;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (vec)
@@ -302,10 +423,27 @@ int dct_bias_act_bwd(const void* dY, const void* act_aux, uint16_t* dZ, float* d
   return (int)hipGetLastError();
 }
 
+static int ln_lpr(int N, const void* a, const void* b2, const void* c) {
+  if (N % 4 || N > 256 || ((((uintptr_t)a) | ((uintptr_t)b2) | ((uintptr_t)c)) & 15)) return 0;
+  int l = 1;
+  while (l * 4 < N) l <<= 1;
+  return l;
+}
+
 int dct_layernorm_fwd(const void* x, const float* w, const float* b, void* y, float* mean, float* rstd, int M, int N,
                       float eps, int in_bf16, int out_bf16, void* stream) {
   if (N > 64 * dct::LN_MAX) return (int)hipErrorInvalidValue;
   if (M <= 0) return 0;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (const int lpr = ln_lpr(N, x, y, w)) {
+    const int rows_per_block = 4 * (64 / lpr);
+    const int grid = grid_cap((M + rows_per_block - 1) / rows_per_block, 1, 4096);
+#define LNF(L) hipLaunchKernelGGL(dct::layernorm_fwd_small<L>, dim3(grid), dim3(256), 0, st, x, w, b, y, mean, rstd, M, N, eps, in_bf16, out_bf16)
+    switch (lpr) { case 1: LNF(1); break; case 2: LNF(2); break; case 4: LNF(4); break; case 8: LNF(8); break;
+                   case 16: LNF(16); break; case 32: LNF(32); break; default: LNF(64); }
+#undef LNF
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(dct::layernorm_fwd_kernel, dim3((M + 3) / 4), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      x, w, b, y, mean, rstd, M, N, eps, in_bf16, out_bf16);
   return (int)hipGetLastError();
@@ -315,6 +453,16 @@ int dct_layernorm_bwd(const void* dy, const void* x, const float* w, const float
                       float* dw, float* db, int M, int N, int bf16_io, void* stream) {
   if (N > 64 * dct::LN_MAX) return (int)hipErrorInvalidValue;
   if (M <= 0) return 0;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (const int lpr = ln_lpr(N, dy, x, dx)) {
+    const int rows_per_block = 4 * (64 / lpr);
+    const int grid = grid_cap((M + rows_per_block - 1) / rows_per_block, 1, 1024);
+#define LNB(L) hipLaunchKernelGGL(dct::layernorm_bwd_small<L>, dim3(grid), dim3(256), 0, st, dy, x, w, mean, rstd, dx, dw, db, M, N, bf16_io)
+    switch (lpr) { case 1: LNB(1); break; case 2: LNB(2); break; case 4: LNB(4); break; case 8: LNB(8); break;
+                   case 16: LNB(16); break; case 32: LNB(32); break; default: LNB(64); }
+#undef LNB
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(dct::layernorm_bwd_kernel, dim3(grid_cap((M + 3) / 4, 1, 1024)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), dy, x, w, mean, rstd, dx, dw, db, M, N, bf16_io);
   return (int)hipGetLastError();

@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.nn import ACT_GELU, attention, layer_norm, linear
+from ..ops.nn import ACT_GELU, attention, layer_norm, linear, linear_residual
 from ..trainer.module import TrainModule
 
 
@@ -36,10 +36,10 @@ class _Block(nn.Module):
         a = layer_norm(h, self.ln1_w, self.ln1_b)
         qkv = linear(a, self.qkv.weight, self.qkv.bias)
         o = attention(qkv, B, self.heads, T, d // self.heads)
-        h = h + linear(o, self.proj.weight, self.proj.bias).float()
+        h = linear_residual(o, self.proj.weight, self.proj.bias, h)
         a = layer_norm(h, self.ln2_w, self.ln2_b)
         f = linear(a, self.fc1.weight, self.fc1.bias, ACT_GELU)
-        return h + linear(f, self.fc2.weight, self.fc2.bias).float()
+        return linear_residual(f, self.fc2.weight, self.fc2.bias, h)
 
 
 class TabTransformer(TrainModule):

@@ -81,6 +81,51 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, act: int =
     return F.relu(y) if act == ACT_RELU else (F.gelu(y) if act == ACT_GELU else y)
 
 
+class _LinearResidualFn(torch.autograd.Function):
+    """out = h + x W^T + b in fp32 from one GEMM epilogue (the residual-stream update)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, h):
+        nat = native()
+        x = x.contiguous()
+        if x.dtype != torch.bfloat16:
+            x = x.to(torch.bfloat16)
+        h = h.contiguous().float()
+        M, K = x.shape
+        N = weight.shape[0]
+        wb = weight.detach().to(torch.bfloat16).contiguous()
+        out = torch.empty(M, N, dtype=torch.float32, device=x.device)
+        nat.gemm_bf16_residual(x.data_ptr(), wb.data_ptr(), out.data_ptr(), bias.data_ptr(), h.data_ptr(), M, N, K,
+                               _stream())
+        ctx.save_for_backward(x, wb)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        nat = native()
+        x, wb = ctx.saved_tensors
+        M, K = x.shape
+        N = wb.shape[0]
+        st = _stream()
+        dz = dout.contiguous().to(torch.bfloat16)
+        db = torch.zeros(N, dtype=torch.float32, device=x.device)
+        dw = torch.empty(N, K, dtype=torch.float32, device=x.device)
+        nat.gemm_bf16_ex(dz.data_ptr(), x.data_ptr(), dw.data_ptr(), 0, N, K, M, N, K, K, 1, 0, 0, 1, 0, 0,
+                         db.data_ptr(), st)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, K, dtype=torch.bfloat16, device=x.device)
+            nat.gemm_bf16(dz.data_ptr(), wb.data_ptr(), dx.data_ptr(), 0, M, K, N, N, K, K, 0, 0, 0, 0, 0, 0, st)
+        return dx, dw, db, dout
+
+
+def linear_residual(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+    """h + x W^T + b (fp32): on GPU one GEMM with the residual folded into its epilogue."""
+    if x.is_cuda:
+        return _LinearResidualFn.apply(x, weight, bias, h)
+    return h.float() + F.linear(x.float(), weight, bias)
+
+
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, eps):
