@@ -212,8 +212,17 @@ def main():
 
     # warmup (also builds / captures the step graphs outside the timed region)
     loop.run_steps(n_items, a.warmup, loss, first_step=0)
-    if getattr(eng, "xg", None) is not None and not eng.xg_verify(fallback=True):
-        eng.run_steps(n_items, a.warmup, loss, first_step=0)  # re-warm on the RCCL path
+    if getattr(eng, "xg", None) is not None:
+        ok = eng.xg_verify(fallback=True)
+        if ok and not _params_in_sync(ctx, eng.p):
+            # the exchange completed but the replicas differ (should never happen): resync and
+            # measure the RCCL path instead of reporting a broken DDP
+            if ctx.rank == 0:
+                print("[dct] replicas diverged under the in-kernel exchange; falling back to RCCL", flush=True)
+            eng.xg_disable()
+            ok = False
+        if not ok:
+            eng.run_steps(n_items, a.warmup, loss, first_step=0)  # re-warm on the RCCL path
     if not (tab or tt) and eng.ddp and eng.xg is None and eng.use_graph:
         eng._get_graph(n_items, min(eng.graph_chunk, a.steps), loss)
     dt = _timed(ctx, lambda: loop.run_steps(n_items, a.steps, loss, first_step=a.warmup))

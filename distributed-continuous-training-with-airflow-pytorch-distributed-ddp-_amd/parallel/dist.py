@@ -152,6 +152,9 @@ def init_distributed(accelerator: str = "auto", backend: str = "auto", timeout_s
                       local_world_size=e["local_world_size"], node_rank=e["node_rank"], backend=backend,
                       device=device)
     if e["world_size"] > 1:
+        # a collective that fails on one rank must abort the job instead of hanging the others
+        # (torchrun --max-restarts then restarts it); RCCL honours the same variable
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", e["master_addr"])
             os.environ.setdefault("MASTER_PORT", str(e["master_port"]))

@@ -32,6 +32,7 @@ from ..ops.fused_mlp import FusedMLPKernel, mlp_num_params
 from ..ops.optim import FlatAdam, adam_flat_
 from ..parallel.dist import DistContext, init_native_comm
 from ..parallel.reducer import NativeBucketReducer, TorchBucketReducer, plan_buckets
+from ..utils.debug import assert_reducer_complete, check_device
 
 
 def adam_hparams_from(optimizer) -> Optional[Dict]:
@@ -345,6 +346,7 @@ class FusedMLPEngine(_EngineBase):
             torch.cuda.synchronize(self.device)
             self.ctx.barrier()  # start the epoch's kernels together (the exchange spins are bounded)
         self.run_steps(n_items, steps, loss_out[:steps])
+        check_device("fused epoch")
         if self.xg is not None:
             self.xg_verify(fallback=False)
         self.global_step += steps
@@ -366,13 +368,18 @@ class FusedMLPEngine(_EngineBase):
             raise RuntimeError(msg)
         if self.ctx.rank == 0:
             print(f"[dct] {msg}; re-syncing from rank 0 and falling back to RCCL", flush=True)
+        self.xg_disable()
+        return False
+
+    def xg_disable(self):
+        """Leave the in-kernel exchange: replicas re-synced from rank 0, RCCL step path from now on."""
         self.xg = None
         if self.comm is None:
-            raise RuntimeError(msg + " and no RCCL communicator is available to fall back to")
+            raise RuntimeError("in-kernel exchange disabled and no RCCL communicator is available to fall back to")
+        torch.cuda.synchronize(self.device)
         for t in (self.p, self.m, self.v, self.step_counter):
             self.ctx.broadcast_(t, src=0)
         torch.cuda.synchronize(self.device)
-        return False
 
     # ------------------------------------------------------------------ eval
     def validate(self, rows: Optional[torch.Tensor] = None, limit: Optional[int] = None) -> Tuple[float, float]:
@@ -469,6 +476,7 @@ class AutogradEngine(_EngineBase):
         loss.backward()
         if self.reducer is not None:
             self.reducer.finalize()
+            assert_reducer_complete(self.reducer)
         if self.optimizer is not None:
             self.optimizer.step()
         else:

@@ -32,6 +32,7 @@ from ..data.sampler import distributed_indices
 from ..parallel.dist import DistContext, init_distributed, shutdown
 from .engines import AutogradEngine, FusedMLPEngine, adam_hparams_from
 from .graph_engine import GraphMLPEngine
+from ..utils.tracing import trace_range
 
 
 def seed_everything(seed: int = 42) -> int:
@@ -289,13 +290,16 @@ class Trainer:
         status = "success"
         try:
             if start_epoch == 0 and self.num_sanity_val_steps > 0 and len(val_rows):
-                self._validate(VB, limit_batches=self.num_sanity_val_steps, sanity=True)
+                with trace_range("sanity_val"):
+                    self._validate(VB, limit_batches=self.num_sanity_val_steps, sanity=True)
             for epoch in range(start_epoch, self.max_epochs):
                 self.current_epoch = epoch
                 t0 = time.perf_counter()
-                n_steps = self._train_epoch(epoch, B, tinfo.get("shuffle", True))
+                with trace_range(f"epoch{epoch}/train"):
+                    n_steps = self._train_epoch(epoch, B, tinfo.get("shuffle", True))
                 train_t = time.perf_counter() - t0
-                val_metrics = self._validate(VB) if len(val_rows) else {}
+                with trace_range(f"epoch{epoch}/validate"):
+                    val_metrics = self._validate(VB) if len(val_rows) else {}
                 epoch_t = time.perf_counter() - t0
                 self.epoch_times.append(epoch_t)
                 samples = len(train_rows)
@@ -305,7 +309,8 @@ class Trainer:
                 extra = {"epoch_time_s": epoch_t, "train_time_s": train_t,
                          "samples_per_sec": samples / max(train_t, 1e-9)}
                 self._log_metrics(extra, self.global_step)
-                self._run_checkpoint_callbacks(n_steps)
+                with trace_range(f"epoch{epoch}/checkpoint"):
+                    self._run_checkpoint_callbacks(n_steps)
                 if self.verbose and self.is_global_zero:
                     vm = " ".join(f"{k}={v:.4f}" for k, v in val_metrics.items())
                     print(f"[dct] epoch {epoch} steps={n_steps} {vm} epoch_time={epoch_t:.3f}s "
