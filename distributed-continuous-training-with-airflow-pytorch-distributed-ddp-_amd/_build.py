@@ -54,6 +54,8 @@ def _flags(debug: bool = False):
     ]
     if debug:
         f.append("-g")
+    if os.environ.get("DCT_PROF_BUILD", "0") == "1":  # in-kernel phase stamps (tools/prof_fused.py)
+        f.append("-DDCT_WAVE_PROF")
     if os.environ.get("DCT_SANITIZE", "0") == "1":  # host-side ASan only (no GPU sanitizer on this pool)
         f += ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
     return f

@@ -583,8 +583,8 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpShape sh, MlpArgs a) {
 
     // ---- dW (+ Adam) on owned blocks, biases
     const int t = t0 + s + 1;
-    const float bc1 = 1.f - __powf(a.b1, (float)t);
-    const float bc2 = 1.f - __powf(a.b2, (float)t);
+    const float bc1 = 1.f - pow_t(log2f(a.b1), (float)t);
+    const float bc2 = 1.f - pow_t(log2f(a.b2), (float)t);
     const float step_size = a.lr / bc1;
     const float rbc2 = __builtin_amdgcn_rsqf(bc2);
 #pragma unroll

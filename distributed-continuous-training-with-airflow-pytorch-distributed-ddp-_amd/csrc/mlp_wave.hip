@@ -261,8 +261,8 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
   if (fuse_upd && __hip_atomic_load(a.pending, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
     // previous step's all-reduced gradients are in grad_out: apply its Adam update first
     const float tt = (float)t0;
-    const float step_size = a.lr / (1.f - __powf(a.b1, tt));
-    const float rbc2 = __builtin_amdgcn_rsqf(1.f - __powf(a.b2, tt));
+    const float step_size = a.lr * __builtin_amdgcn_rcpf(1.f - pow_t(log2f(a.b1), tt));
+    const float rbc2 = __builtin_amdgcn_rsqf(1.f - pow_t(log2f(a.b2), tt));
     if (own1) {
 #pragma unroll
       for (int k = 0; k < D0; ++k)
@@ -344,9 +344,24 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
   load_idx(cur0 + 1, ridx_a);  // idx of batch cur0 + 1
 
   const float keep_scale = (a.dropout > 0.f) ? 1.0f / (1.0f - a.dropout) : 1.0f;
+  const float l2b1 = log2f(a.b1), l2b2 = log2f(a.b2);  // hoisted: bias corrections are exp2 per step
   const uint32_t drop_thr = (uint32_t)(a.dropout * 4294967296.0);
   const bool prof = (a.prof != nullptr) && j == 0;
   if (prof) a.prof[30] = __builtin_amdgcn_s_memrealtime();
+  // diagnostic phase stamps (shader clock, wave-uniform branch; never set in production)
+  const bool profu = a.prof != nullptr;
+  unsigned long long pt[6] = {0, 0, 0, 0, 0, 0}, tprev = 0;
+#ifndef DCT_WAVE_PROF
+#define WSTAMP(k)
+#else
+#define WSTAMP(k)                                                                          \
+  if (profu) {                                                                             \
+    unsigned long long t_;                                                                 \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
+    if ((k) >= 0) pt[(k) < 0 ? 0 : (k)] += t_ - tprev;                                     \
+    tprev = t_;                                                                            \
+  }
+#endif
   constexpr bool XG = XW > 0;
   constexpr int XWN = XW > 0 ? XW : 1;
   __amdgpu_buffer_rsrc_t prs[XWN];
@@ -366,6 +381,7 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
     const int sb = s + cur0;
     const int bs = min(B, a.n_items - sb * B);
     const uint32_t gstep = step_base + (uint32_t)s;
+    WSTAMP(-1)
     // issue: values of batch sb+1 (idx already in registers) and idx of batch sb+2
     load_vals(sb + 1, ridx_a, nxt);
     load_idx(sb + 2, ridx_b);
@@ -399,6 +415,7 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
       }
       h[b] = own1 ? z : 0.f;
     }
+    WSTAMP(0)
     // ---- middle layer (3-layer nets): h2[b] = dropout(relu(W1[j] . h[b] + b1))
     float h2[BMAX];
     if (L == 3) {
@@ -435,10 +452,11 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
     float boc[CM];
 #pragma unroll
     for (int c = 0; c < CM; ++c) boc[c] = rl(bo, c);
+    WSTAMP(1)
     // ---- loss + dlogits (wave-uniform, computed redundantly in every lane)
     float dz[BMAX * CM];
     float lsum = 0.f;
-    const float inv = 1.0f / (float)(bs > 0 ? bs : 1);
+    const float inv = __builtin_amdgcn_rcpf((float)(bs > 0 ? bs : 1));  // bs <= 8: exact
 #pragma unroll
     for (int b = 0; b < BMAX; ++b) {
       const bool live = b < bs;
@@ -458,7 +476,7 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
           se += e[c];
           if (c == y[b]) zy = zz[c];
         }
-        lb = mx + __logf(se) - zy;
+        lb = mx + __builtin_amdgcn_logf(se) * 0.69314718055994531f - zy;  // se in [1, C]: no denormals
         const float rs = __builtin_amdgcn_rcpf(se);
 #pragma unroll
         for (int c = 0; c < CM; ++c) dz[b * CM + c] = live ? (e[c] * rs - (c == y[b] ? 1.f : 0.f)) * inv : 0.f;
@@ -480,6 +498,7 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
       if (!adam) a.grad_out[sh.P] = bl;
     }
 
+    WSTAMP(2)
     // ---- backward (lane-local)
     float gwo[CM], gbo = 0.f;
 #pragma unroll
@@ -553,6 +572,7 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
 #pragma unroll
     for (int b = 0; b < BMAX; ++b) gb0 += dh[b];
 
+    WSTAMP(3)
     if (XG) {  // average the gradients (and the batch loss) across ranks in-kernel
       static_assert(!XG || L == 2, "in-kernel all-reduce is implemented for 2-layer nets");
       constexpr int KX = D0 + CM + 2 + ((D0 + CM) & 1);  // even: 16-B granule pairs
@@ -581,10 +601,11 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
       const float lavg = rl(gv[D0 + 1 + CM], 63);
       if (j == 0 && a.loss_out && !a.cursor) a.loss_out[s] = lavg;
     }
+    WSTAMP(4)
     if (adam) {
       const int t = t0 + s + 1;
-      const float step_size = a.lr / (1.f - __powf(a.b1, (float)t));
-      const float rbc2 = __builtin_amdgcn_rsqf(1.f - __powf(a.b2, (float)t));
+      const float step_size = a.lr * __builtin_amdgcn_rcpf(1.f - pow_t(l2b1, (float)t));
+      const float rbc2 = __builtin_amdgcn_rsqf(1.f - pow_t(l2b2, (float)t));
       if (own1) {
 #pragma unroll
         for (int k = 0; k < D0; ++k)
@@ -627,13 +648,19 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
       }
       if (j < C) a.grad_out[sh.boff[lo] + j] = gbo;
     }
+    WSTAMP(5)
 #pragma unroll
     for (int r = 0; r < NPF; ++r) {
       cur[r] = nxt[r];
       ridx_a[r] = ridx_b[r];
     }
   }
-  if (prof) a.prof[31] = __builtin_amdgcn_s_memrealtime();
+#undef WSTAMP
+  if (prof) {
+    a.prof[31] = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+    for (int k = 0; k < 6; ++k) a.prof[k] = pt[k];
+  }
   if (a.stage) {  // hand the already-fetched next batch to the next launch
     const int nb = cur0 + done;
     const bool ok = nb * B < a.n_items;

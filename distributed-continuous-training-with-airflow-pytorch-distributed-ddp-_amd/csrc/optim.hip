@@ -45,8 +45,8 @@ __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, 
 __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a) {
   if (a.step_counter) {
     const float t = (float)__hip_atomic_load(a.step_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    a.step_size = a.lr / (1.f - __powf(a.b1, t));
-    a.rbc2 = rsqrtf(1.f - __powf(a.b2, t));
+    a.step_size = a.lr / (1.f - pow_t(log2f(a.b1), t));
+    a.rbc2 = rsqrtf(1.f - pow_t(log2f(a.b2), t));
   }
   const int64_t n4 = a.n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;

@@ -19,6 +19,7 @@ from dct_amd.ops.fused_mlp import FusedMLPKernel, mlp_num_params  # noqa: E402
 
 NAMES = {0: "gather", 1: "fwd0", 2: "fwd1", 3: "fwd2", 4: "fwd3", 5: "loss", 7: "dx1", 8: "dx2", 9: "dx3",
          11: "dW+adam"}
+WAVE_NAMES = {0: "bcast+layer0", 1: "hidden+out-reduce", 2: "loss", 3: "backward", 4: "xg-exchange", 5: "adam"}
 
 
 def run(dims, steps, B=4, dropout=0.2):
@@ -46,9 +47,10 @@ def run(dims, steps, B=4, dropout=0.2):
     torch.cuda.synchronize()
     pr = prof.cpu().tolist()
     real_us = (pr[31] - pr[30]) / 100.0  # 100 MHz
-    cyc = sum(pr[i] for i in NAMES)
+    names = WAVE_NAMES if k.plan.use_wave else NAMES
+    cyc = sum(pr[i] for i in names)
     clock_ghz = cyc / (real_us * 1e3) if real_us > 0 else float("nan")
-    phases = {NAMES[i]: round(pr[i] / steps, 1) for i in NAMES if pr[i]}
+    phases = {names[i]: round(pr[i] / steps, 1) for i in names if pr[i]}
     return {"dims": dims, "B": B, "us_per_step_plain": round(plain_us, 3),
             "us_per_step_stamped": round(real_us / steps, 3), "clock_ghz": round(clock_ghz, 3),
             "cycles_per_step": round(cyc / steps, 1), "phase_cycles_per_step": phases,
