@@ -267,6 +267,21 @@ PYBIND11_MODULE(_dct_native, m) {
               "layernorm_bwd");
       });
   m.def(
+      "layernorm_bwd_ex",
+      [](uintptr_t dy, int dy_bf16, uintptr_t x, int x_bf16, uintptr_t w, uintptr_t mean, uintptr_t rstd, uintptr_t dx,
+         int dx_bf16, uintptr_t dx2, uintptr_t dres, uintptr_t dw, uintptr_t db, uintptr_t ws, int M, int N,
+         uintptr_t stream) {
+        check(dct_layernorm_bwd_ex(P<const void>(dy), dy_bf16, P<const void>(x), x_bf16, P<const float>(w),
+                                   P<const float>(mean), P<const float>(rstd), P<void>(dx), dx_bf16, P<uint16_t>(dx2),
+                                   P<const float>(dres), P<float>(dw), P<float>(db), P<float>(ws), M, N,
+                                   reinterpret_cast<void*>(stream)),
+              "layernorm_bwd_ex");
+      },
+      py::arg("dy"), py::arg("dy_bf16"), py::arg("x"), py::arg("x_bf16"), py::arg("w"), py::arg("mean"),
+      py::arg("rstd"), py::arg("dx"), py::arg("dx_bf16"), py::arg("dx2"), py::arg("dres"), py::arg("dw"),
+      py::arg("db"), py::arg("ws"), py::arg("M"), py::arg("N"), py::arg("stream"));
+  m.def("layernorm_bwd_ws_floats", &dct_layernorm_bwd_ws_floats);
+  m.def(
       "attention_fwd",
       [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t lse, int Bsz, int H, int T, int D, int ldq,
          int ldo, float scale, uintptr_t stream) {

@@ -232,13 +232,14 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 __device__ __forceinline__ int mc_swz(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
 
-// one 128 x 64 operand tile -> LDS image (4 glds per thread)
-template <bool MC>
+// one ROWS x 64 operand tile -> LDS image (ROWS/32 glds per thread; the MC image is 128 wide)
+template <bool MC, int ROWS = 128>
 __device__ __forceinline__ void g2_fill(const uint16_t* __restrict__ G, int ld, int R, int r0, int k0, char* img) {
+  static_assert(ROWS == 128 || !MC, "k-major (MC) images are 128 columns wide");
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < ROWS / 32; ++q) {
     const int L = q * 256 + wave * 64 + lane;  // linear 16-B chunk of the image
     const uint16_t* src;
     if (!MC) {
@@ -295,8 +296,14 @@ __device__ __forceinline__ bf16x8 g2_frag(const char* img, int rb, int ks, int l
 // (lane = column) so every atomic instruction covers 16 consecutive columns of 4 rows; the
 // plain-store kernels swap the MFMA operands instead (lane = row, 4 consecutive columns per
 // lane -> 8/16-byte row stores).
-template <bool TA, bool TB, bool SPLIT>
-__global__ __launch_bounds__(GNT, 2) void gemm2_kernel(GemmArgs g, int splits) {
+// BM = 64: half-height tiles for small-K / few-tile shapes (K <= 256 with M in the tens of
+// thousands: the transformer's projections).  Twice the workgroups and half the epilogue per
+// thread, and with a single k-tile only one LDS stage (32 KB) -> 4 resident workgroups per CU,
+// so one tile's global loads overlap another's epilogue.
+template <bool TA, bool TB, bool SPLIT, int BM = 128>
+__global__ __launch_bounds__(GNT, BM == 64 ? 4 : 2) void gemm2_kernel(GemmArgs g, int splits) {
+  static_assert(BM == 128 || (BM == 64 && !TA), "BM = 64 needs a row-major (KC) A image");
+  constexpr int IM = BM / 32;  // 16-row MFMA tiles per wave (2 x 2 waves)
   extern __shared__ __attribute__((aligned(16))) char smem2[];
   // [buf][A,B] images of 16 KB each
   constexpr bool AMC = TA, BMC = !TB;
@@ -308,7 +315,7 @@ __global__ __launch_bounds__(GNT, 2) void gemm2_kernel(GemmArgs g, int splits) {
   const int tile = wgid / splits, split = wgid - tile * splits;
   const int tiles_n = (g.N + GBN - 1) / GBN;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
-  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int m0 = tm * BM, n0 = tn * GBN;
   const int nk_all = g.K / GBK;
   const int per = (nk_all + splits - 1) / splits;
   const int kt0 = split * per;
@@ -316,19 +323,19 @@ __global__ __launch_bounds__(GNT, 2) void gemm2_kernel(GemmArgs g, int splits) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  f32x4 acc[4][4];
+  f32x4 acc[IM][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < IM; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   // colsum: one wave column (wc == 0) of the first N tile sums its A rows
   const bool do_cs = g.colsum != nullptr && tn == 0 && wc == 0;
-  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  float cs[IM] = {};
   auto img = [&](int buf, int op) -> char* { return smem2 + (buf * 2 + op) * G2_BYTES; };
   auto fill = [&](int buf, int kt) {
     const int k0 = kt * GBK;
-    if (!TA) g2_fill<false>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
+    if (!TA) g2_fill<false, BM>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
     else g2_fill<true>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
     if (TB) g2_fill<false>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
     else g2_fill<true>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
@@ -344,19 +351,19 @@ __global__ __launch_bounds__(GNT, 2) void gemm2_kernel(GemmArgs g, int splits) {
       const char* bi = img(cur, 1);
 #pragma unroll
       for (int ks = 0; ks < GBK / 32; ++ks) {
-        bf16x8 af[4], bfr[4];
+        bf16x8 af[IM], bfr[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = g2_frag<AMC>(ai, wr * 64 + i * 16, ks, lane);
+        for (int i = 0; i < IM; ++i) af[i] = g2_frag<AMC>(ai, wr * (BM / 2) + i * 16, ks, lane);
 #pragma unroll
         for (int j = 0; j < 4; ++j) bfr[j] = g2_frag<BMC>(bi, wc * 64 + j * 16, ks, lane);
         if (do_cs) {  // fused bias gradient: row sums of the A fragments (lane: 8 k of row l&15)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < IM; ++i)
 #pragma unroll
             for (int e = 0; e < 8; ++e) cs[i] += bf16_to_f32((uint16_t)af[i][e]);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < IM; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             acc[i][j] = SPLIT ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0)
@@ -368,11 +375,11 @@ __global__ __launch_bounds__(GNT, 2) void gemm2_kernel(GemmArgs g, int splits) {
   }
   if (do_cs) {  // lanes l, l+16, l+32, l+48 hold partial sums of the same row
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < IM; ++i) {
       float v = cs[i];
       v += __shfl_xor(v, 16);
       v += __shfl_xor(v, 32);
-      const int row = m0 + wr * 64 + i * 16 + (lane & 15);
+      const int row = m0 + wr * (BM / 2) + i * 16 + (lane & 15);
       if (lane < 16 && row < g.M) atomicAdd(g.colsum + row, v);
     }
   }
@@ -383,14 +390,14 @@ __global__ __launch_bounds__(GNT, 2) void gemm2_kernel(GemmArgs g, int splits) {
   if (SPLIT) {  // natural layout: col = lane&15, rows 4*(lane>>4) + r
     const int col_l = lane & 15, row_l = (lane >> 4) * 4;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < IM; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = n0 + wc * 64 + j * 16 + col_l;
         if (col >= g.N) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wr * 64 + i * 16 + row_l + r;
+          const int row = m0 + wr * (BM / 2) + i * 16 + row_l + r;
           if (row < g.M) atomicAdd(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col, acc[i][j][r] * g.alpha);
         }
       }
@@ -402,8 +409,8 @@ __global__ __launch_bounds__(GNT, 2) void gemm2_kernel(GemmArgs g, int splits) {
   const bool vec_ok = (g.ldc % 4 == 0) && ((((uintptr_t)g.C) & 15) == 0) &&
                       (!g.aux || (((uintptr_t)g.aux) & 7) == 0);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = m0 + wr * 64 + i * 16 + c16;
+  for (int i = 0; i < IM; ++i) {
+    const int row = m0 + wr * (BM / 2) + i * 16 + c16;
     if (row >= g.M) continue;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -527,12 +534,12 @@ static bool gemm_v2_ok(const dct::GemmArgs& g, int ta, int tb) {
 
 template <bool TA, bool TB>
 static hipError_t launch_gemm2(const dct::GemmArgs& g, hipStream_t st) {
-  const size_t lds = 4 * (size_t)dct::G2_BYTES;
   hipError_t e;
-  const int tiles = ((g.M + dct::GBM - 1) / dct::GBM) * ((g.N + dct::GBN - 1) / dct::GBN);
+  const int tiles_n = (g.N + dct::GBN - 1) / dct::GBN;
+  const int tiles = ((g.M + dct::GBM - 1) / dct::GBM) * tiles_n;
   const int nk = g.K / dct::GBK;
   int splits = 1;
-  if (g.out_f32 && g.epilogue == dct::EPI_NONE && g.alpha == 1.0f && tiles < 256 && nk >= 8) {
+  if (g.out_f32 && g.epilogue == dct::EPI_NONE && !g.residual && g.alpha == 1.0f && tiles < 256 && nk >= 8) {
     splits = std::min(nk / 4, (512 + tiles - 1) / tiles);
     if (splits < 1) splits = 1;
   }
@@ -540,11 +547,22 @@ static hipError_t launch_gemm2(const dct::GemmArgs& g, hipStream_t st) {
     e = hipMemset2DAsync(g.C, (size_t)g.ldc * 4, 0, (size_t)g.N * 4, (size_t)g.M, st);
     if (e != hipSuccess) return e;
   }
-  auto fn = splits > 1 ? dct::gemm2_kernel<TA, TB, true> : dct::gemm2_kernel<TA, TB, false>;
-  e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(fn, dim3(tiles * splits), dim3(dct::GNT), lds, st, g, splits);
-  return hipGetLastError();
+  // one k-tile -> one LDS stage
+  const size_t lds = (nk > 1 ? 4 : 2) * (size_t)dct::G2_BYTES;
+  auto launch = [&](auto fn, int grid) -> hipError_t {
+    hipError_t err = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (err != hipSuccess) return err;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(dct::GNT), lds, st, g, splits);
+    return hipGetLastError();
+  };
+  if constexpr (!TA) {
+    // small K and too few 128-row tiles to fill 256 CUs several times over: half-height tiles
+    static const bool force128 = getenv("DCT_GEMM_BM128") != nullptr;
+    if (splits == 1 && nk <= 4 && tiles < 1024 && !force128)
+      return launch(dct::gemm2_kernel<TA, TB, false, 64>, ((g.M + 63) / 64) * tiles_n);
+  }
+  if (splits > 1) return launch(dct::gemm2_kernel<TA, TB, true>, tiles * splits);
+  return launch(dct::gemm2_kernel<TA, TB, false>, tiles);
 }
 
 extern "C" int dct_bias_act_bwd(const void* dY, const void* act_aux, uint16_t* dZ, float* dbias, int M, int N,
@@ -587,16 +605,7 @@ extern "C" int dct_gemm_bf16_residual(const uint16_t* A, const uint16_t* W, floa
   g.vec_a = ((((uintptr_t)A) & 15) == 0) && (K % 8 == 0);
   g.vec_b = ((((uintptr_t)W) & 15) == 0) && (K % 8 == 0);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (gemm_v2_ok(g, 0, 1)) {
-    // no split-K here: the residual is folded into the (single) writer of each element
-    const int tiles = ((M + dct::GBM - 1) / dct::GBM) * ((N + dct::GBN - 1) / dct::GBN);
-    const size_t lds = 4 * (size_t)dct::G2_BYTES;
-    auto fn = dct::gemm2_kernel<false, true, false>;
-    hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(fn, dim3(tiles), dim3(dct::GNT), lds, st, g, 1);
-    return (int)hipGetLastError();
-  }
+  if (gemm_v2_ok(g, 0, 1)) return (int)launch_gemm2<false, true>(g, st);  // never split-K with a residual
   return (int)launch_gemm<false, true>(g, st);
 }
 

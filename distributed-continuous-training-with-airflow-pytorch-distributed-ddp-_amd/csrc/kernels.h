@@ -58,6 +58,13 @@ int dct_layernorm_fwd(const void* x, const float* w, const float* b, void* y, fl
                       float eps, int in_bf16, int out_bf16, void* stream);
 int dct_layernorm_bwd(const void* dy, const void* x, const float* w, const float* mean, const float* rstd, void* dx,
                       float* dw, float* db, int M, int N, int bf16_io, void* stream);
+// narrow rows (N <= 256, N % 4 == 0, 16-B aligned): per-operand dtypes, + dres (fp32 residual
+// gradient added into dx), optional bf16 copy dx2; dw/db ACCUMULATE (+=) through the slot
+// workspace ws (dct_layernorm_bwd_ws_floats(N) floats, zeroed once, re-zeroed by the kernel).
+int dct_layernorm_bwd_ex(const void* dy, int dy_bf16, const void* x, int x_bf16, const float* w, const float* mean,
+                         const float* rstd, void* dx, int dx_bf16, uint16_t* dx2, const float* dres, float* dw,
+                         float* db, float* ws, int M, int N, void* stream);
+int dct_layernorm_bwd_ws_floats(int N);
 // q/k/v: element (b, t, h, d) at ptr[(b*T + t)*ldq + h*D + d] (a packed QKV projection
 // output); o/dout: at ptr[(b*T + t)*ldo + h*D + d]; lse fp32 [B*H*T].
 int dct_attention_fwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, uint16_t* o, float* lse, int Bsz, int H,

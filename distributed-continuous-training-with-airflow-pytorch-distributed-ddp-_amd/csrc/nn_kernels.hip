@@ -314,24 +314,41 @@ __global__ __launch_bounds__(256) void layernorm_fwd_small(const void* x, const 
   }
 }
 
+// Backward of the narrow LayerNorm, fused for pre-norm residual blocks:
+//   dx = rstd * (g - mean(g) - xhat * mean(g * xhat)) [+ dres],  g = dy * w
+// with the residual-stream gradient dres folded in (saves the autograd add) and an optional
+// bf16 copy of dx (the next GEMM's operand; saves a conversion pass).  dw/db column sums go
+// through NSLOT striped slot rows of a persistent workspace (atomics spread over 16x the
+// addresses: a 1024-way fan-in on N addresses serialised the old kernel to ~30 us at M=32k);
+// layernorm_bwd_fold then adds the slots into dw/db and re-zeroes them.
+struct LnBwdArgs {
+  const void* dy; const void* x; const float* w; const float* mean; const float* rstd;
+  void* dx; uint16_t* dx2; const float* dres; float* dw; float* db; float* ws;
+  int M, N, dy_bf16, x_bf16, dx_bf16;
+};
+constexpr int LN_NSLOT = 16;
+
 template <int LPR>
-__global__ __launch_bounds__(256) void layernorm_bwd_small(const void* dy, const void* x, const float* w,
-                                                           const float* mean_in, const float* rstd_in, void* dx,
-                                                           float* dw, float* db, int M, int N, int bf16_io) {
+__global__ __launch_bounds__(256) void layernorm_bwd_small(LnBwdArgs a) {
   constexpr int RPW = 64 / LPR;
   __shared__ float red[2][256 * 4];
+  const int N = a.N;
   const int lane = threadIdx.x & 63, sub = lane / LPR, li = lane % LPR;
   const int c0 = li * 4;
   const bool act = c0 < N;
   float wv[4] = {1.f, 1.f, 1.f, 1.f};
-  if (act && w) { const float4 t = *reinterpret_cast<const float4*>(w + c0); wv[0] = t.x; wv[1] = t.y; wv[2] = t.z; wv[3] = t.w; }
+  if (act && a.w) { const float4 t = *reinterpret_cast<const float4*>(a.w + c0); wv[0] = t.x; wv[1] = t.y; wv[2] = t.z; wv[3] = t.w; }
   float aw[4] = {0.f, 0.f, 0.f, 0.f}, ab[4] = {0.f, 0.f, 0.f, 0.f};
   const int wave_g = blockIdx.x * 4 + (threadIdx.x >> 6);
-  for (int row = wave_g * RPW + sub; row < M; row += gridDim.x * 4 * RPW) {
+  for (int row = wave_g * RPW + sub; row < a.M; row += gridDim.x * 4 * RPW) {
     const size_t base = (size_t)row * N + c0;
-    float xv[4] = {0.f, 0.f, 0.f, 0.f}, gv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (act) { ld4any(x, base, bf16_io, xv); ld4any(dy, base, bf16_io, gv); }
-    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xv[4] = {0.f, 0.f, 0.f, 0.f}, gv[4] = {0.f, 0.f, 0.f, 0.f}, rv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (act) {
+      ld4any(a.x, base, a.x_bf16, xv);
+      ld4any(a.dy, base, a.dy_bf16, gv);
+      if (a.dres) ld4any(a.dres, base, 0, rv);
+    }
+    const float mean = a.mean[row], rstd = a.rstd[row];
     float xh[4], gw[4], s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -347,21 +364,41 @@ __global__ __launch_bounds__(256) void layernorm_bwd_small(const void* dy, const
     if (act) {
       float o[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = rstd * (gw[e] - s1 - xh[e] * s2);
-      st4any(dx, base, bf16_io, o);
+      for (int e = 0; e < 4; ++e) o[e] = rstd * (gw[e] - s1 - xh[e] * s2) + rv[e];
+      st4any(a.dx, base, a.dx_bf16, o);
+      if (a.dx2) st4any(a.dx2, base, 1, o);
     }
   }
+  if (!a.dw && !a.db) return;
   // column partials: threads with the same li own the same 4 columns
 #pragma unroll
   for (int e = 0; e < 4; ++e) { red[0][threadIdx.x * 4 + e] = aw[e]; red[1][threadIdx.x * 4 + e] = ab[e]; }
   __syncthreads();
+  float* slot = a.ws + (size_t)(blockIdx.x % LN_NSLOT) * 2 * N;
   for (int cc = threadIdx.x; cc < LPR * 4; cc += blockDim.x) {
     const int l = cc / 4, e = cc % 4;
     if (l * 4 >= N) continue;
     float sw = 0.f, sb = 0.f;
     for (int t = l; t < 256; t += LPR) { sw += red[0][t * 4 + e]; sb += red[1][t * 4 + e]; }
-    if (dw) atomicAdd(&dw[l * 4 + e], sw);
-    if (db) atomicAdd(&db[l * 4 + e], sb);
+    atomicAdd(slot + cc, sw);
+    atomicAdd(slot + N + cc, sb);
+  }
+}
+
+// folds the slot rows into dw/db (+=) and re-zeroes them (one block, after the row kernel).
+// A last-block ticket inside the row kernel was tried: 1024 serialised ticket atomics plus an
+// agent-scope release fence (L2 write-back) per block made it 3x slower than this extra launch.
+__global__ __launch_bounds__(256) void layernorm_bwd_fold(float* ws, float* dw, float* db, int N) {
+  for (int cc = threadIdx.x; cc < 2 * N; cc += blockDim.x) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < LN_NSLOT; ++k) {
+      float* p = ws + (size_t)k * 2 * N + cc;
+      s += *p;
+      *p = 0.f;
+    }
+    float* dst = cc < N ? dw : db;
+    if (dst) dst[cc < N ? cc : cc - N] += s;
   }
 }
 
@@ -449,20 +486,33 @@ int dct_layernorm_fwd(const void* x, const float* w, const float* b, void* y, fl
   return (int)hipGetLastError();
 }
 
+int dct_layernorm_bwd_ex(const void* dy, int dy_bf16, const void* x, int x_bf16, const float* w, const float* mean,
+                         const float* rstd, void* dx, int dx_bf16, uint16_t* dx2, const float* dres, float* dw,
+                         float* db, float* ws, int M, int N, void* stream) {
+  if (M <= 0) return 0;
+  const int lpr = ln_lpr(N, dy, x, dx);
+  if (!lpr || !ws || (dres && (((uintptr_t)dres) & 15)) || (dx2 && (((uintptr_t)dx2) & 7)))
+    return (int)hipErrorInvalidValue;
+  dct::LnBwdArgs a{dy, x, w, mean, rstd, dx, dx2, dres, dw, db, ws, M, N, dy_bf16, x_bf16, dx_bf16};
+  const int rows_per_block = 4 * (64 / lpr);
+  const int grid = grid_cap((M + rows_per_block - 1) / rows_per_block, 1, 1024);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define LNB(L) hipLaunchKernelGGL(dct::layernorm_bwd_small<L>, dim3(grid), dim3(256), 0, st, a)
+  switch (lpr) { case 1: LNB(1); break; case 2: LNB(2); break; case 4: LNB(4); break; case 8: LNB(8); break;
+                 case 16: LNB(16); break; case 32: LNB(32); break; default: LNB(64); }
+#undef LNB
+  if (dw || db) hipLaunchKernelGGL(dct::layernorm_bwd_fold, dim3(1), dim3(256), 0, st, ws, dw, db, N);
+  return (int)hipGetLastError();
+}
+
+int dct_layernorm_bwd_ws_floats(int N) { return dct::LN_NSLOT * 2 * N; }
+
 int dct_layernorm_bwd(const void* dy, const void* x, const float* w, const float* mean, const float* rstd, void* dx,
                       float* dw, float* db, int M, int N, int bf16_io, void* stream) {
   if (N > 64 * dct::LN_MAX) return (int)hipErrorInvalidValue;
   if (M <= 0) return 0;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (const int lpr = ln_lpr(N, dy, x, dx)) {
-    const int rows_per_block = 4 * (64 / lpr);
-    const int grid = grid_cap((M + rows_per_block - 1) / rows_per_block, 1, 1024);
-#define LNB(L) hipLaunchKernelGGL(dct::layernorm_bwd_small<L>, dim3(grid), dim3(256), 0, st, dy, x, w, mean, rstd, dx, dw, db, M, N, bf16_io)
-    switch (lpr) { case 1: LNB(1); break; case 2: LNB(2); break; case 4: LNB(4); break; case 8: LNB(8); break;
-                   case 16: LNB(16); break; case 32: LNB(32); break; default: LNB(64); }
-#undef LNB
-    return (int)hipGetLastError();
-  }
+  // generic one-wave-per-row kernel (any N <= 64 * LN_MAX, any alignment); the narrow fused
+  // path needs the caller's slot workspace -> dct_layernorm_bwd_ex
   hipLaunchKernelGGL(dct::layernorm_bwd_kernel, dim3(grid_cap((M + 3) / 4, 1, 1024)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), dy, x, w, mean, rstd, dx, dw, db, M, N, bf16_io);
   return (int)hipGetLastError();

@@ -4,8 +4,9 @@ Each numeric feature f of a row becomes a token ``x_f * E_f + c_f`` (d_model wid
 transformer blocks (LayerNorm -> packed QKV -> feature-token attention -> out projection ->
 residual; LayerNorm -> GELU MLP -> residual) mix the tokens; the mean token goes through a
 final LayerNorm and a linear head.  On MI355X every GEMM / LayerNorm / attention is a native
-HIP kernel (ops/nn.py) with bf16 activations on an fp32 residual stream; on CPU the same module
-runs plain torch ops.  Training contract = the reference LightningModule's (training_step logs
+HIP kernel (ops/nn.py) with bf16 activations on an fp32 residual stream, and each pre-norm sub-block
+is ONE fused autograd node (prenorm_attention / prenorm_ffn); on CPU the same module runs
+plain torch ops.  Training contract = the reference LightningModule's (training_step logs
 ``train_loss``; validation_step logs ``val_loss`` / ``val_acc``; Adam).
 """
 from __future__ import annotations
@@ -16,7 +17,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.nn import ACT_GELU, attention, layer_norm, linear, linear_residual
+from ..ops.nn import layer_norm, linear, prenorm_attention, prenorm_ffn
 from ..trainer.module import TrainModule
 
 
@@ -32,14 +33,9 @@ class _Block(nn.Module):
         self.fc2 = nn.Linear(ffn_mult * d, d)
 
     def forward(self, h: torch.Tensor, B: int, T: int) -> torch.Tensor:
-        d = h.shape[1]
-        a = layer_norm(h, self.ln1_w, self.ln1_b)
-        qkv = linear(a, self.qkv.weight, self.qkv.bias)
-        o = attention(qkv, B, self.heads, T, d // self.heads)
-        h = linear_residual(o, self.proj.weight, self.proj.bias, h)
-        a = layer_norm(h, self.ln2_w, self.ln2_b)
-        f = linear(a, self.fc1.weight, self.fc1.bias, ACT_GELU)
-        return linear_residual(f, self.fc2.weight, self.fc2.bias, h)
+        h = prenorm_attention(h, self.ln1_w, self.ln1_b, self.qkv.weight, self.qkv.bias, self.proj.weight,
+                              self.proj.bias, B, self.heads, T)
+        return prenorm_ffn(h, self.ln2_w, self.ln2_b, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias)
 
 
 class TabTransformer(TrainModule):

@@ -4,6 +4,9 @@ Used by the transformer-style models (models/tabtransformer.py) on MI355X:
   * ``linear``     - MFMA GEMM forward with fused bias / ReLU / GELU epilogue; backward = two
                      GEMMs (dX = dZ W, dW = dZ^T X with the bias gradient fused as a column sum)
                      and one elementwise activation-derivative pass when needed;
+  * ``ffn_residual`` - the GELU MLP sub-block with gelu' and both bias gradients fused into GEMMs;
+  * ``prenorm_attention`` / ``prenorm_ffn`` - whole pre-norm residual sub-blocks as single
+                     autograd nodes (LayerNorm backward fused with the residual-gradient add);
   * ``layer_norm`` - one wave per row, fp32 statistics (fwd) / fused dX, dgamma, dbeta (bwd);
   * ``attention``  - fused feature-token attention over a packed QKV projection (online softmax
                      forward, recompute backward).
@@ -12,7 +15,9 @@ native module is required (``native()`` raises if it is missing - no silent fall
 """
 from __future__ import annotations
 
+import contextlib
 import math
+from typing import Dict, Iterable, Optional
 
 import torch
 import torch.nn.functional as F
@@ -21,10 +26,135 @@ from ._native import native
 
 ACT_NONE, ACT_RELU, ACT_GELU = 0, 1, 2
 _EPI = {ACT_NONE: 1, ACT_RELU: 2, ACT_GELU: 3}  # EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_GELU
+EPI_GELU_GRAD = 5
+_SKINNY_MAX = 8  # csrc/skinny.hip SK_CMAX
 
 
 def _stream():
     return torch.cuda.current_stream().cuda_stream
+
+
+# ----------------------------------------------------------------------------- engine binding
+class _Binding:
+    def __init__(self, params: Iterable[torch.Tensor], shadows: Optional[Dict[int, torch.Tensor]]):
+        self.direct = {id(p) for p in params}
+        self.shadows = shadows or {}
+
+
+_BOUND: Optional[_Binding] = None
+
+
+@contextlib.contextmanager
+def bound_params(params: Iterable[torch.Tensor], bf16_shadows: Optional[Dict[int, torch.Tensor]] = None):
+    """Engine-scoped fast paths for the ops below (trainer/engines.py AutogradEngine):
+
+    * gradient accumulation fusion - the weight-gradient GEMMs / LayerNorm column sums of a
+      bound parameter ACCUMULATE straight into ``p.grad`` (a view of the flat DDP bucket
+      buffer, zeroed once per step) and the op returns ``None`` for it, so there is no per-
+      parameter gradient tensor, fill or AccumulateGrad add.  Post-accumulate-grad hooks still
+      fire (autograd runs them for undefined gradients too), so bucket all-reduces launch as before;
+    * bf16 shadow weights - ``bf16_shadows[id(p)]`` (kept current by the fused Adam) replaces
+      the per-step fp32->bf16 weight conversion.
+    """
+    global _BOUND
+    prev, _BOUND = _BOUND, _Binding(params, bf16_shadows)
+    try:
+        yield
+    finally:
+        _BOUND = prev
+
+
+def _w16(w: torch.Tensor) -> torch.Tensor:
+    b = _BOUND
+    if b is not None:
+        sh = b.shadows.get(id(w))
+        if sh is not None and sh.data_ptr() % 16 == 0:  # the MFMA / skinny paths stage 16-B rows
+            return sh
+    return w.detach().to(torch.bfloat16).contiguous()
+
+
+def _grad_dst(p: torch.Tensor, zero: bool = False):
+    """(buffer, direct): p.grad itself when accumulation into it is bound, else a new tensor."""
+    b = _BOUND
+    if b is not None and id(p) in b.direct:
+        g = p.grad
+        if g is not None and g.dtype == torch.float32 and g.is_contiguous() and g.shape == p.shape:
+            return g, True
+    alloc = torch.zeros if zero else torch.empty
+    return alloc(p.shape, dtype=torch.float32, device=p.device), False
+
+
+# the bf16 copy of the last residual-stream gradient a fused LayerNorm backward produced: the
+# next (earlier) block's backward receives exactly that fp32 tensor as its output gradient
+_BF16_PAIR = None
+
+
+def _remember_bf16(t32: torch.Tensor, t16: torch.Tensor):
+    global _BF16_PAIR
+    _BF16_PAIR = (t32, t32._version, t16)
+
+
+def _bf16_of(t: torch.Tensor) -> torch.Tensor:
+    pr = _BF16_PAIR
+    if pr is not None:
+        t32, ver, t16 = pr
+        if t32 is t or (t32.data_ptr() == t.data_ptr() and t32.shape == t.shape and t32.stride() == t.stride()
+                        and t.dtype == torch.float32 and t._version == ver):
+            return t16
+    t = t.contiguous()
+    return t if t.dtype == torch.bfloat16 else t.to(torch.bfloat16)
+
+
+_LN_WS: Dict[tuple, torch.Tensor] = {}
+
+
+def _ln_ws(device: torch.device, N: int) -> torch.Tensor:
+    """Persistent zeroed slot workspace of the fused LayerNorm backward (re-zeroed by the kernel)."""
+    key = (device.index, N)
+    ws = _LN_WS.get(key)
+    if ws is None:
+        ws = torch.zeros(native().layernorm_bwd_ws_floats(N), dtype=torch.float32, device=device)
+        _LN_WS[key] = ws
+    return ws
+
+
+def _ln_fused_ok(N: int) -> bool:
+    return N % 4 == 0 and N <= 256
+
+
+def _ln_bwd(nat, dy16, x, w, b, mean, rstd, dres=None, want_bf16=False):
+    """Fused narrow LayerNorm backward: dx fp32 (+ dres) [+ bf16 copy]; dw/db into w/b grads."""
+    M, N = x.shape
+    dx = torch.empty(M, N, dtype=torch.float32, device=x.device)
+    dx16 = torch.empty(M, N, dtype=torch.bfloat16, device=x.device) if want_bf16 else None
+    dw, dw_direct = _grad_dst(w, zero=True)
+    db, db_direct = _grad_dst(b, zero=True)
+    nat.layernorm_bwd_ex(dy16.data_ptr(), 1, x.data_ptr(), 0, w.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                         dx.data_ptr(), 0, dx16.data_ptr() if dx16 is not None else 0,
+                         dres.data_ptr() if dres is not None else 0, dw.data_ptr(), db.data_ptr(),
+                         _ln_ws(x.device, N).data_ptr(), M, N, _stream())
+    if dx16 is not None:
+        _remember_bf16(dx, dx16)
+    return dx, None if dw_direct else dw, None if db_direct else db
+
+
+def _dw_gemm(nat, dz16, x16, w, b, st):
+    """dW (+)= dZ^T X with the bias gradient (+)= colsum(dZ) fused; returns the non-direct grads."""
+    M, N = dz16.shape
+    K = x16.shape[1]
+    dw, dw_direct = _grad_dst(w)
+    db, db_direct = _grad_dst(b, zero=True)
+    nat.gemm_bf16_ex(dz16.data_ptr(), x16.data_ptr(), dw.data_ptr(), 0, N, K, M, N, K, K, 1, 0, 0, 1,
+                     1 if dw_direct else 0, 0, db.data_ptr(), st)
+    return None if dw_direct else dw, None if db_direct else db
+
+
+def _mm(nat, a16, b16, M, N, K, st, epi=0, aux=None, out=None):
+    """C[M, N] = A[M, K] B[K, N] (bf16 out) with an optional elementwise backward epilogue."""
+    c = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=a16.device)
+    nat.gemm_bf16(a16.data_ptr(), b16.data_ptr(), c.data_ptr(), 0, M, N, K, K, N, N, 0, 0, epi, 0, 0,
+                  aux.data_ptr() if aux is not None else 0, st)
+    return c
 
 
 class _LinearFn(torch.autograd.Function):
@@ -36,40 +166,55 @@ class _LinearFn(torch.autograd.Function):
             x = x.to(torch.bfloat16)
         M, K = x.shape
         N = weight.shape[0]
-        wb = weight.detach().to(torch.bfloat16).contiguous()
+        wb = _w16(weight)
+        st = _stream()
         y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-        pre = torch.empty_like(y) if act == ACT_GELU else None
-        nat.gemm_bf16(x.data_ptr(), wb.data_ptr(), y.data_ptr(), bias.data_ptr(), M, N, K, K, K, N, 0, 1, _EPI[act], 0,
-                      0, pre.data_ptr() if pre is not None else 0, _stream())
+        ctx.skinny = act == ACT_NONE and N <= _SKINNY_MAX and K % 8 == 0
+        pre = None
+        if ctx.skinny:  # classifier heads: a bandwidth kernel, not a 128x128 MFMA tile
+            nat.skinny_fwd(x.data_ptr(), wb.data_ptr(), bias.data_ptr(), y.data_ptr(), M, K, N, st)
+        else:
+            pre = torch.empty_like(y) if act == ACT_GELU else None
+            nat.gemm_bf16(x.data_ptr(), wb.data_ptr(), y.data_ptr(), bias.data_ptr(), M, N, K, K, K, N, 0, 1,
+                          _EPI[act], 0, 0, pre.data_ptr() if pre is not None else 0, st)
         ctx.act = act
         ctx.save_for_backward(x, wb, y if act == ACT_RELU else pre)
+        ctx.params = (weight, bias)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         nat = native()
         x, wb, aux = ctx.saved_tensors
+        weight, bias = ctx.params
         act = ctx.act
-        dy = dy.contiguous()
-        if dy.dtype != torch.bfloat16:
-            dy = dy.to(torch.bfloat16)
+        dy = _bf16_of(dy)
         M, K = x.shape
         N = wb.shape[0]
         st = _stream()
-        db = torch.zeros(N, dtype=torch.float32, device=x.device)
+        dx = None
+        if ctx.skinny:
+            dw, dw_direct = _grad_dst(weight, zero=True)
+            db, db_direct = _grad_dst(bias, zero=True)
+            nat.skinny_dw(dy.data_ptr(), x.data_ptr(), dw.data_ptr(), db.data_ptr(), M, K, N, st)
+            if ctx.needs_input_grad[0]:
+                dx = torch.empty(M, K, dtype=torch.bfloat16, device=x.device)
+                nat.skinny_dx(dy.data_ptr(), wb.data_ptr(), 0, dx.data_ptr(), M, K, N, st)
+            return dx, None if dw_direct else dw, None if db_direct else db, None
         if act == ACT_NONE:
             dz = dy
-            colsum = db.data_ptr()
+            dw, db = _dw_gemm(nat, dz, x, weight, bias, st)
         else:  # dZ = dY * act'(.) and db in one pass
             dz = torch.empty_like(dy)
+            db, db_direct = _grad_dst(bias, zero=True)
             nat.bias_act_bwd(dy.data_ptr(), aux.data_ptr(), dz.data_ptr(), db.data_ptr(), M, N, N, act, 1, st)
-            colsum = 0
-        dw = torch.empty(N, K, dtype=torch.float32, device=x.device)
-        nat.gemm_bf16_ex(dz.data_ptr(), x.data_ptr(), dw.data_ptr(), 0, N, K, M, N, K, K, 1, 0, 0, 1, 0, 0, colsum, st)
-        dx = None
+            dw, dw_direct = _grad_dst(weight)
+            nat.gemm_bf16_ex(dz.data_ptr(), x.data_ptr(), dw.data_ptr(), 0, N, K, M, N, K, K, 1, 0, 0, 1,
+                             1 if dw_direct else 0, 0, 0, st)
+            dw = None if dw_direct else dw
+            db = None if db_direct else db
         if ctx.needs_input_grad[0]:
-            dx = torch.empty(M, K, dtype=torch.bfloat16, device=x.device)
-            nat.gemm_bf16(dz.data_ptr(), wb.data_ptr(), dx.data_ptr(), 0, M, K, N, N, K, K, 0, 0, 0, 0, 0, 0, st)
+            dx = _mm(nat, dz, wb, M, K, N, st)
         return dx, dw, db, None
 
 
@@ -93,29 +238,25 @@ class _LinearResidualFn(torch.autograd.Function):
         h = h.contiguous().float()
         M, K = x.shape
         N = weight.shape[0]
-        wb = weight.detach().to(torch.bfloat16).contiguous()
+        wb = _w16(weight)
         out = torch.empty(M, N, dtype=torch.float32, device=x.device)
         nat.gemm_bf16_residual(x.data_ptr(), wb.data_ptr(), out.data_ptr(), bias.data_ptr(), h.data_ptr(), M, N, K,
                                _stream())
         ctx.save_for_backward(x, wb)
+        ctx.params = (weight, bias)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         nat = native()
         x, wb = ctx.saved_tensors
+        weight, bias = ctx.params
         M, K = x.shape
         N = wb.shape[0]
         st = _stream()
-        dz = dout.contiguous().to(torch.bfloat16)
-        db = torch.zeros(N, dtype=torch.float32, device=x.device)
-        dw = torch.empty(N, K, dtype=torch.float32, device=x.device)
-        nat.gemm_bf16_ex(dz.data_ptr(), x.data_ptr(), dw.data_ptr(), 0, N, K, M, N, K, K, 1, 0, 0, 1, 0, 0,
-                         db.data_ptr(), st)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx = torch.empty(M, K, dtype=torch.bfloat16, device=x.device)
-            nat.gemm_bf16(dz.data_ptr(), wb.data_ptr(), dx.data_ptr(), 0, M, K, N, N, K, K, 0, 0, 0, 0, 0, 0, st)
+        dz = _bf16_of(dout)
+        dw, db = _dw_gemm(nat, dz, x, weight, bias, st)
+        dx = _mm(nat, dz, wb, M, K, N, st) if ctx.needs_input_grad[0] else None
         return dx, dw, db, dout
 
 
@@ -126,18 +267,85 @@ def linear_residual(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, h
     return h.float() + F.linear(x.float(), weight, bias)
 
 
+def _ffn_fwd(nat, a, w1b, b1, w2b, b2, h, st):
+    M, K = a.shape
+    N = w1b.shape[0]
+    f = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    pre = torch.empty_like(f)
+    nat.gemm_bf16(a.data_ptr(), w1b.data_ptr(), f.data_ptr(), b1.data_ptr(), M, N, K, K, K, N, 0, 1, _EPI[ACT_GELU],
+                  0, 0, pre.data_ptr(), st)
+    out = torch.empty(M, K, dtype=torch.float32, device=a.device)
+    nat.gemm_bf16_residual(f.data_ptr(), w2b.data_ptr(), out.data_ptr(), b2.data_ptr(), h.data_ptr(), M, K, N, st)
+    return f, pre, out
+
+
+def _ffn_bwd(nat, dz2, a, w1b, w2b, f, pre, params, st, want_da=True):
+    """Backward of h + W2 gelu(W1 a + b1) + b2 from dZ2 (bf16): gelu' in the dF GEMM epilogue,
+    both bias gradients as dW-GEMM column sums -> (da, dw1, db1, dw2, db2)."""
+    w1, b1, w2, b2 = params
+    M, K = a.shape
+    N = w1b.shape[0]
+    dw2, db2 = _dw_gemm(nat, dz2, f, w2, b2, st)
+    dpre = _mm(nat, dz2, w2b, M, N, K, st, EPI_GELU_GRAD, pre)
+    dw1, db1 = _dw_gemm(nat, dpre, a, w1, b1, st)
+    da = _mm(nat, dpre, w1b, M, K, N, st) if want_da else None
+    return da, dw1, db1, dw2, db2
+
+
+class _FFNResidualFn(torch.autograd.Function):
+    """out = h + W2 gelu(W1 a + b1) + b2: the transformer MLP sub-block as four GEMMs and nothing else.
+
+    Forward stores the GELU pre-activation from the first GEMM's epilogue; backward folds gelu'
+    into the epilogue of the dF GEMM (EPI_GELU_GRAD) and both bias gradients into the dW GEMMs'
+    column sums, so no elementwise activation-backward pass and no dF intermediate round trip."""
+
+    @staticmethod
+    def forward(ctx, a, w1, b1, w2, b2, h):
+        nat = native()
+        a = a.contiguous()
+        if a.dtype != torch.bfloat16:
+            a = a.to(torch.bfloat16)
+        h = h.contiguous().float()
+        w1b, w2b = _w16(w1), _w16(w2)
+        f, pre, out = _ffn_fwd(nat, a, w1b, b1, w2b, b2, h, _stream())
+        ctx.save_for_backward(a, w1b, w2b, f, pre)
+        ctx.params = (w1, b1, w2, b2)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        a, w1b, w2b, f, pre = ctx.saved_tensors
+        grads = _ffn_bwd(native(), _bf16_of(dout), a, w1b, w2b, f, pre, ctx.params, _stream(),
+                         ctx.needs_input_grad[0])
+        return (*grads, dout)
+
+
+def ffn_residual(a: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor,
+                 h: torch.Tensor) -> torch.Tensor:
+    """h + W2 gelu(W1 a + b1) + b2 (fp32 residual stream; bf16 GEMMs on GPU)."""
+    if a.is_cuda:
+        return _FFNResidualFn.apply(a, w1, b1, w2, b2, h)
+    return h.float() + F.linear(F.gelu(F.linear(a.float(), w1, b1)), w2, b2)
+
+
+def _ln_fwd(nat, h, w, b, eps, st):
+    M, N = h.shape
+    a = torch.empty(M, N, dtype=torch.bfloat16, device=h.device)
+    mean = torch.empty(M, dtype=torch.float32, device=h.device)
+    rstd = torch.empty_like(mean)
+    nat.layernorm_fwd(h.data_ptr(), w.data_ptr(), b.data_ptr(), a.data_ptr(), mean.data_ptr(), rstd.data_ptr(), M, N,
+                      float(eps), 0, 1, st)
+    return a, mean, rstd
+
+
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, eps):
         nat = native()
         x = x.contiguous().float()
-        M, N = x.shape
-        y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-        mean = torch.empty(M, dtype=torch.float32, device=x.device)
-        rstd = torch.empty_like(mean)
-        nat.layernorm_fwd(x.data_ptr(), weight.data_ptr(), bias.data_ptr(), y.data_ptr(), mean.data_ptr(),
-                          rstd.data_ptr(), M, N, float(eps), 0, 1, _stream())
+        y, mean, rstd = _ln_fwd(nat, x, weight, bias, eps, _stream())
         ctx.save_for_backward(x, weight, mean, rstd)
+        ctx.params = (weight, bias)
         return y
 
     @staticmethod
@@ -145,6 +353,8 @@ class _LayerNormFn(torch.autograd.Function):
         nat = native()
         x, weight, mean, rstd = ctx.saved_tensors
         M, N = x.shape
+        if _ln_fused_ok(N):
+            return (*_ln_bwd(nat, _bf16_of(dy), x, weight, ctx.params[1], mean, rstd), None)
         dy = dy.contiguous().float()
         dx = torch.empty_like(x)
         dw = torch.zeros(N, dtype=torch.float32, device=x.device)
@@ -159,6 +369,109 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: f
     if x.is_cuda:
         return _LayerNormFn.apply(x, weight, bias, eps)
     return F.layer_norm(x.float(), (x.shape[-1],), weight, bias, eps)
+
+
+# ----------------------------------------------------------------------------- fused pre-norm blocks
+class _PreNormFFNFn(torch.autograd.Function):
+    """h + FFN(LayerNorm(h)) as one autograd node: LN fwd -> GEMM(+b, GELU, keep pre-act) ->
+    GEMM(+b, +h residual, fp32).  Backward: the FFN chain above, then ONE LayerNorm-backward
+    kernel that also adds the residual-path gradient and emits the bf16 copy the next block's
+    GEMMs consume - no autograd adds, no conversions, no per-parameter gradient tensors when bound."""
+
+    @staticmethod
+    def forward(ctx, h, ln_w, ln_b, w1, b1, w2, b2, eps):
+        nat = native()
+        st = _stream()
+        h = h.contiguous().float()
+        a, mean, rstd = _ln_fwd(nat, h, ln_w, ln_b, eps, st)
+        w1b, w2b = _w16(w1), _w16(w2)
+        f, pre, out = _ffn_fwd(nat, a, w1b, b1, w2b, b2, h, st)
+        ctx.save_for_backward(h, mean, rstd, a, w1b, w2b, f, pre)
+        ctx.params = (ln_w, ln_b, w1, b1, w2, b2)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        nat = native()
+        st = _stream()
+        h, mean, rstd, a, w1b, w2b, f, pre = ctx.saved_tensors
+        ln_w, ln_b = ctx.params[:2]
+        dout = dout.contiguous().float()
+        da, dw1, db1, dw2, db2 = _ffn_bwd(nat, _bf16_of(dout), a, w1b, w2b, f, pre, ctx.params[2:], st)
+        dh, dlw, dlb = _ln_bwd(nat, da, h, ln_w, ln_b, mean, rstd, dres=dout, want_bf16=True)
+        return dh, dlw, dlb, dw1, db1, dw2, db2, None
+
+
+class _PreNormAttnFn(torch.autograd.Function):
+    """h + Wo Attention(Wqkv LayerNorm(h) + bqkv) + bo as one autograd node (feature-token
+    self-attention over T tokens per row, H heads of width D); backward mirrors _PreNormFFNFn."""
+
+    @staticmethod
+    def forward(ctx, h, ln_w, ln_b, wqkv, bqkv, wo, bo, eps, B, H, T):
+        nat = native()
+        st = _stream()
+        h = h.contiguous().float()
+        M, dm = h.shape
+        D = dm // H
+        a, mean, rstd = _ln_fwd(nat, h, ln_w, ln_b, eps, st)
+        wqkvb, wob = _w16(wqkv), _w16(wo)
+        qkv = torch.empty(M, 3 * dm, dtype=torch.bfloat16, device=h.device)
+        nat.gemm_bf16(a.data_ptr(), wqkvb.data_ptr(), qkv.data_ptr(), bqkv.data_ptr(), M, 3 * dm, dm, dm, dm, 3 * dm,
+                      0, 1, _EPI[ACT_NONE], 0, 0, 0, st)
+        o = torch.empty(M, dm, dtype=torch.bfloat16, device=h.device)
+        lse = torch.empty(B * H * T, dtype=torch.float32, device=h.device)
+        base = qkv.data_ptr()
+        scale = 1.0 / math.sqrt(D)
+        nat.attention_fwd(base, base + 2 * dm, base + 4 * dm, o.data_ptr(), lse.data_ptr(), B, H, T, D, 3 * dm, dm,
+                          scale, st)
+        out = torch.empty(M, dm, dtype=torch.float32, device=h.device)
+        nat.gemm_bf16_residual(o.data_ptr(), wob.data_ptr(), out.data_ptr(), bo.data_ptr(), h.data_ptr(), M, dm, dm,
+                               st)
+        ctx.save_for_backward(h, mean, rstd, a, wqkvb, qkv, o, lse, wob)
+        ctx.params = (ln_w, ln_b, wqkv, bqkv, wo, bo)
+        ctx.dims = (B, H, T, D, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        nat = native()
+        st = _stream()
+        h, mean, rstd, a, wqkvb, qkv, o, lse, wob = ctx.saved_tensors
+        ln_w, ln_b, wqkv, bqkv, wo, bo = ctx.params
+        B, H, T, D, scale = ctx.dims
+        M, dm = h.shape
+        dout = dout.contiguous().float()
+        dz = _bf16_of(dout)
+        dwo, dbo = _dw_gemm(nat, dz, o, wo, bo, st)
+        do = _mm(nat, dz, wob, M, dm, dm, st)
+        dqkv = torch.empty_like(qkv)
+        base, dbase = qkv.data_ptr(), dqkv.data_ptr()
+        nat.attention_bwd(base, base + 2 * dm, base + 4 * dm, o.data_ptr(), do.data_ptr(), lse.data_ptr(), dbase,
+                          dbase + 2 * dm, dbase + 4 * dm, B, H, T, D, 3 * dm, dm, scale, st)
+        dwqkv, dbqkv = _dw_gemm(nat, dqkv, a, wqkv, bqkv, st)
+        da = _mm(nat, dqkv, wqkvb, M, dm, 3 * dm, st)
+        dh, dlw, dlb = _ln_bwd(nat, da, h, ln_w, ln_b, mean, rstd, dres=dout, want_bf16=True)
+        return dh, dlw, dlb, dwqkv, dbqkv, dwo, dbo, None, None, None, None
+
+
+def _prenorm_ok(h: torch.Tensor) -> bool:
+    return h.is_cuda and _ln_fused_ok(h.shape[1]) and h.shape[1] % 64 == 0
+
+
+def prenorm_ffn(h, ln_w, ln_b, w1, b1, w2, b2, eps: float = 1e-5):
+    """h + W2 gelu(W1 LN(h) + b1) + b2 - one fused autograd node on MI355X."""
+    if _prenorm_ok(h):
+        return _PreNormFFNFn.apply(h, ln_w, ln_b, w1, b1, w2, b2, eps)
+    return ffn_residual(layer_norm(h, ln_w, ln_b, eps), w1, b1, w2, b2, h)
+
+
+def prenorm_attention(h, ln_w, ln_b, wqkv, bqkv, wo, bo, B: int, H: int, T: int, eps: float = 1e-5):
+    """h + Wo MHA(LN(h)) + bo over T feature tokens per row - one fused autograd node on MI355X."""
+    if _prenorm_ok(h) and T <= 512 and h.shape[1] // H <= 64:
+        return _PreNormAttnFn.apply(h, ln_w, ln_b, wqkv, bqkv, wo, bo, eps, B, H, T)
+    a = layer_norm(h, ln_w, ln_b, eps)
+    o = attention(linear(a, wqkv, bqkv), B, H, T, h.shape[1] // H)
+    return linear_residual(o, wo, bo, h)
 
 
 class _AttentionFn(torch.autograd.Function):

@@ -20,6 +20,7 @@
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 import time
@@ -29,6 +30,7 @@ import torch
 
 from ..data.sampler import distributed_indices
 from ..ops.fused_mlp import FusedMLPKernel, mlp_num_params
+from ..ops.nn import bound_params
 from ..ops.optim import FlatAdam, adam_flat_
 from ..parallel.dist import DistContext, init_native_comm
 from ..parallel.reducer import NativeBucketReducer, TorchBucketReducer, plan_buckets
@@ -447,6 +449,19 @@ class AutogradEngine(_EngineBase):
         else:
             self.optimizer = None
             self.torch_optimizer = opt[0] if isinstance(opt, (list, tuple)) else opt
+        # native-op fast paths (ops/nn.py bound_params): weight-gradient accumulation straight into
+        # the flat bucket buffer, and bf16 shadow weights maintained by the fused Adam
+        self._shadows = None
+        self.flat_p16 = None
+        if dev.type == "cuda" and self.optimizer is not None and os.environ.get("DCT_FUSE_GRADS", "1") != "0":
+            self.flat_p16 = self.flat_p.to(torch.bfloat16)
+            self.optimizer.p_bf16 = self.flat_p16
+            self._shadows = {}
+            off = 0
+            for p in params:
+                n = p.numel()
+                self._shadows[id(p)] = self.flat_p16[off: off + n].view(p.shape)
+                off += n
 
     def _bcast_nccl(self):
         self.ctx.broadcast_(self.flat_p, 0)
@@ -470,10 +485,11 @@ class AutogradEngine(_EngineBase):
         if self.reducer is not None:
             self.reducer.prepare()
         self.model.train()
-        loss = self.model.training_step((x, y), batch_idx)
-        if isinstance(loss, dict):
-            loss = loss["loss"]
-        loss.backward()
+        with self._bound():
+            loss = self.model.training_step((x, y), batch_idx)
+            if isinstance(loss, dict):
+                loss = loss["loss"]
+            loss.backward()
         if self.reducer is not None:
             self.reducer.finalize()
             assert_reducer_complete(self.reducer)
@@ -566,8 +582,15 @@ class AutogradEngine(_EngineBase):
             self.torch_optimizer.load_state_dict(sd)
         self.global_step = global_step
 
+    def _bound(self):
+        if self._shadows is None:
+            return contextlib.nullcontext()
+        return bound_params(self.params, self._shadows)
+
     def sync_to_model(self):
         pass  # parameters ARE views of the flat buffer
 
     def load_from_model(self):
-        pass
+        # parameters ARE views of the flat buffer; only the bf16 shadow must follow external writes
+        if self.flat_p16 is not None:
+            self.flat_p16.copy_(self.flat_p)

@@ -450,3 +450,168 @@ def test_skinny_head_kernels(C, cuda):
     assert torch.allclose(dX.float(), (dZ.float() @ W.float()) * (act.float() > 0), atol=2e-2, rtol=2e-2)
     assert torch.allclose(dW, dZ.float().t() @ X.float(), atol=5e-2, rtol=1e-3)
     assert torch.allclose(db, dZ.float().sum(0), atol=1e-2, rtol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,d,n", [(4096, 64, 256), (1000, 64, 128)])
+def test_ffn_residual_matches_fp32_reference(cuda, M, d, n):
+    """ops.nn.ffn_residual (4 GEMMs, gelu' + bias grads in epilogues) vs an fp32 torch reference."""
+    from dct_amd.ops.nn import ffn_residual
+
+    torch.manual_seed(0)
+    a = torch.randn(M, d, device=cuda).to(torch.bfloat16).requires_grad_()
+    h = torch.randn(M, d, device=cuda, requires_grad=True)
+    w1 = (torch.randn(n, d, device=cuda) / math.sqrt(d)).requires_grad_()
+    b1 = (0.1 * torch.randn(n, device=cuda)).requires_grad_()
+    w2 = (torch.randn(d, n, device=cuda) / math.sqrt(n)).requires_grad_()
+    b2 = (0.1 * torch.randn(d, device=cuda)).requires_grad_()
+    dout = torch.randn(M, d, device=cuda)
+    out = ffn_residual(a, w1, b1, w2, b2, h)
+    out.backward(dout)
+    leaves = [a, w1, b1, w2, b2, h]
+    got = [t.grad.float().clone() for t in leaves]
+    for t in leaves:
+        t.grad = None
+    ref = h + F.linear(F.gelu(F.linear(a.float(), w1, b1)), w2, b2)
+    ref.backward(dout)
+    torch.cuda.synchronize()
+    assert (out - ref).norm() / ref.norm() < 1e-2
+    for name, g, t in zip(["a", "w1", "b1", "w2", "b2", "h"], got, leaves):
+        rel = (g - t.grad.float()).norm() / (t.grad.float().norm() + 1e-12)
+        assert rel < 2e-2, (name, float(rel))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N", [(32768, 64), (1000, 128), (77, 256)])
+def test_layernorm_bwd_fused_residual_and_slots(cuda, M, N):
+    """layernorm_bwd_ex: bf16 dy, fp32 x, + dres, bf16 copy of dx, dw/db accumulated through the
+    slot workspace (run twice: the kernel must leave the workspace zeroed for the next call)."""
+    from dct_amd.ops.nn import _ln_ws
+
+    torch.manual_seed(11)
+    nat = native()
+    st = torch.cuda.current_stream().cuda_stream
+    x = torch.randn(M, N, device=cuda)
+    w = torch.randn(N, device=cuda)
+    b = torch.randn(N, device=cuda)
+    mean = x.mean(1)
+    rstd = torch.rsqrt(x.var(1, unbiased=False) + 1e-5)
+    dy16 = torch.randn(M, N, device=cuda).to(torch.bfloat16)
+    dres = torch.randn(M, N, device=cuda)
+    xx, ww, bb = (t.clone().requires_grad_(True) for t in (x, w, b))
+    F.layer_norm(xx, (N,), ww, bb, 1e-5).backward(dy16.float())
+    ws = _ln_ws(x.device, N)
+    dw = torch.full((N,), 0.5, device=cuda)  # accumulates (+=) into existing grads
+    db = torch.zeros(N, device=cuda)
+    for it in range(2):
+        dx = torch.empty_like(x)
+        dx16 = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+        nat.layernorm_bwd_ex(dy16.data_ptr(), 1, x.data_ptr(), 0, w.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                             dx.data_ptr(), 0, dx16.data_ptr(), dres.data_ptr(), dw.data_ptr(), db.data_ptr(),
+                             ws.data_ptr(), M, N, st)
+        torch.cuda.synchronize()
+        ref_dx = xx.grad + dres
+        assert torch.allclose(dx, ref_dx, atol=1e-3, rtol=1e-3), it
+        assert torch.equal(dx16, dx.to(torch.bfloat16))
+        assert torch.allclose(dw, 0.5 + (it + 1) * ww.grad, atol=2e-2, rtol=1e-3), it
+        assert torch.allclose(db, (it + 1) * bb.grad, atol=2e-2, rtol=1e-3), it
+    assert int(ws.count_nonzero()) == 0
+
+
+def _prenorm_inputs(cuda, M, d, n, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    mk = lambda *s, scale=1.0: (scale * torch.randn(*s, generator=g)).to(cuda).requires_grad_()  # noqa: E731
+    return dict(h=mk(M, d), ln_w=(1 + 0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_(), ln_b=mk(d, scale=0.1),
+                w1=mk(n, d, scale=d ** -0.5), b1=mk(n, scale=0.1), w2=mk(d, n, scale=n ** -0.5), b2=mk(d, scale=0.1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bound", [False, True])
+def test_prenorm_ffn_matches_fp32_reference(cuda, bound):
+    """ops.nn.prenorm_ffn (one fused autograd node) vs fp32 torch; bound=True routes the
+    parameter gradients through bound_params' direct accumulation into pre-set .grad buffers."""
+    from dct_amd.ops.nn import bound_params, prenorm_ffn
+
+    M, d, n = 4096, 64, 256
+    t = _prenorm_inputs(cuda, M, d, n)
+    params = [t[k] for k in ("ln_w", "ln_b", "w1", "b1", "w2", "b2")]
+    dout = torch.randn(M, d, device=cuda)
+    if bound:
+        for p in params:
+            p.grad = torch.zeros_like(p)
+        with bound_params(params):
+            out = prenorm_ffn(t["h"], *params)
+            out.backward(dout)
+    else:
+        out = prenorm_ffn(t["h"], *params)
+        out.backward(dout)
+    got = {k: v.grad.clone() for k, v in t.items()}
+    for v in t.values():
+        v.grad = None
+    a = F.layer_norm(t["h"], (d,), t["ln_w"], t["ln_b"], 1e-5)
+    ref = t["h"] + F.linear(F.gelu(F.linear(a, t["w1"], t["b1"])), t["w2"], t["b2"])
+    ref.backward(dout)
+    torch.cuda.synchronize()
+    assert (out - ref).norm() / ref.norm() < 1e-2
+    for k, v in t.items():
+        rel = (got[k] - v.grad).norm() / (v.grad.norm() + 1e-12)
+        assert rel < 3e-2, (k, float(rel))
+
+
+@pytest.mark.gpu
+def test_prenorm_attention_matches_fp32_reference(cuda):
+    from dct_amd.ops.nn import prenorm_attention
+
+    B, T, H, d = 128, 32, 4, 64
+    M = B * T
+    g = torch.Generator(device="cpu").manual_seed(3)
+    mk = lambda *s, scale=1.0: (scale * torch.randn(*s, generator=g)).to(cuda).requires_grad_()  # noqa: E731
+    t = dict(h=mk(M, d), ln_w=(1 + 0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_(), ln_b=mk(d, scale=0.1),
+             wqkv=mk(3 * d, d, scale=d ** -0.5), bqkv=mk(3 * d, scale=0.1), wo=mk(d, d, scale=d ** -0.5),
+             bo=mk(d, scale=0.1))
+    dout = torch.randn(M, d, device=cuda)
+    out = prenorm_attention(t["h"], t["ln_w"], t["ln_b"], t["wqkv"], t["bqkv"], t["wo"], t["bo"], B, H, T)
+    out.backward(dout)
+    got = {k: v.grad.clone() for k, v in t.items()}
+    for v in t.values():
+        v.grad = None
+    a = F.layer_norm(t["h"], (d,), t["ln_w"], t["ln_b"], 1e-5)
+    q, k, v = (z.reshape(B, T, H, d // H).transpose(1, 2) for z in F.linear(a, t["wqkv"], t["bqkv"]).split(d, 1))
+    o = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(M, d)
+    ref = t["h"] + F.linear(o, t["wo"], t["bo"])
+    ref.backward(dout)
+    torch.cuda.synchronize()
+    assert (out - ref).norm() / ref.norm() < 1e-2
+    for name, tv in t.items():
+        rel = (got[name] - tv.grad).norm() / (tv.grad.norm() + 1e-12)
+        assert rel < 4e-2, (name, float(rel))
+
+
+@pytest.mark.gpu
+def test_skinny_head_linear_and_shadow_weights(cuda):
+    """ops.nn.linear with N <= 8 takes the skinny kernels; under bound_params a registered bf16
+    shadow replaces the weight conversion and gradients accumulate into .grad."""
+    from dct_amd.ops.nn import bound_params, linear
+
+    torch.manual_seed(5)
+    x = torch.randn(512, 64, device=cuda).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(2, 64, device=cuda) / 8).requires_grad_()
+    b = torch.randn(2, device=cuda).requires_grad_()
+    dy = torch.randn(512, 2, device=cuda)
+    w.grad, b.grad = torch.ones_like(w), torch.zeros_like(b)
+    shadow = torch.zeros(2, 64, dtype=torch.bfloat16, device=cuda)
+    shadow.copy_(w.detach())
+    with bound_params([w, b], {id(w): shadow}):
+        y = linear(x, w, b)
+        y.float().backward(dy)
+    ref = F.linear(x.float(), w, b)
+    gx = x.grad.clone()
+    gw, gb = w.grad.clone(), b.grad.clone()
+    x.grad = w.grad = b.grad = None
+    ref.backward(dy)
+    torch.cuda.synchronize()
+    assert torch.allclose(y.float(), ref, atol=3e-2, rtol=2e-2)
+    # dy is rounded to bf16 for the kernels: compare by relative norm, not elementwise
+    assert (gw - 1.0 - w.grad).norm() / w.grad.norm() < 1e-2
+    assert (gb - b.grad).norm() / b.grad.norm() < 1e-2
+    assert (gx.float() - x.grad.float()).norm() / x.grad.float().norm() < 1e-2
