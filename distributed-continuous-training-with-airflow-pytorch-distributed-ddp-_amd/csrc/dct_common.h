@@ -33,4 +33,25 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
 // per call, which was ~40 % of a 2.3 us single-wave optimizer step.)
 __device__ __forceinline__ float pow_t(float log2b, float t) { return __builtin_amdgcn_exp2f(t * log2b); }
 
+// erf(x) by Abramowitz-Stegun 7.1.26 (|err| < 6e-7 in fp32) on one v_rcp_f32 + one v_exp_f32,
+// given e = exp(-x^2).  The ocml erff is ~44 VALU ops with range branches; GEMM epilogues that
+// apply GELU to every output element were bound by it.
+__device__ __forceinline__ float erf_exp(float x, float e) {
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, fabsf(x), 1.f));
+  const float p = fmaf(fmaf(fmaf(fmaf(1.061405429f, t, -1.453152027f), t, 1.421413741f), t, -0.284496736f), t,
+                       0.254829592f) * t;
+  return copysignf(1.f - p * e, x);
+}
+// exact-form (erf) GELU and its derivative; both share exp(-z^2/2) between erf and the pdf
+__device__ __forceinline__ float gelu_f(float z) {
+  const float x = z * 0.70710678118654752f;
+  const float e = __builtin_amdgcn_exp2f(-x * x * 1.4426950408889634f);
+  return 0.5f * z * (1.f + erf_exp(x, e));
+}
+__device__ __forceinline__ float gelu_grad_f(float z) {
+  const float x = z * 0.70710678118654752f;
+  const float e = __builtin_amdgcn_exp2f(-x * x * 1.4426950408889634f);
+  return 0.5f * (1.f + erf_exp(x, e)) + z * 0.3989422804014327f * e;
+}
+
 }  // namespace dct

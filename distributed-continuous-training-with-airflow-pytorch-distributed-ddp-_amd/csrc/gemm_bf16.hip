@@ -34,11 +34,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int GBM = 128, GBN = 128, GBK = 64, GPAD = 8, GLD = GBK + GPAD, GNT = 256;
 
-__device__ __forceinline__ float gelu_f(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_grad_f(float z) {
-  const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
-  return cdf + z * 0.3989422804014327f * __expf(-0.5f * z * z);
-}
 
 // Stage one BMxBK (or BNxBK) tile of an operand into registers.
 // Non-transposed: chunk c -> row c/8, k-chunk c%8 (8 bf16 each)  [storage [R][K]]
@@ -540,7 +535,10 @@ static hipError_t launch_gemm2(const dct::GemmArgs& g, hipStream_t st) {
   const int nk = g.K / dct::GBK;
   int splits = 1;
   if (g.out_f32 && g.epilogue == dct::EPI_NONE && !g.residual && g.alpha == 1.0f && tiles < 256 && nk >= 8) {
-    splits = std::min(nk / 4, (512 + tiles - 1) / tiles);
+    // >= 8 k-tiles per slice: fewer fp32 atomics (measured: 64 slices of 8 beat 128 of 4 by 20-30 %
+    // on the 32k-row transformer dW shapes - tools/bench_dw.py)
+    splits = std::min(nk / 8, (512 + tiles - 1) / tiles);
+    if (const char* f = getenv("DCT_GEMM_SPLITS")) splits = std::min(nk, atoi(f));  // tuning override
     if (splits < 1) splits = 1;
   }
   if (splits > 1 && !g.accumulate) {  // slices accumulate atomically into a zeroed C
@@ -557,7 +555,7 @@ static hipError_t launch_gemm2(const dct::GemmArgs& g, hipStream_t st) {
   };
   if constexpr (!TA) {
     // small K and too few 128-row tiles to fill 256 CUs several times over: half-height tiles
-    static const bool force128 = getenv("DCT_GEMM_BM128") != nullptr;
+    const bool force128 = getenv("DCT_GEMM_BM128") != nullptr;
     if (splits == 1 && nk <= 4 && tiles < 1024 && !force128)
       return launch(dct::gemm2_kernel<TA, TB, false, 64>, ((g.M + 63) / 64) * tiles_n);
   }

@@ -12,11 +12,7 @@
 
 namespace dct {
 
-__device__ __forceinline__ float gelu_grad(float z) {
-  const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
-  const float pdf = 0.3989422804014327f * __expf(-0.5f * z * z);
-  return cdf + z * pdf;
-}
+__device__ __forceinline__ float gelu_grad(float z) { return gelu_grad_f(z); }
 
 __device__ __forceinline__ float ld_any(const void* p, size_t i, int bf16) {
   return bf16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(p)[i]) : reinterpret_cast<const float*>(p)[i];
