@@ -106,6 +106,9 @@ constexpr int XG_MAXW = 8;  // ranks of the in-kernel exchange (one node)
 hipError_t mlp_launch_train_L2(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
 hipError_t mlp_launch_train_L3(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
 hipError_t mlp_launch_train_L4(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
+// register-resident multi-wave kernel for D0 -> 128 -> 128 -> C (mlp_block.hip)
+bool mlp_block_ok(const MlpShape& sh, const MlpArgs& a);
+hipError_t mlp_launch_block(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
 hipError_t mlp_launch_eval_L2(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
 hipError_t mlp_launch_eval_L3(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
 hipError_t mlp_launch_eval_L4(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
