@@ -174,6 +174,9 @@ PYBIND11_MODULE(_dct_native, m) {
       py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("p_bf16"), py::arg("n"), py::arg("lr"),
       py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("t"), py::arg("grad_scale"),
       py::arg("decoupled"), py::arg("step_counter"), py::arg("stream"));
+  m.def("zero_f32", [](uintptr_t p, int64_t n, uintptr_t stream) {
+    check(dct_zero_f32(P<float>(p), n, reinterpret_cast<void*>(stream)), "zero_f32");
+  });
   m.def("f32_to_bf16", [](uintptr_t in, uintptr_t out, int64_t n, uintptr_t stream) {
     check(dct_f32_to_bf16(P<const float>(in), P<uint16_t>(out), n, reinterpret_cast<void*>(stream)), "f32_to_bf16");
   });

@@ -295,7 +295,35 @@ __device__ __forceinline__ bf16x8 g2_frag(const char* img, int rb, int ks, int l
 // thousands: the transformer's projections).  Twice the workgroups and half the epilogue per
 // thread, and with a single k-tile only one LDS stage (32 KB) -> 4 resident workgroups per CU,
 // so one tile's global loads overlap another's epilogue.
-template <bool TA, bool TB, bool SPLIT, int BM = 128>
+// Pipeline depth S (LDS stages of 2 x 16 KB).  With one 128x128 tile per CU (the 4096 x 1024 x 1024
+// MLP layers: 256 tiles on 256 CUs) a single wave per SIMD cannot hide an L2/HBM round trip
+// behind ONE k-step of MFMAs (~0.2 us), so S = 4 keeps three k-tiles in flight (128 KB LDS, one
+// workgroup per CU); grids with several tiles per CU keep S = 2 and hide latency with a second
+// resident workgroup.  The prefetch stays in flight ACROSS the k-step barrier: the barrier is a
+// raw s_barrier (__syncthreads' fence would emit vmcnt(0) and drain the LDS-DMA queue) preceded
+// by a counted vmcnt - every fill issues FILL_OPS loads per thread and loads retire in order, so
+// "stage i landed" = at most FILL_OPS x (fills issued after it) still pending.
+template <int N>
+__device__ __forceinline__ void wait_vm_le() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int FILL_OPS, int S>
+__device__ __forceinline__ void wait_stage(int newer_fills) {
+  static_assert(S == 2 || S == 4, "pipeline depth 2 or 4");
+  if (S == 2 || newer_fills <= 0) wait_vm_le<0>();
+  else if (newer_fills == 1) wait_vm_le<FILL_OPS>();
+  else wait_vm_le<2 * FILL_OPS>();
+}
+
+// workgroup barrier that leaves LDS-DMA loads in flight (this wave's LDS reads retired first)
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <bool TA, bool TB, bool SPLIT, int BM = 128, int S = 2>
 __global__ __launch_bounds__(GNT, BM == 64 ? 4 : 2) void gemm2_kernel(GemmArgs g, int splits) {
   static_assert(BM == 128 || (BM == 64 && !TA), "BM = 64 needs a row-major (KC) A image");
   constexpr int IM = BM / 32;  // 16-row MFMA tiles per wave (2 x 2 waves)
@@ -335,13 +363,17 @@ __global__ __launch_bounds__(GNT, BM == 64 ? 4 : 2) void gemm2_kernel(GemmArgs g
     if (TB) g2_fill<false>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
     else g2_fill<true>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
   };
-  if (kt0 < kt1) {
-    fill(0, kt0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const int cur = (kt - kt0) & 1;
-      if (kt + 1 < kt1) fill(cur ^ 1, kt + 1);
+  constexpr int FILL_OPS = (TA ? 4 : BM / 32) + 4;  // global_load_lds per thread per fill (A + B)
+  const int n = kt1 - kt0;
+  if (n > 0) {
+#pragma unroll
+    for (int s = 0; s < S - 1; ++s)
+      if (s < n) fill(s, kt0 + s);
+    for (int it = 0; it < n; ++it) {
+      wait_stage<FILL_OPS, S>(min(S - 2, n - 1 - it));  // this wave's part of stage `it` has landed
+      raw_barrier();  // every wave's part has; every wave finished reading stage it - 1
+      if (it + S - 1 < n) fill((it + S - 1) & (S - 1), kt0 + it + S - 1);  // refill stage it - 1
+      const int cur = it & (S - 1);
       const char* ai = img(cur, 0);
       const char* bi = img(cur, 1);
 #pragma unroll
@@ -364,8 +396,6 @@ __global__ __launch_bounds__(GNT, BM == 64 ? 4 : 2) void gemm2_kernel(GemmArgs g
             acc[i][j] = SPLIT ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0)
                               : __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
     }
   }
   if (do_cs) {  // lanes l, l+16, l+32, l+48 hold partial sums of the same row
@@ -504,6 +534,16 @@ __global__ __launch_bounds__(GNT, BM == 64 ? 4 : 2) void gemm2_kernel(GemmArgs g
   }
 }
 
+// zero the fp32 C[M, ldc] panel that split-K slices accumulate into (a kernel node, not a
+// hipMemset2DAsync node: see gather_batch_kernel on memset nodes in replayed graphs)
+__global__ __launch_bounds__(256) void zero_panel_kernel(float* __restrict__ C, int ldc, int M, int N) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / N;
+    C[r * ldc + (e - r * N)] = 0.f;
+  }
+}
+
 }  // namespace dct
 
 template <bool TA, bool TB>
@@ -527,6 +567,29 @@ static bool gemm_v2_ok(const dct::GemmArgs& g, int ta, int tb) {
   return true;
 }
 
+static int device_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      cus = v;
+    else
+      cus = 256;
+  }
+  return cus;
+}
+
+// LDS pipeline depth.  Measured on the MLP / transformer shapes (tools/bench_gemm_mlp.py,
+// profiles/gemm_pipeline_ab_r1.log): 4 stages never beat 2 - with 32 KB of operands per k-step a
+// CU's load path (~70 GB/s from L2), not the round-trip latency, bounds these one-tile-per-CU
+// grids - so 2 is the default and 4 stays selectable (DCT_GEMM_STAGES=4) for other shapes.
+static int gemm_stages(int grid, int nk_slice) {
+  if (const char* f = getenv("DCT_GEMM_STAGES")) return (atoi(f) >= 4 && nk_slice >= 3) ? 4 : 2;
+  (void)grid;
+  return 2;
+}
+
 template <bool TA, bool TB>
 static hipError_t launch_gemm2(const dct::GemmArgs& g, hipStream_t st) {
   hipError_t e;
@@ -537,17 +600,26 @@ static hipError_t launch_gemm2(const dct::GemmArgs& g, hipStream_t st) {
   if (g.out_f32 && g.epilogue == dct::EPI_NONE && !g.residual && g.alpha == 1.0f && tiles < 256 && nk >= 8) {
     // >= 8 k-tiles per slice: fewer fp32 atomics (measured: 64 slices of 8 beat 128 of 4 by 20-30 %
     // on the 32k-row transformer dW shapes - tools/bench_dw.py)
-    splits = std::min(nk / 8, (512 + tiles - 1) / tiles);
+    // workgroups to aim for: one per CU.  512 (two slices per CU) doubled the fp32 atomic traffic
+    // for no extra bandwidth: 1024x1024x4096 dW 38 -> 28 us at 256 (profiles/gemm_pipeline_ab_r1.log)
+    int target = device_cus();
+    if (const char* f = getenv("DCT_GEMM_SPLIT_WG")) target = std::max(1, atoi(f));
+    splits = std::min(nk / 8, (target + tiles - 1) / tiles);
     if (const char* f = getenv("DCT_GEMM_SPLITS")) splits = std::min(nk, atoi(f));  // tuning override
     if (splits < 1) splits = 1;
   }
   if (splits > 1 && !g.accumulate) {  // slices accumulate atomically into a zeroed C
-    e = hipMemset2DAsync(g.C, (size_t)g.ldc * 4, 0, (size_t)g.N * 4, (size_t)g.M, st);
+    const int64_t total = (int64_t)g.M * g.N;
+    const int zgrid = (int)std::min<int64_t>(2048, (total + 255) / 256);
+    hipLaunchKernelGGL(dct::zero_panel_kernel, dim3(zgrid), dim3(256), 0, st, reinterpret_cast<float*>(g.C), g.ldc,
+                       g.M, g.N);
+    e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  // one k-tile -> one LDS stage
-  const size_t lds = (nk > 1 ? 4 : 2) * (size_t)dct::G2_BYTES;
-  auto launch = [&](auto fn, int grid) -> hipError_t {
+  const int nk_slice = (nk + splits - 1) / splits;
+  auto launch = [&](auto fn, int grid, int stages) -> hipError_t {
+    // one k-tile -> one LDS stage; otherwise `stages` stages of A + B images
+    const size_t lds = (size_t)(nk_slice > 1 ? 2 * stages : 2) * dct::G2_BYTES;
     hipError_t err = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (err != hipSuccess) return err;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(dct::GNT), lds, st, g, splits);
@@ -557,10 +629,15 @@ static hipError_t launch_gemm2(const dct::GemmArgs& g, hipStream_t st) {
     // small K and too few 128-row tiles to fill 256 CUs several times over: half-height tiles
     const bool force128 = getenv("DCT_GEMM_BM128") != nullptr;
     if (splits == 1 && nk <= 4 && tiles < 1024 && !force128)
-      return launch(dct::gemm2_kernel<TA, TB, false, 64>, ((g.M + 63) / 64) * tiles_n);
+      return launch(dct::gemm2_kernel<TA, TB, false, 64, 2>, ((g.M + 63) / 64) * tiles_n, 2);
   }
-  if (splits > 1) return launch(dct::gemm2_kernel<TA, TB, true>, tiles * splits);
-  return launch(dct::gemm2_kernel<TA, TB, false>, tiles);
+  if (splits > 1) {
+    const int grid = tiles * splits;
+    if (gemm_stages(grid, nk_slice) == 4) return launch(dct::gemm2_kernel<TA, TB, true, 128, 4>, grid, 4);
+    return launch(dct::gemm2_kernel<TA, TB, true, 128, 2>, grid, 2);
+  }
+  if (gemm_stages(tiles, nk) == 4) return launch(dct::gemm2_kernel<TA, TB, false, 128, 4>, tiles, 4);
+  return launch(dct::gemm2_kernel<TA, TB, false, 128, 2>, tiles, 2);
 }
 
 extern "C" int dct_bias_act_bwd(const void* dY, const void* act_aux, uint16_t* dZ, float* dbias, int M, int N,

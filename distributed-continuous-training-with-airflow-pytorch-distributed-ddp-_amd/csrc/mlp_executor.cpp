@@ -5,21 +5,25 @@
 // Reference step (jobs/train_lightning_ddp.py:66-71,88,136 through Lightning/torch DDP):
 //   collate -> forward (Linear/ReLU) -> loss -> autograd backward -> DDP bucket all-reduce -> Adam.
 // MI355X step (all on one compute stream, the all-reduce on the reducer's comm stream):
-//   step_begin (Adam t += 1, zero loss stats; memset grads)
-//   gather_batch          HBM-resident bf16 dataset rows idx[cursor*B + r] -> X_b (16-B copies)
+//   gather_batch          HBM-resident bf16 dataset rows idx[cursor*B + r] -> X_b (16-B copies);
+//                         the same grid zeroes the flat gradient buffer + loss slot g[P] and its
+//                         first thread bumps the device Adam step counter
 //   L x gemm_bf16         A_{l+1} = act(A_l W_l^T + b_l): MFMA GEMM, bias+ReLU/GELU epilogue, bf16 out
-//   loss_fwd_bwd          CE / MSE + dlogits (scaled 1/rows), loss & accuracy sums
-//   loss_to_slot          batch-mean loss -> g[P] (all-reduced with the grads: sync_dist for free)
+//   loss_fwd_bwd          CE / MSE + dlogits (scaled 1/rows); the batch-mean loss is accumulated
+//                         straight into g[P] (all-reduced with the grads: sync_dist for free)
 //   for l = L-1 .. 0:     bias_act_bwd (dZ = dA * act', db = colsum) ; dW_l = dZ^T A_l (fp32 straight
 //                         into the flat gradient buffer = the DDP bucket views) ; mark params ready
 //                         (the reducer launches each full bucket's ncclAvg on its comm stream while
 //                         the earlier layers' backward GEMMs keep running) ; dA_l = dZ W_l
 //   finalize              compute stream waits for the last bucket
-//   adam_flat             fp32 master update + bf16 shadow weights for the next forward's GEMMs
-//   step_end              loss_out[cursor] = reduced loss ; cursor += 1
+//   adam_flat             fp32 master update + bf16 shadow weights for the next forward's GEMMs;
+//                         its first thread writes loss_out[cursor] = reduced loss, cursor += 1
+// (the step prologue, gradient zeroing, loss slot and epilogue ride inside the gather, loss and
+// Adam kernels instead of a memset node and three single-thread launches)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -32,8 +36,16 @@
 extern "C" {
 int dct_gather_batch(const void* X, int row_bytes, const int* Y, const int* idx, const int* cursor, int stride,
                      int B, int n_items, void* xdst, int* ydst, void* stream);
-int dct_step_begin(int* step_counter, float* stats, void* stream);
-int dct_loss_to_slot(const float* stats, float* slot, float inv_rows, void* stream);
+int dct_gather_batch_step(const void* X, int row_bytes, const int* Y, const int* idx, const int* cursor, int stride,
+                          int B, int n_items, void* xdst, int* ydst, int* step_counter, float* zero,
+                          int64_t zero_n, void* stream);
+int dct_loss_fwd_bwd_ex(const void* logits, int logits_bf16, const int* labels, void* dlogits, float* loss_sum,
+                        float* correct_sum, int M, int C, float grad_scale, int loss_kind, float loss_scale,
+                        void* stream);
+int dct_adam_flat_step(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, float lr,
+                       float b1, float b2, float eps, float wd, int64_t t, float grad_scale, int decoupled,
+                       const int* step_counter, int* cursor, const float* loss_slot, float* loss_out, int loss_cap,
+                       void* stream);
 int dct_step_end(int* cursor, const float* slot, float* loss_out, int loss_cap, void* stream);
 }
 
@@ -108,17 +120,15 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
   int* cur = reinterpret_cast<int*>(cursor);
   int* sc = reinterpret_cast<int*>(step_counter);
   if (reducer_) reducer_->prepare();
-  ck(dct_step_begin(sc, stats_, st), "step_begin");
-  ck((int)hipMemsetAsync(g_, 0, (size_t)(P_ + 1) * sizeof(float), st), "memset grads");
-  ck(dct_gather_batch(reinterpret_cast<const void*>(X), row_bytes, reinterpret_cast<const int*>(Y),
-                      reinterpret_cast<const int*>(idx), cur, B_, rows, n_items, acts_[0], y_, st),
+  ck(dct_gather_batch_step(reinterpret_cast<const void*>(X), row_bytes, reinterpret_cast<const int*>(Y),
+                           reinterpret_cast<const int*>(idx), cur, B_, rows, n_items, acts_[0], y_, sc, g_, P_ + 1, st),
      "gather_batch");
   forward(rows, st);
   const int C = dims_[L_];
   int ci = 0;  // dz_[ci] holds dL/d(output of the current layer)
-  ck(dct_loss_fwd_bwd(acts_[L_], 1, y_, dz_[ci], stats_, stats_ + 1, rows, C, 1.0f / (float)rows, loss_kind_, st),
+  ck(dct_loss_fwd_bwd_ex(acts_[L_], 1, y_, dz_[ci], g_ + P_, nullptr, rows, C, 1.0f / (float)rows, loss_kind_,
+                         1.0f / (float)rows, st),
      "loss");
-  ck(dct_loss_to_slot(stats_, g_ + P_, 1.0f / (float)rows, st), "loss_to_slot");
   if (reducer_) reducer_->mark_ready(2 * L_, stream);  // the loss slot rides in the last-layer bucket
   // dz_[ci] = dL/dZ_l (pre-activation gradient of layer l): the loss kernel's dlogits for the
   // head, then each dX GEMM's activation-derivative epilogue (ReLU mask / GELU') for the layer below.
@@ -164,8 +174,9 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
     }
   }
   if (reducer_) reducer_->finalize(stream);
-  ck(dct_adam_flat(p_, g_, m_, v_, pb_, P_, lr_, b1_, b2_, eps_, wd_, 1, 1.0f, decoupled_, sc, st), "adam");
-  ck(dct_step_end(cur, g_ + P_, reinterpret_cast<float*>(loss_out), loss_cap, st), "step_end");
+  ck(dct_adam_flat_step(p_, g_, m_, v_, pb_, P_, lr_, b1_, b2_, eps_, wd_, 1, 1.0f, decoupled_, sc, cur, g_ + P_,
+                        reinterpret_cast<float*>(loss_out), loss_cap, st),
+     "adam");
 }
 
 void MlpStepExecutor::eval_batch(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t idx, int n_items,

@@ -128,4 +128,5 @@ int dct_adam_flat(float* p, const float* g, float* m, float* v, uint16_t* p_bf16
                   float b1, float b2, float eps, float wd, int64_t t, float grad_scale, int decoupled,
                   const int* step_counter, void* stream);
 int dct_f32_to_bf16(const float* in, uint16_t* out, int64_t n, void* stream);
+int dct_zero_f32(float* p, int64_t n, void* stream);
 }

@@ -25,7 +25,7 @@ __device__ __forceinline__ void st_any(void* p, size_t i, float v, int bf16) {
 // ------------------------------------------------------------------------------- loss
 __global__ __launch_bounds__(256) void loss_kernel(const void* logits, int lbf16, const int* labels, void* dlogits,
                                                    float* loss_sum, float* correct_sum, int M, int C,
-                                                   float grad_scale, int loss_kind) {
+                                                   float grad_scale, int loss_kind, float loss_scale) {
   __shared__ float red[2][4];
   float l_acc = 0.f, c_acc = 0.f;
   for (int row = blockIdx.x * blockDim.x + threadIdx.x; row < M; row += gridDim.x * blockDim.x) {
@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void loss_kernel(const void* logits, int lbf16
   if (threadIdx.x == 0) {
     float a = 0.f, b = 0.f;
     for (int i = 0; i < (int)(blockDim.x >> 6); ++i) { a += red[0][i]; b += red[1][i]; }
-    if (loss_sum) atomicAdd(loss_sum, a);
+    if (loss_sum) atomicAdd(loss_sum, a * loss_scale);
     if (correct_sum) atomicAdd(correct_sum, b);
   }
 }
@@ -429,12 +429,20 @@ static inline int grid_cap(int64_t work, int block, int cap = 2048) {
 
 extern "C" {
 
-int dct_loss_fwd_bwd(const void* logits, int logits_bf16, const int* labels, void* dlogits, float* loss_sum,
-                     float* correct_sum, int M, int C, float grad_scale, int loss_kind, void* stream) {
+int dct_loss_fwd_bwd_ex(const void* logits, int logits_bf16, const int* labels, void* dlogits, float* loss_sum,
+                        float* correct_sum, int M, int C, float grad_scale, int loss_kind, float loss_scale,
+                        void* stream) {
   if (M <= 0) return 0;
   hipLaunchKernelGGL(dct::loss_kernel, dim3(grid_cap(M, 256, 1024)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     logits, logits_bf16, labels, dlogits, loss_sum, correct_sum, M, C, grad_scale, loss_kind);
+                     logits, logits_bf16, labels, dlogits, loss_sum, correct_sum, M, C, grad_scale, loss_kind,
+                     loss_scale);
   return (int)hipGetLastError();
+}
+
+int dct_loss_fwd_bwd(const void* logits, int logits_bf16, const int* labels, void* dlogits, float* loss_sum,
+                     float* correct_sum, int M, int C, float grad_scale, int loss_kind, void* stream) {
+  return dct_loss_fwd_bwd_ex(logits, logits_bf16, labels, dlogits, loss_sum, correct_sum, M, C, grad_scale, loss_kind,
+                             1.0f, stream);
 }
 
 int dct_bias_act_bwd(const void* dY, const void* act_aux, uint16_t* dZ, float* dbias, int M, int N, int ldy, int act,

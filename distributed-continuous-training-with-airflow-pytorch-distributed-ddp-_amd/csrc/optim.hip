@@ -27,6 +27,12 @@ struct AdamArgs {
   float grad_scale;
   int decoupled;  // 1 = AdamW
   const int* step_counter;  // optional: t read on device (graph-replayable launches)
+  // optional step epilogue of the graph-captured MLP step (folded in to save a launch per step):
+  // loss_out[*cursor] = *loss_slot (the all-reduced batch loss), then *cursor += 1
+  int* cursor;
+  const float* loss_slot;
+  float* loss_out;
+  int loss_cap;
 };
 
 __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, const AdamArgs& a) {
@@ -43,6 +49,11 @@ __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, 
 }
 
 __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a) {
+  if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int c = a.cursor[0];
+    if (a.loss_out && c >= 0 && c < a.loss_cap) a.loss_out[c] = a.loss_slot[0];
+    a.cursor[0] = c + 1;
+  }
   if (a.step_counter) {
     const float t = (float)__hip_atomic_load(a.step_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     a.step_size = a.lr / (1.f - pow_t(log2f(a.b1), t));
@@ -104,10 +115,12 @@ static inline int grid_for(int64_t work, int block) {
 
 extern "C" {
 
-int dct_adam_flat(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, float lr,
-                  float b1, float b2, float eps, float wd, int64_t t, float grad_scale, int decoupled,
-                  const int* step_counter, void* stream) {
+int dct_adam_flat_step(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, float lr,
+                       float b1, float b2, float eps, float wd, int64_t t, float grad_scale, int decoupled,
+                       const int* step_counter, int* cursor, const float* loss_slot, float* loss_out, int loss_cap,
+                       void* stream) {
   if (n <= 0) return 0;
+  if (cursor && !loss_slot) return (int)hipErrorInvalidValue;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return (int)hipErrorInvalidValue;
   dct::AdamArgs a;
   a.p = p; a.g = g; a.m = m; a.v = v; a.p_bf16 = p_bf16; a.n = n;
@@ -119,9 +132,20 @@ int dct_adam_flat(float* p, const float* g, float* m, float* v, uint16_t* p_bf16
   a.grad_scale = grad_scale;
   a.decoupled = decoupled;
   a.step_counter = step_counter;
+  a.cursor = cursor;
+  a.loss_slot = loss_slot;
+  a.loss_out = loss_out;
+  a.loss_cap = loss_cap;
   hipLaunchKernelGGL(dct::adam_flat_kernel, dim3(grid_for((n + 3) / 4, 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), a);
   return (int)hipGetLastError();
+}
+
+int dct_adam_flat(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, float lr,
+                  float b1, float b2, float eps, float wd, int64_t t, float grad_scale, int decoupled,
+                  const int* step_counter, void* stream) {
+  return dct_adam_flat_step(p, g, m, v, p_bf16, n, lr, b1, b2, eps, wd, t, grad_scale, decoupled, step_counter,
+                            nullptr, nullptr, nullptr, 0, stream);
 }
 
 int dct_f32_to_bf16(const float* in, uint16_t* out, int64_t n, void* stream) {

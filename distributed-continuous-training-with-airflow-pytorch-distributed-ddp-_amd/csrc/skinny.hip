@@ -6,6 +6,7 @@
 // tiny weight panel read through the cache, wave reductions by shuffles.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "dct_common.h"
 
@@ -95,65 +96,65 @@ __global__ __launch_bounds__(256) void skinny_dx_kernel(const uint16_t* __restri
 }
 
 // dW[c][k] += sum_b dZ[b][c] X[b][k], db[c] += sum_b dZ[b][c].
-// Block: 64 lanes x 8 k = 512 columns, 4 row lanes; blockIdx.y splits the rows.
+// Block: 64 lanes x 8 k = 512 columns, 4 row lanes (waves); blockIdx.y splits the rows.  CT = the
+// class count rounded up to 1/2/4/8, so registers and the cross-wave LDS reduction cover only real
+// classes ([wave][c][j][lane]: lanes contiguous, conflict-free; CT = 2 -> 16 KB, several blocks
+// per CU).  The X rows are the only HBM stream; the head's dZ is read as wave-uniform scalars.
+template <int CT>
 __global__ __launch_bounds__(256) void skinny_dw_kernel(const uint16_t* __restrict__ dZ,
                                                         const uint16_t* __restrict__ X, float* __restrict__ dW,
                                                         float* __restrict__ db, int B, int K, int C, int rows_per) {
-  __shared__ float red[4][SK_CMAX][64 * 8 + 1];
+  __shared__ float red[4][CT][8][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int k = (blockIdx.x * 64 + tx) * 8;
   const int r0 = blockIdx.y * rows_per;
   const int r1 = min(B, r0 + rows_per);
-  float acc[SK_CMAX][8];
-  float dbs[SK_CMAX];
+  float acc[CT][8];
+  float dbs[CT];
 #pragma unroll
-  for (int c = 0; c < SK_CMAX; ++c) {
+  for (int c = 0; c < CT; ++c) {
     dbs[c] = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
   }
-  if (k < K) {
-    for (int b = r0 + ty; b < r1; b += 4) {
-      float x[8];
-      unpack8(*reinterpret_cast<const uint4*>(X + (size_t)b * K + k), x);
+  const bool kin = k < K;
+#pragma unroll 4
+  for (int b = r0 + ty; b < r1; b += 4) {
+    float x[8];
+    if (kin) unpack8(*reinterpret_cast<const uint4*>(X + (size_t)b * K + k), x);
 #pragma unroll
-      for (int c = 0; c < SK_CMAX; ++c) {
-        if (c < C) {
-          const float dz = bf16_to_f32(dZ[(size_t)b * C + c]);
-          dbs[c] += dz;
+    for (int c = 0; c < CT; ++c) {
+      const float dz = (c < C) ? bf16_to_f32(dZ[(size_t)b * C + c]) : 0.f;
+      dbs[c] += dz;
+      if (kin) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[c][j] += dz * x[j];
-        }
+        for (int j = 0; j < 8; ++j) acc[c][j] += dz * x[j];
       }
     }
   }
 #pragma unroll
-  for (int c = 0; c < SK_CMAX; ++c)
+  for (int c = 0; c < CT; ++c)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) red[ty][c][tx * 8 + j] = acc[c][j];
+    for (int j = 0; j < 8; ++j) red[ty][c][j][tx] = acc[c][j];
   __syncthreads();
-  if (ty == 0 && k < K) {
-#pragma unroll
-    for (int c = 0; c < SK_CMAX; ++c) {
-      if (c < C) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float v = red[0][c][tx * 8 + j] + red[1][c][tx * 8 + j] + red[2][c][tx * 8 + j] + red[3][c][tx * 8 + j];
-          atomicAdd(dW + (size_t)c * K + k + j, v);
-        }
-      }
+  // 256 threads fold the 4 waves' partials: thread t owns (c, j) pairs t / 64 + 4 i of lane t % 64
+  for (int cj = ty; cj < CT * 8; cj += 4) {
+    const int c = cj >> 3, j = cj & 7;
+    if (c < C && kin) {
+      const float v = red[0][c][j][tx] + red[1][c][j][tx] + red[2][c][j][tx] + red[3][c][j][tx];
+      atomicAdd(dW + (size_t)c * K + k + j, v);
     }
   }
-  if (db && blockIdx.x == 0) {  // bias grads: lane 0 of each row lane saw every row of its stride
+  if (db && blockIdx.x == 0) {  // bias grads: every row lane saw every row of its stride
     __syncthreads();
     if (tx == 0) {
 #pragma unroll
-      for (int c = 0; c < SK_CMAX; ++c) red[ty][c][0] = dbs[c];
+      for (int c = 0; c < CT; ++c) red[ty][c][0][0] = dbs[c];
     }
     __syncthreads();
     if (threadIdx.x < C) {
       const int c = threadIdx.x;
-      atomicAdd(db + c, red[0][c][0] + red[1][c][0] + red[2][c][0] + red[3][c][0]);
+      atomicAdd(db + c, red[0][c][0][0] + red[1][c][0][0] + red[2][c][0][0] + red[3][c][0][0]);
     }
   }
 }
@@ -185,14 +186,22 @@ int dct_skinny_dx(const uint16_t* dZ, const uint16_t* W, const uint16_t* aux, ui
 }
 
 int dct_skinny_dw(const uint16_t* dZ, const uint16_t* X, float* dW, float* db, int B, int K, int C, void* stream) {
-  if (C > dct::SK_CMAX || K % 8 || (((uintptr_t)X) & 15)) return (int)hipErrorInvalidValue;
+  if (C > dct::SK_CMAX || C < 1 || K % 8 || (((uintptr_t)X) & 15)) return (int)hipErrorInvalidValue;
   if (B <= 0) return 0;
   const int kb = (K + 511) / 512;
-  int splits = (B + 63) / 64;  // >= 64 rows per block
-  splits = splits > 128 ? 128 : splits;
+  // ~512 blocks of >= 32 rows: the row stream spread over every CU, few atomics per column
+  int splits = (512 + kb - 1) / kb;
+  const int max_splits = (B + 31) / 32;
+  splits = splits > max_splits ? max_splits : splits;
+  splits = splits < 1 ? 1 : splits;
+  if (const char* f = getenv("DCT_SKINNY_DW_SPLITS")) splits = atoi(f) > 0 ? atoi(f) : splits;  // debug / A-B
   const int rows_per = (B + splits - 1) / splits;
-  hipLaunchKernelGGL(dct::skinny_dw_kernel, dim3(kb, splits), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), dZ,
-                     X, dW, db, B, K, C, rows_per);
+  const dim3 grid(kb, (B + rows_per - 1) / rows_per);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (C == 1) hipLaunchKernelGGL(dct::skinny_dw_kernel<1>, grid, dim3(256), 0, st, dZ, X, dW, db, B, K, C, rows_per);
+  else if (C == 2) hipLaunchKernelGGL(dct::skinny_dw_kernel<2>, grid, dim3(256), 0, st, dZ, X, dW, db, B, K, C, rows_per);
+  else if (C <= 4) hipLaunchKernelGGL(dct::skinny_dw_kernel<4>, grid, dim3(256), 0, st, dZ, X, dW, db, B, K, C, rows_per);
+  else hipLaunchKernelGGL(dct::skinny_dw_kernel<8>, grid, dim3(256), 0, st, dZ, X, dW, db, B, K, C, rows_per);
   return (int)hipGetLastError();
 }
 

@@ -15,8 +15,22 @@ __global__ __launch_bounds__(256) void gather_batch_kernel(const uint4* __restri
                                                            const int* __restrict__ Y, const int* __restrict__ idx,
                                                            const int* __restrict__ cursor, int stride, int B,
                                                            int n_items, uint4* __restrict__ xdst,
-                                                           int* __restrict__ ydst) {
-  const int c = *cursor;
+                                                           int* __restrict__ ydst, int* __restrict__ step_counter,
+                                                           float* __restrict__ zero, int64_t zero_n) {
+  const int c = cursor ? *cursor : 0;
+  // the training step's prologue rides along: Adam step counter += 1 (read by adam_flat at the
+  // end of the step) and the flat gradient buffer (+ loss slot) zeroed by the whole grid.  A
+  // kernel, not hipMemsetAsync: a captured memset node was not reliably ordered after the
+  // previous replay's Adam kernel (back-to-back hipGraphLaunch, ROCm 7) and Adam read zeroed grads.
+  if (step_counter && blockIdx.x == 0 && threadIdx.x == 0) step_counter[0] += 1;
+  if (zero) {
+    const int64_t n4 = zero_n >> 2;
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float4* z4 = reinterpret_cast<float4*>(zero);
+    for (int64_t i = t; i < n4; i += gs) z4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t < zero_n - (n4 << 2)) zero[(n4 << 2) + t] = 0.f;
+  }
   const int total = B * row_vec;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const int r = e / row_vec;
@@ -57,16 +71,39 @@ __global__ void step_end_kernel(int* cursor, const float* slot, float* loss_out,
 
 extern "C" {
 
-int dct_gather_batch(const void* X, int row_bytes, const int* Y, const int* idx, const int* cursor, int stride,
-                     int B, int n_items, void* xdst, int* ydst, void* stream) {
+int dct_gather_batch_step(const void* X, int row_bytes, const int* Y, const int* idx, const int* cursor, int stride,
+                          int B, int n_items, void* xdst, int* ydst, int* step_counter, float* zero,
+                          int64_t zero_n, void* stream) {
   if (B <= 0) return 0;
   if (row_bytes % 16 || (((uintptr_t)X) | ((uintptr_t)xdst)) & 15) return (int)hipErrorInvalidValue;
+  if (zero && (((uintptr_t)zero) & 15)) return (int)hipErrorInvalidValue;
   const int rv = row_bytes / 16;
-  int grid = (B * rv + 255) / 256;
-  grid = grid > 1024 ? 1024 : (grid < 1 ? 1 : grid);
+  int64_t work = (int64_t)B * rv;
+  if (zero && (zero_n + 3) / 4 > work) work = (zero_n + 3) / 4;
+  int grid = (int)((work + 255) / 256);
+  grid = grid > 2048 ? 2048 : (grid < 1 ? 1 : grid);
   hipLaunchKernelGGL(dct::gather_batch_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     (const uint4*)X, rv, Y, idx, cursor, stride, B, n_items, (uint4*)xdst, ydst);
+                     (const uint4*)X, rv, Y, idx, cursor, stride, B, n_items, (uint4*)xdst, ydst, step_counter, zero,
+                     zero_n);
   return (int)hipGetLastError();
+}
+
+// Zero n fp32 values with a kernel (graph-captured steps: a kernel node instead of a memset node,
+// see gather_batch_kernel).
+int dct_zero_f32(float* p, int64_t n, void* stream) {
+  if (n <= 0) return 0;
+  if (((uintptr_t)p) & 15) return (int)hipErrorInvalidValue;
+  int grid = (int)(((n + 3) / 4 + 255) / 256);
+  grid = grid > 2048 ? 2048 : (grid < 1 ? 1 : grid);
+  hipLaunchKernelGGL(dct::gather_batch_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     nullptr, 0, nullptr, nullptr, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, p, n);
+  return (int)hipGetLastError();
+}
+
+int dct_gather_batch(const void* X, int row_bytes, const int* Y, const int* idx, const int* cursor, int stride,
+                     int B, int n_items, void* xdst, int* ydst, void* stream) {
+  return dct_gather_batch_step(X, row_bytes, Y, idx, cursor, stride, B, n_items, xdst, ydst, nullptr, nullptr, 0,
+                               stream);
 }
 
 int dct_step_begin(int* step_counter, float* stats, void* stream) {

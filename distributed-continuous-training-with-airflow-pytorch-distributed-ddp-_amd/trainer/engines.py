@@ -480,8 +480,18 @@ class AutogradEngine(_EngineBase):
     def steps_per_epoch(self) -> int:
         return math.ceil(math.ceil(len(self.train_rows) / self.ctx.world_size) / self.B)
 
+    def _zero_grads(self):
+        if self.flat_g.is_cuda:
+            # a native kernel rather than zero_(): torch lowers it to a memset node, which replayed
+            # graphs did not reliably order after the previous replay's Adam (csrc/step_kernels.hip)
+            from ..ops._native import native
+
+            native().zero_f32(self.flat_g.data_ptr(), self.flat_g.numel(), torch.cuda.current_stream().cuda_stream)
+        else:
+            self.flat_g.zero_()
+
     def _step_body(self, x, y, batch_idx: int):
-        self.flat_g.zero_()
+        self._zero_grads()
         if self.reducer is not None:
             self.reducer.prepare()
         self.model.train()

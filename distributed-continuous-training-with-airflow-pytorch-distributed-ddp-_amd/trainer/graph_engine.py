@@ -167,7 +167,11 @@ class GraphMLPEngine:
         local = distributed_indices(len(self.train_rows), self.ctx.world_size, self.ctx.rank, shuffle=shuffle,
                                     seed=self.seed, epoch=epoch)
         rows = self.train_rows[local].to(torch.int32)
-        self.idx[: rows.numel()].copy_(rows.to(self.device, non_blocking=True))
+        # pinned source + one stream sync per epoch: an async copy from PAGEABLE host memory is not
+        # reliably ordered before the hipGraphLaunch replays that read idx (observed on ROCm 7:
+        # replays of epoch >= 1 read a partly stale index list -> run-to-run divergence)
+        self.idx[: rows.numel()].copy_(rows.pin_memory(), non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
         return rows.numel()
 
     # ------------------------------------------------------------------ train

@@ -245,6 +245,30 @@ def test_gemm_bf16(M, N, K, ta, tb, cuda):
     assert torch.allclose(C, 2 * ref, atol=4e-3 * math.sqrt(K), rtol=2e-3)
 
 
+@pytest.mark.parametrize("stages", ["2", "4"])
+@pytest.mark.parametrize("M,N,K,ta,tb,out_f32", [
+    (2048, 1024, 1024, 0, 1, 0),  # 128 tiles x 16 k-tiles: the 4-stage LDS-DMA pipeline
+    (1024, 768, 640, 0, 0, 0),    # NN (transposed-read B image), 10 k-tiles
+    (512, 256, 8192, 1, 0, 1),    # dW shape: split-K slices of 8 k-tiles, 4 stages each
+    (768, 384, 192, 1, 0, 1),     # 3 k-tiles: prologue as deep as the whole loop
+    (256, 512, 128, 0, 1, 0),     # 2 k-tiles: fewer tiles than pipeline stages
+])
+def test_gemm_pipeline_depths(M, N, K, ta, tb, out_f32, stages, cuda, monkeypatch):
+    """The LDS pipeline depth (2 or 4 stages, counted vmcnt across a raw barrier) must not change
+    the product: each depth against the fp32 torch reference of the same bf16 operands."""
+    monkeypatch.setenv("DCT_GEMM_STAGES", stages)
+    torch.manual_seed(12)
+    A = _bf(torch.randn(K, M, device=cuda) if ta else torch.randn(M, K, device=cuda))
+    B = _bf(torch.randn(N, K, device=cuda) if tb else torch.randn(K, N, device=cuda))
+    C = torch.empty(M, N, device=cuda, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    native().gemm_bf16(A.data_ptr(), B.data_ptr(), C.data_ptr(), 0, M, N, K, A.stride(0), B.stride(0), N, ta, tb, 0,
+                       out_f32, 0, 0, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = (A.float().t() if ta else A.float()) @ (B.float().t() if tb else B.float())
+    tol = 2e-3 * math.sqrt(K) if out_f32 else 0.02 * math.sqrt(K)
+    assert (C.float() - ref).abs().max().item() < tol, (C.float() - ref).abs().max().item()
+
+
 @pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0)])
 def test_gemm_bf16_out_and_fast_path_match_generic(ta, tb, cuda, monkeypatch):
     """bf16 output; the fast path and the generic kernel agree."""
