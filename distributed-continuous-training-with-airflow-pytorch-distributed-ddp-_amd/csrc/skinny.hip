@@ -104,7 +104,7 @@ template <int CT>
 __global__ __launch_bounds__(256) void skinny_dw_kernel(const uint16_t* __restrict__ dZ,
                                                         const uint16_t* __restrict__ X, float* __restrict__ dW,
                                                         float* __restrict__ db, int B, int K, int C, int rows_per) {
-  __shared__ float red[4][CT][8][64];
+  __shared__ float red[4][CT][8][65];  // +1 pad: the column-ordered fold below reads j-major
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int k = (blockIdx.x * 64 + tx) * 8;
   const int r0 = blockIdx.y * rows_per;
@@ -137,12 +137,21 @@ __global__ __launch_bounds__(256) void skinny_dw_kernel(const uint16_t* __restri
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[ty][c][j][tx] = acc[c][j];
   __syncthreads();
-  // 256 threads fold the 4 waves' partials: thread t owns (c, j) pairs t / 64 + 4 i of lane t % 64
-  for (int cj = ty; cj < CT * 8; cj += 4) {
-    const int c = cj >> 3, j = cj & 7;
-    if (c < C && kin) {
-      const float v = red[0][c][j][tx] + red[1][c][j][tx] + red[2][c][j][tx] + red[3][c][j][tx];
-      atomicAdd(dW + (size_t)c * K + k + j, v);
+  // fold the 4 waves' partials in COLUMN order: thread t owns columns t and t + 256 of the block's
+  // 512, so each atomic wave-instruction covers 256 contiguous bytes (the full-rate atomic shape;
+  // a lane-per-8-columns pattern ran the head dW at 42 us)
+  const int kbase = blockIdx.x * 512;
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    if (c >= C) break;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int col = threadIdx.x + 256 * h;
+      const int j = col & 7, l = col >> 3;
+      if (kbase + col < K) {
+        const float v = red[0][c][j][l] + red[1][c][j][l] + red[2][c][j][l] + red[3][c][j][l];
+        atomicAdd(dW + (size_t)c * K + kbase + col, v);
+      }
     }
   }
   if (db && blockIdx.x == 0) {  // bias grads: every row lane saw every row of its stride
@@ -189,9 +198,9 @@ int dct_skinny_dw(const uint16_t* dZ, const uint16_t* X, float* dW, float* db, i
   if (C > dct::SK_CMAX || C < 1 || K % 8 || (((uintptr_t)X) & 15)) return (int)hipErrorInvalidValue;
   if (B <= 0) return 0;
   const int kb = (K + 511) / 512;
-  // ~512 blocks of >= 32 rows: the row stream spread over every CU, few atomics per column
-  int splits = (512 + kb - 1) / kb;
-  const int max_splits = (B + 31) / 32;
+  // ~256 blocks of >= 64 rows: the row stream spread over every CU, few atomics per column
+  int splits = (256 + kb - 1) / kb;
+  const int max_splits = (B + 63) / 64;
   splits = splits > max_splits ? max_splits : splits;
   splits = splits < 1 ? 1 : splits;
   if (const char* f = getenv("DCT_SKINNY_DW_SPLITS")) splits = atoi(f) > 0 ? atoi(f) : splits;  // debug / A-B

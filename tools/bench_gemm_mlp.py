@@ -50,6 +50,10 @@ VARIANTS = {
     "s4_splits128": {"DCT_GEMM_STAGES": "4", "DCT_GEMM_SPLITS": "128"},
 }
 ENV_KEYS = ("DCT_GEMM_STAGES", "DCT_GEMM_SPLIT_WG", "DCT_GEMM_SPLITS")
+if os.environ.get("AB_SET") == "dw":  # split-K sweep on the transformer dW shapes only
+    SHAPES = [s for s in SHAPES if s[0].startswith("tt_dw") or s[0] == "dw_l1"]
+    VARIANTS = {f"{st}_sp{sp}": {"DCT_GEMM_STAGES": st[1], "DCT_GEMM_SPLITS": str(sp)}
+                for st in ("s2", "s4") for sp in (8, 16, 32, 64)}
 
 
 def main():
