@@ -218,16 +218,46 @@ def build_training_dag(t: Optional[Targets] = None) -> DAG:
 _FAKE_CLIENT = None
 
 
+def _backend() -> str:
+    if os.environ.get("DCT_AZURE_FAKE", "0") == "1":
+        return "fake"
+    return os.environ.get("DCT_AZURE_BACKEND", "azure").lower()
+
+
 def get_azure_client():
-    """Real MLClient, or an in-memory fake when DCT_AZURE_FAKE=1 (dry runs / tests)."""
+    """The deployment target of the two deploy DAGs (``DCT_AZURE_BACKEND``):
+    ``azure`` (default) - the real MLClient; ``fake`` (or ``DCT_AZURE_FAKE=1``) - an in-memory fake
+    for dry runs; ``local`` - the local online endpoint (deploy/local_endpoint.py): the server at
+    ``DCT_LOCAL_ENDPOINT_URL`` (key ``DCT_LOCAL_ENDPOINT_KEY``) or, without a URL, in this process."""
     from ..deploy.azure import AzureConfig, FakeMLClient, get_ml_client
 
     global _FAKE_CLIENT
-    if os.environ.get("DCT_AZURE_FAKE", "0") == "1":
+    backend = _backend()
+    if backend in ("fake", "local"):
         if _FAKE_CLIENT is None:
-            _FAKE_CLIENT = FakeMLClient()
+            if backend == "fake":
+                _FAKE_CLIENT = FakeMLClient()
+            else:
+                from ..deploy.local_endpoint import LocalMLClient
+
+                _FAKE_CLIENT = LocalMLClient(os.environ.get("DCT_LOCAL_ENDPOINT_URL") or None,
+                                             os.environ.get("DCT_LOCAL_ENDPOINT_KEY") or None)
         return _FAKE_CLIENT
     return get_ml_client(AzureConfig.from_env())
+
+
+def _health_gate(client, cfg, old: str, new: str, phase: str):
+    """Before widening traffic to the new slot: on the local backend probe it (sample request +
+    error rate over what it served so far) and roll back to the old slot if it is unhealthy
+    (reference D11 only slept between phases)."""
+    if _backend() != "local" or new == old:
+        return
+    from ..deploy.azure import rollback
+    from ..deploy.local_endpoint import health_probe
+
+    if not health_probe(client, cfg.endpoint_name)(new):
+        rollback(client, cfg, old, new)
+        raise RuntimeError(f"deployment {new!r} failed its health check during {phase}; rolled back to {old!r}")
 
 
 def task_prepare_package(**context):
@@ -271,14 +301,18 @@ def task_canary(ti=None, **context):
     from ..deploy.azure import AzureConfig, start_canary
 
     old, new = _slots(ti)
-    start_canary(get_azure_client(), AzureConfig.from_env(), old, new)
+    client, cfg = get_azure_client(), AzureConfig.from_env()
+    _health_gate(client, cfg, old, new, "shadow")
+    start_canary(client, cfg, old, new)
 
 
 def task_full_rollout(ti=None, **context):
     from ..deploy.azure import AzureConfig, full_rollout
 
     old, new = _slots(ti)
-    full_rollout(get_azure_client(), AzureConfig.from_env(), old, new)
+    client, cfg = get_azure_client(), AzureConfig.from_env()
+    _health_gate(client, cfg, old, new, "canary")
+    full_rollout(client, cfg, old, new)
 
 
 def build_manual_deploy_dag() -> DAG:
