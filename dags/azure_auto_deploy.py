@@ -1,0 +1,15 @@
+"""Airflow DAG file for ``azure_automated_rollout`` (reference: dags/azure_auto_deploy.py): prepare_package -> new slot -> shadow 20 % -> canary 10 % -> full, health-gated.
+
+Mount the repository at ``/workspace`` and point ``AIRFLOW__CORE__DAGS_FOLDER`` at this directory
+(docker/compose.yaml).  The DAG itself is built by ``dct_amd.orchestration.dags.build_rollout_dag``; this
+file only exposes it at module level, which is how Airflow discovers DAGs.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import dct_amd  # noqa: E402,F401
+from dct_amd.orchestration.dags import build_rollout_dag  # noqa: E402
+
+dag = build_rollout_dag()
