@@ -288,7 +288,9 @@ __device__ __forceinline__ bf16x8 g2_frag(const char* img, int rb, int ks, int l
 }
 
 // SPLIT: split-K slices reduce with float atomics.  Those keep the MFMA's natural C layout
-// (lane = column) so every atomic instruction covers 16 consecutive columns of 4 rows; the
+// (lane = column) so every atomic instruction covers 16 consecutive columns of 4 rows (restaging
+// through LDS into 256-byte row runs measured 0-20 % SLOWER on every dW shape:
+// profiles/gemm_splitk_lds_restage_ab_r1.log); the
 // plain-store kernels swap the MFMA operands instead (lane = row, 4 consecutive columns per
 // lane -> 8/16-byte row stores).
 // BM = 64: half-height tiles for small-K / few-tile shapes (K <= 256 with M in the tens of

@@ -5,7 +5,8 @@ transformer blocks (LayerNorm -> packed QKV -> feature-token attention -> out pr
 residual; LayerNorm -> GELU MLP -> residual) mix the tokens; the mean token goes through a
 final LayerNorm and a linear head.  On MI355X every GEMM / LayerNorm / attention is a native
 HIP kernel (ops/nn.py) with bf16 activations on an fp32 residual stream, and each pre-norm sub-block
-is ONE fused autograd node (prenorm_attention / prenorm_ffn); on CPU the same module runs
+is ONE fused autograd node (prenorm_attention / prenorm_ffn) - at the benchmark shape the whole
+block's forward is one kernel (ops/nn.py tt_block, csrc/tt_block.hip); on CPU the same module runs
 plain torch ops.  Training contract = the reference LightningModule's (training_step logs
 ``train_loss``; validation_step logs ``val_loss`` / ``val_acc``; Adam).
 """
@@ -17,7 +18,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.nn import layer_norm, linear, prenorm_attention, prenorm_ffn
+from ..ops.nn import layer_norm, linear, tt_block
 from ..trainer.module import TrainModule
 
 
@@ -33,9 +34,9 @@ class _Block(nn.Module):
         self.fc2 = nn.Linear(ffn_mult * d, d)
 
     def forward(self, h: torch.Tensor, B: int, T: int) -> torch.Tensor:
-        h = prenorm_attention(h, self.ln1_w, self.ln1_b, self.qkv.weight, self.qkv.bias, self.proj.weight,
-                              self.proj.bias, B, self.heads, T)
-        return prenorm_ffn(h, self.ln2_w, self.ln2_b, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias)
+        return tt_block(h, self.ln1_w, self.ln1_b, self.qkv.weight, self.qkv.bias, self.proj.weight, self.proj.bias,
+                        self.ln2_w, self.ln2_b, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias,
+                        B, self.heads, T)
 
 
 class TabTransformer(TrainModule):

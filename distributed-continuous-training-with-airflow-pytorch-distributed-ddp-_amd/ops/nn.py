@@ -392,14 +392,19 @@ class _PreNormFFNFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        nat = native()
-        st = _stream()
-        h, mean, rstd, a, w1b, w2b, f, pre = ctx.saved_tensors
-        ln_w, ln_b = ctx.params[:2]
-        dout = dout.contiguous().float()
-        da, dw1, db1, dw2, db2 = _ffn_bwd(nat, _bf16_of(dout), a, w1b, w2b, f, pre, ctx.params[2:], st)
-        dh, dlw, dlb = _ln_bwd(nat, da, h, ln_w, ln_b, mean, rstd, dres=dout, want_bf16=True)
-        return dh, dlw, dlb, dw1, db1, dw2, db2, None
+        return (*_prenorm_ffn_bwd(dout, ctx.saved_tensors, ctx.params), None)
+
+
+def _prenorm_ffn_bwd(dout, saved, params):
+    """(dh, dln_w, dln_b, dw1, db1, dw2, db2) of h + FFN(LN(h)) from the forward's saved tensors."""
+    nat = native()
+    st = _stream()
+    h, mean, rstd, a, w1b, w2b, f, pre = saved
+    ln_w, ln_b = params[:2]
+    dout = dout.contiguous().float()
+    da, dw1, db1, dw2, db2 = _ffn_bwd(nat, _bf16_of(dout), a, w1b, w2b, f, pre, params[2:], st)
+    dh, dlw, dlb = _ln_bwd(nat, da, h, ln_w, ln_b, mean, rstd, dres=dout, want_bf16=True)
+    return dh, dlw, dlb, dw1, db1, dw2, db2
 
 
 class _PreNormAttnFn(torch.autograd.Function):
@@ -434,24 +439,73 @@ class _PreNormAttnFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        return (*_prenorm_attn_bwd(dout, ctx.saved_tensors, ctx.params, ctx.dims), None, None, None, None)
+
+
+def _prenorm_attn_bwd(dout, saved, params, dims):
+    """(dh, dln_w, dln_b, dwqkv, dbqkv, dwo, dbo) of h + Wo MHA(LN(h)) + bo from the saved tensors."""
+    nat = native()
+    st = _stream()
+    h, mean, rstd, a, wqkvb, qkv, o, lse, wob = saved
+    ln_w, ln_b, wqkv, bqkv, wo, bo = params
+    B, H, T, D, scale = dims
+    M, dm = h.shape
+    dout = dout.contiguous().float()
+    dz = _bf16_of(dout)
+    dwo, dbo = _dw_gemm(nat, dz, o, wo, bo, st)
+    do = _mm(nat, dz, wob, M, dm, dm, st)
+    dqkv = torch.empty_like(qkv)
+    base, dbase = qkv.data_ptr(), dqkv.data_ptr()
+    nat.attention_bwd(base, base + 2 * dm, base + 4 * dm, o.data_ptr(), do.data_ptr(), lse.data_ptr(), dbase,
+                      dbase + 2 * dm, dbase + 4 * dm, B, H, T, D, 3 * dm, dm, scale, st)
+    dwqkv, dbqkv = _dw_gemm(nat, dqkv, a, wqkv, bqkv, st)
+    da = _mm(nat, dqkv, wqkvb, M, dm, 3 * dm, st)
+    dh, dlw, dlb = _ln_bwd(nat, da, h, ln_w, ln_b, mean, rstd, dres=dout, want_bf16=True)
+    return dh, dlw, dlb, dwqkv, dbqkv, dwo, dbo
+
+
+class _TTBlockFn(torch.autograd.Function):
+    """A whole pre-norm transformer block (attention sub-block then FFN sub-block) as ONE kernel
+    forward (csrc/tt_block.hip: one workgroup per sample, all intermediates in LDS) for the
+    TabTransformer shape (64 tokens, d_model 64, 4 heads, FFN 256).  It writes exactly the tensors
+    the two unfused nodes save, so the backward is theirs, FFN first."""
+
+    @staticmethod
+    def forward(ctx, h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, eps, B, H, T):
         nat = native()
         st = _stream()
-        h, mean, rstd, a, wqkvb, qkv, o, lse, wob = ctx.saved_tensors
-        ln_w, ln_b, wqkv, bqkv, wo, bo = ctx.params
-        B, H, T, D, scale = ctx.dims
+        h = h.contiguous().float()
         M, dm = h.shape
-        dout = dout.contiguous().float()
-        dz = _bf16_of(dout)
-        dwo, dbo = _dw_gemm(nat, dz, o, wo, bo, st)
-        do = _mm(nat, dz, wob, M, dm, dm, st)
-        dqkv = torch.empty_like(qkv)
-        base, dbase = qkv.data_ptr(), dqkv.data_ptr()
-        nat.attention_bwd(base, base + 2 * dm, base + 4 * dm, o.data_ptr(), do.data_ptr(), lse.data_ptr(), dbase,
-                          dbase + 2 * dm, dbase + 4 * dm, B, H, T, D, 3 * dm, dm, scale, st)
-        dwqkv, dbqkv = _dw_gemm(nat, dqkv, a, wqkv, bqkv, st)
-        da = _mm(nat, dqkv, wqkvb, M, dm, 3 * dm, st)
-        dh, dlw, dlb = _ln_bwd(nat, da, h, ln_w, ln_b, mean, rstd, dres=dout, want_bf16=True)
-        return dh, dlw, dlb, dwqkv, dbqkv, dwo, dbo, None, None, None, None
+        FF = w1.shape[0]
+        dev = h.device
+        wqkvb, wob, w1b, w2b = _w16(wqkv), _w16(wo), _w16(w1), _w16(w2)
+        bf, f32 = torch.bfloat16, torch.float32
+        a1, a2 = torch.empty(M, dm, dtype=bf, device=dev), torch.empty(M, dm, dtype=bf, device=dev)
+        st4 = torch.empty(4, M, dtype=f32, device=dev)  # mean1, rstd1, mean2, rstd2
+        qkv = torch.empty(M, 3 * dm, dtype=bf, device=dev)
+        o = torch.empty(M, dm, dtype=bf, device=dev)
+        lse = torch.empty(B * H * T, dtype=f32, device=dev)
+        h1, out = torch.empty(M, dm, dtype=f32, device=dev), torch.empty(M, dm, dtype=f32, device=dev)
+        f, pre = torch.empty(M, FF, dtype=bf, device=dev), torch.empty(M, FF, dtype=bf, device=dev)
+        vecs = [t.contiguous() for t in (ln1_w, ln1_b, bqkv, bo, ln2_w, ln2_b, b1, b2)]
+        ptrs = [h, vecs[0], vecs[1], wqkvb, vecs[2], wob, vecs[3], vecs[4], vecs[5], w1b, vecs[6], w2b, vecs[7],
+                a1, st4[0], st4[1], qkv, o, lse, h1, a2, st4[2], st4[3], f, pre, out]
+        scale = 1.0 / math.sqrt(dm // H)
+        nat.tt_block_fwd([t.data_ptr() for t in ptrs], B, T, dm, H, FF, float(eps), scale, st)
+        ctx.save_for_backward(h, st4, a1, wqkvb, qkv, o, lse, wob, h1, a2, w1b, w2b, f, pre)
+        ctx.params = (ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2)
+        ctx.dims = (B, H, T, dm // H, scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        h, st4, a1, wqkvb, qkv, o, lse, wob, h1, a2, w1b, w2b, f, pre = ctx.saved_tensors
+        p = ctx.params
+        dh1, dl2w, dl2b, dw1, db1, dw2, db2 = _prenorm_ffn_bwd(dout, (h1, st4[2], st4[3], a2, w1b, w2b, f, pre),
+                                                               p[6:])
+        dh, dl1w, dl1b, dwqkv, dbqkv, dwo, dbo = _prenorm_attn_bwd(
+            dh1, (h, st4[0], st4[1], a1, wqkvb, qkv, o, lse, wob), p[:6], ctx.dims)
+        return (dh, dl1w, dl1b, dwqkv, dbqkv, dwo, dbo, dl2w, dl2b, dw1, db1, dw2, db2, None, None, None, None)
 
 
 def _prenorm_ok(h: torch.Tensor) -> bool:
@@ -463,6 +517,23 @@ def prenorm_ffn(h, ln_w, ln_b, w1, b1, w2, b2, eps: float = 1e-5):
     if _prenorm_ok(h):
         return _PreNormFFNFn.apply(h, ln_w, ln_b, w1, b1, w2, b2, eps)
     return ffn_residual(layer_norm(h, ln_w, ln_b, eps), w1, b1, w2, b2, h)
+
+
+def tt_block_fusable(h: torch.Tensor, H: int, T: int, ffn: int) -> bool:
+    """The whole-block fused forward covers the TabTransformer benchmark shape exactly."""
+    import os
+    return (h.is_cuda and h.dim() == 2 and h.shape[1] == 64 and H == 4 and T == 64 and ffn == 256
+            and os.environ.get("DCT_TT_FUSED", "1") != "0")
+
+
+def tt_block(h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, B: int, H: int, T: int,
+             eps: float = 1e-5):
+    """One pre-norm transformer block: h + MHA(LN1 h), then + FFN(LN2 .) - one fused kernel
+    forward on MI355X for the benchmark shape, two fused nodes otherwise."""
+    if tt_block_fusable(h, H, T, w1.shape[0]):
+        return _TTBlockFn.apply(h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, eps, B, H, T)
+    h = prenorm_attention(h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, B, H, T, eps)
+    return prenorm_ffn(h, ln2_w, ln2_b, w1, b1, w2, b2, eps)
 
 
 def prenorm_attention(h, ln_w, ln_b, wqkv, bqkv, wo, bo, B: int, H: int, T: int, eps: float = 1e-5):

@@ -641,6 +641,56 @@ def test_prenorm_attention_matches_fp32_reference(cuda):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("B", [1, 37, 512])
+def test_tt_block_fused_matches_fp32_reference_and_unfused(cuda, B, monkeypatch):
+    """ops.nn.tt_block at the TabTransformer shape (64 tokens, d 64, 4 heads, FFN 256): the
+    whole-block kernel forward (csrc/tt_block.hip) vs an fp32 torch block, and vs the unfused
+    two-node path (same backward) - outputs and every gradient."""
+    from dct_amd.ops import nn as nnops
+
+    T, H, d, n = 64, 4, 64, 256
+    M = B * T
+    g = torch.Generator(device="cpu").manual_seed(11)
+    mk = lambda *s, scale=1.0: (scale * torch.randn(*s, generator=g)).to(cuda).requires_grad_()  # noqa: E731
+    t = dict(h=mk(M, d), ln1_w=(1 + 0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_(),
+             ln1_b=mk(d, scale=0.1), wqkv=mk(3 * d, d, scale=d ** -0.5), bqkv=mk(3 * d, scale=0.1),
+             wo=mk(d, d, scale=d ** -0.5), bo=mk(d, scale=0.1),
+             ln2_w=(1 + 0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_(), ln2_b=mk(d, scale=0.1),
+             w1=mk(n, d, scale=d ** -0.5), b1=mk(n, scale=0.1), w2=mk(d, n, scale=n ** -0.5), b2=mk(d, scale=0.1))
+    keys = ["ln1_w", "ln1_b", "wqkv", "bqkv", "wo", "bo", "ln2_w", "ln2_b", "w1", "b1", "w2", "b2"]
+    dout = torch.randn(M, d, device=cuda)
+
+    def run(fused):
+        monkeypatch.setenv("DCT_TT_FUSED", "1" if fused else "0")
+        assert nnops.tt_block_fusable(t["h"], H, T, n) == fused
+        out = nnops.tt_block(t["h"], *[t[k] for k in keys], B, H, T)
+        out.backward(dout)
+        grads = {k: v.grad.clone() for k, v in t.items()}
+        for v in t.values():
+            v.grad = None
+        return out.detach(), grads
+
+    out_f, g_f = run(True)
+    out_u, g_u = run(False)
+    a = F.layer_norm(t["h"], (d,), t["ln1_w"], t["ln1_b"], 1e-5)
+    q, k, v = (z.reshape(B, T, H, d // H).transpose(1, 2) for z in F.linear(a, t["wqkv"], t["bqkv"]).split(d, 1))
+    o = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(M, d)
+    h1 = t["h"] + F.linear(o, t["wo"], t["bo"])
+    a2 = F.layer_norm(h1, (d,), t["ln2_w"], t["ln2_b"], 1e-5)
+    ref = h1 + F.linear(F.gelu(F.linear(a2, t["w1"], t["b1"])), t["w2"], t["b2"])
+    ref.backward(dout)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out_f).all()
+    assert (out_f - ref).norm() / ref.norm() < 1e-2
+    assert (out_f - out_u).norm() / out_u.norm() < 2e-3  # same bf16 roundings, different sum order
+    for name, tv in t.items():
+        rel = (g_f[name] - tv.grad).norm() / (tv.grad.norm() + 1e-12)
+        assert rel < 5e-2, (name, float(rel))
+        rel_u = (g_f[name] - g_u[name]).norm() / (g_u[name].norm() + 1e-12)
+        assert rel_u < 2e-2, (name, float(rel_u))
+
+
+@pytest.mark.gpu
 def test_skinny_head_linear_and_shadow_weights(cuda):
     """ops.nn.linear with N <= 8 takes the skinny kernels; under bound_params a registered bf16
     shadow replaces the weight conversion and gradients accumulate into .grad."""

@@ -41,9 +41,10 @@ def test_cpu_fit_learns(tmp_path):
 
 
 @pytest.mark.gpu
-def test_hip_path_matches_torch_reference(cuda):
+@pytest.mark.parametrize("F_", [32, 64])  # 64 features = the whole-block fused kernel shape
+def test_hip_path_matches_torch_reference(cuda, F_):
     torch.manual_seed(1)
-    F_, B = 32, 64
+    B = 64
     ref = TabTransformer(num_features=F_, d_model=64, heads=4, layers=2)
     hip = TabTransformer(num_features=F_, d_model=64, heads=4, layers=2)
     hip.load_state_dict(ref.state_dict())
