@@ -300,6 +300,13 @@ PYBIND11_MODULE(_dct_native, m) {
               "tt_block_fwd");
       });
   m.def(
+      "tt_block_bwd",
+      [](std::vector<uintptr_t> ptrs, int Bsz, int T, int DM, int H, int FF, float scale, uintptr_t stream) {
+        check(dct_tt_block_bwd(ptrs.data(), (int)ptrs.size(), Bsz, T, DM, H, FF, scale,
+                               reinterpret_cast<void*>(stream)),
+              "tt_block_bwd");
+      });
+  m.def(
       "attention_bwd",
       [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t dout, uintptr_t lse, uintptr_t dq, uintptr_t dk,
          uintptr_t dv, int Bsz, int H, int T, int D, int ldq, int ldo, float scale, uintptr_t stream) {

@@ -74,5 +74,7 @@ int dct_attention_bwd(const uint16_t* q, const uint16_t* k, const uint16_t* v, c
                       int T, int D, int ldq, int ldo, float scale, void* stream);
 int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps, float scale,
                      void* stream);
+int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
+                     void* stream);
 int dct_gather_rows(const void* src, const int* idx, void* dst, int64_t n_rows, int row_bytes, void* stream);
 }

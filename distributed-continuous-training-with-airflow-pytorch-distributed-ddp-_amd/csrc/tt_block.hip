@@ -77,9 +77,36 @@ struct Args {
   uint16_t* a2; float* mean2; float* rstd2;
   uint16_t* f; uint16_t* pre;
   float* out;
+  uint16_t* wT;  // transposed bf16 weights for the backward: W2^T | W1^T | Wo^T | Wqkv^T
   int B;
   float eps, scale;
 };
+
+// offsets (elements) of the transposed weights in Args::wT / BwdArgs::wT
+constexpr int WT_W2 = 0, WT_W1 = FF * DM, WT_WO = 2 * FF * DM, WT_QKV = 2 * FF * DM + DM * DM;
+constexpr int WT_TOTAL = WT_QKV + 3 * DM * DM;
+
+// wT <- transposes of this step's bf16 weights (grid-stride side task of the forward kernel:
+// the backward's dX products need W^T rows as MFMA B fragments)
+__device__ __forceinline__ void transpose_weights(const Args& a) {
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < WT_TOTAL; e += gridDim.x * 256) {
+    uint16_t v;
+    if (e < WT_W1) {            // W2 [DM][FF] -> W2^T [FF][DM]
+      const int j = e / DM, n = e - j * DM;
+      v = a.w2[n * FF + j];
+    } else if (e < WT_WO) {     // W1 [FF][DM] -> W1^T [DM][FF]
+      const int q = e - WT_W1, i = q / FF, j = q - i * FF;
+      v = a.w1[j * DM + i];
+    } else if (e < WT_QKV) {    // Wo [DM][DM] -> Wo^T
+      const int q = e - WT_WO, i = q / DM, n = q - i * DM;
+      v = a.wo[n * DM + i];
+    } else {                    // Wqkv [3DM][DM] -> Wqkv^T [DM][3DM]
+      const int q = e - WT_QKV, i = q / (3 * DM), j = q - i * (3 * DM);
+      v = a.wqkv[j * DM + i];
+    }
+    a.wT[e] = v;
+  }
+}
 
 // 64-row LDS tile -> contiguous global rows, 16-byte chunks over the whole workgroup
 template <int ROW_BYTES, int LD_BYTES>
@@ -330,6 +357,362 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
   }
   __syncthreads();
   store_tile<DM * 4, HS_LD * 4>(a.out + (size_t)row0 * DM, HS);
+  transpose_weights(a);
+}
+
+// ============================================================================ backward
+// dX chain of the same block for one sample per workgroup (the dW products stay split-K GEMMs
+// over all B*64 rows, fed by the dZ tensors written here):
+//   dF   = bf16(dout) W2 ; dpre = dF * gelu'(pre)              -> dpre (global, for dW1 / db1)
+//   da2  = dpre W1 ; dh1 = dout + LN2_bwd(da2)                  -> bf16(dh1) (global, for dWo / dbo)
+//   do   = bf16(dh1) Wo ; attention backward per head           -> dqkv (global, for dWqkv / dbqkv)
+//   da1  = dqkv Wqkv ; dh = dh1 + LN1_bwd(da1)                  -> dh fp32 + bf16 copy
+// LayerNorm weight/bias gradients: per-column partials reduced over the workgroup in LDS, one
+// global atomic per column per workgroup.  LayerNorm backwards run directly on the MFMA C layout
+// (row sums = 4 tiles in-lane + xor-shuffles over the 16 lanes of a row group).
+// LDS (80 KB -> 2 workgroups per CU): G fp32 residual gradient rows; X bf16 A-operand rows;
+// R pre/dpre, later qkv/dqkv (dq, dk, dv written in place over q, k, v of the wave's own head);
+// O / dO for the attention backward.
+struct BwdArgs {
+  const float* dout;  // [M][DM] fp32
+  const float* h; const float* mean1; const float* rstd1; const float* ln1_w;
+  const uint16_t* qkv; const uint16_t* o; const float* lse;
+  const float* h1; const float* mean2; const float* rstd2; const float* ln2_w;
+  const uint16_t* pre;
+  const uint16_t* wT;
+  uint16_t* dpre; uint16_t* dh1_16; uint16_t* dqkv; float* dh; uint16_t* dh16;
+  float *dln1_w, *dln1_b, *dln2_w, *dln2_b;
+  float scale;
+};
+
+constexpr int XB_LD = DM + 8;  // bf16 rows (144 B)
+constexpr int G_BYTES = T * HS_LD * 4;
+constexpr int X_BYTES = T * XB_LD * 2;
+constexpr int BWD_LDS = G_BYTES + X_BYTES + R_BYTES + 2 * X_BYTES + 4 * DM * 4 + NH * T * 4;
+
+__device__ __forceinline__ float rowsum16(float v) {  // over the 16 lanes of a row group
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 8);
+  return v;
+}
+
+// Copy this wave's 16 rows of an LDS bf16 tile to global rows (16-byte chunks).
+template <int ROW_BYTES, int LD_BYTES>
+__device__ __forceinline__ void store_rows16(void* gdst, const void* s, int wv, int lane) {
+  constexpr int CPR = ROW_BYTES / 16;
+  for (int idx = lane; idx < 16 * CPR; idx += 64) {
+    const int r = 16 * wv + idx / CPR, c = idx % CPR;
+    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(gdst) + r * ROW_BYTES + c * 16) =
+        *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(s) + r * LD_BYTES + c * 16);
+  }
+}
+// global rows -> LDS tile (all 64 rows, whole workgroup)
+template <int ROW_BYTES, int LD_BYTES>
+__device__ __forceinline__ void load_tile(void* s, const void* gsrc) {
+  constexpr int CPR = ROW_BYTES / 16;
+  for (int idx = threadIdx.x; idx < T * CPR; idx += 256) {
+    const int r = idx / CPR, c = idx - r * CPR;
+    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(s) + r * LD_BYTES + c * 16) =
+        *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(gsrc) + r * ROW_BYTES + c * 16);
+  }
+}
+
+// LayerNorm backward on the C layout of the wave's 16 rows: lane (c, g) holds da[t][r] for row
+// 16w + 4g + r, column 16t + c.  dres / result live in G (fp32, same positions).
+// dx = rstd (gw - mean(gw) - xhat mean(gw xhat)) + dres, gw = da * w.
+__device__ __forceinline__ void ln_bwd_c(const f32x4 (&da)[4], const float* x, const float* mean, const float* rstd,
+                                         const float* w, float* G, float* red_w, float* red_b, int row0, int wv,
+                                         int c, int g) {
+  float cw[4], cb[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) { cw[t] = 0.f; cb[t] = 0.f; }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int rl = 16 * wv + 4 * g + r;
+    const float mu = mean[row0 + rl], rs = rstd[row0 + rl];
+    float xh[4], gw[4], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int col = 16 * t + c;
+      xh[t] = (x[(size_t)(row0 + rl) * DM + col] - mu) * rs;
+      gw[t] = da[t][r] * w[col];
+      s1 += gw[t];
+      s2 += gw[t] * xh[t];
+      cw[t] += da[t][r] * xh[t];
+      cb[t] += da[t][r];
+    }
+    s1 = rowsum16(s1) * (1.f / DM);
+    s2 = rowsum16(s2) * (1.f / DM);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) G[rl * HS_LD + 16 * t + c] += rs * (gw[t] - s1 - xh[t] * s2);
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const float vw = sum4g(cw[t]), vb = sum4g(cb[t]);
+    if (g == 0) {
+      atomicAdd(red_w + 16 * t + c, vw);
+      atomicAdd(red_b + 16 * t + c, vb);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* G = reinterpret_cast<float*>(smem);
+  uint16_t* X = reinterpret_cast<uint16_t*>(smem + G_BYTES);
+  uint16_t* R = reinterpret_cast<uint16_t*>(smem + G_BYTES + X_BYTES);
+  uint16_t* Os = reinterpret_cast<uint16_t*>(smem + G_BYTES + X_BYTES + R_BYTES);
+  uint16_t* dOs = Os + T * XB_LD;
+  float* red = reinterpret_cast<float*>(smem + G_BYTES + 3 * X_BYTES + R_BYTES);  // [4][DM]
+  float* sdl = red + 4 * DM;                                                       // [NH][T]
+  const int bidx = blockIdx.x, row0 = bidx * T;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const uint16_t* W2T = a.wT + WT_W2;
+  const uint16_t* W1T = a.wT + WT_W1;
+  const uint16_t* WoT = a.wT + WT_WO;
+  const uint16_t* WqT = a.wT + WT_QKV;
+
+  // ---- P0: pre -> R (whole tile); dout rows -> G (fp32) and X (bf16); zero the LN partials
+  load_tile<FF * 2, F_LD * 2>(R, a.pre + (size_t)row0 * FF);
+  red[threadIdx.x] = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = 16 * wv + 4 * g + r, col = 16 * t + c;
+      const float v = a.dout[(size_t)(row0 + rl) * DM + col];
+      G[rl * HS_LD + col] = v;
+      X[rl * XB_LD + col] = f32_to_bf16(v);
+    }
+  __syncthreads();
+
+  // ---- P1: dpre = (bf16(dout) W2) * gelu'(pre), own rows, in place over pre in R
+  {
+    f32x4 acc[FF / 16];
+#pragma unroll
+    for (int t = 0; t < FF / 16; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < DM / 32; ++ks) {
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(X + (16 * wv + c) * XB_LD + 32 * ks + 8 * g);
+#pragma unroll
+      for (int t = 0; t < FF / 16; ++t)
+        acc[t] = mfma32(af, *reinterpret_cast<const bf16x8*>(W2T + (size_t)(16 * t + c) * DM + 32 * ks + 8 * g), acc[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < FF / 16; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        uint16_t* pp = R + (16 * wv + 4 * g + r) * F_LD + 16 * t + c;
+        *pp = f32_to_bf16(acc[t][r] * gelu_grad_f(bf16_to_f32(*pp)));
+      }
+  }
+  store_rows16<FF * 2, F_LD * 2>(a.dpre + (size_t)row0 * FF, R, wv, lane);
+
+  // ---- P2/P3: da2 = dpre W1 (own rows); dh1 = dout + LN2_bwd(da2) into G
+  {
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < FF / 32; ++ks) {
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(R + (16 * wv + c) * F_LD + 32 * ks + 8 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        acc[t] = mfma32(af, *reinterpret_cast<const bf16x8*>(W1T + (size_t)(16 * t + c) * FF + 32 * ks + 8 * g), acc[t]);
+    }
+    ln_bwd_c(acc, a.h1, a.mean2, a.rstd2, a.ln2_w, G, red + 2 * DM, red + 3 * DM, row0, wv, c, g);
+  }
+  // bf16(dh1) -> X (own rows) -> global
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = 16 * wv + 4 * g + r, col = 16 * t + c;
+      X[rl * XB_LD + col] = f32_to_bf16(G[rl * HS_LD + col]);
+    }
+  store_rows16<DM * 2, XB_LD * 2>(a.dh1_16 + (size_t)row0 * DM, X, wv, lane);
+
+  // ---- P4: do = bf16(dh1) Wo (own rows) -> dOs
+  {
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < DM / 32; ++ks) {
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(X + (16 * wv + c) * XB_LD + 32 * ks + 8 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        acc[t] = mfma32(af, *reinterpret_cast<const bf16x8*>(WoT + (size_t)(16 * t + c) * DM + 32 * ks + 8 * g), acc[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dOs[(16 * wv + 4 * g + r) * XB_LD + 16 * t + c] = f32_to_bf16(acc[t][r]);
+  }
+  __syncthreads();  // every wave is done with R (dpre) and has written its dO rows
+
+  // ---- P5: qkv -> R, o -> Os
+  load_tile<3 * DM * 2, QKV_LD * 2>(R, a.qkv + (size_t)row0 * 3 * DM);
+  load_tile<DM * 2, XB_LD * 2>(Os, a.o + (size_t)row0 * DM);
+  __syncthreads();
+
+  // ---- P6: attention backward of head wv; dq, dk, dv overwrite q, k, v of the head in R
+  {
+    uint16_t* Qh = R + DH * wv;
+    uint16_t* Kh = R + DM + DH * wv;
+    uint16_t* Vh = R + 2 * DM + DH * wv;
+    const uint16_t* Oh = Os + DH * wv;
+    const uint16_t* Gh = dOs + DH * wv;
+    const float* lb = a.lse + ((size_t)bidx * NH + wv) * T;
+    float* dl = sdl + wv * T;
+    {  // delta_q = rowsum(dO_q * O_q) over the head's 16 columns
+      float sacc = 0.f;
+#pragma unroll
+      for (int d = 0; d < DH; d += 4) {
+        const bf16x4 o4 = *reinterpret_cast<const bf16x4*>(Oh + lane * XB_LD + d);
+        const bf16x4 g4 = *reinterpret_cast<const bf16x4*>(Gh + lane * XB_LD + d);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sacc += bf16_to_f32((uint16_t)o4[e]) * bf16_to_f32((uint16_t)g4[e]);
+      }
+      dl[lane] = sacc;
+    }
+    auto ld4 = [](const uint16_t* p) { return *reinterpret_cast<const bf16x4*>(p); };
+    auto ld4col = [](const uint16_t* p, int ld) {
+      bf16x4 r;
+      r[0] = (short)p[0]; r[1] = (short)p[ld]; r[2] = (short)p[2 * ld]; r[3] = (short)p[3 * ld];
+      return r;
+    };
+    bf16x4 qf[4], kf[4], gf[4], vf[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      qf[j] = ld4(Qh + (16 * j + c) * QKV_LD + 4 * g);
+      kf[j] = ld4(Kh + (16 * j + c) * QKV_LD + 4 * g);
+      vf[j] = ld4(Vh + (16 * j + c) * QKV_LD + 4 * g);
+      gf[j] = ld4(Gh + (16 * j + c) * XB_LD + 4 * g);
+    }
+    f32x4 dv[4], dk[4], dq[4];
+    {  // pass A: S = Q K^T, dP = dO V^T (C: row = query, col = key) -> dV = P^T dO, dK = dS^T Q
+      f32x4 sc[4][4], dp[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          sc[j][i] = mfma16(qf[j], kf[i], (f32x4){0.f, 0.f, 0.f, 0.f});
+          dp[j][i] = mfma16(gf[j], vf[i], (f32x4){0.f, 0.f, 0.f, 0.f});
+        }
+      bf16x4 pa[4][4], dsa[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qi = 16 * j + 4 * g + r;
+          const float lq = lb[qi], dq_ = dl[qi];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p = __expf(sc[j][i][r] * a.scale - lq);
+            sc[j][i][r] = p;
+            dp[j][i][r] = p * (dp[j][i][r] - dq_);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { pa[i][j] = pack4(sc[j][i]); dsa[i][j] = pack4(dp[j][i]); }
+      }
+      bf16x4 gcol[4], qcol[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        gcol[j] = ld4col(Gh + (16 * j + 4 * g) * XB_LD + c, XB_LD);
+        qcol[j] = ld4col(Qh + (16 * j + 4 * g) * QKV_LD + c, QKV_LD);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        dv[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        dk[i] = dv[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          dv[i] = mfma16(pa[i][j], gcol[j], dv[i]);
+          dk[i] = mfma16(dsa[i][j], qcol[j], dk[i]);
+        }
+      }
+    }
+    {  // pass B: S^T = K Q^T, dP^T = V dO^T (C: row = key, col = query) -> dQ = dS K
+      f32x4 st[4][4], dpt[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          st[i][j] = mfma16(kf[i], qf[j], (f32x4){0.f, 0.f, 0.f, 0.f});
+          dpt[i][j] = mfma16(vf[i], gf[j], (f32x4){0.f, 0.f, 0.f, 0.f});
+        }
+      bf16x4 dsq[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int qi = 16 * j + c;
+        const float lq = lb[qi], dq_ = dl[qi];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          f32x4 tv;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) tv[r] = __expf(st[i][j][r] * a.scale - lq) * (dpt[i][j][r] - dq_);
+          dsq[j][i] = pack4(tv);
+        }
+      }
+      bf16x4 kcol[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) kcol[i] = ld4col(Kh + (16 * i + 4 * g) * QKV_LD + c, QKV_LD);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        dq[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dq[j] = mfma16(dsq[j][i], kcol[i], dq[j]);
+      }
+    }
+    // all of this head's reads of q, k, v are done (same wave, LDS in order) -> overwrite in place
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = (16 * i + 4 * g + r) * QKV_LD + c;
+        Qh[rr] = f32_to_bf16(dq[i][r] * a.scale);
+        Kh[rr] = f32_to_bf16(dk[i][r] * a.scale);
+        Vh[rr] = f32_to_bf16(dv[i][r]);
+      }
+  }
+  __syncthreads();
+
+  // ---- P7: dqkv out; da1 = dqkv Wqkv (own rows); dh = dh1 + LN1_bwd(da1) into G
+  store_tile<3 * DM * 2, QKV_LD * 2>(a.dqkv + (size_t)row0 * 3 * DM, R);
+  {
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 3 * DM / 32; ++ks) {
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(R + (16 * wv + c) * QKV_LD + 32 * ks + 8 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        acc[t] = mfma32(af, *reinterpret_cast<const bf16x8*>(WqT + (size_t)(16 * t + c) * (3 * DM) + 32 * ks + 8 * g),
+                        acc[t]);
+    }
+    ln_bwd_c(acc, a.h, a.mean1, a.rstd1, a.ln1_w, G, red, red + DM, row0, wv, c, g);
+  }
+  // dh (fp32) and its bf16 copy, own rows (X is free: its last reader was P4 of this wave)
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = 16 * wv + 4 * g + r, col = 16 * t + c;
+      X[rl * XB_LD + col] = f32_to_bf16(G[rl * HS_LD + col]);
+    }
+  store_rows16<DM * 2, XB_LD * 2>(a.dh16 + (size_t)row0 * DM, X, wv, lane);
+  store_rows16<DM * 4, HS_LD * 4>(a.dh + (size_t)row0 * DM, G, wv, lane);
+  __syncthreads();
+  {  // LayerNorm parameter gradients: one atomic per column per workgroup
+    float* dsts[4] = {a.dln1_w, a.dln1_b, a.dln2_w, a.dln2_b};
+    atomicAdd(dsts[threadIdx.x >> 6] + (threadIdx.x & 63), red[threadIdx.x]);
+  }
 }
 
 }  // namespace ttb
@@ -337,12 +720,12 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
 
 extern "C" {
 
-// ptrs (26, in order): h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2,
-//   a1, mean1, rstd1, qkv, o, lse, h1, a2, mean2, rstd2, f, pre, out
+// ptrs (27, in order): h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2,
+//   a1, mean1, rstd1, qkv, o, lse, h1, a2, mean2, rstd2, f, pre, out, wT
 int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps, float scale,
                      void* stream) {
   using namespace dct::ttb;
-  if (n_ptrs != 26 || T != dct::ttb::T || DM != dct::ttb::DM || H != NH || FF != dct::ttb::FF || Bsz <= 0)
+  if (n_ptrs != 27 || T != dct::ttb::T || DM != dct::ttb::DM || H != NH || FF != dct::ttb::FF || Bsz <= 0)
     return (int)hipErrorInvalidValue;
   uintptr_t any = 0;
   for (int i = 0; i < n_ptrs; ++i) {
@@ -360,7 +743,7 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
   a.a1 = (uint16_t*)p[13]; a.mean1 = (float*)p[14]; a.rstd1 = (float*)p[15];
   a.qkv = (uint16_t*)p[16]; a.o = (uint16_t*)p[17]; a.lse = (float*)p[18];
   a.h1 = (float*)p[19]; a.a2 = (uint16_t*)p[20]; a.mean2 = (float*)p[21]; a.rstd2 = (float*)p[22];
-  a.f = (uint16_t*)p[23]; a.pre = (uint16_t*)p[24]; a.out = (float*)p[25];
+  a.f = (uint16_t*)p[23]; a.pre = (uint16_t*)p[24]; a.out = (float*)p[25]; a.wT = (uint16_t*)p[26];
   a.B = Bsz; a.eps = eps; a.scale = scale;
   static bool attr = false;
   if (!attr) {
@@ -370,6 +753,39 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
     attr = true;
   }
   hipLaunchKernelGGL(tt_block_fwd_kernel, dim3(Bsz), dim3(256), LDS_BYTES, reinterpret_cast<hipStream_t>(stream), a);
+  return (int)hipGetLastError();
+}
+
+// ptrs (22, in order): dout, h, mean1, rstd1, ln1_w, qkv, o, lse, h1, mean2, rstd2, ln2_w, pre, wT,
+//   dpre, dh1_16, dqkv, dh, dh16, dln1_w, dln1_b, dln2_w, dln2_b  (23 with the last four)
+int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
+                     void* stream) {
+  using namespace dct::ttb;
+  if (n_ptrs != 23 || T != dct::ttb::T || DM != dct::ttb::DM || H != NH || FF != dct::ttb::FF || Bsz <= 0)
+    return (int)hipErrorInvalidValue;
+  uintptr_t any = 0;
+  for (int i = 0; i < n_ptrs; ++i) {
+    if (!p[i]) return (int)hipErrorInvalidValue;
+    if (i < 19) any |= p[i];
+  }
+  if (any & 15) return (int)hipErrorInvalidValue;
+  BwdArgs a;
+  a.dout = (const float*)p[0]; a.h = (const float*)p[1]; a.mean1 = (const float*)p[2]; a.rstd1 = (const float*)p[3];
+  a.ln1_w = (const float*)p[4]; a.qkv = (const uint16_t*)p[5]; a.o = (const uint16_t*)p[6]; a.lse = (const float*)p[7];
+  a.h1 = (const float*)p[8]; a.mean2 = (const float*)p[9]; a.rstd2 = (const float*)p[10]; a.ln2_w = (const float*)p[11];
+  a.pre = (const uint16_t*)p[12]; a.wT = (const uint16_t*)p[13];
+  a.dpre = (uint16_t*)p[14]; a.dh1_16 = (uint16_t*)p[15]; a.dqkv = (uint16_t*)p[16]; a.dh = (float*)p[17];
+  a.dh16 = (uint16_t*)p[18];
+  a.dln1_w = (float*)p[19]; a.dln1_b = (float*)p[20]; a.dln2_w = (float*)p[21]; a.dln2_b = (float*)p[22];
+  a.scale = scale;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)tt_block_bwd_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, BWD_LDS);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(tt_block_bwd_kernel, dim3(Bsz), dim3(256), BWD_LDS, reinterpret_cast<hipStream_t>(stream), a);
   return (int)hipGetLastError();
 }
 

@@ -487,25 +487,65 @@ class _TTBlockFn(torch.autograd.Function):
         lse = torch.empty(B * H * T, dtype=f32, device=dev)
         h1, out = torch.empty(M, dm, dtype=f32, device=dev), torch.empty(M, dm, dtype=f32, device=dev)
         f, pre = torch.empty(M, FF, dtype=bf, device=dev), torch.empty(M, FF, dtype=bf, device=dev)
+        wT = torch.empty(2 * FF * dm + 4 * dm * dm, dtype=bf, device=dev)  # W2^T | W1^T | Wo^T | Wqkv^T
         vecs = [t.contiguous() for t in (ln1_w, ln1_b, bqkv, bo, ln2_w, ln2_b, b1, b2)]
         ptrs = [h, vecs[0], vecs[1], wqkvb, vecs[2], wob, vecs[3], vecs[4], vecs[5], w1b, vecs[6], w2b, vecs[7],
-                a1, st4[0], st4[1], qkv, o, lse, h1, a2, st4[2], st4[3], f, pre, out]
+                a1, st4[0], st4[1], qkv, o, lse, h1, a2, st4[2], st4[3], f, pre, out, wT]
         scale = 1.0 / math.sqrt(dm // H)
         nat.tt_block_fwd([t.data_ptr() for t in ptrs], B, T, dm, H, FF, float(eps), scale, st)
-        ctx.save_for_backward(h, st4, a1, wqkvb, qkv, o, lse, wob, h1, a2, w1b, w2b, f, pre)
+        ctx.save_for_backward(h, st4, a1, wqkvb, qkv, o, lse, wob, h1, a2, w1b, w2b, f, pre, wT, vecs[0], vecs[4])
         ctx.params = (ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2)
         ctx.dims = (B, H, T, dm // H, scale)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        h, st4, a1, wqkvb, qkv, o, lse, wob, h1, a2, w1b, w2b, f, pre = ctx.saved_tensors
+        h, st4, a1, wqkvb, qkv, o, lse, wob, h1, a2, w1b, w2b, f, pre, wT, ln1w, ln2w = ctx.saved_tensors
         p = ctx.params
+        B, H, T, D, scale = ctx.dims
+        if _TT_FUSED_BWD:
+            return (*_tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, p, B, H, T,
+                                         scale), None, None, None, None)
         dh1, dl2w, dl2b, dw1, db1, dw2, db2 = _prenorm_ffn_bwd(dout, (h1, st4[2], st4[3], a2, w1b, w2b, f, pre),
                                                                p[6:])
         dh, dl1w, dl1b, dwqkv, dbqkv, dwo, dbo = _prenorm_attn_bwd(
             dh1, (h, st4[0], st4[1], a1, wqkvb, qkv, o, lse, wob), p[:6], ctx.dims)
         return (dh, dl1w, dl1b, dwqkv, dbqkv, dwo, dbo, dl2w, dl2b, dw1, db1, dw2, db2, None, None, None, None)
+
+
+_TT_FUSED_BWD = True
+
+
+def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, params, B, H, T, scale):
+    """Backward of the fused block: ONE kernel for the whole dX chain (csrc/tt_block.hip
+    tt_block_bwd_kernel: dF/gelu', W1, LN2, Wo, attention, Wqkv, LN1 per sample) writing the dZ
+    operands of the four dW GEMMs, which then run split-K over all rows with the bias gradients
+    fused as column sums."""
+    nat = native()
+    st = _stream()
+    ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2 = params
+    dout = dout.contiguous().float()
+    M, dm = h.shape
+    FF = pre.shape[1]
+    dev, bf = h.device, torch.bfloat16
+    dpre = torch.empty(M, FF, dtype=bf, device=dev)
+    dh1_16 = torch.empty(M, dm, dtype=bf, device=dev)
+    dqkv = torch.empty(M, 3 * dm, dtype=bf, device=dev)
+    dh = torch.empty(M, dm, dtype=torch.float32, device=dev)
+    dh16 = torch.empty(M, dm, dtype=bf, device=dev)
+    lg = [_grad_dst(t, zero=True) for t in (ln1_w, ln1_b, ln2_w, ln2_b)]
+    ptrs = [dout, h, st4[0], st4[1], ln1w, qkv, o, lse, h1, st4[2], st4[3], ln2w, pre, wT,
+            dpre, dh1_16, dqkv, dh, dh16] + [g for g, _ in lg]
+    nat.tt_block_bwd([t.data_ptr() for t in ptrs], B, T, dm, H, FF, scale, st)
+    dout16 = _bf16_of(dout)
+    dw2, db2 = _dw_gemm(nat, dout16, f, w2, b2, st)
+    dw1, db1 = _dw_gemm(nat, dpre, a2, w1, b1, st)
+    dwo, dbo = _dw_gemm(nat, dh1_16, o, wo, bo, st)
+    dwqkv, dbqkv = _dw_gemm(nat, dqkv, a1, wqkv, bqkv, st)
+    _remember_bf16(dh, dh16)
+    (dl1w, d1), (dl1b, d2), (dl2w, d3), (dl2b, d4) = lg
+    return (dh, None if d1 else dl1w, None if d2 else dl1b, dwqkv, dbqkv, dwo, dbo, None if d3 else dl2w,
+            None if d4 else dl2b, dw1, db1, dw2, db2)
 
 
 def _prenorm_ok(h: torch.Tensor) -> bool:
@@ -520,8 +560,10 @@ def prenorm_ffn(h, ln_w, ln_b, w1, b1, w2, b2, eps: float = 1e-5):
 
 
 def tt_block_fusable(h: torch.Tensor, H: int, T: int, ffn: int) -> bool:
-    """The whole-block fused forward covers the TabTransformer benchmark shape exactly."""
+    """The whole-block fused kernels cover the TabTransformer benchmark shape exactly."""
     import os
+    global _TT_FUSED_BWD
+    _TT_FUSED_BWD = os.environ.get("DCT_TT_FUSED_BWD", "1") != "0"
     return (h.is_cuda and h.dim() == 2 and h.shape[1] == 64 and H == 4 and T == 64 and ffn == 256
             and os.environ.get("DCT_TT_FUSED", "1") != "0")
 

@@ -644,8 +644,8 @@ def test_prenorm_attention_matches_fp32_reference(cuda):
 @pytest.mark.parametrize("B", [1, 37, 512])
 def test_tt_block_fused_matches_fp32_reference_and_unfused(cuda, B, monkeypatch):
     """ops.nn.tt_block at the TabTransformer shape (64 tokens, d 64, 4 heads, FFN 256): the
-    whole-block kernel forward (csrc/tt_block.hip) vs an fp32 torch block, and vs the unfused
-    two-node path (same backward) - outputs and every gradient."""
+    whole-block kernels (csrc/tt_block.hip: forward, and the backward dX chain + split-K dW GEMMs)
+    vs an fp32 torch block, and vs the unfused two-node path - outputs and every gradient."""
     from dct_amd.ops import nn as nnops
 
     T, H, d, n = 64, 4, 64, 256
@@ -660,8 +660,9 @@ def test_tt_block_fused_matches_fp32_reference_and_unfused(cuda, B, monkeypatch)
     keys = ["ln1_w", "ln1_b", "wqkv", "bqkv", "wo", "bo", "ln2_w", "ln2_b", "w1", "b1", "w2", "b2"]
     dout = torch.randn(M, d, device=cuda)
 
-    def run(fused):
+    def run(fused, fused_bwd=True):
         monkeypatch.setenv("DCT_TT_FUSED", "1" if fused else "0")
+        monkeypatch.setenv("DCT_TT_FUSED_BWD", "1" if fused_bwd else "0")
         assert nnops.tt_block_fusable(t["h"], H, T, n) == fused
         out = nnops.tt_block(t["h"], *[t[k] for k in keys], B, H, T)
         out.backward(dout)
@@ -670,7 +671,8 @@ def test_tt_block_fused_matches_fp32_reference_and_unfused(cuda, B, monkeypatch)
             v.grad = None
         return out.detach(), grads
 
-    out_f, g_f = run(True)
+    out_f, g_f = run(True)               # fused forward + fused backward kernel
+    out_fu, g_fu = run(True, False)      # fused forward + the unfused backward nodes
     out_u, g_u = run(False)
     a = F.layer_norm(t["h"], (d,), t["ln1_w"], t["ln1_b"], 1e-5)
     q, k, v = (z.reshape(B, T, H, d // H).transpose(1, 2) for z in F.linear(a, t["wqkv"], t["bqkv"]).split(d, 1))
@@ -688,6 +690,8 @@ def test_tt_block_fused_matches_fp32_reference_and_unfused(cuda, B, monkeypatch)
         assert rel < 5e-2, (name, float(rel))
         rel_u = (g_f[name] - g_u[name]).norm() / (g_u[name].norm() + 1e-12)
         assert rel_u < 2e-2, (name, float(rel_u))
+        rel_fu = (g_fu[name] - g_u[name]).norm() / (g_u[name].norm() + 1e-12)
+        assert rel_fu < 2e-2, (name, float(rel_fu))
 
 
 @pytest.mark.gpu
