@@ -306,6 +306,20 @@ PYBIND11_MODULE(_dct_native, m) {
                                reinterpret_cast<void*>(stream)),
               "tt_block_bwd");
       });
+  m.def("tt_embed_fwd", [](uintptr_t x, uintptr_t E, uintptr_t c, uintptr_t h, int B, int F, int D, uintptr_t st) {
+    check(dct_tt_embed_fwd(P<const float>(x), P<const float>(E), P<const float>(c), P<float>(h), B, F, D,
+                           reinterpret_cast<void*>(st)), "tt_embed_fwd");
+  });
+  m.def("tt_embed_bwd", [](uintptr_t x, uintptr_t dh, uintptr_t dE, uintptr_t dc, int B, int F, int D, uintptr_t st) {
+    check(dct_tt_embed_bwd(P<const float>(x), P<const float>(dh), P<float>(dE), P<float>(dc), B, F, D,
+                           reinterpret_cast<void*>(st)), "tt_embed_bwd");
+  });
+  m.def("tt_head_fwd", [](std::vector<uintptr_t> p, int B, int T, int D, int C, float eps, uintptr_t st) {
+    check(dct_tt_head_fwd(p.data(), (int)p.size(), B, T, D, C, eps, reinterpret_cast<void*>(st)), "tt_head_fwd");
+  });
+  m.def("tt_head_bwd", [](std::vector<uintptr_t> p, int B, int T, int D, int C, float eps, uintptr_t st) {
+    check(dct_tt_head_bwd(p.data(), (int)p.size(), B, T, D, C, eps, reinterpret_cast<void*>(st)), "tt_head_bwd");
+  });
   m.def(
       "attention_bwd",
       [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t dout, uintptr_t lse, uintptr_t dq, uintptr_t dk,

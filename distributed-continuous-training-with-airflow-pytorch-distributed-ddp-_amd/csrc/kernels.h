@@ -76,5 +76,9 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
                      void* stream);
 int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
                      void* stream);
+int dct_tt_embed_fwd(const float* x, const float* E, const float* c, float* h, int B, int F, int Dm, void* stream);
+int dct_tt_embed_bwd(const float* x, const float* dh, float* dE, float* dc, int B, int F, int Dm, void* stream);
+int dct_tt_head_fwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C, float eps, void* stream);
+int dct_tt_head_bwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C, float eps, void* stream);
 int dct_gather_rows(const void* src, const int* idx, void* dst, int64_t n_rows, int row_bytes, void* stream);
 }

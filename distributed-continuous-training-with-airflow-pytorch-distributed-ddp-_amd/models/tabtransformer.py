@@ -18,7 +18,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.nn import layer_norm, linear, tt_block
+from ..ops.nn import layer_norm, linear, tt_block, tt_embed, tt_head_loss
 from ..trainer.module import TrainModule
 
 
@@ -53,18 +53,24 @@ class TabTransformer(TrainModule):
         self.ln_w, self.ln_b = nn.Parameter(torch.ones(d_model)), nn.Parameter(torch.zeros(d_model))
         self.head = nn.Linear(d_model, num_classes)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def _trunk(self, x: torch.Tensor) -> torch.Tensor:
         B = x.shape[0]
-        h = (x.float()[:, :, None] * self.feat_w + self.feat_b).reshape(B * self.F, self.d)
+        h = tt_embed(x, self.feat_w, self.feat_b)
         for blk in self.blocks:
             h = blk(h, B, self.F)
-        pooled = h.reshape(B, self.F, self.d).mean(1)
+        return h
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B = x.shape[0]
+        pooled = self._trunk(x).reshape(B, self.F, self.d).mean(1)
         z = layer_norm(pooled, self.ln_w, self.ln_b)
         return linear(z, self.head.weight, self.head.bias).float()
 
     def training_step(self, batch, batch_idx):
         x, y = batch
-        loss = F.cross_entropy(self(x), y)
+        # pooled LN -> Linear -> mean CE as one kernel each way on MI355X (ops/nn.py tt_head_loss)
+        loss = tt_head_loss(self._trunk(x), y, x.shape[0], self.F, self.ln_w, self.ln_b, self.head.weight,
+                            self.head.bias)
         self.log("train_loss", loss, sync_dist=True)
         return loss
 

@@ -630,3 +630,85 @@ def attention(qkv: torch.Tensor, B: int, H: int, T: int, D: int) -> torch.Tensor
     q, k, v = (t.reshape(B, T, H, D).transpose(1, 2) for t in qkv.float().split(H * D, dim=1))
     o = F.scaled_dot_product_attention(q, k, v)
     return o.transpose(1, 2).reshape(B * T, H * D)
+
+
+# ----------------------------------------------------------------------------- TabTransformer ends
+class _TTEmbedFn(torch.autograd.Function):
+    """h[b*F + f, :] = x[b, f] * E[f, :] + c[f, :] (csrc/tt_io.hip); backward = batch reductions."""
+
+    @staticmethod
+    def forward(ctx, x, E, c):
+        B, F_ = x.shape
+        D = E.shape[1]
+        x = x.contiguous().float()
+        h = torch.empty(B * F_, D, dtype=torch.float32, device=x.device)
+        native().tt_embed_fwd(x.data_ptr(), E.contiguous().data_ptr(), c.contiguous().data_ptr(), h.data_ptr(), B,
+                              F_, D, _stream())
+        ctx.save_for_backward(x)
+        ctx.params = (E, c)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        (x,) = ctx.saved_tensors
+        E, c = ctx.params
+        B, F_ = x.shape
+        dE, dE_direct = _grad_dst(E, zero=True)
+        dc, dc_direct = _grad_dst(c, zero=True)
+        native().tt_embed_bwd(x.data_ptr(), dh.contiguous().float().data_ptr(), dE.data_ptr(), dc.data_ptr(), B, F_,
+                              E.shape[1], _stream())
+        return None, None if dE_direct else dE, None if dc_direct else dc
+
+
+def tt_embed(x: torch.Tensor, E: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
+    """Feature-token embedding [B, F] -> [B*F, D] (native on MI355X for D == 64)."""
+    B, F_ = x.shape
+    if x.is_cuda and E.shape[1] == 64:
+        return _TTEmbedFn.apply(x, E, c)
+    return (x.float()[:, :, None] * E + c).reshape(B * F_, E.shape[1])
+
+
+class _TTHeadLossFn(torch.autograd.Function):
+    """mean_b CE(Linear(LN(mean_t h[b, t, :])), y_b) in one kernel; the backward kernel recomputes the
+    per-sample chain and writes dh (fp32 + the bf16 copy the last block's dW GEMM consumes)."""
+
+    @staticmethod
+    def forward(ctx, h, y, ln_w, ln_b, W, bias, B, T, eps):
+        h = h.contiguous().float()
+        y = y.contiguous().long()
+        vec = [t.contiguous() for t in (ln_w, ln_b, W, bias)]
+        loss = torch.zeros((), dtype=torch.float32, device=h.device)
+        native().tt_head_fwd([h.data_ptr(), y.data_ptr()] + [t.data_ptr() for t in vec] + [loss.data_ptr()], B, T,
+                             h.shape[1], W.shape[0], float(eps), _stream())
+        ctx.save_for_backward(h, y, *vec)
+        ctx.params = (ln_w, ln_b, W, bias)
+        ctx.dims = (B, T, eps)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        h, y, lw, lb, Wc, bc = ctx.saved_tensors
+        B, T, eps = ctx.dims
+        dh = torch.empty_like(h)
+        dh16 = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
+        gs = [_grad_dst(p, zero=True) for p in ctx.params]
+        dloss = dloss.contiguous().float()
+        ptrs = [h, y, lw, lb, Wc, bc, dloss, dh, dh16] + [g for g, _ in gs]
+        native().tt_head_bwd([t.data_ptr() for t in ptrs], B, T, h.shape[1], Wc.shape[0], float(eps), _stream())
+        _remember_bf16(dh, dh16)
+        return (dh, None, *[None if direct else g for g, direct in gs], None, None, None)
+
+
+def tt_head_fusable(h: torch.Tensor, num_classes: int) -> bool:
+    import os
+    return (h.is_cuda and h.shape[1] == 64 and 1 <= num_classes <= 8
+            and os.environ.get("DCT_TT_FUSED_HEAD", "1") != "0")
+
+
+def tt_head_loss(h, y, B: int, T: int, ln_w, ln_b, W, bias, eps: float = 1e-5):
+    """Mean cross-entropy of the pooled-token classifier head (LN -> Linear) - one kernel each way."""
+    if tt_head_fusable(h, W.shape[0]):
+        return _TTHeadLossFn.apply(h, y, ln_w, ln_b, W, bias, B, T, eps)
+    pooled = h.reshape(B, T, h.shape[1]).mean(1)
+    z = layer_norm(pooled, ln_w, ln_b, eps)
+    return F.cross_entropy(linear(z, W, bias).float(), y)

@@ -695,6 +695,40 @@ def test_tt_block_fused_matches_fp32_reference_and_unfused(cuda, B, monkeypatch)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("B,C", [(1, 2), (37, 2), (512, 2), (64, 5)])
+def test_tt_embed_and_head_loss_match_fp32_reference(cuda, B, C):
+    """csrc/tt_io.hip: feature-token embedding fwd/bwd and the pooled LN -> Linear -> mean-CE head
+    (loss forward, recomputing backward) vs fp32 torch, every gradient including dh."""
+    from dct_amd.ops.nn import tt_embed, tt_head_loss
+
+    F_, d = 64, 64
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randn(B, F_, generator=g).to(cuda)
+    y = torch.randint(0, C, (B,), generator=g).to(cuda)
+    mk = lambda *s, scale=1.0: (scale * torch.randn(*s, generator=g)).to(cuda).requires_grad_()  # noqa: E731
+    E, c = mk(F_, d, scale=0.2), mk(F_, d, scale=0.1)
+    lw = (1 + 0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_()
+    lb, W, bias = mk(d, scale=0.1), mk(C, d, scale=0.3), mk(C, scale=0.1)
+    params = [E, c, lw, lb, W, bias]
+    h = tt_embed(x, E, c)
+    h2 = h * 1.5  # an op between embedding and head, so dh flows through autograd
+    loss = tt_head_loss(h2, y, B, F_, lw, lb, W, bias)
+    loss.backward()
+    got = [p.grad.clone() for p in params]
+    for p in params:
+        p.grad = None
+    hr = (x[:, :, None] * E + c).reshape(B * F_, d) * 1.5
+    z = F.layer_norm(hr.reshape(B, F_, d).mean(1), (d,), lw, lb, 1e-5)
+    ref = F.cross_entropy(F.linear(z, W, bias), y)
+    ref.backward()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - ref.item()) < 1e-4 * max(1.0, abs(ref.item()))
+    for p, gg in zip(params, got):
+        rel = (gg - p.grad).norm() / (p.grad.norm() + 1e-12)
+        assert rel < 1e-3, float(rel)
+
+
+@pytest.mark.gpu
 def test_skinny_head_linear_and_shadow_weights(cuda):
     """ops.nn.linear with N <= 8 takes the skinny kernels; under bound_params a registered bf16
     shadow replaces the weight conversion and gradients accumulate into .grad."""
