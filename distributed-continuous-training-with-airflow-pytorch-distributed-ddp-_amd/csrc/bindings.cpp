@@ -320,6 +320,23 @@ PYBIND11_MODULE(_dct_native, m) {
   m.def("tt_head_bwd", [](std::vector<uintptr_t> p, int B, int T, int D, int C, float eps, uintptr_t st) {
     check(dct_tt_head_bwd(p.data(), (int)p.size(), B, T, D, C, eps, reinterpret_cast<void*>(st)), "tt_head_bwd");
   });
+  m.def("gemm_bf16_dw_grouped",
+        [](std::vector<uintptr_t> dz, std::vector<uintptr_t> x, std::vector<uintptr_t> c, std::vector<int> M,
+           std::vector<int> N, int K, std::vector<uintptr_t> colsum, int accumulate, uintptr_t stream) {
+          const size_t n = dz.size();
+          if (x.size() != n || c.size() != n || M.size() != n || N.size() != n || (colsum.size() && colsum.size() != n))
+            throw std::invalid_argument("gemm_bf16_dw_grouped: list lengths differ");
+          std::vector<const uint16_t*> pz(n), px(n);
+          std::vector<float*> pc(n), pcs(n);
+          for (size_t i = 0; i < n; ++i) {
+            pz[i] = P<const uint16_t>(dz[i]); px[i] = P<const uint16_t>(x[i]); pc[i] = P<float>(c[i]);
+            pcs[i] = colsum.size() ? P<float>(colsum[i]) : nullptr;
+          }
+          check(dct_gemm_bf16_dw_grouped((int)n, pz.data(), px.data(), pc.data(), M.data(), N.data(), K,
+                                         colsum.size() ? pcs.data() : nullptr, accumulate,
+                                         reinterpret_cast<void*>(stream)),
+                "gemm_bf16_dw_grouped");
+        });
   m.def(
       "attention_bwd",
       [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t dout, uintptr_t lse, uintptr_t dq, uintptr_t dk,

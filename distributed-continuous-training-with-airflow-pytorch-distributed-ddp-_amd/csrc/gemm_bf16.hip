@@ -325,18 +325,21 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <bool TA, bool TB, bool SPLIT, int BM = 128, int S = 2>
-__global__ __launch_bounds__(GNT, BM == 64 ? 4 : 2) void gemm2_kernel(GemmArgs g, int splits) {
+// bijective XCD-aware remap: consecutive work ids land on the same XCD (shared L2)
+__device__ __forceinline__ int xcd_wgid() {
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+}
+
+template <bool TA, bool TB, bool SPLIT, int BM, int S>
+__device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wgid) {
   static_assert(BM == 128 || (BM == 64 && !TA), "BM = 64 needs a row-major (KC) A image");
   constexpr int IM = BM / 32;  // 16-row MFMA tiles per wave (2 x 2 waves)
   extern __shared__ __attribute__((aligned(16))) char smem2[];
   // [buf][A,B] images of 16 KB each
   constexpr bool AMC = TA, BMC = !TB;
-  const int nwg = gridDim.x;
-  const int orig = blockIdx.x;
-  const int xcd = orig & 7;
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int tile = wgid / splits, split = wgid - tile * splits;
   const int tiles_n = (g.N + GBN - 1) / GBN;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
@@ -425,7 +428,11 @@ __global__ __launch_bounds__(GNT, BM == 64 ? 4 : 2) void gemm2_kernel(GemmArgs g
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = m0 + wr * (BM / 2) + i * 16 + row_l + r;
-          if (row < g.M) atomicAdd(reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col, acc[i][j][r] * g.alpha);
+          if (row < g.M) {
+            float* dst = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
+            if (g.split_probe) *dst = acc[i][j][r] * g.alpha;
+            else atomicAdd(dst, acc[i][j][r] * g.alpha);
+          }
         }
       }
     return;
@@ -536,6 +543,30 @@ __global__ __launch_bounds__(GNT, BM == 64 ? 4 : 2) void gemm2_kernel(GemmArgs g
   }
 }
 
+template <bool TA, bool TB, bool SPLIT, int BM = 128, int S = 2>
+__global__ __launch_bounds__(GNT, BM == 64 ? 4 : 2) void gemm2_kernel(GemmArgs g, int splits) {
+  gemm2_body<TA, TB, SPLIT, BM, S>(g, splits, xcd_wgid());
+}
+
+// Grouped split-K launch: up to DW_GROUP independent problems (the dW GEMMs of one transformer
+// block) in ONE grid, so the per-launch fixed cost (ramp, first-load latency, tail) is paid once.
+constexpr int DW_GROUP = 4;
+struct GemmGroup {
+  GemmArgs g[DW_GROUP];
+  int splits[DW_GROUP];
+  int start[DW_GROUP + 1];  // first work id of each problem; start[n] = total
+  int n;
+};
+
+template <bool TA, bool TB, int S>
+__global__ __launch_bounds__(GNT, 2) void gemm2_grouped_kernel(GemmGroup gg) {
+  const int w = xcd_wgid();
+  int p = 0;
+#pragma unroll
+  for (int i = 1; i < DW_GROUP; ++i) p += (i < gg.n && w >= gg.start[i]) ? 1 : 0;
+  gemm2_body<TA, TB, true, 128, S>(gg.g[p], gg.splits[p], w - gg.start[p]);
+}
+
 // zero the fp32 C[M, ldc] panel that split-K slices accumulate into (a kernel node, not a
 // hipMemset2DAsync node: see gather_batch_kernel on memset nodes in replayed graphs)
 __global__ __launch_bounds__(256) void zero_panel_kernel(float* __restrict__ C, int ldc, int M, int N) {
@@ -593,7 +624,8 @@ static int gemm_stages(int grid, int nk_slice) {
 }
 
 template <bool TA, bool TB>
-static hipError_t launch_gemm2(const dct::GemmArgs& g, hipStream_t st) {
+static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
+  g.split_probe = getenv("DCT_GEMM_SPLIT_PROBE") != nullptr;
   hipError_t e;
   const int tiles_n = (g.N + dct::GBN - 1) / dct::GBN;
   const int tiles = ((g.M + dct::GBM - 1) / dct::GBM) * tiles_n;
@@ -670,6 +702,63 @@ extern "C" int dct_gemm_bf16_ex(const uint16_t* A, const uint16_t* B, void* C, c
   // generic path: the A rows' sums by the column-sum kernel (op(A) = A^T when trans_a: A is [K][M])
   if (trans_a) return dct_bias_act_bwd(A, nullptr, nullptr, colsum, K, M, lda, 0, 1, stream);
   return (int)hipErrorNotSupported;
+}
+
+// Grouped dW: C_i (+)= dZ_i^T X_i (+ colsum_i += column sums of dZ_i) for i < n (n <= 4), one
+// launch.  dZ_i [K][M_i] and X_i [K][N_i] bf16 row-major (K = rows of the batch), C_i fp32 [M_i][N_i].
+// Falls back to one launch per problem when a problem does not fit the grouped split-K kernel.
+extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const uint16_t* const* X, float* const* C,
+                                        const int* M, const int* N, int K, float* const* colsum, int accumulate,
+                                        void* stream) {
+  if (n <= 0 || n > dct::DW_GROUP || K <= 0) return n == 0 ? 0 : (int)hipErrorInvalidValue;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  dct::GemmGroup gg{};
+  gg.n = n;
+  bool grouped = getenv("DCT_GEMM_NO_GROUP") == nullptr;
+  int total = 0, max_slice = 1;
+  for (int i = 0; i < n; ++i) {
+    dct::GemmArgs& g = gg.g[i];
+    g.A = dZ[i]; g.B = X[i]; g.C = C[i]; g.bias = nullptr; g.aux = nullptr;
+    g.M = M[i]; g.N = N[i]; g.K = K; g.lda = M[i]; g.ldb = N[i]; g.ldc = N[i];
+    g.epilogue = dct::EPI_NONE; g.out_f32 = 1; g.accumulate = accumulate; g.alpha = 1.0f;
+    g.vec_a = ((((uintptr_t)dZ[i]) & 15) == 0) && (M[i] % 8 == 0);
+    g.vec_b = ((((uintptr_t)X[i]) & 15) == 0) && (N[i] % 8 == 0);
+    g.colsum = colsum ? colsum[i] : nullptr;
+    g.residual = nullptr;
+    g.split_probe = 0;
+    const int tiles = ((g.M + dct::GBM - 1) / dct::GBM) * ((g.N + dct::GBN - 1) / dct::GBN);
+    const int nk = g.K / dct::GBK;
+    if (!gemm_v2_ok(g, 1, 0) || tiles >= 256 || nk < 8) { grouped = false; break; }
+    int splits = std::min(nk / 8, (device_cus() + tiles - 1) / tiles);
+    if (splits < 1) splits = 1;
+    gg.splits[i] = splits;
+    gg.start[i] = total;
+    total += tiles * splits;
+    max_slice = std::max(max_slice, (nk + splits - 1) / splits);
+  }
+  if (!grouped) {
+    for (int i = 0; i < n; ++i) {
+      const int e = dct_gemm_bf16_ex(dZ[i], X[i], C[i], nullptr, M[i], N[i], K, M[i], N[i], N[i], 1, 0, dct::EPI_NONE, 1,
+                                     accumulate, nullptr, colsum ? colsum[i] : nullptr, stream);
+      if (e) return e;
+    }
+    return 0;
+  }
+  gg.start[n] = total;
+  hipError_t e;
+  if (!accumulate) {
+    for (int i = 0; i < n; ++i) {
+      const int64_t tot = (int64_t)M[i] * N[i];
+      hipLaunchKernelGGL(dct::zero_panel_kernel, dim3((int)std::min<int64_t>(2048, (tot + 255) / 256)), dim3(256), 0,
+                         st, C[i], N[i], M[i], N[i]);
+    }
+  }
+  const size_t lds = (size_t)(max_slice > 1 ? 4 : 2) * dct::G2_BYTES;
+  auto fn = dct::gemm2_grouped_kernel<true, false, 2>;
+  e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(fn, dim3(total), dim3(dct::GNT), lds, st, gg);
+  return (int)hipGetLastError();
 }
 
 extern "C" int dct_gemm_bf16_residual(const uint16_t* A, const uint16_t* W, float* C, const float* bias,

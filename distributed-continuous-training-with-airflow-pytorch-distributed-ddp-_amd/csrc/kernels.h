@@ -22,6 +22,7 @@ struct GemmArgs {
   float alpha;
   float* colsum;  // optional: colsum[m] += sum_k op(A)[m][k] (the bias gradient of a dW GEMM)
   const float* residual;  // optional (fp32 out): C = residual + op(A) op(B) + bias, ld = ldc
+  int split_probe;        // debug timing probe: split-K slices plain-store (wrong result) instead of atomics
 };
 
 }  // namespace dct
@@ -80,5 +81,7 @@ int dct_tt_embed_fwd(const float* x, const float* E, const float* c, float* h, i
 int dct_tt_embed_bwd(const float* x, const float* dh, float* dE, float* dc, int B, int F, int Dm, void* stream);
 int dct_tt_head_fwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C, float eps, void* stream);
 int dct_tt_head_bwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C, float eps, void* stream);
+int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const uint16_t* const* X, float* const* C,
+                             const int* M, const int* N, int K, float* const* colsum, int accumulate, void* stream);
 int dct_gather_rows(const void* src, const int* idx, void* dst, int64_t n_rows, int row_bytes, void* stream);
 }

@@ -149,6 +149,24 @@ def _dw_gemm(nat, dz16, x16, w, b, st):
     return None if dw_direct else dw, None if db_direct else db
 
 
+def _dw_gemm_grouped(nat, items, st):
+    """Several dW (+)= dZ^T X products over the same rows (bias grads fused) in ONE launch
+    (csrc/gemm_bf16.hip dct_gemm_bf16_dw_grouped); returns [(dw, db)] with None for direct grads."""
+    rows = items[0][0].shape[0]
+    dws, dbs, out = [], [], []
+    for dz16, x16, w, b in items:
+        assert dz16.shape[0] == rows and x16.shape[0] == rows
+        dw, dw_direct = _grad_dst(w, zero=True)  # zeroed when not direct: the launch accumulates
+        db, db_direct = _grad_dst(b, zero=True)
+        dws.append(dw)
+        dbs.append(db)
+        out.append((None if dw_direct else dw, None if db_direct else db))
+    nat.gemm_bf16_dw_grouped([it[0].data_ptr() for it in items], [it[1].data_ptr() for it in items],
+                             [d.data_ptr() for d in dws], [it[0].shape[1] for it in items],
+                             [it[1].shape[1] for it in items], rows, [d.data_ptr() for d in dbs], 1, st)
+    return out
+
+
 def _mm(nat, a16, b16, M, N, K, st, epi=0, aux=None, out=None):
     """C[M, N] = A[M, K] B[K, N] (bf16 out) with an optional elementwise backward epilogue."""
     c = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=a16.device)
@@ -538,10 +556,8 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
             dpre, dh1_16, dqkv, dh, dh16] + [g for g, _ in lg]
     nat.tt_block_bwd([t.data_ptr() for t in ptrs], B, T, dm, H, FF, scale, st)
     dout16 = _bf16_of(dout)
-    dw2, db2 = _dw_gemm(nat, dout16, f, w2, b2, st)
-    dw1, db1 = _dw_gemm(nat, dpre, a2, w1, b1, st)
-    dwo, dbo = _dw_gemm(nat, dh1_16, o, wo, bo, st)
-    dwqkv, dbqkv = _dw_gemm(nat, dqkv, a1, wqkv, bqkv, st)
+    (dw2, db2), (dw1, db1), (dwo, dbo), (dwqkv, dbqkv) = _dw_gemm_grouped(
+        nat, [(dout16, f, w2, b2), (dpre, a2, w1, b1), (dh1_16, o, wo, bo), (dqkv, a1, wqkv, bqkv)], st)
     _remember_bf16(dh, dh16)
     (dl1w, d1), (dl1b, d2), (dl2w, d3), (dl2b, d4) = lg
     return (dh, None if d1 else dl1w, None if d2 else dl1b, dwqkv, dbqkv, dwo, dbo, None if d3 else dl2w,

@@ -729,6 +729,36 @@ def test_tt_embed_and_head_loss_match_fp32_reference(cuda, B, C):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("accumulate", [0, 1])
+@pytest.mark.parametrize("grouped", [True, False])
+def test_gemm_dw_grouped(cuda, accumulate, grouped, monkeypatch):
+    """dct_gemm_bf16_dw_grouped: four dW = dZ^T X products (+ bias column sums) of different shapes
+    in one split-K launch (and the per-problem fallback) vs fp32 torch."""
+    from dct_amd.ops._native import native
+
+    if not grouped:
+        monkeypatch.setenv("DCT_GEMM_NO_GROUP", "1")
+    g = torch.Generator(device="cpu").manual_seed(9)
+    rows = 4096
+    shapes = [(64, 256), (256, 64), (64, 64), (192, 64)]
+    dz = [torch.randn(rows, m, generator=g).to(cuda).to(torch.bfloat16) for m, _ in shapes]
+    xs = [torch.randn(rows, n, generator=g).to(cuda).to(torch.bfloat16) for _, n in shapes]
+    c0 = [torch.randn(m, n, generator=g).to(cuda) for m, n in shapes]
+    cs0 = [torch.randn(m, generator=g).to(cuda) for m, _ in shapes]
+    C = [c.clone() if accumulate else torch.full_like(c, 7.0) for c in c0]
+    CS = [c.clone() for c in cs0]
+    st = torch.cuda.current_stream().cuda_stream
+    native().gemm_bf16_dw_grouped([t.data_ptr() for t in dz], [t.data_ptr() for t in xs], [t.data_ptr() for t in C],
+                                  [m for m, _ in shapes], [n for _, n in shapes], rows, [t.data_ptr() for t in CS],
+                                  accumulate, st)
+    torch.cuda.synchronize()
+    for i in range(4):
+        ref = dz[i].float().t() @ xs[i].float() + (c0[i] if accumulate else 0)
+        assert (C[i] - ref).norm() / ref.norm() < 1e-3, i
+        assert torch.allclose(CS[i], cs0[i] + dz[i].float().sum(0), rtol=1e-3, atol=1e-2), i
+
+
+@pytest.mark.gpu
 def test_skinny_head_linear_and_shadow_weights(cuda):
     """ops.nn.linear with N <= 8 takes the skinny kernels; under bound_params a registered bf16
     shadow replaces the weight conversion and gradients accumulate into .grad."""

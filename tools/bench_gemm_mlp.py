@@ -49,17 +49,16 @@ VARIANTS = {
     "s2_splits128": {"DCT_GEMM_STAGES": "2", "DCT_GEMM_SPLITS": "128"},
     "s4_splits128": {"DCT_GEMM_STAGES": "4", "DCT_GEMM_SPLITS": "128"},
 }
-ENV_KEYS = ("DCT_GEMM_STAGES", "DCT_GEMM_SPLIT_WG", "DCT_GEMM_SPLITS", "DCT_GEMM_SPLIT_LDS")
+ENV_KEYS = ("DCT_GEMM_STAGES", "DCT_GEMM_SPLIT_WG", "DCT_GEMM_SPLITS", "DCT_GEMM_SPLIT_PROBE")
 if os.environ.get("AB_SET") == "dw":  # split-K sweep on the transformer dW shapes only
     SHAPES = [s for s in SHAPES if s[0].startswith("tt_dw") or s[0] == "dw_l1"]
     VARIANTS = {f"{st}_sp{sp}": {"DCT_GEMM_STAGES": st[1], "DCT_GEMM_SPLITS": str(sp)}
                 for st in ("s2", "s4") for sp in (8, 16, 32, 64)}
 
-if os.environ.get("AB_SET") == "lds":  # split-K epilogue: natural-layout atomics vs LDS-restaged rows
+if os.environ.get("AB_SET") == "probe":  # split-K: atomics vs plain stores (timing probe, wrong results)
     SHAPES = [s for s in SHAPES if s[0].startswith(("tt_dw", "dw_"))]
-    VARIANTS = {"nat_default": {"DCT_GEMM_SPLIT_LDS": "0"}, "lds_default": {"DCT_GEMM_SPLIT_LDS": "1"}}
-    VARIANTS.update({f"{e}_sp{sp}": {"DCT_GEMM_SPLIT_LDS": "1" if e == "lds" else "0", "DCT_GEMM_SPLITS": str(sp)}
-                     for e in ("nat", "lds") for sp in (16, 32, 64, 128)})
+    VARIANTS = {f"{e}_sp{sp}": ({"DCT_GEMM_SPLIT_PROBE": "1"} if e == "plain" else {}) | {"DCT_GEMM_SPLITS": str(sp)}
+                for e in ("atom", "plain") for sp in (4, 16, 64, 128, 256, 512)}
 
 
 def main():
