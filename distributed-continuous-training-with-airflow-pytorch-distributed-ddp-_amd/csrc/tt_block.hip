@@ -26,6 +26,10 @@
 namespace dct {
 namespace ttb {
 
+// phase timestamps for tools/debug/tt_phase_prof.py (a.prof == nullptr in production)
+#define TT_MARK(k) \
+  if (a.prof && threadIdx.x == 0) a.prof[(size_t)blockIdx.x * 16 + (k)] = wall_clock64()
+
 constexpr int T = 64, DM = 64, NH = 4, DH = 16, FF = 256;
 constexpr int HS_LD = DM + 4;       // fp32 residual rows (272 B)
 constexpr int AS_LD = DM + 8;       // bf16 LN output / attention output rows (144 B)
@@ -78,6 +82,7 @@ struct Args {
   uint16_t* f; uint16_t* pre;
   float* out;
   uint16_t* wT;  // transposed bf16 weights for the backward: W2^T | W1^T | Wo^T | Wqkv^T
+  uint64_t* prof;  // optional phase timestamps (wall clock), 16 per workgroup
   int B;
   float eps, scale;
 };
@@ -180,9 +185,11 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int c = lane & 15, g = lane >> 4;
 
+  TT_MARK(0);
   // ---- P1: LN1 (rows of this wave)
   layer_norm_rows(a.h, true, HS, AS, a.ln1_w, a.ln1_b, a.mean1, a.rstd1, row0, a.eps);
   __syncthreads();
+  TT_MARK(1);
 
   // ---- P2: a1 out; QKV = a1 Wqkv^T + bqkv for head wv (Q, K, V column tiles wv, 4+wv, 8+wv)
   store_tile<DM * 2, AS_LD * 2>(a.a1 + (size_t)row0 * DM, AS);
@@ -217,6 +224,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
   }
   __syncthreads();
 
+  TT_MARK(2);
   // ---- P3: qkv out; attention of head wv over the 64 tokens (S^T = K Q^T; P V)
   store_tile<3 * DM * 2, QKV_LD * 2>(a.qkv + (size_t)row0 * 3 * DM, RS);
   {
@@ -281,6 +289,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
   }
   __syncthreads();
 
+  TT_MARK(3);
   // ---- P4: o out; h1 = h + o Wo^T + bo (rows of this wave); LN2 of the same rows
   store_tile<DM * 2, AS_LD * 2>(a.o + (size_t)row0 * DM, OS);
   {
@@ -305,6 +314,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
   layer_norm_rows(nullptr, false, HS, AS, a.ln2_w, a.ln2_b, a.mean2, a.rstd2, row0, a.eps);
   __syncthreads();
 
+  TT_MARK(4);
   // ---- P5: h1, a2 out; F = gelu(a2 W1^T + b1) (rows of this wave), pre-activation out
   store_tile<DM * 4, HS_LD * 4>(a.h1 + (size_t)row0 * DM, HS);
   store_tile<DM * 2, AS_LD * 2>(a.a2 + (size_t)row0 * DM, AS);
@@ -334,6 +344,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
   }
   __syncthreads();
 
+  TT_MARK(5);
   // ---- P6: f out; out = h1 + F W2^T + b2 (rows of this wave)
   store_tile<FF * 2, F_LD * 2>(a.f + (size_t)row0 * FF, RS);
   {
@@ -356,8 +367,10 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
     }
   }
   __syncthreads();
+  TT_MARK(6);
   store_tile<DM * 4, HS_LD * 4>(a.out + (size_t)row0 * DM, HS);
   transpose_weights(a);
+  TT_MARK(7);
 }
 
 // ============================================================================ backward
@@ -382,6 +395,7 @@ struct BwdArgs {
   const uint16_t* wT;
   uint16_t* dpre; uint16_t* dh1_16; uint16_t* dqkv; float* dh; uint16_t* dh16;
   float *dln1_w, *dln1_b, *dln2_w, *dln2_b;
+  uint64_t* prof;
   float scale;
 };
 
@@ -475,6 +489,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
   const uint16_t* WoT = a.wT + WT_WO;
   const uint16_t* WqT = a.wT + WT_QKV;
 
+  TT_MARK(0);
   // ---- P0: pre -> R (whole tile); dout rows -> G (fp32) and X (bf16); zero the LN partials
   load_tile<FF * 2, F_LD * 2>(R, a.pre + (size_t)row0 * FF);
   red[threadIdx.x] = 0.f;
@@ -489,6 +504,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
     }
   __syncthreads();
 
+  TT_MARK(1);
   // ---- P1: dpre = (bf16(dout) W2) * gelu'(pre), own rows, in place over pre in R
   {
     f32x4 acc[FF / 16];
@@ -511,6 +527,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
   }
   store_rows16<FF * 2, F_LD * 2>(a.dpre + (size_t)row0 * FF, R, wv, lane);
 
+  TT_MARK(2);
   // ---- P2/P3: da2 = dpre W1 (own rows); dh1 = dout + LN2_bwd(da2) into G
   {
     f32x4 acc[4];
@@ -535,6 +552,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
     }
   store_rows16<DM * 2, XB_LD * 2>(a.dh1_16 + (size_t)row0 * DM, X, wv, lane);
 
+  TT_MARK(3);
   // ---- P4: do = bf16(dh1) Wo (own rows) -> dOs
   {
     f32x4 acc[4];
@@ -554,11 +572,13 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
   }
   __syncthreads();  // every wave is done with R (dpre) and has written its dO rows
 
+  TT_MARK(4);
   // ---- P5: qkv -> R, o -> Os
   load_tile<3 * DM * 2, QKV_LD * 2>(R, a.qkv + (size_t)row0 * 3 * DM);
   load_tile<DM * 2, XB_LD * 2>(Os, a.o + (size_t)row0 * DM);
   __syncthreads();
 
+  TT_MARK(5);
   // ---- P6: attention backward of head wv; dq, dk, dv overwrite q, k, v of the head in R
   {
     uint16_t* Qh = R + DH * wv;
@@ -682,6 +702,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
   }
   __syncthreads();
 
+  TT_MARK(6);
   // ---- P7: dqkv out; da1 = dqkv Wqkv (own rows); dh = dh1 + LN1_bwd(da1) into G
   store_tile<3 * DM * 2, QKV_LD * 2>(a.dqkv + (size_t)row0 * 3 * DM, R);
   {
@@ -698,6 +719,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
     }
     ln_bwd_c(acc, a.h, a.mean1, a.rstd1, a.ln1_w, G, red, red + DM, row0, wv, c, g);
   }
+  TT_MARK(7);
   // dh (fp32) and its bf16 copy, own rows (X is free: its last reader was P4 of this wave)
 #pragma unroll
   for (int t = 0; t < 4; ++t)
@@ -713,6 +735,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
     float* dsts[4] = {a.dln1_w, a.dln1_b, a.dln2_w, a.dln2_b};
     atomicAdd(dsts[threadIdx.x >> 6] + (threadIdx.x & 63), red[threadIdx.x]);
   }
+  TT_MARK(8);
 }
 
 }  // namespace ttb
@@ -725,10 +748,10 @@ extern "C" {
 int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps, float scale,
                      void* stream) {
   using namespace dct::ttb;
-  if (n_ptrs != 27 || T != dct::ttb::T || DM != dct::ttb::DM || H != NH || FF != dct::ttb::FF || Bsz <= 0)
+  if ((n_ptrs != 27 && n_ptrs != 28) || T != dct::ttb::T || DM != dct::ttb::DM || H != NH || FF != dct::ttb::FF || Bsz <= 0)
     return (int)hipErrorInvalidValue;
   uintptr_t any = 0;
-  for (int i = 0; i < n_ptrs; ++i) {
+  for (int i = 0; i < 27; ++i) {
     if (!p[i]) return (int)hipErrorInvalidValue;
     any |= p[i];
   }
@@ -744,6 +767,7 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
   a.qkv = (uint16_t*)p[16]; a.o = (uint16_t*)p[17]; a.lse = (float*)p[18];
   a.h1 = (float*)p[19]; a.a2 = (uint16_t*)p[20]; a.mean2 = (float*)p[21]; a.rstd2 = (float*)p[22];
   a.f = (uint16_t*)p[23]; a.pre = (uint16_t*)p[24]; a.out = (float*)p[25]; a.wT = (uint16_t*)p[26];
+  a.prof = n_ptrs == 28 ? (uint64_t*)p[27] : nullptr;
   a.B = Bsz; a.eps = eps; a.scale = scale;
   static bool attr = false;
   if (!attr) {
@@ -761,10 +785,10 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
 int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
                      void* stream) {
   using namespace dct::ttb;
-  if (n_ptrs != 23 || T != dct::ttb::T || DM != dct::ttb::DM || H != NH || FF != dct::ttb::FF || Bsz <= 0)
+  if ((n_ptrs != 23 && n_ptrs != 24) || T != dct::ttb::T || DM != dct::ttb::DM || H != NH || FF != dct::ttb::FF || Bsz <= 0)
     return (int)hipErrorInvalidValue;
   uintptr_t any = 0;
-  for (int i = 0; i < n_ptrs; ++i) {
+  for (int i = 0; i < 23; ++i) {
     if (!p[i]) return (int)hipErrorInvalidValue;
     if (i < 19) any |= p[i];
   }
@@ -777,6 +801,7 @@ int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
   a.dpre = (uint16_t*)p[14]; a.dh1_16 = (uint16_t*)p[15]; a.dqkv = (uint16_t*)p[16]; a.dh = (float*)p[17];
   a.dh16 = (uint16_t*)p[18];
   a.dln1_w = (float*)p[19]; a.dln1_b = (float*)p[20]; a.dln2_w = (float*)p[21]; a.dln2_b = (float*)p[22];
+  a.prof = n_ptrs == 24 ? (uint64_t*)p[23] : nullptr;
   a.scale = scale;
   static bool attr = false;
   if (!attr) {

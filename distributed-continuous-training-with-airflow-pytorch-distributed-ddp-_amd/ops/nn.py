@@ -510,6 +510,8 @@ class _TTBlockFn(torch.autograd.Function):
         ptrs = [h, vecs[0], vecs[1], wqkvb, vecs[2], wob, vecs[3], vecs[4], vecs[5], w1b, vecs[6], w2b, vecs[7],
                 a1, st4[0], st4[1], qkv, o, lse, h1, a2, st4[2], st4[3], f, pre, out, wT]
         scale = 1.0 / math.sqrt(dm // H)
+        if _TT_PROF is not None:  # tools/debug/tt_phase_prof.py
+            ptrs.append(_tt_prof_buf("fwd", B, dev))
         nat.tt_block_fwd([t.data_ptr() for t in ptrs], B, T, dm, H, FF, float(eps), scale, st)
         ctx.save_for_backward(h, st4, a1, wqkvb, qkv, o, lse, wob, h1, a2, w1b, w2b, f, pre, wT, vecs[0], vecs[4])
         ctx.params = (ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2)
@@ -532,6 +534,13 @@ class _TTBlockFn(torch.autograd.Function):
 
 
 _TT_FUSED_BWD = True
+_TT_PROF = None  # {"fwd": [...], "bwd": [...]} of per-workgroup phase timestamp buffers when profiling
+
+
+def _tt_prof_buf(kind: str, B: int, dev) -> torch.Tensor:
+    buf = torch.zeros(B * 16, dtype=torch.int64, device=dev)
+    _TT_PROF.setdefault(kind, []).append(buf)
+    return buf
 
 
 def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, params, B, H, T, scale):
@@ -554,6 +563,8 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
     lg = [_grad_dst(t, zero=True) for t in (ln1_w, ln1_b, ln2_w, ln2_b)]
     ptrs = [dout, h, st4[0], st4[1], ln1w, qkv, o, lse, h1, st4[2], st4[3], ln2w, pre, wT,
             dpre, dh1_16, dqkv, dh, dh16] + [g for g, _ in lg]
+    if _TT_PROF is not None:
+        ptrs.append(_tt_prof_buf("bwd", B, dev))
     nat.tt_block_bwd([t.data_ptr() for t in ptrs], B, T, dm, H, FF, scale, st)
     dout16 = _bf16_of(dout)
     (dw2, db2), (dw1, db1), (dwo, dbo), (dwqkv, dbqkv) = _dw_gemm_grouped(
