@@ -292,79 +292,91 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
   TT_MARK(3);
   // ---- P4: o out; h1 = h + o Wo^T + bo (rows of this wave); LN2 of the same rows
   store_tile<DM * 2, AS_LD * 2>(a.o + (size_t)row0 * DM, OS);
-  {
+  // Row-parallel GEMMs split by COLUMNS across the waves (wave wv: column tile(s) wv for all 64
+  // rows): each wave then streams only its quarter of the weight from L2 - the row split had
+  // every wave fetch the whole matrix (4x the L2 traffic; fc1 was 10 us of a 30 us block).
+  {  // proj: column tile wv
     f32x4 acc[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < DM / 32; ++ks) {
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(OS + (16 * wv + c) * AS_LD + 32 * ks + 8 * g);
+      const bf16x8 bw = *reinterpret_cast<const bf16x8*>(a.wo + (size_t)(16 * wv + c) * DM + 32 * ks + 8 * g);
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        acc[t] = mfma32(af, *reinterpret_cast<const bf16x8*>(a.wo + (size_t)(16 * t + c) * DM + 32 * ks + 8 * g), acc[t]);
+      for (int i = 0; i < 4; ++i)
+        acc[i] = mfma32(*reinterpret_cast<const bf16x8*>(OS + (16 * i + c) * AS_LD + 32 * ks + 8 * g), bw, acc[i]);
     }
+    const int col = 16 * wv + c;
+    const float bv = a.bo[col];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int col = 16 * t + c;
-      const float bv = a.bo[col];
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) HS[(16 * wv + 4 * g + r) * HS_LD + col] += acc[t][r] + bv;
-    }
+      for (int r = 0; r < 4; ++r) HS[(16 * i + 4 * g + r) * HS_LD + col] += acc[i][r] + bv;
   }
+  __syncthreads();  // LN2 rows need every wave's columns
   layer_norm_rows(nullptr, false, HS, AS, a.ln2_w, a.ln2_b, a.mean2, a.rstd2, row0, a.eps);
   __syncthreads();
 
   TT_MARK(4);
-  // ---- P5: h1, a2 out; F = gelu(a2 W1^T + b1) (rows of this wave), pre-activation out
+  // ---- P5: h1, a2 out; F = gelu(a2 W1^T + b1) for columns 64wv..64wv+63, pre-activation out
   store_tile<DM * 4, HS_LD * 4>(a.h1 + (size_t)row0 * DM, HS);
   store_tile<DM * 2, AS_LD * 2>(a.a2 + (size_t)row0 * DM, AS);
   {
-    f32x4 acc[FF / 16];
+    f32x4 acc[4][4];  // [row tile][column tile of this wave]
 #pragma unroll
-    for (int t = 0; t < FF / 16; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[i][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < DM / 32; ++ks) {
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(AS + (16 * wv + c) * AS_LD + 32 * ks + 8 * g);
+      bf16x8 af[4], bw[4];
 #pragma unroll
-      for (int t = 0; t < FF / 16; ++t)
-        acc[t] = mfma32(af, *reinterpret_cast<const bf16x8*>(a.w1 + (size_t)(16 * t + c) * DM + 32 * ks + 8 * g), acc[t]);
+      for (int t = 0; t < 4; ++t)
+        bw[t] = *reinterpret_cast<const bf16x8*>(a.w1 + (size_t)(64 * wv + 16 * t + c) * DM + 32 * ks + 8 * g);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(AS + (16 * i + c) * AS_LD + 32 * ks + 8 * g);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[i][t] = mfma32(af[i], bw[t], acc[i][t]);
     }
-    uint16_t* pre = a.pre + (size_t)(row0 + 16 * wv + 4 * g) * FF;
 #pragma unroll
-    for (int t = 0; t < FF / 16; ++t) {
-      const int col = 16 * t + c;
+    for (int t = 0; t < 4; ++t) {
+      const int col = 64 * wv + 16 * t + c;
       const float bv = a.b1[col];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float z = acc[t][r] + bv;
-        pre[r * FF + col] = f32_to_bf16(z);
-        RS[(16 * wv + 4 * g + r) * F_LD + col] = f32_to_bf16(gelu_f(z));
-      }
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * i + 4 * g + r;
+          const float z = acc[i][t][r] + bv;
+          a.pre[(size_t)(row0 + row) * FF + col] = f32_to_bf16(z);
+          RS[row * F_LD + col] = f32_to_bf16(gelu_f(z));
+        }
     }
   }
   __syncthreads();
 
   TT_MARK(5);
-  // ---- P6: f out; out = h1 + F W2^T + b2 (rows of this wave)
+  // ---- P6: f out; out = h1 + F W2^T + b2 for column tile wv
   store_tile<FF * 2, F_LD * 2>(a.f + (size_t)row0 * FF, RS);
   {
     f32x4 acc[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < FF / 32; ++ks) {
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(RS + (16 * wv + c) * F_LD + 32 * ks + 8 * g);
+      const bf16x8 bw = *reinterpret_cast<const bf16x8*>(a.w2 + (size_t)(16 * wv + c) * FF + 32 * ks + 8 * g);
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        acc[t] = mfma32(af, *reinterpret_cast<const bf16x8*>(a.w2 + (size_t)(16 * t + c) * FF + 32 * ks + 8 * g), acc[t]);
+      for (int i = 0; i < 4; ++i)
+        acc[i] = mfma32(*reinterpret_cast<const bf16x8*>(RS + (16 * i + c) * F_LD + 32 * ks + 8 * g), bw, acc[i]);
     }
+    const int col = 16 * wv + c;
+    const float bv = a.b2[col];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int col = 16 * t + c;
-      const float bv = a.b2[col];
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) HS[(16 * wv + 4 * g + r) * HS_LD + col] += acc[t][r] + bv;
-    }
+      for (int r = 0; r < 4; ++r) HS[(16 * i + 4 * g + r) * HS_LD + col] += acc[i][r] + bv;
   }
   __syncthreads();
   TT_MARK(6);
