@@ -445,43 +445,70 @@ __device__ __forceinline__ void load_tile(void* s, const void* gsrc) {
   }
 }
 
-// LayerNorm backward on the C layout of the wave's 16 rows: lane (c, g) holds da[t][r] for row
-// 16w + 4g + r, column 16t + c.  dres / result live in G (fp32, same positions).
-// dx = rstd (gw - mean(gw) - xhat mean(gw xhat)) + dres, gw = da * w.
-__device__ __forceinline__ void ln_bwd_c(const f32x4 (&da)[4], const float* x, const float* mean, const float* rstd,
-                                         const float* w, float* G, float* red_w, float* red_b, int row0, int wv,
-                                         int c, int g) {
-  float cw[4], cb[4];
+// LayerNorm backward of the wave's 16 rows in row layout (lane -> row 16w + (lane&15), columns
+// 16g..16g+15): da from the fp32 scratch tile S (the column-split dX GEMM wrote it), x from global,
+// dres / result in G.  dx = rstd (gw - mean(gw) - xhat mean(gw xhat)) + dres, gw = da * w;
+// weight / bias partial column sums reduced over the wave's rows, then LDS atomics into red.
+__device__ __forceinline__ void ln_bwd_rows(const float* S, const float* x, const float* mean, const float* rstd,
+                                            const float* w, float* G, float* red_w, float* red_b, int row0, int wv,
+                                            int lane) {
+  const int rl = 16 * wv + (lane & 15), g = lane >> 4;
+  const float mu = mean[row0 + rl], rs = rstd[row0 + rl];
+  float da[16], xh[16], gw[16], s1 = 0.f, s2 = 0.f;
+  const float4* xp = reinterpret_cast<const float4*>(x + (size_t)(row0 + rl) * DM + 16 * g);
+  const float4* sp = reinterpret_cast<const float4*>(S + rl * HS_LD + 16 * g);
+  const float4* wp = reinterpret_cast<const float4*>(w + 16 * g);
 #pragma unroll
-  for (int t = 0; t < 4; ++t) { cw[t] = 0.f; cb[t] = 0.f; }
+  for (int q = 0; q < 4; ++q) {
+    const float4 xv = xp[q], dv = sp[q], ww = wp[q];
+    const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ds[4] = {dv.x, dv.y, dv.z, dv.w}, ws[4] = {ww.x, ww.y, ww.z, ww.w};
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int rl = 16 * wv + 4 * g + r;
-    const float mu = mean[row0 + rl], rs = rstd[row0 + rl];
-    float xh[4], gw[4], s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int col = 16 * t + c;
-      xh[t] = (x[(size_t)(row0 + rl) * DM + col] - mu) * rs;
-      gw[t] = da[t][r] * w[col];
-      s1 += gw[t];
-      s2 += gw[t] * xh[t];
-      cw[t] += da[t][r] * xh[t];
-      cb[t] += da[t][r];
-    }
-    s1 = rowsum16(s1) * (1.f / DM);
-    s2 = rowsum16(s2) * (1.f / DM);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) G[rl * HS_LD + 16 * t + c] += rs * (gw[t] - s1 - xh[t] * s2);
-  }
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const float vw = sum4g(cw[t]), vb = sum4g(cb[t]);
-    if (g == 0) {
-      atomicAdd(red_w + 16 * t + c, vw);
-      atomicAdd(red_b + 16 * t + c, vb);
+    for (int e = 0; e < 4; ++e) {
+      const int k = 4 * q + e;
+      da[k] = ds[e];
+      xh[k] = (xs[e] - mu) * rs;
+      gw[k] = ds[e] * ws[e];
+      s1 += gw[k];
+      s2 += gw[k] * xh[k];
     }
   }
+  s1 = sum4g(s1) * (1.f / DM);
+  s2 = sum4g(s2) * (1.f / DM);
+  float4* gp = reinterpret_cast<float4*>(G + rl * HS_LD + 16 * g);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float4 v = gp[q];
+    v.x += rs * (gw[4 * q] - s1 - xh[4 * q] * s2);
+    v.y += rs * (gw[4 * q + 1] - s1 - xh[4 * q + 1] * s2);
+    v.z += rs * (gw[4 * q + 2] - s1 - xh[4 * q + 2] * s2);
+    v.w += rs * (gw[4 * q + 3] - s1 - xh[4 * q + 3] * s2);
+    gp[q] = v;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const float vw = rowsum16(da[k] * xh[k]), vb = rowsum16(da[k]);
+    if ((lane & 15) == 0) {
+      atomicAdd(red_w + 16 * g + k, vw);
+      atomicAdd(red_b + 16 * g + k, vb);
+    }
+  }
+}
+
+// G own rows (row layout) -> bf16 X own rows
+__device__ __forceinline__ void rows_to_bf16(const float* G, uint16_t* X, int wv, int lane) {
+  const int rl = 16 * wv + (lane & 15), g = lane >> 4;
+  const float4* gp = reinterpret_cast<const float4*>(G + rl * HS_LD + 16 * g);
+  bf16x8 o[2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 v = gp[q];
+    o[q >> 1][4 * (q & 1)] = (short)f32_to_bf16(v.x);
+    o[q >> 1][4 * (q & 1) + 1] = (short)f32_to_bf16(v.y);
+    o[q >> 1][4 * (q & 1) + 2] = (short)f32_to_bf16(v.z);
+    o[q >> 1][4 * (q & 1) + 3] = (short)f32_to_bf16(v.w);
+  }
+  *reinterpret_cast<bf16x8*>(X + rl * XB_LD + 16 * g) = o[0];
+  *reinterpret_cast<bf16x8*>(X + rl * XB_LD + 16 * g + 8) = o[1];
 }
 
 __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
@@ -491,6 +518,8 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
   uint16_t* R = reinterpret_cast<uint16_t*>(smem + G_BYTES + X_BYTES);
   uint16_t* Os = reinterpret_cast<uint16_t*>(smem + G_BYTES + X_BYTES + R_BYTES);
   uint16_t* dOs = Os + T * XB_LD;
+  float* S = reinterpret_cast<float*>(Os);  // fp32 [T][HS_LD] scratch over Os + dOs (free outside P4-P6)
+  static_assert(T * HS_LD * 4 <= 2 * X_BYTES, "scratch must fit in Os + dOs");
   float* red = reinterpret_cast<float*>(smem + G_BYTES + 3 * X_BYTES + R_BYTES);  // [4][DM]
   float* sdl = red + 4 * DM;                                                       // [NH][T]
   const int bidx = blockIdx.x, row0 = bidx * T;
@@ -517,72 +546,90 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
   __syncthreads();
 
   TT_MARK(1);
-  // ---- P1: dpre = (bf16(dout) W2) * gelu'(pre), own rows, in place over pre in R
+  // ---- P1: dpre = (bf16(dout) W2) * gelu'(pre) for columns 64wv..64wv+63 (all rows), in place over
+  // pre in R.  The dX products are split by COLUMNS across the waves, so each wave streams a
+  // quarter of the transposed weight from L2 (a row split fetches all of it per wave).
   {
-    f32x4 acc[FF / 16];
+    f32x4 acc[4][4];  // [row tile][column tile of this wave]
 #pragma unroll
-    for (int t = 0; t < FF / 16; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[i][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < DM / 32; ++ks) {
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(X + (16 * wv + c) * XB_LD + 32 * ks + 8 * g);
+      bf16x8 af[4], bw[4];
 #pragma unroll
-      for (int t = 0; t < FF / 16; ++t)
-        acc[t] = mfma32(af, *reinterpret_cast<const bf16x8*>(W2T + (size_t)(16 * t + c) * DM + 32 * ks + 8 * g), acc[t]);
+      for (int t = 0; t < 4; ++t)
+        bw[t] = *reinterpret_cast<const bf16x8*>(W2T + (size_t)(64 * wv + 16 * t + c) * DM + 32 * ks + 8 * g);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(X + (16 * i + c) * XB_LD + 32 * ks + 8 * g);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[i][t] = mfma32(af[i], bw[t], acc[i][t]);
     }
 #pragma unroll
-    for (int t = 0; t < FF / 16; ++t)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        uint16_t* pp = R + (16 * wv + 4 * g + r) * F_LD + 16 * t + c;
-        *pp = f32_to_bf16(acc[t][r] * gelu_grad_f(bf16_to_f32(*pp)));
-      }
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          uint16_t* pp = R + (16 * i + 4 * g + r) * F_LD + 64 * wv + 16 * t + c;
+          *pp = f32_to_bf16(acc[i][t][r] * gelu_grad_f(bf16_to_f32(*pp)));
+        }
+    // dpre out: this wave's 64-column block of all 64 rows (128 B per row, 16-byte chunks)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int idx = q * 64 + lane, rr = idx >> 3, cc = idx & 7;
+      *reinterpret_cast<uint4*>(a.dpre + (size_t)(row0 + rr) * FF + 64 * wv + cc * 8) =
+          *reinterpret_cast<const uint4*>(R + rr * F_LD + 64 * wv + cc * 8);
+    }
   }
-  store_rows16<FF * 2, F_LD * 2>(a.dpre + (size_t)row0 * FF, R, wv, lane);
+  __syncthreads();  // da2 reads every wave's dpre columns
 
   TT_MARK(2);
-  // ---- P2/P3: da2 = dpre W1 (own rows); dh1 = dout + LN2_bwd(da2) into G
+  // ---- P2/P3: da2 = dpre W1 (column tile wv, all rows) -> fp32 scratch S; dh1 = dout + LN2_bwd(da2)
   {
     f32x4 acc[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < FF / 32; ++ks) {
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(R + (16 * wv + c) * F_LD + 32 * ks + 8 * g);
+      const bf16x8 bw = *reinterpret_cast<const bf16x8*>(W1T + (size_t)(16 * wv + c) * FF + 32 * ks + 8 * g);
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        acc[t] = mfma32(af, *reinterpret_cast<const bf16x8*>(W1T + (size_t)(16 * t + c) * FF + 32 * ks + 8 * g), acc[t]);
+      for (int i = 0; i < 4; ++i)
+        acc[i] = mfma32(*reinterpret_cast<const bf16x8*>(R + (16 * i + c) * F_LD + 32 * ks + 8 * g), bw, acc[i]);
     }
-    ln_bwd_c(acc, a.h1, a.mean2, a.rstd2, a.ln2_w, G, red + 2 * DM, red + 3 * DM, row0, wv, c, g);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) S[(16 * i + 4 * g + r) * HS_LD + 16 * wv + c] = acc[i][r];
   }
-  // bf16(dh1) -> X (own rows) -> global
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int rl = 16 * wv + 4 * g + r, col = 16 * t + c;
-      X[rl * XB_LD + col] = f32_to_bf16(G[rl * HS_LD + col]);
-    }
+  __syncthreads();
+  ln_bwd_rows(S, a.h1, a.mean2, a.rstd2, a.ln2_w, G, red + 2 * DM, red + 3 * DM, row0, wv, lane);
+  rows_to_bf16(G, X, wv, lane);
   store_rows16<DM * 2, XB_LD * 2>(a.dh1_16 + (size_t)row0 * DM, X, wv, lane);
+  __syncthreads();  // do reads all rows of X; S (over Os / dOs) fully consumed
 
   TT_MARK(3);
-  // ---- P4: do = bf16(dh1) Wo (own rows) -> dOs
+  // ---- P4: do = bf16(dh1) Wo (column tile wv, all rows) -> dOs
   {
     f32x4 acc[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < DM / 32; ++ks) {
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(X + (16 * wv + c) * XB_LD + 32 * ks + 8 * g);
+      const bf16x8 bw = *reinterpret_cast<const bf16x8*>(WoT + (size_t)(16 * wv + c) * DM + 32 * ks + 8 * g);
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        acc[t] = mfma32(af, *reinterpret_cast<const bf16x8*>(WoT + (size_t)(16 * t + c) * DM + 32 * ks + 8 * g), acc[t]);
+      for (int i = 0; i < 4; ++i)
+        acc[i] = mfma32(*reinterpret_cast<const bf16x8*>(X + (16 * i + c) * XB_LD + 32 * ks + 8 * g), bw, acc[i]);
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dOs[(16 * wv + 4 * g + r) * XB_LD + 16 * t + c] = f32_to_bf16(acc[t][r]);
+      for (int r = 0; r < 4; ++r) dOs[(16 * i + 4 * g + r) * XB_LD + 16 * wv + c] = f32_to_bf16(acc[i][r]);
   }
-  __syncthreads();  // every wave is done with R (dpre) and has written its dO rows
+  __syncthreads();  // every wave is done with R (dpre) and has written its dO columns
 
   TT_MARK(4);
   // ---- P5: qkv -> R, o -> Os
@@ -715,31 +762,28 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
   __syncthreads();
 
   TT_MARK(6);
-  // ---- P7: dqkv out; da1 = dqkv Wqkv (own rows); dh = dh1 + LN1_bwd(da1) into G
+  // ---- P7: dqkv out; da1 = dqkv Wqkv (column tile wv, all rows) -> S; dh = dh1 + LN1_bwd(da1)
   store_tile<3 * DM * 2, QKV_LD * 2>(a.dqkv + (size_t)row0 * 3 * DM, R);
   {
     f32x4 acc[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i) acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 3 * DM / 32; ++ks) {
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(R + (16 * wv + c) * QKV_LD + 32 * ks + 8 * g);
+      const bf16x8 bw = *reinterpret_cast<const bf16x8*>(WqT + (size_t)(16 * wv + c) * (3 * DM) + 32 * ks + 8 * g);
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        acc[t] = mfma32(af, *reinterpret_cast<const bf16x8*>(WqT + (size_t)(16 * t + c) * (3 * DM) + 32 * ks + 8 * g),
-                        acc[t]);
+      for (int i = 0; i < 4; ++i)
+        acc[i] = mfma32(*reinterpret_cast<const bf16x8*>(R + (16 * i + c) * QKV_LD + 32 * ks + 8 * g), bw, acc[i]);
     }
-    ln_bwd_c(acc, a.h, a.mean1, a.rstd1, a.ln1_w, G, red, red + DM, row0, wv, c, g);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) S[(16 * i + 4 * g + r) * HS_LD + 16 * wv + c] = acc[i][r];
   }
+  __syncthreads();
   TT_MARK(7);
-  // dh (fp32) and its bf16 copy, own rows (X is free: its last reader was P4 of this wave)
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int rl = 16 * wv + 4 * g + r, col = 16 * t + c;
-      X[rl * XB_LD + col] = f32_to_bf16(G[rl * HS_LD + col]);
-    }
+  ln_bwd_rows(S, a.h, a.mean1, a.rstd1, a.ln1_w, G, red, red + DM, row0, wv, lane);
+  rows_to_bf16(G, X, wv, lane);
   store_rows16<DM * 2, XB_LD * 2>(a.dh16 + (size_t)row0 * DM, X, wv, lane);
   store_rows16<DM * 4, HS_LD * 4>(a.dh + (size_t)row0 * DM, G, wv, lane);
   __syncthreads();

@@ -12,8 +12,8 @@ from dct_amd.ops import nn as nnops  # noqa: E402
 
 FWD = ["LN1", "a1 out + QKV", "qkv out + attention", "o out + proj + LN2", "h1/a2 out + fc1 GELU",
        "f out + fc2", "out store + W^T"]
-BWD = ["pre stage + dout", "dF W2 gelu' + dpre out", "da2 W1 + LN2 bwd + dh1 out", "do Wo + barrier",
-       "qkv/o stage", "attention bwd", "dqkv out + da1 + LN1 bwd", "dh out + LN grads"]
+BWD = ["pre stage + dout", "dF W2 gelu' + dpre out", "da2 W1 + LN2 bwd + dh1 out", "do Wo",
+       "qkv/o stage", "attention bwd", "dqkv out + da1 W", "LN1 bwd + dh out + LN grads"]
 
 
 def report(name, bufs, labels, B):
