@@ -484,14 +484,24 @@ __device__ __forceinline__ void ln_bwd_rows(const float* S, const float* x, cons
     v.w += rs * (gw[4 * q + 3] - s1 - xh[4 * q + 3] * s2);
     gp[q] = v;
   }
+  // column sums over the wave's 16 rows by recursive halving across the 16 lanes of a row group:
+  // 15 shuffles per quantity (not 16 x 4), lane j ends with column 16g + j
+  float vw[16], vb[16];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const float vw = rowsum16(da[k] * xh[k]), vb = rowsum16(da[k]);
-    if ((lane & 15) == 0) {
-      atomicAdd(red_w + 16 * g + k, vw);
-      atomicAdd(red_b + 16 * g + k, vb);
+  for (int k = 0; k < 16; ++k) { vw[k] = da[k] * xh[k]; vb[k] = da[k]; }
+#pragma unroll
+  for (int half = 8; half >= 1; half >>= 1) {
+    const bool hi = (lane & half) != 0;
+#pragma unroll
+    for (int k = 0; k < half; ++k) {
+      const float sw = hi ? vw[k] : vw[k + half], kw = hi ? vw[k + half] : vw[k];
+      const float sb = hi ? vb[k] : vb[k + half], kb = hi ? vb[k + half] : vb[k];
+      vw[k] = kw + __shfl_xor(sw, half);
+      vb[k] = kb + __shfl_xor(sb, half);
     }
   }
+  atomicAdd(red_w + 16 * g + (lane & 15), vw[0]);
+  atomicAdd(red_b + 16 * g + (lane & 15), vb[0]);
 }
 
 // G own rows (row layout) -> bf16 X own rows
