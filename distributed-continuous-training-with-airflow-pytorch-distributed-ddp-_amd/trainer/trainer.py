@@ -307,7 +307,8 @@ class Trainer:
                 if val_metrics:
                     self._log_metrics(val_metrics, self.global_step)
                 extra = {"epoch_time_s": epoch_t, "train_time_s": train_t,
-                         "samples_per_sec": samples / max(train_t, 1e-9)}
+                         "samples_per_sec": samples / max(train_t, 1e-9),
+                         "step_time_ms": 1e3 * train_t / max(n_steps, 1)}
                 self._log_metrics(extra, self.global_step)
                 with trace_range(f"epoch{epoch}/checkpoint"):
                     self._run_checkpoint_callbacks(n_steps)
