@@ -729,7 +729,9 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
     const int tiles = ((g.M + dct::GBM - 1) / dct::GBM) * ((g.N + dct::GBN - 1) / dct::GBN);
     const int nk = g.K / dct::GBK;
     if (!gemm_v2_ok(g, 1, 0) || tiles >= 256 || nk < 8) { grouped = false; break; }
-    int splits = std::min(nk / 8, (device_cus() + tiles - 1) / tiles);
+    int target = device_cus();
+    if (const char* f = getenv("DCT_GEMM_SPLIT_WG")) target = std::max(1, atoi(f));
+    int splits = std::min(nk / 8, (target + tiles - 1) / tiles);
     if (splits < 1) splits = 1;
     gg.splits[i] = splits;
     gg.start[i] = total;
@@ -753,8 +755,9 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
                          st, C[i], N[i], M[i], N[i]);
     }
   }
-  const size_t lds = (size_t)(max_slice > 1 ? 4 : 2) * dct::G2_BYTES;
-  auto fn = dct::gemm2_grouped_kernel<true, false, 2>;
+  const bool s4 = getenv("DCT_GEMM_STAGES") && atoi(getenv("DCT_GEMM_STAGES")) >= 4 && max_slice >= 3;
+  const size_t lds = (size_t)(max_slice > 1 ? (s4 ? 8 : 4) : 2) * dct::G2_BYTES;
+  auto fn = s4 ? dct::gemm2_grouped_kernel<true, false, 4> : dct::gemm2_grouped_kernel<true, false, 2>;
   e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(fn, dim3(total), dim3(dct::GNT), lds, st, gg);
