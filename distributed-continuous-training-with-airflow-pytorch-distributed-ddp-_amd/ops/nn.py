@@ -599,7 +599,8 @@ def tt_block(h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, 
              eps: float = 1e-5):
     """One pre-norm transformer block: h + MHA(LN1 h), then + FFN(LN2 .) - one fused kernel
     forward on MI355X for the benchmark shape, two fused nodes otherwise."""
-    if tt_block_fusable(h, H, T, w1.shape[0]):
+    vecs = (ln1_w, ln1_b, bqkv, bo, ln2_w, ln2_b, b1, b2)  # read with 16-byte vector loads
+    if tt_block_fusable(h, H, T, w1.shape[0]) and all(v.is_contiguous() and v.data_ptr() % 16 == 0 for v in vecs):
         return _TTBlockFn.apply(h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, eps, B, H, T)
     h = prenorm_attention(h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, B, H, T, eps)
     return prenorm_ffn(h, ln2_w, ln2_b, w1, b1, w2, b2, eps)
@@ -690,7 +691,7 @@ class _TTEmbedFn(torch.autograd.Function):
 def tt_embed(x: torch.Tensor, E: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
     """Feature-token embedding [B, F] -> [B*F, D] (native on MI355X for D == 64)."""
     B, F_ = x.shape
-    if x.is_cuda and E.shape[1] == 64:
+    if x.is_cuda and E.shape[1] == 64 and all(t.is_contiguous() and t.data_ptr() % 16 == 0 for t in (E, c)):
         return _TTEmbedFn.apply(x, E, c)
     return (x.float()[:, :, None] * E + c).reshape(B * F_, E.shape[1])
 
