@@ -662,7 +662,12 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
   if constexpr (!TA) {
     // small K and too few 128-row tiles to fill 256 CUs several times over: half-height tiles
     const bool force128 = getenv("DCT_GEMM_BM128") != nullptr;
-    if (splits == 1 && nk <= 4 && tiles < 1024 && !force128)
+    // ... and whenever 128-row tiles would give at most one workgroup per CU (the 4096 x 1024 MLP
+    // layers: 256 tiles): two half-height tiles per CU overlap one's loads with the other's MFMAs,
+    // 16.7 -> 14.5 us fwd / 17.4 -> 15.5 us dX at 4096x1024x1024, ahead of hipBLASLt (17.8 / 17.2;
+    // profiles/gemm_bm64_ab_r1.log)
+    const int bm64_nk = getenv("DCT_GEMM_BM64_NK") ? atoi(getenv("DCT_GEMM_BM64_NK")) : 4;  // A/B knob
+    if (splits == 1 && (nk <= bm64_nk || tiles <= device_cus()) && tiles < 1024 && !force128)
       return launch(dct::gemm2_kernel<TA, TB, false, 64, 2>, ((g.M + 63) / 64) * tiles_n, 2);
   }
   if (splits > 1) {

@@ -49,12 +49,16 @@ VARIANTS = {
     "s2_splits128": {"DCT_GEMM_STAGES": "2", "DCT_GEMM_SPLITS": "128"},
     "s4_splits128": {"DCT_GEMM_STAGES": "4", "DCT_GEMM_SPLITS": "128"},
 }
-ENV_KEYS = ("DCT_GEMM_STAGES", "DCT_GEMM_SPLIT_WG", "DCT_GEMM_SPLITS", "DCT_GEMM_SPLIT_PROBE")
+ENV_KEYS = ("DCT_GEMM_STAGES", "DCT_GEMM_SPLIT_WG", "DCT_GEMM_SPLITS", "DCT_GEMM_SPLIT_PROBE", "DCT_GEMM_BM64_NK")
 if os.environ.get("AB_SET") == "dw":  # split-K sweep on the transformer dW shapes only
     SHAPES = [s for s in SHAPES if s[0].startswith("tt_dw") or s[0] == "dw_l1"]
     VARIANTS = {f"{st}_sp{sp}": {"DCT_GEMM_STAGES": st[1], "DCT_GEMM_SPLITS": str(sp)}
                 for st in ("s2", "s4") for sp in (8, 16, 32, 64)}
 
+if os.environ.get("AB_SET") == "bm64":  # half-height tiles (2 workgroups per CU) on the big MLP GEMMs
+    SHAPES = [s for s in SHAPES if not s[0].startswith(("tt_dw", "dw_"))]
+    VARIANTS = {"bm128": {}, "bm64": {"DCT_GEMM_BM64_NK": "64"}, "bm64_s4": {"DCT_GEMM_BM64_NK": "64",
+                                                                              "DCT_GEMM_STAGES": "4"}}
 if os.environ.get("AB_SET") == "probe":  # split-K: atomics vs plain stores (timing probe, wrong results)
     SHAPES = [s for s in SHAPES if s[0].startswith(("tt_dw", "dw_"))]
     VARIANTS = {f"{e}_sp{sp}": ({"DCT_GEMM_SPLIT_PROBE": "1"} if e == "plain" else {}) | {"DCT_GEMM_SPLITS": str(sp)}
