@@ -147,9 +147,9 @@ class _StepLoop:
         return self.rows.numel()
 
     def run_steps(self, n_items, steps, loss_out, first_step=0):
-        B = self.eng.B
-        for s in range(first_step, first_step + steps):
-            loss_out[s] = self.eng.train_step(self.rows[s * B:(s + 1) * B], s)
+        # device-side batch loop: one captured graph per step, batch gather / loss record / cursor
+        # on the device (trainer/engines.py AutogradEngine.run_device_steps)
+        self.eng.run_device_steps(self.rows, first_step, steps, loss_out)
 
     def validate(self, limit=None):
         import torch

@@ -174,6 +174,24 @@ PYBIND11_MODULE(_dct_native, m) {
       py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("p_bf16"), py::arg("n"), py::arg("lr"),
       py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("t"), py::arg("grad_scale"),
       py::arg("decoupled"), py::arg("step_counter"), py::arg("stream"));
+  m.def("adam_flat_step",
+        [](uintptr_t p, uintptr_t g, uintptr_t mo, uintptr_t vo, uintptr_t p_bf16, int64_t n, float lr, float b1,
+           float b2, float eps, float wd, int64_t t, float grad_scale, int decoupled, uintptr_t step_counter,
+           uintptr_t cursor, uintptr_t loss_slot, uintptr_t loss_out, int loss_cap, uintptr_t stream) {
+          check(dct_adam_flat_step(P<float>(p), P<const float>(g), P<float>(mo), P<float>(vo), P<uint16_t>(p_bf16), n,
+                                   lr, b1, b2, eps, wd, t, grad_scale, decoupled, P<const int>(step_counter),
+                                   P<int>(cursor), P<const float>(loss_slot), P<float>(loss_out), loss_cap,
+                                   reinterpret_cast<void*>(stream)),
+                "adam_flat_step");
+        });
+  m.def("ag_step_prologue",
+        [](uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t idx, uintptr_t cursor, int B, int64_t n_items,
+           uintptr_t xdst, uintptr_t ydst, uintptr_t step_counter, uintptr_t zero, int64_t zero_n, uintptr_t stream) {
+          check(dct_ag_step_prologue(P<const void>(X), row_bytes, P<const int64_t>(Y), P<const int64_t>(idx),
+                                     P<const int>(cursor), B, n_items, P<void>(xdst), P<int64_t>(ydst),
+                                     P<int>(step_counter), P<float>(zero), zero_n, reinterpret_cast<void*>(stream)),
+                "ag_step_prologue");
+        });
   m.def("zero_f32", [](uintptr_t p, int64_t n, uintptr_t stream) {
     check(dct_zero_f32(P<float>(p), n, reinterpret_cast<void*>(stream)), "zero_f32");
   });

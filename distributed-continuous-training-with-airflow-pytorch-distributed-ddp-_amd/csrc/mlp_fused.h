@@ -129,4 +129,11 @@ int dct_adam_flat(float* p, const float* g, float* m, float* v, uint16_t* p_bf16
                   const int* step_counter, void* stream);
 int dct_f32_to_bf16(const float* in, uint16_t* out, int64_t n, void* stream);
 int dct_zero_f32(float* p, int64_t n, void* stream);
+int dct_adam_flat_step(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, float lr,
+                       float b1, float b2, float eps, float wd, int64_t t, float grad_scale, int decoupled,
+                       const int* step_counter, int* cursor, const float* loss_slot, float* loss_out, int loss_cap,
+                       void* stream);
+int dct_ag_step_prologue(const void* X, int row_bytes, const int64_t* Y, const int64_t* idx, const int* cursor, int B,
+                         int64_t n_items, void* xdst, int64_t* ydst, int* step_counter, float* zero, int64_t zero_n,
+                         void* stream);
 }

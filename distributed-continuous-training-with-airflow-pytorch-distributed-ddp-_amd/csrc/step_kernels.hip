@@ -43,6 +43,40 @@ __global__ __launch_bounds__(256) void gather_batch_kernel(const uint4* __restri
   }
 }
 
+// Prologue of the graph-replayed AUTOGRAD step (trainer/engines.py AutogradEngine device loop):
+// batch rows idx[(*cursor) * B + r] (int64 dataset rows) -> fp32 feature rows + int64 labels in
+// the captured step's static inputs, Adam step counter += 1, flat gradient buffer zeroed - one
+// launch instead of two index_selects + a counter add + a zero kernel (and no host-side batch
+// slicing between replays).  The cursor is advanced by the Adam epilogue at the end of the step.
+__global__ __launch_bounds__(256) void ag_prologue_kernel(const uint4* __restrict__ X, int row_vec,
+                                                          const int64_t* __restrict__ Y,
+                                                          const int64_t* __restrict__ idx,
+                                                          const int* __restrict__ cursor, int B, int64_t n_items,
+                                                          uint4* __restrict__ xdst, int64_t* __restrict__ ydst,
+                                                          int* __restrict__ step_counter, float* __restrict__ zero,
+                                                          int64_t zero_n) {
+  const int64_t c = *cursor;
+  if (step_counter && blockIdx.x == 0 && threadIdx.x == 0) step_counter[0] += 1;
+  if (zero) {
+    const int64_t n4 = zero_n >> 2;
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float4* z4 = reinterpret_cast<float4*>(zero);
+    for (int64_t i = t; i < n4; i += gs) z4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t < zero_n - (n4 << 2)) zero[(n4 << 2) + t] = 0.f;
+  }
+  const int total = B * row_vec;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int r = e / row_vec;
+    const int v = e - r * row_vec;
+    int64_t q = c * B + r;
+    q = q < n_items ? q : (n_items > 0 ? q % n_items : 0);
+    const int64_t row = idx[q];
+    xdst[e] = X[(size_t)row * row_vec + v];
+    if (v == 0) ydst[r] = Y[row];
+  }
+}
+
 // step prologue: Adam step counter += 1 (read by adam_flat), loss/correct sums = 0
 __global__ void step_begin_kernel(int* step_counter, float* stats) {
   if (threadIdx.x == 0) {
@@ -104,6 +138,22 @@ int dct_gather_batch(const void* X, int row_bytes, const int* Y, const int* idx,
                      int B, int n_items, void* xdst, int* ydst, void* stream) {
   return dct_gather_batch_step(X, row_bytes, Y, idx, cursor, stride, B, n_items, xdst, ydst, nullptr, nullptr, 0,
                                stream);
+}
+
+int dct_ag_step_prologue(const void* X, int row_bytes, const int64_t* Y, const int64_t* idx, const int* cursor, int B,
+                         int64_t n_items, void* xdst, int64_t* ydst, int* step_counter, float* zero, int64_t zero_n,
+                         void* stream) {
+  if (B <= 0 || !cursor) return (int)hipErrorInvalidValue;
+  if (row_bytes % 16 || (((uintptr_t)X) | ((uintptr_t)xdst)) & 15) return (int)hipErrorInvalidValue;
+  if (zero && (((uintptr_t)zero) & 15)) return (int)hipErrorInvalidValue;
+  const int rv = row_bytes / 16;
+  int64_t work = (int64_t)B * rv;
+  if (zero && (zero_n + 3) / 4 > work) work = (zero_n + 3) / 4;
+  int grid = (int)((work + 255) / 256);
+  grid = grid > 2048 ? 2048 : (grid < 1 ? 1 : grid);
+  hipLaunchKernelGGL(dct::ag_prologue_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     (const uint4*)X, rv, Y, idx, cursor, B, n_items, (uint4*)xdst, ydst, step_counter, zero, zero_n);
+  return (int)hipGetLastError();
 }
 
 int dct_step_begin(int* step_counter, float* stats, void* stream) {

@@ -86,7 +86,10 @@ class FlatAdam:
     def lr(self):
         return self.param_groups[0]["lr"]
 
-    def step(self, grad_scale: float = 1.0):
+    def step(self, grad_scale: float = 1.0, bump_counter: bool = True, epilogue=None):
+        """One update.  ``bump_counter=False``: a step-prologue kernel already advanced the device
+        step counter.  ``epilogue=(cursor, loss, loss_out)``: the Adam kernel also records
+        loss_out[*cursor] = loss and advances the device batch cursor (graph-replayed loops)."""
         self.step_count += 1
         g = self.param_groups[0]
         counter = None
@@ -94,7 +97,17 @@ class FlatAdam:
             # the Adam step count lives on the device (advanced by a kernel, read by the Adam
             # kernel), so a captured step graph replays with the right bias correction
             counter = self._device_counter()
-            counter.add_(1)
+            if bump_counter:
+                counter.add_(1)
+        if epilogue is not None:
+            cursor, loss, loss_out = epilogue
+            b1, b2 = g["betas"]
+            native().adam_flat_step(ptr(self.p), ptr(self.g), ptr(self.m), ptr(self.v), ptr(self.p_bf16),
+                                    self.p.numel(), float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                                    float(g["weight_decay"]), max(1, self.step_count), float(grad_scale), 0,
+                                    ptr(counter), ptr(cursor), ptr(loss), ptr(loss_out), loss_out.numel(),
+                                    stream_handle(self.p.device))
+            return
         adam_flat_(self.p, self.g, self.m, self.v, self.step_count, g["lr"], g["betas"], g["eps"],
                    g["weight_decay"], grad_scale=grad_scale, p_bf16=self.p_bf16, step_counter=counter)
 

@@ -580,6 +580,94 @@ class AutogradEngine(_EngineBase):
         self.optimizer.step_count += 1
         return self._loss_static
 
+    # ------------------------------------------------------------------ device-side batch loop
+    # Steps over a device-resident list of dataset rows with NO host work between replays: the
+    # captured graph starts with ONE prologue kernel (batch gather at the device cursor, Adam
+    # step counter += 1, gradient zeroing) and ends with the Adam kernel, which also records the
+    # step's loss at loss_out[cursor] and advances the cursor (csrc/step_kernels.hip,
+    # csrc/optim.hip).  Replaces, per step: host batch slicing, two index_selects, a counter add,
+    # a zero kernel and the loss copy.
+    def device_loop_ok(self) -> bool:
+        return (self.device.type == "cuda" and self.optimizer is not None and self.X.dim() == 2
+                and self.X.shape[1] % 4 == 0 and os.environ.get("DCT_GRAPH", "1") != "0"
+                and os.environ.get("DCT_DEVICE_LOOP", "1") != "0" and not getattr(self, "_graph_failed", False))
+
+    def run_device_steps(self, rows_dev: torch.Tensor, first_step: int, steps: int, loss_out: torch.Tensor):
+        """Steps first_step .. first_step + steps - 1 over rows_dev (int64, device) batches of B;
+        losses land in loss_out[step] (fp32, device)."""
+        if not self.device_loop_ok():
+            for s in range(first_step, first_step + steps):
+                loss_out[s] = self.train_step(rows_dev[s * self.B:(s + 1) * self.B], s)
+            return
+        from ..ops._native import native
+
+        nat = native()
+        s = first_step
+        end = first_step + steps
+        while s < end and getattr(self, "_dgraph", None) is None and self._eager_full_dev() < self.GRAPH_WARMUP:
+            loss_out[s] = self.train_step(rows_dev[s * self.B:(s + 1) * self.B], s)  # warm-up (capture stream)
+            s += 1
+        if s >= end:
+            return
+        key = (rows_dev.data_ptr(), rows_dev.numel(), loss_out.data_ptr(), loss_out.numel())
+        if getattr(self, "_dgraph", None) is None or self._dgraph_key != key:
+            try:
+                self._capture_device_graph(nat, rows_dev, loss_out, s)
+            except Exception as e:  # noqa: BLE001 - eager steps stay correct
+                print(f"[dct] HIP graph capture of the device-loop step failed ({e!r}); running eagerly", flush=True)
+                self._graph_failed = True
+                self._dgraph = None
+                torch.cuda.synchronize(self.device)
+                for t in range(s, end):
+                    loss_out[t] = self.train_step(rows_dev[t * self.B:(t + 1) * self.B], t)
+                return
+            self._dgraph_key = key
+        self._dcursor.fill_(s)
+        for _ in range(end - s):
+            self._dgraph.replay()
+        self.optimizer.step_count += end - s
+        self.global_step += end - s
+
+    def _eager_full_dev(self) -> int:
+        return getattr(self, "_eager_full", 0)
+
+    def _prologue(self, nat, rows_dev):
+        st = torch.cuda.current_stream().cuda_stream
+        nat.ag_step_prologue(self.X.data_ptr(), self.X.shape[1] * 4, self.Y.data_ptr(), rows_dev.data_ptr(),
+                             self._dcursor.data_ptr(), self.B, rows_dev.numel(), self._x_dev.data_ptr(),
+                             self._y_dev.data_ptr(), self.optimizer._device_counter().data_ptr(),
+                             self.flat_g.data_ptr(), self.flat_g.numel(), st)
+
+    def _capture_device_graph(self, nat, rows_dev, loss_out, first):
+        if not (self.X.is_contiguous() and self.Y.is_contiguous() and self.X.dtype == torch.float32):
+            raise RuntimeError("device loop needs contiguous fp32 features / int64 labels")
+        self._x_dev = torch.empty(self.B, self.X.shape[1], dtype=torch.float32, device=self.device)
+        self._y_dev = torch.empty(self.B, dtype=torch.int64, device=self.device)
+        self._dcursor = torch.full((1,), first, dtype=torch.int32, device=self.device)
+        g = torch.cuda.CUDAGraph()
+        s = self._capture_stream()
+        s.wait_stream(torch.cuda.current_stream())
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                self._prologue(nat, rows_dev)
+                if self.reducer is not None:
+                    self.reducer.prepare()
+                self.model.train()
+                with self._bound():
+                    loss = self.model.training_step((self._x_dev, self._y_dev), first)
+                    if isinstance(loss, dict):
+                        loss = loss["loss"]
+                    loss.backward()
+                if self.reducer is not None:
+                    self.reducer.finalize()
+                self.optimizer.step(bump_counter=False, epilogue=(self._dcursor, loss.detach(), loss_out))
+        torch.cuda.current_stream().wait_stream(s)
+        self._dgraph = g
+        self._dloss = loss
+        self.graph_used = True
+        self.optimizer.step_count -= 1  # capture recorded without executing
+
     def optimizer_state_dict(self) -> Dict:
         if self.optimizer is not None:
             return self.optimizer.state_dict()
