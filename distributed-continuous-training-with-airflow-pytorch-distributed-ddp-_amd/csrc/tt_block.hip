@@ -83,6 +83,7 @@ struct Args {
   float* out;
   uint16_t* wT;  // transposed bf16 weights for the backward: W2^T | W1^T | Wo^T | Wqkv^T
   uint64_t* prof;  // optional phase timestamps (wall clock), 16 per workgroup
+  int save;        // 0: inference (no_grad) - only `out` is written, no saved tensors / W^T
   int B;
   float eps, scale;
 };
@@ -168,7 +169,7 @@ __device__ __forceinline__ void layer_norm_rows(const float* src, bool from_glob
   }
   *reinterpret_cast<bf16x8*>(AS + r * AS_LD + 16 * g) = o0;
   *reinterpret_cast<bf16x8*>(AS + r * AS_LD + 16 * g + 8) = o1;
-  if (g == 0) {
+  if (g == 0 && mean_out) {
     mean_out[row0 + r] = mean;
     rstd_out[row0 + r] = rstd;
   }
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
   TT_MARK(1);
 
   // ---- P2: a1 out; QKV = a1 Wqkv^T + bqkv for head wv (Q, K, V column tiles wv, 4+wv, 8+wv)
-  store_tile<DM * 2, AS_LD * 2>(a.a1 + (size_t)row0 * DM, AS);
+  if (a.save) store_tile<DM * 2, AS_LD * 2>(a.a1 + (size_t)row0 * DM, AS);
   {
     f32x4 acc[3][4];
 #pragma unroll
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
 
   TT_MARK(2);
   // ---- P3: qkv out; attention of head wv over the 64 tokens (S^T = K Q^T; P V)
-  store_tile<3 * DM * 2, QKV_LD * 2>(a.qkv + (size_t)row0 * 3 * DM, RS);
+  if (a.save) store_tile<3 * DM * 2, QKV_LD * 2>(a.qkv + (size_t)row0 * 3 * DM, RS);
   {
     const uint16_t* Qs = RS + DH * wv;
     const uint16_t* Ks = RS + DM + DH * wv;
@@ -282,7 +283,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) OS[(16 * j + 4 * g + r) * AS_LD + DH * wv + c] = f32_to_bf16(acc[r]);
     }
-    if (g == 0) {
+    if (g == 0 && a.save) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) a.lse[((size_t)bidx * NH + wv) * T + 16 * j + c] = lsev[j];
     }
@@ -291,7 +292,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
 
   TT_MARK(3);
   // ---- P4: o out; h1 = h + o Wo^T + bo (rows of this wave); LN2 of the same rows
-  store_tile<DM * 2, AS_LD * 2>(a.o + (size_t)row0 * DM, OS);
+  if (a.save) store_tile<DM * 2, AS_LD * 2>(a.o + (size_t)row0 * DM, OS);
   // Row-parallel GEMMs split by COLUMNS across the waves (wave wv: column tile(s) wv for all 64
   // rows): each wave then streams only its quarter of the weight from L2 - the row split had
   // every wave fetch the whole matrix (4x the L2 traffic; fc1 was 10 us of a 30 us block).
@@ -319,8 +320,10 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
 
   TT_MARK(4);
   // ---- P5: h1, a2 out; F = gelu(a2 W1^T + b1) for columns 64wv..64wv+63, pre-activation out
-  store_tile<DM * 4, HS_LD * 4>(a.h1 + (size_t)row0 * DM, HS);
-  store_tile<DM * 2, AS_LD * 2>(a.a2 + (size_t)row0 * DM, AS);
+  if (a.save) {
+    store_tile<DM * 4, HS_LD * 4>(a.h1 + (size_t)row0 * DM, HS);
+    store_tile<DM * 2, AS_LD * 2>(a.a2 + (size_t)row0 * DM, AS);
+  }
   {
     f32x4 acc[4][4];  // [row tile][column tile of this wave]
 #pragma unroll
@@ -350,7 +353,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
         for (int r = 0; r < 4; ++r) {
           const int row = 16 * i + 4 * g + r;
           const float z = acc[i][t][r] + bv;
-          a.pre[(size_t)(row0 + row) * FF + col] = f32_to_bf16(z);
+          if (a.save) a.pre[(size_t)(row0 + row) * FF + col] = f32_to_bf16(z);
           RS[row * F_LD + col] = f32_to_bf16(gelu_f(z));
         }
     }
@@ -359,7 +362,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
 
   TT_MARK(5);
   // ---- P6: f out; out = h1 + F W2^T + b2 for column tile wv
-  store_tile<FF * 2, F_LD * 2>(a.f + (size_t)row0 * FF, RS);
+  if (a.save) store_tile<FF * 2, F_LD * 2>(a.f + (size_t)row0 * FF, RS);
   {
     f32x4 acc[4];
 #pragma unroll
@@ -381,7 +384,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
   __syncthreads();
   TT_MARK(6);
   store_tile<DM * 4, HS_LD * 4>(a.out + (size_t)row0 * DM, HS);
-  transpose_weights(a);
+  if (a.save) transpose_weights(a);
   TT_MARK(7);
 }
 
@@ -816,9 +819,12 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
   using namespace dct::ttb;
   if ((n_ptrs != 27 && n_ptrs != 28) || T != dct::ttb::T || DM != dct::ttb::DM || H != NH || FF != dct::ttb::FF || Bsz <= 0)
     return (int)hipErrorInvalidValue;
+  // inference (no saved tensors) when a1 (p[13]) is null: then only inputs, weights and out are used
+  const bool save = p[13] != 0;
   uintptr_t any = 0;
   for (int i = 0; i < 27; ++i) {
-    if (!p[i]) return (int)hipErrorInvalidValue;
+    const bool needed = i < 13 || i == 25 || save;
+    if (needed && !p[i]) return (int)hipErrorInvalidValue;
     any |= p[i];
   }
   if (any & 15) return (int)hipErrorInvalidValue;  // 16-byte vector loads / stores everywhere
@@ -834,6 +840,7 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
   a.h1 = (float*)p[19]; a.a2 = (uint16_t*)p[20]; a.mean2 = (float*)p[21]; a.rstd2 = (float*)p[22];
   a.f = (uint16_t*)p[23]; a.pre = (uint16_t*)p[24]; a.out = (float*)p[25]; a.wT = (uint16_t*)p[26];
   a.prof = n_ptrs == 28 ? (uint64_t*)p[27] : nullptr;
+  a.save = save ? 1 : 0;
   a.B = Bsz; a.eps = eps; a.scale = scale;
   static bool attr = false;
   if (!attr) {

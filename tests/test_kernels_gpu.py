@@ -671,7 +671,11 @@ def test_tt_block_fused_matches_fp32_reference_and_unfused(cuda, B, monkeypatch)
             v.grad = None
         return out.detach(), grads
 
+    monkeypatch.setenv("DCT_TT_FUSED", "1")
+    with torch.no_grad():  # inference mode of the block kernel: only the output is written
+        out_inf = nnops.tt_block(t["h"], *[t[k] for k in keys], B, H, T)
     out_f, g_f = run(True)               # fused forward + fused backward kernel
+    assert torch.equal(out_inf, out_f)
     out_fu, g_fu = run(True, False)      # fused forward + the unfused backward nodes
     out_u, g_u = run(False)
     a = F.layer_norm(t["h"], (d,), t["ln1_w"], t["ln1_b"], 1e-5)

@@ -62,15 +62,16 @@ def test_hip_path_matches_torch_reference(cuda, F_):
 
 
 @pytest.mark.gpu
-def test_hip_fit_with_graph_capture(cuda):
+@pytest.mark.parametrize("F_", [32, 64])  # 64 features: whole-block fused kernels + native ends
+def test_hip_fit_with_graph_capture(cuda, F_):
     from dct_amd.trainer import Trainer
 
     torch.manual_seed(0)
-    X, Y = _data(2048, 32)
+    X, Y = _data(2048, F_)
     ds = TensorDataset(X, Y)
     tl = DataLoader(torch.utils.data.Subset(ds, range(1792)), batch_size=128, shuffle=True)
     vl = DataLoader(torch.utils.data.Subset(ds, range(1792, 2048)), batch_size=128)
-    m = TabTransformer(num_features=32, d_model=64, heads=4, layers=2, lr=3e-3)
+    m = TabTransformer(num_features=F_, d_model=64, heads=4, layers=2, lr=3e-3)
     tr = Trainer(max_epochs=4, accelerator="gpu", engine="autograd", verbose=False, num_sanity_val_steps=0)
     tr.fit(m, tl, vl)
     assert tr.engine.graph_used
