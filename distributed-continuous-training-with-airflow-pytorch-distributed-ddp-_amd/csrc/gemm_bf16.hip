@@ -730,13 +730,15 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
     g.vec_b = ((((uintptr_t)X[i]) & 15) == 0) && (N[i] % 8 == 0);
     g.colsum = colsum ? colsum[i] : nullptr;
     g.residual = nullptr;
-    g.split_probe = 0;
+    g.split_probe = getenv("DCT_GEMM_SPLIT_PROBE") != nullptr;  // timing probe only: plain stores, wrong sums
     const int tiles = ((g.M + dct::GBM - 1) / dct::GBM) * ((g.N + dct::GBN - 1) / dct::GBN);
     const int nk = g.K / dct::GBK;
     if (!gemm_v2_ok(g, 1, 0) || tiles >= 256 || nk < 8) { grouped = false; break; }
     int target = device_cus();
     if (const char* f = getenv("DCT_GEMM_SPLIT_WG")) target = std::max(1, atoi(f));
-    int splits = std::min(nk / 8, (target + tiles - 1) / tiles);
+    int min_kt = 8;  // k-tiles per split slice
+    if (const char* f = getenv("DCT_GEMM_DW_MINK")) min_kt = std::max(2, atoi(f));
+    int splits = std::min(nk / min_kt, (target + tiles - 1) / tiles);
     if (splits < 1) splits = 1;
     gg.splits[i] = splits;
     gg.start[i] = total;
