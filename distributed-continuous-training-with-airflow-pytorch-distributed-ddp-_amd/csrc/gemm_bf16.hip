@@ -417,6 +417,72 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
   // accumulator is the TRANSPOSED tile: lane (c = lane&15, g = lane>>4) holds row 16i + c and the
   // 4 CONSECUTIVE columns 16j + 4g .. +3 -> 8-byte bf16 / 16-byte fp32 row stores instead of
   // 2-byte scattered ones (and 4-wide bias / aux loads).
+  if (SPLIT && g.split_ws) {
+    // Workspace split-K (opt-in, DCT_GEMM_SPLIT_WS=1: the deterministic mode): every slice stores
+    // its partial tile (element-major, 1 KB per store instruction across the workgroup), the LAST
+    // slice to arrive at the tile sums all partials in slice order and writes C once, so dW is
+    // bit-reproducible run to run.  Agent-scope stores/loads + fences keep the partials coherent
+    // across the 8 XCDs' L2s - and those fences (L2 writeback per workgroup) make it SLOWER than
+    // the fp32 atomics: tabular 4x1024 step 0.203 -> 0.291 ms (profiles/gemm_splitk_ws_ab_r1.log).
+    constexpr int NE = IM * 16;
+    float* slot = g.split_ws + ((size_t)tile * splits + split) * (BM * GBN);
+#pragma unroll
+    for (int i = 0; i < IM; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          __hip_atomic_store(slot + ((i * 4 + j) * 4 + r) * GNT + tid, acc[i][j][r], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    __shared__ int is_last;
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) {
+      const int prev = __hip_atomic_fetch_add(g.split_cnt + tile, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      is_last = (prev == splits - 1);
+      if (is_last) __hip_atomic_store(g.split_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!is_last) return;
+    __threadfence();
+    float sum[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) sum[e] = 0.f;
+    const float* base = g.split_ws + (size_t)tile * splits * (BM * GBN);
+    for (int sp = 0; sp < splits; ++sp) {
+      if (sp == split) {
+#pragma unroll
+        for (int i = 0; i < IM; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sum[(i * 4 + j) * 4 + r] += acc[i][j][r];
+      } else {
+        const float* ps = base + (size_t)sp * (BM * GBN);
+#pragma unroll
+        for (int e = 0; e < NE; ++e)
+          sum[e] += __hip_atomic_load(ps + e * GNT + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < IM; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wc * 64 + j * 16 + col_l;
+        if (col >= g.N) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wr * (BM / 2) + i * 16 + row_l + r;
+          if (row < g.M) {
+            float* dst = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
+            const float v = sum[(i * 4 + j) * 4 + r] * g.alpha;
+            *dst = g.accumulate ? *dst + v : v;
+          }
+        }
+      }
+    return;
+  }
   if (SPLIT) {  // natural layout: col = lane&15, rows 4*(lane>>4) + r
     const int col_l = lane & 15, row_l = (lane >> 4) * 4;
 #pragma unroll
@@ -600,6 +666,43 @@ static bool gemm_v2_ok(const dct::GemmArgs& g, int ta, int tb) {
   return true;
 }
 
+// Split-K workspace (see the SPLIT && split_ws epilogue).  Allocated once per process, outside
+// any stream capture (the graph engines run one eager warm step before capturing); a captured
+// graph keeps using the buffer it recorded, so a buffer is never freed, only superseded.
+// One compute stream per device issues the split GEMMs, so one workspace serves them in order.
+static float* g_split_ws = nullptr;
+static int* g_split_cnt = nullptr;
+static size_t g_split_ws_bytes = 0;
+static int g_split_dev = -1;
+constexpr int SPLIT_CNT_N = 4096;
+static bool split_workspace(size_t bytes, int tiles, hipStream_t st, float** ws, int** cnt) {
+  if (!getenv("DCT_GEMM_SPLIT_WS") || tiles > SPLIT_CNT_N) return false;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (g_split_ws && g_split_dev == dev && g_split_ws_bytes >= bytes) {
+    *ws = g_split_ws; *cnt = g_split_cnt;
+    return true;
+  }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+  if (g_split_dev != -1 && g_split_dev != dev) return false;  // one device per process
+  const size_t want = std::max<size_t>(bytes, (size_t)64 << 20);
+  float* w = nullptr;
+  int* c = nullptr;
+  if (hipMalloc(&w, want) != hipSuccess) { (void)hipGetLastError(); return false; }
+  if (!g_split_cnt) {
+    if (hipMalloc(&c, SPLIT_CNT_N * sizeof(int)) != hipSuccess || hipMemset(c, 0, SPLIT_CNT_N * sizeof(int)) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    if (hipDeviceSynchronize() != hipSuccess) return false;
+    g_split_cnt = c;
+  }
+  g_split_ws = w; g_split_ws_bytes = want; g_split_dev = dev;
+  *ws = g_split_ws; *cnt = g_split_cnt;
+  return true;
+}
+
 static int device_cus() {
   static int cus = 0;
   if (cus == 0) {
@@ -642,7 +745,11 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
     if (const char* f = getenv("DCT_GEMM_SPLITS")) splits = std::min(nk, atoi(f));  // tuning override
     if (splits < 1) splits = 1;
   }
-  if (splits > 1 && !g.accumulate) {  // slices accumulate atomically into a zeroed C
+  if (splits > 1 && !g.split_probe) {
+    const size_t bytes = (size_t)tiles * splits * dct::GBM * dct::GBN * sizeof(float);
+    if (!split_workspace(bytes, tiles, st, &g.split_ws, &g.split_cnt)) g.split_ws = nullptr, g.split_cnt = nullptr;
+  }
+  if (splits > 1 && !g.accumulate && !g.split_ws) {  // slices accumulate atomically into a zeroed C
     const int64_t total = (int64_t)g.M * g.N;
     const int zgrid = (int)std::min<int64_t>(2048, (total + 255) / 256);
     hipLaunchKernelGGL(dct::zero_panel_kernel, dim3(zgrid), dim3(256), 0, st, reinterpret_cast<float*>(g.C), g.ldc,

@@ -23,6 +23,8 @@ struct GemmArgs {
   float* colsum;  // optional: colsum[m] += sum_k op(A)[m][k] (the bias gradient of a dW GEMM)
   const float* residual;  // optional (fp32 out): C = residual + op(A) op(B) + bias, ld = ldc
   int split_probe;        // debug timing probe: split-K slices plain-store (wrong result) instead of atomics
+  float* split_ws;        // optional split-K workspace [tiles][splits][BM*GBN]: slices store partials, the
+  int* split_cnt;         // last slice of a tile (split_cnt[tile] arrival counter) sums them in slice order
 };
 
 }  // namespace dct

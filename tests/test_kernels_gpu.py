@@ -790,3 +790,31 @@ def test_skinny_head_linear_and_shadow_weights(cuda):
     assert (gw - 1.0 - w.grad).norm() / w.grad.norm() < 1e-2
     assert (gb - b.grad).norm() / b.grad.norm() < 1e-2
     assert (gx.float() - x.grad.float()).norm() / x.grad.float().norm() < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K,accumulate", [(1024, 1024, 4096, 0), (512, 256, 8192, 1), (300, 200, 4096, 0),
+                                               (1024, 256, 4096, 1)])
+def test_gemm_splitk_workspace_fixup_deterministic(M, N, K, accumulate, cuda, monkeypatch):
+    """dW-shaped split-K (TN, fp32 out): the opt-in workspace path (slices store partials, the last
+    slice sums them in slice order) matches fp32 torch and the atomic path, and is bit-reproducible."""
+    torch.manual_seed(11)
+    A = _bf(torch.randn(K, M, device=cuda))  # dZ [K, M] -> op(A) = A^T
+    B = _bf(torch.randn(K, N, device=cuda))
+    C0 = torch.randn(M, N, device=cuda) if accumulate else torch.zeros(M, N, device=cuda)
+    st = torch.cuda.current_stream().cuda_stream
+    monkeypatch.setenv("DCT_GEMM_SPLIT_WS", "1")
+
+    def run():
+        C = C0.clone()
+        native().gemm_bf16(A.data_ptr(), B.data_ptr(), C.data_ptr(), 0, M, N, K, M, N, N, 1, 0, 0, 1, accumulate, 0,
+                           st)
+        torch.cuda.synchronize()
+        return C
+
+    c1, c2 = run(), run()
+    ref = C0 + A.float().t() @ B.float()
+    assert torch.equal(c1, c2)
+    assert torch.allclose(c1, ref, atol=2e-3 * math.sqrt(K), rtol=1e-3)
+    monkeypatch.delenv("DCT_GEMM_SPLIT_WS")
+    ca = run()
+    assert torch.allclose(c1, ca, atol=1e-3 * math.sqrt(K), rtol=1e-4)
