@@ -23,7 +23,10 @@ __device__ __forceinline__ void unpack8(const uint4& v, float (&f)[8]) {
   }
 }
 
-// Y[b][c] = X[b] . W[c] + bias[c]: one wave per row, each lane 8 k per 512-k chunk
+// Y[b][c] = X[b] . W[c] + bias[c]: one wave per row, each lane 8 k per 512-k chunk.  CT = C rounded up
+// to 1/2/4/8; class rows past C re-read row C-1 (never stored): loads stay unconditional, since a
+// guarded load compiles to a branch that drains every load in flight (s_waitcnt vmcnt(0)).
+template <int CT>
 __global__ __launch_bounds__(256) void skinny_fwd_kernel(const uint16_t* __restrict__ X,
                                                          const uint16_t* __restrict__ W,
                                                          const float* __restrict__ bias, uint16_t* __restrict__ Y,
@@ -31,24 +34,26 @@ __global__ __launch_bounds__(256) void skinny_fwd_kernel(const uint16_t* __restr
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
-  float acc[SK_CMAX];
+  float acc[CT];
 #pragma unroll
-  for (int c = 0; c < SK_CMAX; ++c) acc[c] = 0.f;
+  for (int c = 0; c < CT; ++c) acc[c] = 0.f;
   for (int k = lane * 8; k < K; k += 512) {
+    uint4 raw[CT + 1];
+    raw[CT] = *reinterpret_cast<const uint4*>(X + (size_t)b * K + k);
+#pragma unroll
+    for (int c = 0; c < CT; ++c) raw[c] = *reinterpret_cast<const uint4*>(W + (size_t)(c < C ? c : C - 1) * K + k);
     float x[8];
-    unpack8(*reinterpret_cast<const uint4*>(X + (size_t)b * K + k), x);
+    unpack8(raw[CT], x);
 #pragma unroll
-    for (int c = 0; c < SK_CMAX; ++c) {
-      if (c < C) {
-        float w[8];
-        unpack8(*reinterpret_cast<const uint4*>(W + (size_t)c * K + k), w);
+    for (int c = 0; c < CT; ++c) {
+      float w[8];
+      unpack8(raw[c], w);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[c] += x[e] * w[e];
-      }
+      for (int e = 0; e < 8; ++e) acc[c] += x[e] * w[e];
     }
   }
 #pragma unroll
-  for (int c = 0; c < SK_CMAX; ++c) {
+  for (int c = 0; c < CT; ++c) {
     if (c < C) {
       float v = wave_sum(acc[c]);
       if (lane == 0) Y[(size_t)b * C + c] = f32_to_bf16(v + (bias ? bias[c] : 0.f));
@@ -56,7 +61,8 @@ __global__ __launch_bounds__(256) void skinny_fwd_kernel(const uint16_t* __restr
   }
 }
 
-// dX[b][k..k+8) = sum_c dZ[b][c] W[c][k..k+8)  (masked by the ReLU output aux > 0)
+// dX[b][k..k+8) = sum_c dZ[b][c] W[c][k..k+8)  (masked by the ReLU output aux > 0); CT as above
+template <int CT>
 __global__ __launch_bounds__(256) void skinny_dx_kernel(const uint16_t* __restrict__ dZ,
                                                         const uint16_t* __restrict__ W,
                                                         const uint16_t* __restrict__ aux, uint16_t* __restrict__ dX,
@@ -69,20 +75,27 @@ __global__ __launch_bounds__(256) void skinny_dx_kernel(const uint16_t* __restri
     float o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = 0.f;
-#pragma unroll
-    for (int c = 0; c < SK_CMAX; ++c) {
-      if (c < C) {
-        const float dz = bf16_to_f32(dZ[(size_t)b * C + c]);
-        float w[8];
-        unpack8(*reinterpret_cast<const uint4*>(W + (size_t)c * K + k), w);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] += dz * w[j];
-      }
-    }
     const size_t off = (size_t)b * K + k;
+    const uint4 araw = aux ? *reinterpret_cast<const uint4*>(aux + off) : make_uint4(0, 0, 0, 0);
+    uint4 wraw[CT];
+    float dz[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const int cc = c < C ? c : C - 1;
+      wraw[c] = *reinterpret_cast<const uint4*>(W + (size_t)cc * K + k);
+      const float z = bf16_to_f32(dZ[(size_t)b * C + cc]);
+      dz[c] = c < C ? z : 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      float w[8];
+      unpack8(wraw[c], w);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += dz[c] * w[j];
+    }
     if (aux) {
       float a[8];
-      unpack8(*reinterpret_cast<const uint4*>(aux + off), a);
+      unpack8(araw, a);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = a[j] > 0.f ? o[j] : 0.f;
     }
@@ -98,13 +111,16 @@ __global__ __launch_bounds__(256) void skinny_dx_kernel(const uint16_t* __restri
 // dW[c][k] += sum_b dZ[b][c] X[b][k], db[c] += sum_b dZ[b][c].
 // Block: 64 lanes x 8 k = 512 columns, 4 row lanes (waves); blockIdx.y splits the rows.  CT = the
 // class count rounded up to 1/2/4/8, so registers and the cross-wave LDS reduction cover only real
-// classes ([wave][c][j][lane]: lanes contiguous, conflict-free; CT = 2 -> 16 KB, several blocks
-// per CU).  The X rows are the only HBM stream; the head's dZ is read as wave-uniform scalars.
+// classes (CT = 2 -> 16 KB of LDS partials, several blocks per CU).  The X rows are the only HBM stream; the head's dZ is read as wave-uniform scalars.
 template <int CT>
 __global__ __launch_bounds__(256) void skinny_dw_kernel(const uint16_t* __restrict__ dZ,
                                                         const uint16_t* __restrict__ X, float* __restrict__ dW,
                                                         float* __restrict__ db, int B, int K, int C, int rows_per) {
-  __shared__ float red[4][CT][8][65];  // +1 pad: the column-ordered fold below reads j-major
+  // partials in column order ([wave][c][col], col = lane * 8 + j): each lane writes its 8 columns as two
+  // 16-byte stores and the fold reads lane-contiguous columns (the [j][lane] layout read 8 columns per
+  // lane group from 8 rows of the tile: ~59% of its LDS cycles were bank conflicts, profiles/pmc_*)
+  __shared__ float4 red4[4][CT][128];
+  float (*red)[CT][512] = reinterpret_cast<float (*)[CT][512]>(red4);
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int k = (blockIdx.x * 64 + tx) * 8;
   const int r0 = blockIdx.y * rows_per;
@@ -117,25 +133,45 @@ __global__ __launch_bounds__(256) void skinny_dw_kernel(const uint16_t* __restri
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[c][j] = 0.f;
   }
-  const bool kin = k < K;
-#pragma unroll 4
-  for (int b = r0 + ty; b < r1; b += 4) {
-    float x[8];
-    if (kin) unpack8(*reinterpret_cast<const uint4*>(X + (size_t)b * K + k), x);
+  // Rows go in batches of U per wave: all U row loads (and their dZ scalars) are issued before any
+  // FMA, so a wave pays one HBM latency per batch.  The loop this replaces guarded its dZ loads, which
+  // compiled to a branch + s_waitcnt vmcnt(0) per load and drained every X load in flight: its time grew
+  // with rows per block, 11.5 us at 64 rows and 39 us at 256 (profiles/skinny_dw_split_sweep_r1.txt).  Rows past
+  // r1 re-read row r0 with dz = 0; lanes past K read column 0 and their sums are never stored.
+  constexpr int U = CT <= 2 ? 8 : 4;
+  const int kc = k < K ? k : 0;
+  for (int b0 = r0 + ty; b0 < r1; b0 += 4 * U) {
+    uint4 raw[U];
+    float dz[U][CT];
 #pragma unroll
-    for (int c = 0; c < CT; ++c) {
-      const float dz = (c < C) ? bf16_to_f32(dZ[(size_t)b * C + c]) : 0.f;
-      dbs[c] += dz;
-      if (kin) {
+    for (int u = 0; u < U; ++u) {
+      const int b = b0 + 4 * u;
+      const bool ok = b < r1;
+      const int bs = ok ? b : r0;
+      raw[u] = *reinterpret_cast<const uint4*>(X + (size_t)bs * K + kc);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[c][j] += dz * x[j];
+      for (int c = 0; c < CT; ++c) {  // unconditional load, masked after: a guarded load compiles to a
+        const float z = bf16_to_f32(dZ[(size_t)bs * C + (c < C ? c : C - 1)]);  // branch + vmcnt(0) drain
+        dz[u][c] = (ok && c < C) ? z : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float x[8];
+      unpack8(raw[u], x);
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        dbs[c] += dz[u][c];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[c][j] += dz[u][c] * x[j];
       }
     }
   }
 #pragma unroll
-  for (int c = 0; c < CT; ++c)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) red[ty][c][j][tx] = acc[c][j];
+  for (int c = 0; c < CT; ++c) {
+    red4[ty][c][2 * tx] = make_float4(acc[c][0], acc[c][1], acc[c][2], acc[c][3]);
+    red4[ty][c][2 * tx + 1] = make_float4(acc[c][4], acc[c][5], acc[c][6], acc[c][7]);
+  }
   __syncthreads();
   // fold the 4 waves' partials in COLUMN order: thread t owns columns t and t + 256 of the block's
   // 512, so each atomic wave-instruction covers 256 contiguous bytes (the full-rate atomic shape;
@@ -147,9 +183,8 @@ __global__ __launch_bounds__(256) void skinny_dw_kernel(const uint16_t* __restri
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int col = threadIdx.x + 256 * h;
-      const int j = col & 7, l = col >> 3;
       if (kbase + col < K) {
-        const float v = red[0][c][j][l] + red[1][c][j][l] + red[2][c][j][l] + red[3][c][j][l];
+        const float v = red[0][c][col] + red[1][c][col] + red[2][c][col] + red[3][c][col];
         atomicAdd(dW + (size_t)c * K + kbase + col, v);
       }
     }
@@ -158,12 +193,12 @@ __global__ __launch_bounds__(256) void skinny_dw_kernel(const uint16_t* __restri
     __syncthreads();
     if (tx == 0) {
 #pragma unroll
-      for (int c = 0; c < CT; ++c) red[ty][c][0][0] = dbs[c];
+      for (int c = 0; c < CT; ++c) red[ty][c][0] = dbs[c];
     }
     __syncthreads();
     if (threadIdx.x < C) {
       const int c = threadIdx.x;
-      atomicAdd(db + c, red[0][c][0][0] + red[1][c][0][0] + red[2][c][0][0] + red[3][c][0][0]);
+      atomicAdd(db + c, red[0][c][0] + red[1][c][0] + red[2][c][0] + red[3][c][0]);
     }
   }
 }
@@ -174,23 +209,30 @@ extern "C" {
 
 int dct_skinny_fwd(const uint16_t* X, const uint16_t* W, const float* bias, uint16_t* Y, int B, int K, int C,
                    void* stream) {
-  if (C > dct::SK_CMAX || K % 8 || (((uintptr_t)X | (uintptr_t)W) & 15)) return (int)hipErrorInvalidValue;
+  if (C > dct::SK_CMAX || C < 1 || K % 8 || (((uintptr_t)X | (uintptr_t)W) & 15)) return (int)hipErrorInvalidValue;
   if (B <= 0) return 0;
-  hipLaunchKernelGGL(dct::skinny_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), X,
-                     W, bias, Y, B, K, C);
+  const dim3 grid((B + 3) / 4);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (C == 1) hipLaunchKernelGGL(dct::skinny_fwd_kernel<1>, grid, dim3(256), 0, st, X, W, bias, Y, B, K, C);
+  else if (C == 2) hipLaunchKernelGGL(dct::skinny_fwd_kernel<2>, grid, dim3(256), 0, st, X, W, bias, Y, B, K, C);
+  else if (C <= 4) hipLaunchKernelGGL(dct::skinny_fwd_kernel<4>, grid, dim3(256), 0, st, X, W, bias, Y, B, K, C);
+  else hipLaunchKernelGGL(dct::skinny_fwd_kernel<8>, grid, dim3(256), 0, st, X, W, bias, Y, B, K, C);
   return (int)hipGetLastError();
 }
 
 int dct_skinny_dx(const uint16_t* dZ, const uint16_t* W, const uint16_t* aux, uint16_t* dX, int B, int K, int C,
                   void* stream) {
-  if (C > dct::SK_CMAX || K % 8 || (((uintptr_t)W | (uintptr_t)dX | (uintptr_t)aux) & 15))
+  if (C > dct::SK_CMAX || C < 1 || K % 8 || (((uintptr_t)W | (uintptr_t)dX | (uintptr_t)aux) & 15))
     return (int)hipErrorInvalidValue;
   if (B <= 0) return 0;
   const int64_t total = (int64_t)B * (K / 8);
   int grid = (int)((total + 255) / 256);
   grid = grid > 4096 ? 4096 : grid;
-  hipLaunchKernelGGL(dct::skinny_dx_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), dZ, W,
-                     aux, dX, B, K, C);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (C == 1) hipLaunchKernelGGL(dct::skinny_dx_kernel<1>, dim3(grid), dim3(256), 0, st, dZ, W, aux, dX, B, K, C);
+  else if (C == 2) hipLaunchKernelGGL(dct::skinny_dx_kernel<2>, dim3(grid), dim3(256), 0, st, dZ, W, aux, dX, B, K, C);
+  else if (C <= 4) hipLaunchKernelGGL(dct::skinny_dx_kernel<4>, dim3(grid), dim3(256), 0, st, dZ, W, aux, dX, B, K, C);
+  else hipLaunchKernelGGL(dct::skinny_dx_kernel<8>, dim3(grid), dim3(256), 0, st, dZ, W, aux, dX, B, K, C);
   return (int)hipGetLastError();
 }
 
