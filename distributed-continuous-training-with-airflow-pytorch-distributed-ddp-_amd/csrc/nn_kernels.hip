@@ -31,6 +31,57 @@ __global__ __launch_bounds__(256) void loss_kernel(const void* logits, int lbf16
   for (int row = blockIdx.x * blockDim.x + threadIdx.x; row < M; row += gridDim.x * blockDim.x) {
     const size_t base = (size_t)row * C;
     const int y = labels[row];
+    if (C <= 8) {
+      // heads of <= 8 classes: the row's logits are loaded once, unconditionally (class slots past C
+      // re-read column C-1 and are masked), then every pass runs from registers; the generic loop below
+      // re-reads memory per pass and its guarded loads drain the load queue (s_waitcnt vmcnt(0)).
+      float z[8];
+      if (lbf16) {
+        const uint16_t* lg = reinterpret_cast<const uint16_t*>(logits) + base;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) z[c] = bf16_to_f32(lg[c < C ? c : C - 1]);
+      } else {
+        const float* lg = reinterpret_cast<const float*>(logits) + base;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) z[c] = lg[c < C ? c : C - 1];
+      }
+      float mx = z[0], zy = z[0];
+      int am = 0;
+#pragma unroll
+      for (int c = 1; c < 8; ++c)
+        if (c < C && z[c] > mx) { mx = z[c]; am = c; }
+#pragma unroll
+      for (int c = 1; c < 8; ++c)
+        if (c == y) zy = z[c];
+      c_acc += (am == y) ? 1.f : 0.f;
+      if (loss_kind == 0) {
+        float e[8], s = 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          e[c] = c < C ? __expf(z[c] - mx) : 0.f;
+          s += e[c];
+        }
+        l_acc += mx + __logf(s) - zy;
+        if (dlogits) {
+          const float rs = 1.f / s;
+#pragma unroll
+          for (int c = 0; c < 8; ++c)
+            if (c < C) st_any(dlogits, base + c, (e[c] * rs - (c == y ? 1.f : 0.f)) * grad_scale, lbf16);
+        }
+      } else {
+        float acc = 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          if (c < C) {
+            const float d = z[c] - (c == y ? 1.f : 0.f);
+            acc += d * d;
+            if (dlogits) st_any(dlogits, base + c, 2.f * d * grad_scale / (float)C, lbf16);
+          }
+        }
+        l_acc += acc / (float)C;
+      }
+      continue;
+    }
     float mx = -3.402823466e+38f;
     int am = 0;
     for (int c = 0; c < C; ++c) {
