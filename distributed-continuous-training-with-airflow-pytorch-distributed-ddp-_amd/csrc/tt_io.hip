@@ -82,12 +82,24 @@ __device__ __forceinline__ float wsum(float v) {
 
 // per-sample chain shared by both kernels: lane = dimension d
 struct HeadFwd {
-  float xhat, rstd, z;
-  float logit[CMAX];
+  float xhat, rstd, z, lnw;
+  float logit[CMAX], w[CMAX];  // w[k] = head W[k][d]
 };
 
 __device__ __forceinline__ HeadFwd head_chain(const HeadArgs& a, int b, int d) {
   HeadFwd r;
+  // parameter loads first and unconditionally (class slots past C re-read class C-1 and are masked), so
+  // their latency hides under the token stream; loads guarded by k < C compiled to branches that each
+  // drained the load queue (s_waitcnt vmcnt(0))
+  r.lnw = a.ln_w[d];
+  const float lnb = a.ln_b[d];
+  float bk[CMAX];
+#pragma unroll
+  for (int k = 0; k < CMAX; ++k) {
+    const int kc = k < a.C ? k : a.C - 1;
+    r.w[k] = a.W[kc * D + d];
+    bk[k] = a.bias[kc];
+  }
   // mean over tokens with 16-byte loads: lane (tq = lane >> 4, dq = lane & 15) sums dims 4dq..4dq+3
   // of tokens tq, tq + 4, ...; then lane d fetches its dimension from lane d / 4 (tq = 0)
   const float* hb = a.h + (size_t)b * a.T * D;
@@ -108,15 +120,16 @@ __device__ __forceinline__ HeadFwd head_chain(const HeadArgs& a, int b, int d) {
   const float dv = p - mean;
   r.rstd = rsqrtf(wsum(dv * dv) * (1.f / D) + a.eps);
   r.xhat = dv * r.rstd;
-  r.z = r.xhat * a.ln_w[d] + a.ln_b[d];
+  r.z = r.xhat * r.lnw + lnb;
 #pragma unroll
-  for (int k = 0; k < CMAX; ++k) r.logit[k] = (k < a.C) ? wsum(r.z * a.W[k * D + d]) + a.bias[k] : -3.402823466e+38f;
+  for (int k = 0; k < CMAX; ++k) r.logit[k] = (k < a.C) ? wsum(r.z * r.w[k]) + bk[k] : -3.402823466e+38f;
   return r;
 }
 
 __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6), d = threadIdx.x & 63;
   if (b >= a.B) return;
+  const int yb = (int)a.y[b];
   const HeadFwd r = head_chain(a, b, d);
   if (d == 0) {
     float m = r.logit[0];
@@ -125,7 +138,6 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
     float se = 0.f;
 #pragma unroll
     for (int k = 0; k < CMAX; ++k) se += (k < a.C) ? __expf(r.logit[k] - m) : 0.f;
-    const int yb = (int)a.y[b];
     float ly = 0.f;
 #pragma unroll
     for (int k = 0; k < CMAX; ++k) ly = (k == yb) ? r.logit[k] : ly;
@@ -143,6 +155,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
 #pragma unroll
   for (int k = 0; k < CMAX; ++k) { gW[k] = 0.f; gbias[k] = 0.f; }
   if (live) {
+    const int yb = (int)a.y[b];
+    const float dls = a.dloss[0];
     const HeadFwd r = head_chain(a, b, d);
     float m = r.logit[0];
 #pragma unroll
@@ -150,19 +164,18 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
     float se = 0.f;
 #pragma unroll
     for (int k = 0; k < CMAX; ++k) se += (k < a.C) ? __expf(r.logit[k] - m) : 0.f;
-    const float scale = a.dloss[0] / a.B, inv = 1.f / se;
-    const int yb = (int)a.y[b];
+    const float scale = dls / a.B, inv = 1.f / se;
     float dz = 0.f;
 #pragma unroll
     for (int k = 0; k < CMAX; ++k) {
       const float dl = (k < a.C) ? (__expf(r.logit[k] - m) * inv - (k == yb ? 1.f : 0.f)) * scale : 0.f;
       gW[k] = dl * r.z;
       gbias[k] = dl;
-      if (k < a.C) dz = fmaf(dl, a.W[k * D + d], dz);
+      dz = fmaf(dl, r.w[k], dz);  // dl = 0 past C
     }
     gw = dz * r.xhat;
     gb = dz;
-    const float g = dz * a.ln_w[d];
+    const float g = dz * r.lnw;
     const float m1 = wsum(g) * (1.f / D), m2 = wsum(g * r.xhat) * (1.f / D);
     const float dp = r.rstd * (g - m1 - r.xhat * m2) * (1.f / a.T);
     // broadcast over tokens with 16-byte stores: lane (tq, dq) writes dims 4dq..4dq+3 of tokens tq, tq + 4, ...
