@@ -109,6 +109,11 @@ class ModelCheckpoint:
                     del_path = self.kth_best_model_path
                     self.best_k_models.pop(del_path, None)
                 path = self._unique_path(metrics, del_path)
+                if math.isnan(cur):
+                    # Lightning 2.1 _update_best_and_save: a NaN score is stored as the worst value,
+                    # so it can never be the "best" checkpoint once a real score arrives
+                    cur = float("inf") if self.mode == "min" else float("-inf")
+                    self.current_score = cur
                 self.best_k_models[path] = cur
                 reverse = self.mode == "max"
                 ordered = sorted(self.best_k_models.items(), key=lambda kv: kv[1], reverse=not reverse)

@@ -16,7 +16,10 @@ next to the trainer, in CI, or anywhere without an Azure subscription:
   response is discarded; requests, errors and latency are counted);
 * :class:`EndpointServer` serves an endpoint over HTTP - ``POST /score``, ``GET /`` (state and
   per-deployment statistics) - plus an admin API (``PUT /deployments/<name>``, ``DELETE
-  /deployments/<name>``, ``PUT /traffic``), optionally behind the endpoint key (``auth_mode=key``);
+  /deployments/<name>``, ``PUT /traffic``).  The admin API ALWAYS needs the endpoint key (the
+  Azure control plane it imitates is authenticated) and only loads packages that resolve inside
+  the server's ``package_root``; the scoring routes need the key too unless the server is started
+  with ``require_key=False`` (``--no-require-key``);
 * :class:`LocalMLClient` is the subset of ``azure.ai.ml.MLClient`` that :mod:`deploy.azure` drives
   (``online_endpoints`` / ``online_deployments``), backed by in-process endpoints or by a running
   server's admin API, so ``force_deploy`` and ``automated_rollout`` run unchanged against a live
@@ -28,6 +31,7 @@ from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import hmac
 import importlib.util
 import json
 import os
@@ -98,10 +102,11 @@ class Deployment:
 class LocalEndpoint:
     """Deployments + traffic / mirror maps with Azure's routing semantics."""
 
-    def __init__(self, name: str, auth_mode: str = "key", seed: int = 0):
+    def __init__(self, name: str, auth_mode: str = "key", seed: int = 0, key: Optional[str] = None):
         self.name = name
         self.auth_mode = auth_mode
-        self.key = uuid.uuid4().hex if auth_mode == "key" else None
+        # the key guards the admin API whatever the scoring auth mode is
+        self.key = key or uuid.uuid4().hex
         self.deployments: Dict[str, Deployment] = {}
         self.traffic: Dict[str, int] = {}
         self.mirror_traffic: Dict[str, int] = {}
@@ -205,10 +210,11 @@ def _make_handler(srv: "EndpointServer"):
             n = int(self.headers.get("Content-Length") or 0)
             return self.rfile.read(n) if n else b""
 
-        def _authorized(self) -> bool:
-            if not srv.require_key or ep.key is None:
+        def _authorized(self, admin: bool = False) -> bool:
+            if not admin and not (srv.require_key and ep.auth_mode == "key"):
                 return True
-            if self.headers.get("Authorization", "") == f"Bearer {ep.key}":
+            given = self.headers.get("Authorization", "").encode()
+            if hmac.compare_digest(given, f"Bearer {ep.key}".encode()):
                 return True
             self._send(401, {"error": "missing or invalid endpoint key"})
             return False
@@ -244,7 +250,7 @@ def _make_handler(srv: "EndpointServer"):
             self._run(go)
 
         def do_PUT(self):
-            if not self._authorized():
+            if not self._authorized(admin=True):
                 return
             path = self.path.rstrip("/")
             try:
@@ -253,8 +259,8 @@ def _make_handler(srv: "EndpointServer"):
                 return self._send(400, {"error": "body is not JSON"})
             if path.startswith("/deployments/"):
                 name = path[len("/deployments/"):]
-                return self._run(lambda: (200, ep.add_deployment(name, body["package_dir"],
-                                                                 body.get("scoring_script", "score.py")).snapshot(),
+                return self._run(lambda: (200, ep.add_deployment(name, srv.resolve_package(body["package_dir"]),
+                                                                 _script_name(body.get("scoring_script"))).snapshot(),
                                           None))
             if path == "/traffic":
                 def go():
@@ -264,7 +270,7 @@ def _make_handler(srv: "EndpointServer"):
             self._send(404, {"error": f"no route {self.path}"})
 
         def do_DELETE(self):
-            if not self._authorized():
+            if not self._authorized(admin=True):
                 return
             path = self.path.rstrip("/")
             if path.startswith("/deployments/"):
@@ -279,12 +285,36 @@ def _make_handler(srv: "EndpointServer"):
     return H
 
 
+def _script_name(name: Optional[str]) -> str:
+    """The scoring script is a file name inside the package, never a path."""
+    name = name or "score.py"
+    if os.path.basename(name) != name or not name.endswith(".py") or name.startswith("."):
+        raise EndpointError(400, f"invalid scoring script name {name!r}")
+    return name
+
+
 class EndpointServer:
-    def __init__(self, endpoint: LocalEndpoint, host: str = "127.0.0.1", port: int = 0, require_key: bool = False):
+    """HTTP face of a :class:`LocalEndpoint`.
+
+    ``package_root``: the directory admin-API deployments must resolve into (symlinks followed);
+    ``None`` refuses every admin-API deployment.  ``require_key``: scoring routes need the key as
+    well (admin routes always do)."""
+
+    def __init__(self, endpoint: LocalEndpoint, host: str = "127.0.0.1", port: int = 0, require_key: bool = True,
+                 package_root: Optional[str] = None):
         self.endpoint = endpoint
         self.require_key = require_key
+        self.package_root = os.path.realpath(package_root) if package_root else None
         self.httpd = ThreadingHTTPServer((host, port), _make_handler(self))
         self.thread: Optional[threading.Thread] = None
+
+    def resolve_package(self, package_dir: str) -> str:
+        if self.package_root is None:
+            raise EndpointError(403, "this endpoint server accepts no packages over the admin API (no package root)")
+        p = os.path.realpath(package_dir)
+        if os.path.commonpath([self.package_root, p]) != self.package_root:
+            raise EndpointError(403, f"package {package_dir!r} is outside the server's package root")
+        return p
 
     @property
     def url(self) -> str:
@@ -450,14 +480,21 @@ def main(argv=None) -> int:
     ap.add_argument("--port", type=int, default=5001)
     ap.add_argument("--package", default=os.environ.get("DEPLOY_DIR"), help="initial deployment (100 %% traffic)")
     ap.add_argument("--deployment", default=os.environ.get("DEPLOYMENT_NAME", "blue"))
-    ap.add_argument("--require-key", action="store_true")
+    ap.add_argument("--no-require-key", dest="require_key", action="store_false",
+                    help="serve /score and GET / without the key (the admin API always needs it)")
+    ap.add_argument("--package-root", default=os.environ.get("DCT_PACKAGE_ROOT"),
+                    help="admin-API deployments must resolve inside this directory "
+                         "(default: DCT_PACKAGE_ROOT, else the parent of --package)")
     a = ap.parse_args(argv)
-    ep = LocalEndpoint(a.name)
+    # a shared key lets the deploy DAGs (DCT_LOCAL_ENDPOINT_KEY) drive the admin API
+    ep = LocalEndpoint(a.name, key=os.environ.get("DCT_LOCAL_ENDPOINT_KEY") or None)
     if a.package:
         ep.add_deployment(a.deployment, a.package)
         ep.set_traffic({a.deployment: 100})
-    srv = EndpointServer(ep, a.host, a.port, a.require_key)
-    print(f"endpoint {a.name} on {srv.url}" + (f" (key {ep.key})" if a.require_key else ""), flush=True)
+    root = a.package_root or (os.path.dirname(os.path.abspath(a.package)) if a.package else None)
+    srv = EndpointServer(ep, a.host, a.port, a.require_key, package_root=root)
+    shown = ep.key if not os.environ.get("DCT_LOCAL_ENDPOINT_KEY") else "from DCT_LOCAL_ENDPOINT_KEY"
+    print(f"endpoint {a.name} on {srv.url} (key {shown}; package root {root})", flush=True)
     try:
         srv.httpd.serve_forever()
     except KeyboardInterrupt:

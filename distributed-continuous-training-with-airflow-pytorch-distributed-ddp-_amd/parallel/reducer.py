@@ -17,7 +17,9 @@ Two executors with one interface:
     all-reduces on a dedicated comm HIP stream, ordered after the producing backward kernels
     by HIP events, joined into the compute stream once at ``finalize``.
   * ``TorchBucketReducer`` - ``torch.distributed`` async all-reduces (gloo on CPU: the
-    plumbing config of BASELINE.json; or nccl), averaged at ``finalize``.
+    plumbing config of BASELINE.json; or nccl), averaged at ``finalize``.  With
+    ``host_staging`` (gloo process group, gradients on the GPU: several ranks sharing one device,
+    where RCCL refuses to run) each bucket goes through host memory.
 """
 from __future__ import annotations
 
@@ -67,10 +69,11 @@ def plan_buckets(numels: Sequence[int], elem_bytes: int = 4, bucket_cap_bytes: i
 
 
 class TorchBucketReducer:
-    def __init__(self, flat_grad: torch.Tensor, plan: BucketPlan, world_size: int):
+    def __init__(self, flat_grad: torch.Tensor, plan: BucketPlan, world_size: int, host_staging: bool = False):
         self.flat = flat_grad
         self.plan = plan
         self.world = world_size
+        self.host_staging = bool(host_staging)
         self.expected = [0] * len(plan.offsets)
         for b in plan.param_bucket:
             self.expected[b] += 1
@@ -85,7 +88,8 @@ class TorchBucketReducer:
         off, cnt = self.plan.offsets[b], self.plan.counts[b]
         view = self.flat[off: off + cnt]
         if self.world > 1:
-            self.works.append((dist.all_reduce(view, op=dist.ReduceOp.SUM, async_op=True), view))
+            buf = view.cpu() if self.host_staging else view  # D2H copy waits for the producing kernels
+            self.works.append((dist.all_reduce(buf, op=dist.ReduceOp.SUM, async_op=True), view, buf))
 
     def mark_ready(self, param_idx: int, stream=None) -> int:
         b = self.plan.param_bucket[param_idx]
@@ -103,9 +107,11 @@ class TorchBucketReducer:
         while self.next < len(self.expected):
             self._launch(self.next)
             self.next += 1
-        for w, view in self.works:
+        for w, view, buf in self.works:
             w.wait()
-            view.div_(self.world)
+            buf.div_(self.world)
+            if buf is not view:
+                view.copy_(buf)
         self.works = []
 
     @property

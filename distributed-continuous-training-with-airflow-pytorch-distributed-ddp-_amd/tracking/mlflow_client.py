@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import json
 import os
+import re
 import shutil
 import time
 import uuid
@@ -105,6 +106,10 @@ def _sort_runs(runs: List[Run], order_by) -> List[Run]:
 
 
 # ----------------------------------------------------------------------------- file store
+_EXP_ID_RE = re.compile(r"[0-9]{1,18}")
+_RUN_ID_RE = re.compile(r"[0-9a-f]{32}")
+
+
 class FileStore:
     def __init__(self, root: str):
         self.root = os.path.abspath(root)
@@ -165,9 +170,27 @@ class FileStore:
         self._write_exp_meta(exp_id, name)
         return exp_id
 
+    @staticmethod
+    def _check_exp_id(exp_id) -> str:
+        """Experiment ids are decimal strings (MLflow's file store); anything else could walk out
+        of the store root when joined into a path."""
+        exp_id = str(exp_id)
+        if not _EXP_ID_RE.fullmatch(exp_id):
+            raise ValueError(f"invalid experiment id {exp_id!r}")
+        return exp_id
+
+    @staticmethod
+    def _check_run_id(run_id) -> str:
+        """Run ids are 32 lowercase hex characters (uuid4().hex, as MLflow creates them)."""
+        run_id = str(run_id)
+        if not _RUN_ID_RE.fullmatch(run_id):
+            raise ValueError(f"invalid run id {run_id!r}")
+        return run_id
+
     def _run_dir(self, run_id: str, exp_id: Optional[str] = None) -> str:
+        run_id = self._check_run_id(run_id)
         if exp_id is not None:
-            return os.path.join(self.root, exp_id, run_id)
+            return os.path.join(self.root, self._check_exp_id(exp_id), run_id)
         for e in os.listdir(self.root):
             d = os.path.join(self.root, e, run_id)
             if os.path.isdir(d):
@@ -175,6 +198,9 @@ class FileStore:
         raise KeyError(f"run {run_id} not found")
 
     def create_run(self, experiment_id: str, run_name: str = "", tags: Optional[Dict[str, str]] = None) -> RunInfo:
+        experiment_id = self._check_exp_id(experiment_id)
+        if not os.path.exists(os.path.join(self.root, experiment_id, "meta.yaml")):
+            raise KeyError(f"experiment {experiment_id} not found")
         run_id = uuid.uuid4().hex
         d = os.path.join(self.root, experiment_id, run_id)
         for sub in ("metrics", "params", "tags", "artifacts"):
@@ -218,6 +244,7 @@ class FileStore:
             f.write(str(value))
 
     def log_batch(self, run_id: str, metrics=(), params=(), tags=()):
+        self._run_dir(run_id)  # validates the id and that the run exists, even for an empty batch
         for m in metrics:
             self.log_metric(run_id, m["key"], m["value"], m.get("timestamp"), m.get("step", 0))
         for p in params:
@@ -263,7 +290,7 @@ class FileStore:
         return Run(info, data)
 
     def metric_history(self, run_id: str, key: str) -> List[Dict[str, Any]]:
-        p = os.path.join(self._run_dir(run_id), "metrics", key)
+        p = os.path.join(self._run_dir(run_id), "metrics", self._safe_key(key))
         out = []
         if os.path.exists(p):
             with open(p) as f:
@@ -275,11 +302,11 @@ class FileStore:
     def search_runs(self, experiment_ids: Sequence[str], order_by=None, max_results: int = 1000) -> List[Run]:
         runs = []
         for e in experiment_ids:
-            d = os.path.join(self.root, str(e))
+            d = os.path.join(self.root, self._check_exp_id(e))
             if not os.path.isdir(d):
                 continue
             for r in os.listdir(d):
-                if os.path.exists(os.path.join(d, r, "meta.yaml")):
+                if _RUN_ID_RE.fullmatch(r) and os.path.exists(os.path.join(d, r, "meta.yaml")):
                     run = self.get_run(r)
                     runs.append(run)
         return _sort_runs(runs, order_by)[:max_results]

@@ -65,8 +65,10 @@ def make_handler(state: _State):
             return json.loads(self.rfile.read(n) or b"{}") if n else {}
 
         def _art_path(self, rel):
-            p = os.path.abspath(os.path.join(state.artifacts_root, unquote(rel)))
-            if not p.startswith(state.artifacts_root):
+            root = state.artifacts_root
+            p = os.path.abspath(os.path.join(root, unquote(rel)))
+            # component-wise containment: a plain prefix test lets "../mlartifacts_x/f" through
+            if os.path.commonpath([root, p]) != root:
                 raise PermissionError(rel)
             return p
 
@@ -108,6 +110,10 @@ def make_handler(state: _State):
                 return self._err(404, "ENDPOINT_NOT_FOUND", u.path)
             except KeyError as e:
                 return self._err(404, "RESOURCE_DOES_NOT_EXIST", str(e))
+            except PermissionError as e:
+                return self._err(403, "PERMISSION_DENIED", f"path outside the artifact root: {e}")
+            except ValueError as e:
+                return self._err(400, "INVALID_PARAMETER_VALUE", str(e))
             except Exception as e:  # noqa: BLE001
                 return self._err(500, "INTERNAL_ERROR", repr(e))
 
@@ -145,6 +151,10 @@ def make_handler(state: _State):
                 return self._err(404, "ENDPOINT_NOT_FOUND", u.path)
             except KeyError as e:
                 return self._err(404, "RESOURCE_DOES_NOT_EXIST", str(e))
+            except PermissionError as e:
+                return self._err(403, "PERMISSION_DENIED", f"path outside the artifact root: {e}")
+            except ValueError as e:
+                return self._err(400, "INVALID_PARAMETER_VALUE", str(e))
             except Exception as e:  # noqa: BLE001
                 return self._err(500, "INTERNAL_ERROR", repr(e))
 
@@ -166,6 +176,8 @@ def make_handler(state: _State):
                         remaining -= len(chunk)
                 os.replace(p + ".part", p)
                 return self._send(200, {})
+            except PermissionError as e:
+                return self._err(403, "PERMISSION_DENIED", f"path outside the artifact root: {e}")
             except Exception as e:  # noqa: BLE001
                 return self._err(500, "INTERNAL_ERROR", repr(e))
 

@@ -432,11 +432,17 @@ class AutogradEngine(_EngineBase):
         self.plan = plan_buckets(numels, 4, bucket_cap_bytes, first_bucket_bytes)
         self.reducer = None
         if ctx.is_distributed:
-            if dev.type == "cuda":
+            if dev.type == "cuda" and ctx.backend == "nccl":
                 comm = init_native_comm(ctx)
                 self.reducer = NativeBucketReducer(comm, self.flat_g, self.plan)
             else:
-                self.reducer = TorchBucketReducer(self.flat_g, self.plan, ctx.world_size)
+                # gloo: the CPU plumbing config, or GPU ranks sharing one device (init_distributed
+                # falls back to gloo there because RCCL refuses it) - buckets staged through host
+                # memory, which no HIP graph can capture
+                staged = dev.type == "cuda"
+                self.reducer = TorchBucketReducer(self.flat_g, self.plan, ctx.world_size, host_staging=staged)
+                if staged:
+                    self._graph_failed = True
             self._hooks = []
             for i, p in enumerate(params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
@@ -510,9 +516,16 @@ class AutogradEngine(_EngineBase):
         return loss
 
     def train_step(self, rows: torch.Tensor, batch_idx: int):
+        """One optimizer step.  ``last_step_mode`` tells the Trainer how training_step ran:
+        ``eager``; ``captured`` (traced into the step graph, then replayed - the tensors it logged
+        are the graph's static outputs); ``replayed`` (training_step and self.log did NOT run)."""
         rows_d = rows.to(self.device)
+        self.last_step_mode = "eager"
         if self._graph_ok(rows_d.numel()):
+            self.last_step_mode = "replayed" if getattr(self, "_graph", None) is not None else "captured"
             loss = self._graph_step(rows_d, batch_idx)
+            if getattr(self, "_graph_failed", False):
+                self.last_step_mode = "eager"
         elif getattr(self, "_warming", False):
             # graph warmup steps run on the capture stream (torch's capture recipe): autograd's
             # AccumulateGrad nodes then already live on that stream when the step is captured

@@ -264,6 +264,7 @@ class Trainer:
     # ------------------------------------------------------------------ fit
     def fit(self, model, train_dataloaders=None, val_dataloaders=None, ckpt_path: Optional[str] = None):
         self._model = model
+        self._graph_step_logs = None
         self.ctx = init_distributed(self.accelerator, self.strategy.backend, self.strategy.timeout_s)
         object.__setattr__(model, "_trainer", self)
         seed = int(os.environ.get("PL_GLOBAL_SEED", "0"))
@@ -369,7 +370,15 @@ class Trainer:
             rows = rows_all[bi * B: (bi + 1) * B]
             self._cur_batch_size = len(rows)
             self._step_logs = {}
-            eng.train_step(rows, bi)
+            loss = eng.train_step(rows, bi)
+            mode = getattr(eng, "last_step_mode", "eager")
+            if mode == "captured":
+                # what training_step logged while it was traced into the step graph are the graph's
+                # static outputs: every replay refreshes them, so they stand for later steps too
+                self._graph_step_logs = dict(self._step_logs)
+            elif mode == "replayed" and not self._step_logs:
+                # a replay runs no Python: reuse the captured logs, else the step's loss
+                self._step_logs = dict(getattr(self, "_graph_step_logs", None) or {"train_loss": (loss, True)})
             self.global_step += 1
             self._maybe_fault(self.global_step)
             if self.global_step % self.log_every_n_steps == 0 and self._step_logs:

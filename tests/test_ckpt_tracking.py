@@ -166,3 +166,56 @@ def test_rest_client_against_tracking_server(tmp_path, proxy):
         assert hist is None
     finally:
         srv.stop()
+
+
+def test_model_checkpoint_nan_first_score_does_not_lock_in(tmp_path):
+    """Lightning 2.1 stores a NaN monitor value as +inf (min mode): the next real score replaces it."""
+    cb = ModelCheckpoint(dirpath=str(tmp_path), filename="weather-best-{epoch:02d}-{val_loss:.2f}", monitor="val_loss",
+                         mode="min", save_top_k=1, save_last=False)
+
+    def save(p):
+        open(p, "w").write("x")
+
+    cb.on_validation_end({"val_loss": float("nan"), "epoch": 0}, save, True, 0)
+    assert cb.best_model_score == float("inf")
+    cb.on_validation_end({"val_loss": 0.9, "epoch": 1}, save, True, 1)
+    assert cb.best_model_path.endswith("epoch=01-val_loss=0.90.ckpt") and cb.best_model_score == pytest.approx(0.9)
+    assert sorted(os.listdir(tmp_path)) == ["weather-best-epoch=01-val_loss=0.90.ckpt"]
+    (tmp_path / "max").mkdir()
+    cbx = ModelCheckpoint(dirpath=str(tmp_path / "max"), monitor="val_acc", mode="max", save_top_k=1)
+    cbx.on_validation_end({"val_acc": float("nan"), "epoch": 0}, save, True, 0)
+    assert cbx.best_model_score == float("-inf")
+    cbx.on_validation_end({"val_acc": 0.5, "epoch": 1}, save, True, 1)
+    assert cbx.best_model_score == pytest.approx(0.5)
+
+
+def test_tracking_server_rejects_paths_outside_its_roots(tmp_path):
+    """Artifact paths are contained component-wise (a sibling dir sharing the root's name prefix is
+    outside), and experiment / run ids must be MLflow-shaped before they reach a path."""
+    import requests
+
+    root = tmp_path / "srv"
+    srv = TrackingServer(str(root), serve_artifacts=True).start()
+    try:
+        api = srv.url + "/api/2.0"
+        sibling = str(srv.state.artifacts_root) + "_x"
+        r = requests.put(api + "/mlflow-artifacts/artifacts/%2e%2e/" + os.path.basename(sibling) + "/f", data=b"x",
+                         timeout=30)
+        assert r.status_code == 403 and not os.path.exists(os.path.join(sibling, "f"))
+        r = requests.put(api + "/mlflow-artifacts/artifacts/%2e%2e/%2e%2e/evil", data=b"x", timeout=30)
+        assert r.status_code == 403 and not (tmp_path / "evil").exists()
+        r = requests.post(api + "/mlflow/runs/create", json={"experiment_id": "../.."}, timeout=30)
+        assert r.status_code == 400
+        r = requests.post(api + "/mlflow/runs/create", json={"experiment_id": "977"}, timeout=30)
+        assert r.status_code == 404
+        for bad in ("../../0", "0" * 31 + "/", "a" * 33):
+            r = requests.post(api + "/mlflow/runs/log-batch", json={"run_id": bad, "metrics": []}, timeout=30)
+            assert r.status_code == 400, bad
+            r = requests.get(api + "/mlflow/runs/get", params={"run_id": bad}, timeout=30)
+            assert r.status_code == 400, bad
+        r = requests.post(api + "/mlflow/runs/search", json={"experiment_ids": ["../"]}, timeout=30)
+        assert r.status_code == 400
+        ok = requests.put(api + "/mlflow-artifacts/artifacts/1/abc/artifacts/m.ckpt", data=b"y", timeout=30)
+        assert ok.status_code == 200
+    finally:
+        srv.stop()

@@ -116,7 +116,7 @@ def test_http_server_admin_api_key_auth_and_remote_client(tmp_path):
     m1 = _package(str(tmp_path / "p1"), 0)
     m2 = _package(str(tmp_path / "p2"), 1)
     ep = LocalEndpoint("weather-api")
-    srv = EndpointServer(ep, require_key=True).start()
+    srv = EndpointServer(ep, require_key=True, package_root=str(tmp_path)).start()
     try:
         assert requests.post(srv.url + "/score", json={"data": X}, timeout=30).status_code == 401
         client = LocalMLClient(base_url=srv.url, key=ep.key)
@@ -158,9 +158,10 @@ def test_deploy_dags_against_a_local_endpoint_server(tmp_path, monkeypatch):
     mc.log_batch(run, metrics=[{"key": "val_loss", "value": 0.3, "step": 1}])
     mc.log_artifact(run, str(tmp_path / "trained" / "model.ckpt"), "best_checkpoints")
     ep = LocalEndpoint("weather-api")
-    srv = EndpointServer(ep).start()
+    srv = EndpointServer(ep, require_key=False, package_root=str(tmp_path)).start()
     try:
         for k, v in {"MLFLOW_TRACKING_URI": uri, "DCT_AZURE_BACKEND": "local", "DCT_LOCAL_ENDPOINT_URL": srv.url,
+                     "DCT_LOCAL_ENDPOINT_KEY": ep.key,
                      "ENDPOINT_NAME": "weather-api", "DEPLOY_DIR": str(tmp_path / "deploy"),
                      "DCT_ROLLOUT_WAIT_S": "0"}.items():
             monkeypatch.setenv(k, v)
@@ -175,3 +176,45 @@ def test_deploy_dags_against_a_local_endpoint_server(tmp_path, monkeypatch):
         assert torch.allclose(torch.tensor(r.json()["probabilities"]), _probs(model, X), atol=1e-6)
     finally:
         srv.stop()
+
+
+def test_admin_api_always_needs_the_key_and_stays_inside_the_package_root(tmp_path):
+    """The admin API loads and runs a package's score.py: it must need the endpoint key even when
+    scoring is open, and must refuse packages outside the server's package root."""
+    _package(str(tmp_path / "root" / "p1"), 0)
+    _package(str(tmp_path / "outside"), 1)
+    ep = LocalEndpoint("weather-api")
+    srv = EndpointServer(ep, require_key=False, package_root=str(tmp_path / "root")).start()
+    try:
+        body = {"package_dir": str(tmp_path / "root" / "p1")}
+        assert requests.put(srv.url + "/deployments/blue", json=body, timeout=30).status_code == 401
+        bad = {"Authorization": "Bearer " + "0" * 32}
+        assert requests.put(srv.url + "/deployments/blue", json=body, headers=bad, timeout=30).status_code == 401
+        assert requests.delete(srv.url + "/deployments/blue", timeout=30).status_code == 401
+        assert requests.put(srv.url + "/traffic", json={"traffic": {}}, timeout=30).status_code == 401
+        hdr = {"Authorization": f"Bearer {ep.key}"}
+        for pkg in (str(tmp_path / "outside"), str(tmp_path / "root" / ".." / "outside")):
+            r = requests.put(srv.url + "/deployments/green", json={"package_dir": pkg}, headers=hdr, timeout=30)
+            assert r.status_code == 403 and "green" not in ep.deployments
+        os.symlink(str(tmp_path / "outside"), str(tmp_path / "root" / "link"))
+        r = requests.put(srv.url + "/deployments/green", json={"package_dir": str(tmp_path / "root" / "link")},
+                         headers=hdr, timeout=30)
+        assert r.status_code == 403
+        r = requests.put(srv.url + "/deployments/blue", json={**body, "scoring_script": "../x.py"}, headers=hdr,
+                         timeout=30)
+        assert r.status_code == 400
+        assert requests.put(srv.url + "/deployments/blue", json=body, headers=hdr, timeout=30).status_code == 200
+        assert requests.put(srv.url + "/traffic", json={"traffic": {"blue": 100}}, headers=hdr,
+                            timeout=30).status_code == 200
+        # scoring is open on this server (require_key=False)
+        assert requests.post(srv.url + "/score", json={"data": X}, timeout=30).status_code == 200
+    finally:
+        srv.stop()
+    closed = EndpointServer(LocalEndpoint("x")).start()  # no package root: admin deployments refused
+    try:
+        hdr = {"Authorization": f"Bearer {closed.endpoint.key}"}
+        r = requests.put(closed.url + "/deployments/blue", json={"package_dir": str(tmp_path / "outside")},
+                         headers=hdr, timeout=30)
+        assert r.status_code == 403
+    finally:
+        closed.stop()

@@ -113,3 +113,29 @@ def test_ddp_step_path_world1_matches_persistent(fused_update, graph, monkeypatc
     assert torch.allclose(l0, l1, atol=1e-5), (l0 - l1).abs().max()
     assert (p0 - p1).abs().max() < 1e-3 and (p0 - p1).abs().median() < 1e-6
     assert torch.allclose(m0, m1, atol=1e-5)
+
+
+def test_autograd_engine_logs_train_loss_after_graph_replays(monkeypatch):
+    """From step GRAPH_WARMUP on the autograd engine replays its captured step graph, so
+    training_step / self.log never run again: train_loss must still be logged every 5 steps and
+    equal the eager run's values."""
+    def run(graph: str):
+        monkeypatch.setenv("DCT_GRAPH", graph)
+        tl, vl = _loaders(400)
+        torch.manual_seed(0)
+        model = MLPClassifier(5, hidden=(64,), dropout=0.0)
+        logger = InMemoryLogger()
+        tr = Trainer(max_epochs=1, accelerator="gpu", engine="autograd", logger=logger, log_every_n_steps=5,
+                     num_sanity_val_steps=0, verbose=False)
+        tr.fit(model, tl, vl)
+        assert tr.engine.name == "autograd" and tr.engine.graph_used == (graph == "1")
+        return logger.history("train_loss"), tr.callback_metrics["train_loss"]
+
+    hist_g, last_g = run("1")
+    hist_e, last_e = run("0")
+    steps = [s for s, _ in hist_g]
+    assert steps == [s for s, _ in hist_e] == list(range(4, 80, 5))
+    vg = torch.tensor([v for _, v in hist_g])
+    ve = torch.tensor([v for _, v in hist_e])
+    assert torch.isfinite(vg).all() and torch.allclose(vg, ve, atol=1e-4), (vg - ve).abs().max()
+    assert abs(last_g - last_e) < 1e-4
