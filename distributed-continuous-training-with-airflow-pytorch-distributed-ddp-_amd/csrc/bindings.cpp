@@ -51,6 +51,91 @@ struct MlpPlan {
   const dct::MlpShape* sh() const { return reinterpret_cast<const dct::MlpShape*>(shape.data()); }
 };
 
+
+// Validated MlpArgs of a training launch (the kernels trust their arguments).
+static dct::MlpArgs make_train_args(const MlpPlan& plan, uintptr_t p, uintptr_t mo, uintptr_t vo, uintptr_t grad_out,
+                                    uintptr_t X, int ldx, uintptr_t Y, uintptr_t idx, int n_items, int B, int steps,
+                                    int t0, float lr, float b1, float b2, float eps, float wd, float dropout,
+                                    uint32_t seed, uint32_t step_base, uintptr_t loss_out, int mode, int loss_kind,
+                                    uintptr_t step_counter, uintptr_t cursor, uintptr_t prof, uintptr_t pending,
+                                    uintptr_t stage, uintptr_t xg_recv, uintptr_t xg_peers, int xg_world, int xg_rank,
+                                    uintptr_t xg_status, int64_t xg_timeout, int xg_poll) {
+  if (!plan.supported) throw std::runtime_error("MLP too large for the fused kernel");
+  if (steps < 1 || n_items < 1 || B < 1) throw std::invalid_argument("empty launch");
+  if (!cursor && (int64_t)(steps - 1) * B >= n_items) throw std::invalid_argument("more steps than batches");
+  dct::MlpArgs a{};
+  a.p = P<float>(p);
+  a.m = P<float>(mo);
+  a.v = P<float>(vo);
+  a.grad_out = P<float>(grad_out);
+  a.X = P<const float>(X);
+  a.ldx = ldx;
+  a.Y = P<const int>(Y);
+  a.idx = P<const int>(idx);
+  a.n_items = n_items;
+  a.B = B;
+  a.steps = steps;
+  a.t0 = t0;
+  a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd;
+  a.dropout = dropout;
+  a.seed = seed;
+  a.step_base = step_base;
+  a.loss_out = P<float>(loss_out);
+  a.mode = mode;
+  a.loss_kind = loss_kind;
+  a.step_counter = P<int>(step_counter);
+  a.cursor = P<int>(cursor);
+  a.prof = P<unsigned long long>(prof);
+  a.pending = P<int>(pending);
+  a.stage = P<uint32_t>(stage);
+  a.xg_recv = P<unsigned long long>(xg_recv);
+  a.xg_peers = P<unsigned long long* const>(xg_peers);
+  a.xg_world = xg_world;
+  a.xg_rank = xg_rank;
+  a.xg_status = P<unsigned int>(xg_status);
+  a.xg_timeout = xg_timeout;
+  a.xg_poll = xg_poll;
+  if (xg_world > 1 && !(plan.use_wave && dct_mlp_wave_supported(plan.sh()->dims, plan.sh()->L, B)))
+    throw std::invalid_argument("in-kernel all-reduce needs the single-wave kernel");
+  if (pending && (mode != 1 || !plan.use_wave || !mo || !vo))
+    throw std::invalid_argument("update-then-grad needs grad mode, m/v and the single-wave kernel");
+  if (cursor && mode != 1) throw std::invalid_argument("cursor is only valid in grad mode");
+  if (mode == 1 && !grad_out) throw std::invalid_argument("grad mode needs grad_out");
+  if (mode == 1 && steps != 1) throw std::invalid_argument("grad mode runs exactly one step");
+  return a;
+}
+
+static void launch_train(const MlpPlan& plan, const dct::MlpArgs& a, uintptr_t stream) {
+  const dct::MlpShape* sh = plan.sh();
+  if (plan.use_wave && dct_mlp_wave_supported(sh->dims, sh->L, a.B))
+    check(dct_mlp_wave_train(sh->dims, sh->L, &a, reinterpret_cast<void*>(stream)), "mlp_wave_train");
+  else
+    check(dct_mlp_train(plan.shape.data(), &a, reinterpret_cast<void*>(stream)), "mlp_train");
+}
+
+// A training launch with every operand bound once (FusedMLPKernel.prepare_train validates
+// them in Python): run(first_step, steps, stream) only offsets the index list and the loss
+// slots, so a persistent epoch launch costs one short positional call instead of ~35
+// keyword arguments and the Python-side operand checks.
+struct MlpLaunch {
+  MlpPlan plan;
+  dct::MlpArgs base{};
+  int64_t n_items = 0;   // index entries bound at base.idx
+  int64_t loss_len = 0;  // loss slots bound at base.loss_out (0 = none)
+  void run(int first_step, int steps, uintptr_t stream) const {
+    if (first_step < 0 || steps < 1) throw std::invalid_argument("MlpLaunch.run: bad step range");
+    const int64_t off = (int64_t)first_step * base.B;
+    if (off + (int64_t)(steps - 1) * base.B >= n_items) throw std::invalid_argument("MlpLaunch.run: past the index list");
+    if (base.loss_out && first_step + steps > loss_len) throw std::invalid_argument("MlpLaunch.run: past the loss buffer");
+    dct::MlpArgs a = base;
+    a.idx = base.idx + off;
+    a.n_items = (int)(n_items - off);
+    a.steps = steps;
+    if (base.loss_out) a.loss_out = base.loss_out + first_step;
+    launch_train(plan, a, stream);
+  }
+};
+
 PYBIND11_MODULE(_dct_native, m) {
   m.doc() = "MI355X-native kernels and runtime for dct_amd";
 
@@ -68,6 +153,10 @@ PYBIND11_MODULE(_dct_native, m) {
   m.def("synchronize", []() { check((int)hipDeviceSynchronize(), "hipDeviceSynchronize"); });
 
   // ------------------------------------------------------------------ fused MLP
+  py::class_<MlpLaunch>(m, "MlpLaunch")
+      .def("run", &MlpLaunch::run, py::arg("first_step"), py::arg("steps"), py::arg("stream"))
+      .def_readonly("n_items", &MlpLaunch::n_items)
+      .def_readonly("loss_len", &MlpLaunch::loss_len);
   py::class_<MlpPlan>(m, "MlpPlan")
       .def(py::init<const std::vector<int>&, int>(), py::arg("dims"), py::arg("bmax"))
       .def_readonly("supported", &MlpPlan::supported)
@@ -85,53 +174,11 @@ PYBIND11_MODULE(_dct_native, m) {
              int loss_kind, uintptr_t step_counter, uintptr_t cursor, uintptr_t prof, uintptr_t pending,
              uintptr_t stage, uintptr_t stream, uintptr_t xg_recv, uintptr_t xg_peers, int xg_world, int xg_rank,
              uintptr_t xg_status, int64_t xg_timeout, int xg_poll) {
-            if (!plan.supported) throw std::runtime_error("MLP too large for the fused kernel");
-            if (steps < 1 || n_items < 1 || B < 1) throw std::invalid_argument("empty launch");
-            if (!cursor && (int64_t)(steps - 1) * B >= n_items) throw std::invalid_argument("more steps than batches");
-            dct::MlpArgs a{};
-            a.p = P<float>(p);
-            a.m = P<float>(mo);
-            a.v = P<float>(vo);
-            a.grad_out = P<float>(grad_out);
-            a.X = P<const float>(X);
-            a.ldx = ldx;
-            a.Y = P<const int>(Y);
-            a.idx = P<const int>(idx);
-            a.n_items = n_items;
-            a.B = B;
-            a.steps = steps;
-            a.t0 = t0;
-            a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd;
-            a.dropout = dropout;
-            a.seed = seed;
-            a.step_base = step_base;
-            a.loss_out = P<float>(loss_out);
-            a.mode = mode;
-            a.loss_kind = loss_kind;
-            a.step_counter = P<int>(step_counter);
-            a.cursor = P<int>(cursor);
-            a.prof = P<unsigned long long>(prof);
-            a.pending = P<int>(pending);
-            a.stage = P<uint32_t>(stage);
-            a.xg_recv = P<unsigned long long>(xg_recv);
-            a.xg_peers = P<unsigned long long* const>(xg_peers);
-            a.xg_world = xg_world;
-            a.xg_rank = xg_rank;
-            a.xg_status = P<unsigned int>(xg_status);
-            a.xg_timeout = xg_timeout;
-            a.xg_poll = xg_poll;
-            if (xg_world > 1 && !(plan.use_wave && dct_mlp_wave_supported(plan.sh()->dims, plan.sh()->L, B)))
-              throw std::invalid_argument("in-kernel all-reduce needs the single-wave kernel");
-            if (pending && (mode != 1 || !plan.use_wave || !mo || !vo))
-              throw std::invalid_argument("update-then-grad needs grad mode, m/v and the single-wave kernel");
-            if (cursor && mode != 1) throw std::invalid_argument("cursor is only valid in grad mode");
-            if (mode == 1 && !grad_out) throw std::invalid_argument("grad mode needs grad_out");
-            if (mode == 1 && steps != 1) throw std::invalid_argument("grad mode runs exactly one step");
-            const dct::MlpShape* sh = plan.sh();
-            if (plan.use_wave && dct_mlp_wave_supported(sh->dims, sh->L, B))
-              check(dct_mlp_wave_train(sh->dims, sh->L, &a, reinterpret_cast<void*>(stream)), "mlp_wave_train");
-            else
-              check(dct_mlp_train(plan.shape.data(), &a, reinterpret_cast<void*>(stream)), "mlp_train");
+            const dct::MlpArgs a = make_train_args(plan, p, mo, vo, grad_out, X, ldx, Y, idx, n_items, B, steps, t0, lr,
+                                                   b1, b2, eps, wd, dropout, seed, step_base, loss_out, mode,
+                                                   loss_kind, step_counter, cursor, prof, pending, stage, xg_recv,
+                                                   xg_peers, xg_world, xg_rank, xg_status, xg_timeout, xg_poll);
+            launch_train(plan, a, stream);
           },
           py::arg("p"), py::arg("m"), py::arg("v"), py::arg("grad_out"), py::arg("X"), py::arg("ldx"), py::arg("Y"),
           py::arg("idx"), py::arg("n_items"), py::arg("B"), py::arg("steps"), py::arg("t0"), py::arg("lr"),
@@ -140,6 +187,27 @@ PYBIND11_MODULE(_dct_native, m) {
           py::arg("cursor"), py::arg("prof") = 0, py::arg("pending") = 0, py::arg("stage") = 0,
           py::arg("stream") = 0, py::arg("xg_recv") = 0, py::arg("xg_peers") = 0, py::arg("xg_world") = 0,
           py::arg("xg_rank") = 0, py::arg("xg_status") = 0, py::arg("xg_timeout") = 200000000LL, py::arg("xg_poll") = 0)
+      .def(
+          "prepare_train",
+          [](const MlpPlan& plan, uintptr_t p, uintptr_t mo, uintptr_t vo, uintptr_t X, int ldx, uintptr_t Y,
+             uintptr_t idx, int n_items, int B, float lr, float b1, float b2, float eps, float wd, float dropout,
+             uint32_t seed, uintptr_t loss_out, int64_t loss_len, int loss_kind, uintptr_t step_counter,
+             uintptr_t xg_recv, uintptr_t xg_peers, int xg_world, int xg_rank, uintptr_t xg_status,
+             int64_t xg_timeout, int xg_poll) {
+            auto l = std::make_unique<MlpLaunch>(MlpLaunch{plan});
+            l->base = make_train_args(plan, p, mo, vo, 0, X, ldx, Y, idx, n_items, B, 1, 0, lr, b1, b2, eps, wd,
+                                      dropout, seed, 0, loss_out, 0, loss_kind, step_counter, 0, 0, 0, 0, xg_recv,
+                                      xg_peers, xg_world, xg_rank, xg_status, xg_timeout, xg_poll);
+            l->n_items = n_items;
+            l->loss_len = loss_out ? loss_len : 0;
+            return l;
+          },
+          py::arg("p"), py::arg("m"), py::arg("v"), py::arg("X"), py::arg("ldx"), py::arg("Y"), py::arg("idx"),
+          py::arg("n_items"), py::arg("B"), py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"),
+          py::arg("dropout"), py::arg("seed"), py::arg("loss_out"), py::arg("loss_len"), py::arg("loss_kind"),
+          py::arg("step_counter"), py::arg("xg_recv") = 0, py::arg("xg_peers") = 0, py::arg("xg_world") = 0,
+          py::arg("xg_rank") = 0, py::arg("xg_status") = 0, py::arg("xg_timeout") = 200000000LL,
+          py::arg("xg_poll") = 0)
       .def(
           "eval",
           [](const MlpPlan& plan, uintptr_t p, uintptr_t X, int ldx, uintptr_t Y, uintptr_t idx, int n_items,

@@ -32,6 +32,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "dct_common.h"
 #include "mlp_fused.h"
 
@@ -719,6 +721,321 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
   }
 }
 
+
+// ============================================================================ row-parallel
+// Row-parallel variant of the 2-layer train step (mode 0): ONE WAVE PER BATCH ROW.
+//
+// The single-wave kernel above is issue-bound, not latency-bound: one wave64 issues every
+// VALU instruction over 4 cycles on ONE SIMD16 of the CU, and a step is ~650 instructions
+// (~3k cycles, 1.35 us).  Here wave w (NW = 4 or 8 waves on the CU's 4 SIMDs; rows >= B idle) runs the
+// forward, loss and backward of batch row w only - per wave ~1/4 of the row-dependent work -
+// then the per-row gradients are summed through LDS (one s_barrier per step, rows added in
+// order 0..B-1 so every wave obtains the same bits) and every wave applies the identical Adam
+// update to its own register copy of the parameters (wave 0 alone writes them back).
+// Lane j still owns hidden unit j: W0[j][:], b0[j], Wout[:, j], bout[j < C] and their moments.
+// With XW > 0 wave 0 also runs the in-kernel xGMI exchange of the summed gradients (same
+// protocol and granule layout as xg_allreduce above) and hands the rank average to the other
+// waves through LDS behind a second barrier; a timeout is broadcast the same way, so all waves
+// leave the step loop together.
+template <int NW, int D0, int CM, bool EX, int XW>
+__global__ __launch_bounds__(64 * NW) void mlp_rows_kernel(WaveShape sh, MlpArgs a) {
+  constexpr int KG = D0 + 1 + CM + 1;         // per-lane gradients: W0 row, b0, Wout column, bout
+  constexpr int Q4 = (KG + 3) / 4;            // float4 groups per lane in the LDS slots
+  __shared__ float4 gslot[2][NW][Q4][64];  // [step parity][row][group][lane]
+  __shared__ float lslot[2][NW];           // per-row losses
+  __shared__ float4 gavg[XW > 0 ? Q4 : 1][64];  // rank-averaged gradients (XW > 0)
+  __shared__ int xabort;
+  const int j = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave = batch row (rows >= B idle)
+  const int d0 = EX ? D0 : sh.d0, H1 = sh.h1, C = EX ? CM : sh.C;
+  const bool own1 = j < H1;
+  constexpr bool XG = XW > 0;
+
+  // ---------------------------------------------------------------- parameters -> registers
+  float w0[D0], mw0[D0], vw0[D0];
+  float b0 = 0.f, mb0 = 0.f, vb0 = 0.f;
+  float wo[CM], mwo[CM], vwo[CM];
+  float bo = 0.f, mbo = 0.f, vbo = 0.f;
+#pragma unroll
+  for (int k = 0; k < D0; ++k) {
+    const bool ok = own1 && k < d0;
+    const int f = sh.woff[0] + j * d0 + k;
+    w0[k] = ok ? a.p[f] : 0.f;
+    mw0[k] = ok ? a.m[f] : 0.f;
+    vw0[k] = ok ? a.v[f] : 0.f;
+  }
+  if (own1) {
+    b0 = a.p[sh.boff[0] + j];
+    mb0 = a.m[sh.boff[0] + j];
+    vb0 = a.v[sh.boff[0] + j];
+  }
+#pragma unroll
+  for (int c = 0; c < CM; ++c) {
+    const bool ok = own1 && c < C;
+    const int f = sh.woff[1] + c * H1 + j;
+    wo[c] = ok ? a.p[f] : 0.f;
+    mwo[c] = ok ? a.m[f] : 0.f;
+    vwo[c] = ok ? a.v[f] : 0.f;
+  }
+  if (j < C) {
+    bo = a.p[sh.boff[1] + j];
+    mbo = a.m[sh.boff[1] + j];
+    vbo = a.v[sh.boff[1] + j];
+  }
+  int t0 = a.t0;
+  uint32_t step_base = a.step_base;
+  if (a.step_counter) {
+    t0 = __hip_atomic_load(a.step_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    step_base = (uint32_t)t0;
+  }
+  const int B = a.B;
+
+  // ---------------------------------------------------------------- row prefetch
+  // lane k < D0 holds x[row][k], lane D0 the label.  Depth 2: the row index of step s+2 and the
+  // values of step s+1 are issued at the top of step s, so no load wait lands inside a step.
+  auto load_idx = [&](int sbatch) -> int {
+    int qi = sbatch * B + w;
+    qi = (qi < a.n_items && qi >= 0) ? qi : 0;
+    return a.idx[qi];
+  };
+  auto load_val = [&](int sbatch, int ridx) -> uint32_t {
+    const bool live = (w < min(B, a.n_items - sbatch * B));
+    const bool isx = j < D0;
+    const bool ok = live && (isx ? j < d0 : j == D0);
+    const int k = (isx && j < d0) ? j : 0;
+    const uint32_t* src = isx ? reinterpret_cast<const uint32_t*>(a.X) + (size_t)ridx * a.ldx + k
+                              : reinterpret_cast<const uint32_t*>(a.Y) + ridx;
+    const uint32_t v = *src;
+    return ok ? v : 0u;
+  };
+  int ridx_a = load_idx(0);
+  uint32_t cur = load_val(0, ridx_a);
+  ridx_a = load_idx(1);
+
+  const float keep_scale = (a.dropout > 0.f) ? 1.0f / (1.0f - a.dropout) : 1.0f;
+  const float l2b1 = log2f(a.b1), l2b2 = log2f(a.b2);
+  const uint32_t drop_thr = (uint32_t)(a.dropout * 4294967296.0);
+  constexpr int XWN = XW > 0 ? XW : 1;
+  __amdgpu_buffer_rsrc_t prs[XWN];
+  __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(a.xg_recv, 0, 0, 0x00020000);
+  constexpr int KX = D0 + CM + 2 + ((D0 + CM) & 1);  // exchange granules per lane (even)
+  if (XG && w == 0) {
+    const int nbytes = 2 * a.xg_world * KX * 64 * 8;
+    rrs = __builtin_amdgcn_make_buffer_rsrc(a.xg_recv, 0, nbytes, 0x00020000);
+#pragma unroll
+    for (int q = 0; q < XWN; ++q) {
+      void* pq = (q < a.xg_world) ? (void*)a.xg_peers[q] : (void*)a.xg_recv;
+      prs[q] = __builtin_amdgcn_make_buffer_rsrc(pq, 0, nbytes, 0x00020000);
+    }
+  }
+  int done = a.steps;
+
+  for (int s = 0; s < a.steps; ++s) {
+    const int sb = s;
+    const int bs = min(B, a.n_items - sb * B);
+    const bool live = w < bs;
+    const uint32_t gstep = step_base + (uint32_t)s;
+    const int par = s & 1;
+    const uint32_t nxt = load_val(sb + 1, ridx_a);
+    const int ridx_b = load_idx(sb + 2);
+
+    float x[D0];
+#pragma unroll
+    for (int k = 0; k < D0; ++k) x[k] = __int_as_float(__builtin_amdgcn_readlane((int)cur, k));
+    const int y = __builtin_amdgcn_readlane((int)cur, D0);
+
+    // ---- layer 0 for this row: h = dropout(relu(W0[j] . x + b0))
+    float h;
+    {
+      float z = b0;
+#pragma unroll
+      for (int k = 0; k < D0; ++k) z = fmaf(w0[k], x[k], z);
+      z = fmaxf(z, 0.f);
+      if (drop_thr) {
+        const uint32_t hkey = (a.seed * 0x9E3779B1u) ^ (gstep * 0x85EBCA77u);
+        const uint32_t r = wave_hash(hkey ^ ((uint32_t)(w * 64 + j) * 0xC2B2AE3Du));
+        z = (r < drop_thr) ? 0.f : z * keep_scale;
+      }
+      h = own1 ? z : 0.f;
+    }
+    // ---- output layer: logits[c] = sum_j Wout[c][j] h_j + bout[c]  (cross-lane, wave-uniform)
+    float zc[CM];
+#pragma unroll
+    for (int c = 0; c < CM; ++c) zc[c] = wo[c] * h;
+    wave_sum_n(zc);
+#pragma unroll
+    for (int c = 0; c < CM; ++c) zc[c] += rl(bo, c);
+
+    // ---- loss + dlogits of this row (wave-uniform)
+    float dz[CM];
+    float lb = 0.f;
+    const float inv = __builtin_amdgcn_rcpf((float)(bs > 0 ? bs : 1));  // bs <= 8: exact
+    if (a.loss_kind == 0) {
+      if constexpr (EX && CM == 2) {
+        // two classes: softmax = logistic of the margin; one exp, one log, one rcp
+        const float d = zc[1] - zc[0];
+        const float t = __builtin_amdgcn_exp2f(-fabsf(d) * 1.4426950408889634f);  // exp(-|d|)
+        const float se = 1.f + t;
+        const float rs = __builtin_amdgcn_rcpf(se);
+        const float mx = fmaxf(zc[0], zc[1]);
+        const float lse = mx + __builtin_amdgcn_logf(se) * 0.69314718055994531f;
+        const float p1 = d >= 0.f ? rs : t * rs;  // softmax prob of class 1
+        lb = lse - (y == 1 ? zc[1] : zc[0]);
+        dz[1] = (p1 - (y == 1 ? 1.f : 0.f)) * inv;
+        dz[0] = -dz[1];
+      } else {
+        float mx = -3.402823466e+38f;
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+          if (c < C) mx = fmaxf(mx, zc[c]);
+        float e[CM], se = 0.f, zy = 0.f;
+#pragma unroll
+        for (int c = 0; c < CM; ++c) {
+          e[c] = (c < C) ? __builtin_amdgcn_exp2f((zc[c] - mx) * 1.4426950408889634f) : 0.f;
+          se += e[c];
+          zy = (c == y) ? zc[c] : zy;
+        }
+        lb = mx + __builtin_amdgcn_logf(se) * 0.69314718055994531f - zy;
+        const float rs = __builtin_amdgcn_rcpf(se);
+#pragma unroll
+        for (int c = 0; c < CM; ++c) dz[c] = (e[c] * rs - (c == y ? 1.f : 0.f)) * inv;
+      }
+    } else {
+      const float sc = 2.f / (float)C;
+#pragma unroll
+      for (int c = 0; c < CM; ++c) {
+        const float d = (c < C) ? zc[c] - (c == y ? 1.f : 0.f) : 0.f;
+        lb += d * d;
+        dz[c] = d * sc * inv;
+      }
+      lb *= 1.f / (float)C;
+    }
+#pragma unroll
+    for (int c = 0; c < CM; ++c) dz[c] = live ? dz[c] : 0.f;
+    lb = live ? lb : 0.f;
+
+    // ---- backward of this row (lane-local) -> per-lane gradient vector
+    float g[Q4 * 4];
+    {
+      float gsum = 0.f;
+#pragma unroll
+      for (int c = 0; c < CM; ++c) gsum = fmaf(dz[c], wo[c], gsum);
+      const float dh = (h > 0.f) ? gsum * keep_scale : 0.f;
+#pragma unroll
+      for (int k = 0; k < D0; ++k) g[k] = dh * x[k];
+      g[D0] = dh;
+#pragma unroll
+      for (int c = 0; c < CM; ++c) g[D0 + 1 + c] = dz[c] * h;
+      float gbo = 0.f;
+#pragma unroll
+      for (int c = 0; c < CM; ++c) gbo = (c == j) ? dz[c] : gbo;
+      g[D0 + 1 + CM] = gbo;
+#pragma unroll
+      for (int k = KG; k < Q4 * 4; ++k) g[k] = 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < Q4; ++q) gslot[par][w][q][j] = make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+    if (j == 0) lslot[par][w] = lb;
+    __syncthreads();
+    // ---- batch gradient: rows summed in order 0..NW-1 (identical bits in every wave)
+#pragma unroll
+    for (int q = 0; q < Q4; ++q) {
+      float4 acc = gslot[par][0][q][j];
+#pragma unroll
+      for (int r = 1; r < NW; ++r) {
+        const float4 v = gslot[par][r][q][j];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+      g[4 * q] = acc.x; g[4 * q + 1] = acc.y; g[4 * q + 2] = acc.z; g[4 * q + 3] = acc.w;
+    }
+    float bl = 0.f;
+    if (w == 0) {
+#pragma unroll
+      for (int r = 0; r < NW; ++r) bl += lslot[par][r];
+      bl *= inv;
+    }
+    if (XG) {  // rank average of the batch gradients: wave 0 exchanges, LDS hands it to the rest
+      static_assert(!XG || KX >= KG, "granules cover the gradients");
+      if (w == 0) {
+        float gv[KX];
+#pragma unroll
+        for (int k = 0; k < KX; ++k) gv[k] = (k < KG) ? g[k] : 0.f;
+        // the bias slot carries the batch loss in lane 63 (lanes >= C own no bias)
+        gv[KG - 1] = (j < C) ? g[KG - 1] : (j == 63 ? bl : 0.f);
+        const bool ok = xg_allreduce<KX, XWN>(gv, a, prs, rrs, gstep, j);
+#pragma unroll
+        for (int q = 0; q < Q4; ++q) {
+          float4 o;
+          o.x = (4 * q + 0 < KG) ? gv[4 * q + 0] : 0.f;
+          o.y = (4 * q + 1 < KG) ? gv[4 * q + 1] : 0.f;
+          o.z = (4 * q + 2 < KG) ? gv[4 * q + 2] : 0.f;
+          o.w = (4 * q + 3 < KG) ? gv[4 * q + 3] : 0.f;
+          gavg[q][j] = o;
+        }
+        if (j == 0) xabort = ok ? 0 : 1;
+        bl = rl(gv[KG - 1], 63);
+      }
+      __syncthreads();
+      if (xabort) {
+        done = s;
+        break;
+      }
+#pragma unroll
+      for (int q = 0; q < Q4; ++q) {
+        const float4 v = gavg[q][j];
+        g[4 * q] = v.x; g[4 * q + 1] = v.y; g[4 * q + 2] = v.z; g[4 * q + 3] = v.w;
+      }
+      if (j >= C) g[KG - 1] = 0.f;  // lane 63's loss slot is not a gradient
+    }
+    if (w == 0 && j == 0 && a.loss_out) a.loss_out[s] = bl;
+
+    // ---- Adam (every wave, identical inputs -> identical parameters)
+    {
+      const int t = t0 + s + 1;
+      const float step_size = a.lr * __builtin_amdgcn_rcpf(1.f - pow_t(l2b1, (float)t));
+      const float rbc2 = __builtin_amdgcn_rsqf(1.f - pow_t(l2b2, (float)t));
+      if (own1) {
+#pragma unroll
+        for (int k = 0; k < D0; ++k)
+          if (k < d0) adam1(w0[k], g[k], mw0[k], vw0[k], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+        adam1(b0, g[D0], mb0, vb0, a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+#pragma unroll
+        for (int c = 0; c < CM; ++c)
+          if (c < C) adam1(wo[c], g[D0 + 1 + c], mwo[c], vwo[c], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+      }
+      if (j < C) adam1(bo, g[D0 + 1 + CM], mbo, vbo, a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+    }
+    cur = nxt;
+    ridx_a = ridx_b;
+  }
+  if (w != 0) return;
+  if (a.step_counter && j == 0)
+    __hip_atomic_store(a.step_counter, t0 + done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // ---- write back params + moments (wave 0; every wave holds the same values)
+#pragma unroll
+  for (int k = 0; k < D0; ++k) {
+    if (own1 && k < d0) {
+      const int f = sh.woff[0] + j * d0 + k;
+      a.p[f] = w0[k]; a.m[f] = mw0[k]; a.v[f] = vw0[k];
+    }
+  }
+  if (own1) {
+    const int f = sh.boff[0] + j;
+    a.p[f] = b0; a.m[f] = mb0; a.v[f] = vb0;
+#pragma unroll
+    for (int c = 0; c < CM; ++c) {
+      if (c < C) {
+        const int f2 = sh.woff[1] + c * H1 + j;
+        a.p[f2] = wo[c]; a.m[f2] = mwo[c]; a.v[f2] = vwo[c];
+      }
+    }
+  }
+  if (j < C) {
+    const int f = sh.boff[1] + j;
+    a.p[f] = bo; a.m[f] = mbo; a.v[f] = vbo;
+  }
+}
+
 }  // namespace dct
 
 namespace {
@@ -739,6 +1056,34 @@ hipError_t launch_wave_d0(const WaveShape& sh, const MlpArgs& a, hipStream_t st)
   if (sh.d0 <= 8) return launch_wave<L, BMAX, 8, 4, false, XW>(sh, a, st);
   if (sh.d0 <= 16) return launch_wave<L, BMAX, 16, 4, false, XW>(sh, a, st);
   return hipErrorInvalidValue;
+}
+
+template <int D0, int CM, bool EX, int XW>
+hipError_t launch_rows(const WaveShape& sh, const MlpArgs& a, hipStream_t st) {
+  if (a.B <= 4)
+    hipLaunchKernelGGL((dct::mlp_rows_kernel<4, D0, CM, EX, XW>), dim3(1), dim3(64 * 4), 0, st, sh, a);
+  else
+    hipLaunchKernelGGL((dct::mlp_rows_kernel<8, D0, CM, EX, XW>), dim3(1), dim3(64 * 8), 0, st, sh, a);
+  return hipGetLastError();
+}
+
+template <int XW>
+hipError_t launch_rows_d0(const WaveShape& sh, const MlpArgs& a, hipStream_t st) {
+  if (sh.C > 4) return hipErrorInvalidValue;
+  if (sh.d0 == 5 && sh.C == 2) return launch_rows<5, 2, true, XW>(sh, a, st);  // WeatherClassifier
+  if (sh.d0 <= 8) return launch_rows<8, 4, false, XW>(sh, a, st);
+  if (sh.d0 <= 16) return launch_rows<16, 4, false, XW>(sh, a, st);
+  return hipErrorInvalidValue;
+}
+
+// the row-parallel kernel takes plain train-mode launches of 2-layer nets (DCT_MLP_ROWS=0: off)
+bool rows_eligible(int L, const MlpArgs& a) {
+  static const bool enabled = [] {
+    const char* e = std::getenv("DCT_MLP_ROWS");
+    return !(e && e[0] == '0');
+  }();
+  return enabled && L == 2 && a.mode == 0 && !a.cursor && !a.pending && !a.stage && !a.prof && a.B >= 1 &&
+         a.B <= 8 && a.m && a.v;
 }
 
 template <int BMAX>
@@ -790,8 +1135,14 @@ int dct_mlp_wave_train(const int* dims, int L, const dct::MlpArgs* a, void* stre
     if (L != 2 || a->mode != 0 || !a->xg_recv || !a->xg_peers || !a->xg_status || a->xg_world > dct::XG_MAXW ||
         a->xg_rank < 0 || a->xg_rank >= a->xg_world || a->cursor || a->pending)
       return (int)hipErrorInvalidValue;
+    if (rows_eligible(L, *a)) {
+      if (a->xg_world <= 2) return (int)launch_rows_d0<2>(sh, *a, st);
+      if (a->xg_world <= 4) return (int)launch_rows_d0<4>(sh, *a, st);
+      return (int)launch_rows_d0<8>(sh, *a, st);
+    }
     return (int)(a->B <= 4 ? launch_wave_xg<4>(sh, *a, st) : launch_wave_xg<8>(sh, *a, st));
   }
+  if (rows_eligible(L, *a)) return (int)launch_rows_d0<0>(sh, *a, st);
   if (L == 2) return (int)(a->B <= 4 ? launch_wave_d0<2, 4, 0>(sh, *a, st) : launch_wave_d0<2, 8, 0>(sh, *a, st));
   return (int)(a->B <= 4 ? launch_wave_d0<3, 4, 0>(sh, *a, st) : launch_wave_d0<3, 8, 0>(sh, *a, st));
 }

@@ -206,6 +206,7 @@ class FusedMLPEngine(_EngineBase):
         vl = math.ceil(max(1, len(self.val_rows)) / self.ctx.world_size)
         self.val_idx = torch.zeros(max(1, vl), dtype=torch.int32, device=dev)
         self.eval_acc = torch.zeros(2, dtype=torch.float32, device=dev)
+        self._bound = None  # launches bound to the previous tables
 
     def steps_per_epoch(self) -> int:
         n_local = math.ceil(len(self.train_rows) / self.ctx.world_size)
@@ -219,13 +220,20 @@ class FusedMLPEngine(_EngineBase):
         return rows.numel()
 
     # ------------------------------------------------------------------ train
-    def _launch_persistent(self, n_items: int, steps: int, loss_out: torch.Tensor, idx_off: int = 0):
-        a = self.adam
-        self.kernel.train(self.p, self.m, self.v, self.X, self.Y, self.idx[idx_off:], n_items=n_items,
-                          batch=self.B, steps=steps, t0=0, lr=a["lr"], betas=a["betas"], eps=a["eps"],
-                          weight_decay=a["weight_decay"], dropout=self.dropout, seed=self.rank_seed,
-                          loss_out=loss_out, loss=self.loss, step_counter=self.step_counter,
-                          xg=self.xg, xg_timeout_s=getattr(self, "xg_timeout_s", 20.0))
+    def _bound_launch(self, n_items: int, loss_out: torch.Tensor):
+        """The persistent train launch bound to (index list, loss buffer, exchange): validated once,
+        then every run_steps call is one short native call (ops/fused_mlp.py BoundTrain)."""
+        key = (n_items, loss_out.data_ptr(), loss_out.numel())
+        bl = getattr(self, "_bound", None)
+        if bl is None or self._bound_key != key:
+            a = self.adam
+            bl = self.kernel.prepare_train(self.p, self.m, self.v, self.X, self.Y, self.idx, n_items=n_items,
+                                           batch=self.B, lr=a["lr"], betas=a["betas"], eps=a["eps"],
+                                           weight_decay=a["weight_decay"], dropout=self.dropout, seed=self.rank_seed,
+                                           loss_out=loss_out, loss=self.loss, step_counter=self.step_counter,
+                                           xg=self.xg, xg_timeout_s=getattr(self, "xg_timeout_s", 20.0))
+            self._bound, self._bound_key = bl, key
+        return bl
 
     @property
     def step_mode(self) -> str:
@@ -245,13 +253,12 @@ class FusedMLPEngine(_EngineBase):
         if (first_step + steps - 1) * self.B >= n_items or loss_out.numel() < first_step + steps:
             raise ValueError("step range exceeds the epoch's batches / loss buffer")
         if not self.ddp or self.xg is not None:
+            bl = self._bound_launch(n_items, loss_out)
             chunk = self.steps_per_launch or steps
             s = 0
             while s < steps:
                 k = min(chunk, steps - s)
-                b = first_step + s
-                off = b * self.B
-                self._launch_persistent(n_items - off, k, loss_out[b: b + k], idx_off=off)
+                bl.run(first_step + s, k)
                 s += k
             return
         self.cursor.fill_(first_step)
@@ -376,6 +383,7 @@ class FusedMLPEngine(_EngineBase):
     def xg_disable(self):
         """Leave the in-kernel exchange: replicas re-synced from rank 0, RCCL step path from now on."""
         self.xg = None
+        self._bound = None
         if self.comm is None:
             raise RuntimeError("in-kernel exchange disabled and no RCCL communicator is available to fall back to")
         torch.cuda.synchronize(self.device)

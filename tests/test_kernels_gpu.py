@@ -818,3 +818,38 @@ def test_gemm_splitk_workspace_fixup_deterministic(M, N, K, accumulate, cuda, mo
     monkeypatch.delenv("DCT_GEMM_SPLIT_WS")
     ca = run()
     assert torch.allclose(c1, ca, atol=1e-3 * math.sqrt(K), rtol=1e-4)
+
+
+@pytest.mark.parametrize("dims", [[5, 64, 2], [5, 128, 128, 2]])
+def test_bound_train_launch_matches_keyword_launch(dims, cuda):
+    """BoundTrain (operands bound once, run(first_step, steps)) trains exactly like the keyword
+    launch over the same slices of the index list, including the loss slots and step counter."""
+    torch.manual_seed(1)
+    P = mlp_num_params(dims)
+    k = FusedMLPKernel(dims, bmax=4)
+    N = 512
+    X = torch.randn(N, dims[0], device=cuda)
+    Y = torch.randint(0, dims[-1], (N,), device=cuda, dtype=torch.int32)
+    idx = torch.randperm(N, device=cuda).to(torch.int32)
+    p0 = torch.randn(P, device=cuda) * 0.2
+    runs = []
+    for bound in (False, True):
+        p, m, v = p0.clone(), torch.zeros(P, device=cuda), torch.zeros(P, device=cuda)
+        ctr = torch.zeros(1, dtype=torch.int32, device=cuda)
+        loss = torch.full((64,), -1.0, device=cuda)
+        if bound:
+            bl = k.prepare_train(p, m, v, X, Y, idx, n_items=N, batch=4, lr=0.01, dropout=0.2, seed=7,
+                                 loss_out=loss, step_counter=ctr)
+            bl.run(0, 5)
+            bl.run(5, 20)
+            with pytest.raises(Exception):
+                bl.run(60, 10)  # past the loss buffer
+        else:
+            for first, steps in ((0, 5), (5, 20)):
+                k.train(p, m, v, X, Y, idx[first * 4:], n_items=N - first * 4, batch=4, steps=steps, t0=0, lr=0.01,
+                        dropout=0.2, seed=7, loss_out=loss[first:first + steps], step_counter=ctr)
+        torch.cuda.synchronize()
+        runs.append((p, m, v, loss, ctr))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+    assert int(runs[1][4]) == 25 and bool((runs[1][3][:25] > 0).all()) and bool((runs[1][3][25:] == -1).all())
