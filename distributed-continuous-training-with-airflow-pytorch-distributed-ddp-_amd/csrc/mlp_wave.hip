@@ -725,62 +725,74 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
 // ============================================================================ row-parallel
 // Row-parallel variant of the 2-layer train step (mode 0): ONE WAVE PER BATCH ROW.
 //
-// The single-wave kernel above is issue-bound, not latency-bound: one wave64 issues every
-// VALU instruction over 4 cycles on ONE SIMD16 of the CU, and a step is ~650 instructions
-// (~3k cycles, 1.35 us).  Here wave w (NW = 4 or 8 waves on the CU's 4 SIMDs; rows >= B idle) runs the
-// forward, loss and backward of batch row w only - per wave ~1/4 of the row-dependent work -
-// then the per-row gradients are summed through LDS (one s_barrier per step, rows added in
-// order 0..B-1 so every wave obtains the same bits) and every wave applies the identical Adam
-// update to its own register copy of the parameters (wave 0 alone writes them back).
-// Lane j still owns hidden unit j: W0[j][:], b0[j], Wout[:, j], bout[j < C] and their moments.
-// With XW > 0 wave 0 also runs the in-kernel xGMI exchange of the summed gradients (same
-// protocol and granule layout as xg_allreduce above) and hands the rank average to the other
-// waves through LDS behind a second barrier; a timeout is broadcast the same way, so all waves
-// leave the step loop together.
-template <int NW, int D0, int CM, bool EX, int XW>
-__global__ __launch_bounds__(64 * NW) void mlp_rows_kernel(WaveShape sh, MlpArgs a) {
-  constexpr int KG = D0 + 1 + CM + 1;         // per-lane gradients: W0 row, b0, Wout column, bout
-  constexpr int Q4 = (KG + 3) / 4;            // float4 groups per lane in the LDS slots
-  __shared__ float4 gslot[2][NW][Q4][64];  // [step parity][row][group][lane]
-  __shared__ float lslot[2][NW];           // per-row losses
-  __shared__ float4 gavg[XW > 0 ? Q4 : 1][64];  // rank-averaged gradients (XW > 0)
-  __shared__ int xabort;
+// The single-wave kernel above is issue-bound: one wave64 issues every VALU instruction over
+// 4 cycles on ONE SIMD16 of the CU, and a step is ~650 instructions (~3k cycles, 1.35 us).
+// Here wave w (NW = 4 or 8 waves spread over the CU's 4 SIMDs; rows >= B idle) runs the
+// forward, loss and backward of batch row w only, then the per-row gradients meet in LDS:
+//   * XW == 0: parameter slot k (lane j owns W0[j][:], b0[j], Wout[:, j], bout[j < C] as
+//     slots 0..KG-1) belongs to wave k % NW.  After barrier 1 the owner sums slot k over the
+//     rows (order 0..NW-1), runs Adam on it (moments live only in the owner) and publishes the
+//     new value; after barrier 2 every wave reads the parameters it does not own.  Adam's
+//     ~12 VALU ops and 2 quarter-rate transcendentals per slot are spread over the SIMDs.
+//   * XW > 0: every wave sums all slots; wave 0 runs the in-kernel xGMI exchange of the batch
+//     gradients (same protocol and granule layout as xg_allreduce above) and hands the rank
+//     average (plus a timeout flag, so all waves leave the loop together) to the others
+//     through LDS behind barrier 2; every wave then applies the identical Adam update to its
+//     own register copy.
+// Row sums run in a fixed order, so the result is bit-identical across waves and ranks.
+template <int NW, int KG, bool XG>
+struct RowsLds {
+  float gslot[2][NW][KG][64];    // [step parity][row][slot][lane] per-row gradients
+  float lslot[2][NW];            // per-row losses
+  float pslot[XG ? 1 : KG][64];  // parameters published by their owner (XW == 0)
+  float gavg[XG ? KG : 1][64];   // rank-averaged gradients (XW > 0)
+  int xabort;
+};
+
+// The whole per-wave program with the wave id W as a compile-time constant, so slot ownership
+// (k % NW == W) folds away instead of becoming a branch per slot.
+template <int NW, int W, int D0, int CM, bool EX, int XW>
+__device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs& a,
+                                              RowsLds<NW, D0 + CM + 2, (XW > 0)>& L) {
+  constexpr int KG = D0 + 1 + CM + 1;  // per-lane parameter slots: W0 row, b0, Wout column, bout
+  constexpr int KB = D0;               // slot of b0
+  constexpr int KO = D0 + 1;           // first slot of the Wout column
+  constexpr int KC = D0 + 1 + CM;      // slot of bout (lanes < C)
+  constexpr bool XG = XW > 0;
+  auto& gslot = L.gslot;
+  auto& lslot = L.lslot;
+  auto& pslot = L.pslot;
+  auto& gavg = L.gavg;
+  auto& xabort = L.xabort;
   const int j = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave = batch row (rows >= B idle)
+  constexpr int w = W;  // wave = batch row
   const int d0 = EX ? D0 : sh.d0, H1 = sh.h1, C = EX ? CM : sh.C;
   const bool own1 = j < H1;
-  constexpr bool XG = XW > 0;
+
+  // lane j's slot k: live in this lane?  flat index in p/m/v
+  auto slot_live = [&](int k) -> bool {
+    if (k < KB) return own1 && k < d0;
+    if (k == KB) return own1;
+    if (k < KC) return own1 && (k - KO) < C;
+    return j < C;
+  };
+  auto slot_flat = [&](int k) -> int {
+    if (k < KB) return sh.woff[0] + j * d0 + (k < d0 ? k : 0);
+    if (k == KB) return sh.boff[0] + j;
+    if (k < KC) return sh.woff[1] + (k - KO) * H1 + j;
+    return sh.boff[1] + j;
+  };
+  auto owned = [](int k) constexpr -> bool { return XG || (k % NW) == W; };
 
   // ---------------------------------------------------------------- parameters -> registers
-  float w0[D0], mw0[D0], vw0[D0];
-  float b0 = 0.f, mb0 = 0.f, vb0 = 0.f;
-  float wo[CM], mwo[CM], vwo[CM];
-  float bo = 0.f, mbo = 0.f, vbo = 0.f;
+  float pr[KG], mr[KG], vr[KG];
 #pragma unroll
-  for (int k = 0; k < D0; ++k) {
-    const bool ok = own1 && k < d0;
-    const int f = sh.woff[0] + j * d0 + k;
-    w0[k] = ok ? a.p[f] : 0.f;
-    mw0[k] = ok ? a.m[f] : 0.f;
-    vw0[k] = ok ? a.v[f] : 0.f;
-  }
-  if (own1) {
-    b0 = a.p[sh.boff[0] + j];
-    mb0 = a.m[sh.boff[0] + j];
-    vb0 = a.v[sh.boff[0] + j];
-  }
-#pragma unroll
-  for (int c = 0; c < CM; ++c) {
-    const bool ok = own1 && c < C;
-    const int f = sh.woff[1] + c * H1 + j;
-    wo[c] = ok ? a.p[f] : 0.f;
-    mwo[c] = ok ? a.m[f] : 0.f;
-    vwo[c] = ok ? a.v[f] : 0.f;
-  }
-  if (j < C) {
-    bo = a.p[sh.boff[1] + j];
-    mbo = a.m[sh.boff[1] + j];
-    vbo = a.v[sh.boff[1] + j];
+  for (int k = 0; k < KG; ++k) {
+    const bool ok = slot_live(k);
+    const int f = ok ? slot_flat(k) : 0;
+    pr[k] = ok ? a.p[f] : 0.f;
+    mr[k] = (ok && owned(k)) ? a.m[f] : 0.f;
+    vr[k] = (ok && owned(k)) ? a.v[f] : 0.f;
   }
   int t0 = a.t0;
   uint32_t step_base = a.step_base;
@@ -791,26 +803,36 @@ __global__ __launch_bounds__(64 * NW) void mlp_rows_kernel(WaveShape sh, MlpArgs
   const int B = a.B;
 
   // ---------------------------------------------------------------- row prefetch
-  // lane k < D0 holds x[row][k], lane D0 the label.  Depth 2: the row index of step s+2 and the
-  // values of step s+1 are issued at the top of step s, so no load wait lands inside a step.
+  // Lane k < D0 fetches x[row][k], lane D0 the label.  The random row gathers miss L2, and a
+  // step (~0.5 us) is shorter than that latency, so loads run PF steps ahead: the row index of
+  // step s+2PF and the values of step s+PF are issued at step s, into ring registers indexed by
+  // s % PF.  The step loop is unrolled PF times so the ring never rotates through register moves
+  // (a move of a register with a load in flight would wait for that load).
+  // Lane j loads the index of row (j & 7): the loaded value is not wave-uniform, so the compiler
+  // keeps it in a VGPR instead of a v_readfirstlane right behind the load (which would wait on
+  // it); the row's index is picked with v_readlane when the value load is issued.
+  constexpr int PF = 4;
   auto load_idx = [&](int sbatch) -> int {
-    int qi = sbatch * B + w;
+    int qi = sbatch * B + (j & 7);
     qi = (qi < a.n_items && qi >= 0) ? qi : 0;
     return a.idx[qi];
   };
-  auto load_val = [&](int sbatch, int ridx) -> uint32_t {
-    const bool live = (w < min(B, a.n_items - sbatch * B));
-    const bool isx = j < D0;
-    const bool ok = live && (isx ? j < d0 : j == D0);
-    const int k = (isx && j < d0) ? j : 0;
-    const uint32_t* src = isx ? reinterpret_cast<const uint32_t*>(a.X) + (size_t)ridx * a.ldx + k
-                              : reinterpret_cast<const uint32_t*>(a.Y) + ridx;
-    const uint32_t v = *src;
-    return ok ? v : 0u;
+  auto load_val = [&](int ridx_v) -> uint32_t {
+    const int ridx = __builtin_amdgcn_readlane(ridx_v, w);
+    const int k = (j < d0) ? j : 0;
+    const uint32_t* src = (j < D0) ? reinterpret_cast<const uint32_t*>(a.X) + (size_t)ridx * a.ldx + k
+                                   : reinterpret_cast<const uint32_t*>(a.Y) + ridx;
+    return *src;
   };
-  int ridx_a = load_idx(0);
-  uint32_t cur = load_val(0, ridx_a);
-  ridx_a = load_idx(1);
+  uint32_t vr_ring[PF];
+  int ir_ring[PF];
+#pragma unroll
+  for (int i = 0; i < PF; ++i) ir_ring[i] = load_idx(i);
+#pragma unroll
+  for (int i = 0; i < PF; ++i) {
+    vr_ring[i] = load_val(ir_ring[i]);
+    ir_ring[i] = load_idx(i + PF);
+  }
 
   const float keep_scale = (a.dropout > 0.f) ? 1.0f / (1.0f - a.dropout) : 1.0f;
   const float l2b1 = log2f(a.b1), l2b2 = log2f(a.b2);
@@ -819,6 +841,7 @@ __global__ __launch_bounds__(64 * NW) void mlp_rows_kernel(WaveShape sh, MlpArgs
   __amdgpu_buffer_rsrc_t prs[XWN];
   __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(a.xg_recv, 0, 0, 0x00020000);
   constexpr int KX = D0 + CM + 2 + ((D0 + CM) & 1);  // exchange granules per lane (even)
+  static_assert(KX >= KG, "exchange granules cover the gradients");
   if (XG && w == 0) {
     const int nbytes = 2 * a.xg_world * KX * 64 * 8;
     rrs = __builtin_amdgcn_make_buffer_rsrc(a.xg_recv, 0, nbytes, 0x00020000);
@@ -830,26 +853,30 @@ __global__ __launch_bounds__(64 * NW) void mlp_rows_kernel(WaveShape sh, MlpArgs
   }
   int done = a.steps;
 
-  for (int s = 0; s < a.steps; ++s) {
-    const int sb = s;
-    const int bs = min(B, a.n_items - sb * B);
+  // one optimizer step; returns false when the launch must stop (exchange timeout)
+  auto step = [&](const int s, uint32_t& vslot, int& islot) -> bool {
+    const int bs = min(B, a.n_items - s * B);
     const bool live = w < bs;
     const uint32_t gstep = step_base + (uint32_t)s;
     const int par = s & 1;
-    const uint32_t nxt = load_val(sb + 1, ridx_a);
-    const int ridx_b = load_idx(sb + 2);
+    const uint32_t cur = vslot;
+    vslot = load_val(islot);       // values of step s + PF (index loaded PF steps ago)
+    islot = load_idx(s + 2 * PF);  // index of step s + 2 PF
 
     float x[D0];
 #pragma unroll
-    for (int k = 0; k < D0; ++k) x[k] = __int_as_float(__builtin_amdgcn_readlane((int)cur, k));
-    const int y = __builtin_amdgcn_readlane((int)cur, D0);
+    for (int k = 0; k < D0; ++k) {
+      const float xv = __int_as_float(__builtin_amdgcn_readlane((int)cur, k));
+      x[k] = (live && k < d0) ? xv : 0.f;  // dead rows: zeros, never a stale NaN
+    }
+    const int y = live ? __builtin_amdgcn_readlane((int)cur, D0) : 0;
 
     // ---- layer 0 for this row: h = dropout(relu(W0[j] . x + b0))
     float h;
     {
-      float z = b0;
+      float z = pr[KB];
 #pragma unroll
-      for (int k = 0; k < D0; ++k) z = fmaf(w0[k], x[k], z);
+      for (int k = 0; k < D0; ++k) z = fmaf(pr[k], x[k], z);
       z = fmaxf(z, 0.f);
       if (drop_thr) {
         const uint32_t hkey = (a.seed * 0x9E3779B1u) ^ (gstep * 0x85EBCA77u);
@@ -861,10 +888,10 @@ __global__ __launch_bounds__(64 * NW) void mlp_rows_kernel(WaveShape sh, MlpArgs
     // ---- output layer: logits[c] = sum_j Wout[c][j] h_j + bout[c]  (cross-lane, wave-uniform)
     float zc[CM];
 #pragma unroll
-    for (int c = 0; c < CM; ++c) zc[c] = wo[c] * h;
+    for (int c = 0; c < CM; ++c) zc[c] = pr[KO + c] * h;
     wave_sum_n(zc);
 #pragma unroll
-    for (int c = 0; c < CM; ++c) zc[c] += rl(bo, c);
+    for (int c = 0; c < CM; ++c) zc[c] += rl(pr[KC], c);
 
     // ---- loss + dlogits of this row (wave-uniform)
     float dz[CM];
@@ -914,39 +941,37 @@ __global__ __launch_bounds__(64 * NW) void mlp_rows_kernel(WaveShape sh, MlpArgs
     for (int c = 0; c < CM; ++c) dz[c] = live ? dz[c] : 0.f;
     lb = live ? lb : 0.f;
 
-    // ---- backward of this row (lane-local) -> per-lane gradient vector
-    float g[Q4 * 4];
+    // ---- backward of this row (lane-local) -> per-row gradient of every slot
+    float g[KG];
     {
       float gsum = 0.f;
 #pragma unroll
-      for (int c = 0; c < CM; ++c) gsum = fmaf(dz[c], wo[c], gsum);
+      for (int c = 0; c < CM; ++c) gsum = fmaf(dz[c], pr[KO + c], gsum);
       const float dh = (h > 0.f) ? gsum * keep_scale : 0.f;
 #pragma unroll
       for (int k = 0; k < D0; ++k) g[k] = dh * x[k];
-      g[D0] = dh;
+      g[KB] = dh;
 #pragma unroll
-      for (int c = 0; c < CM; ++c) g[D0 + 1 + c] = dz[c] * h;
+      for (int c = 0; c < CM; ++c) g[KO + c] = dz[c] * h;
       float gbo = 0.f;
 #pragma unroll
       for (int c = 0; c < CM; ++c) gbo = (c == j) ? dz[c] : gbo;
-      g[D0 + 1 + CM] = gbo;
-#pragma unroll
-      for (int k = KG; k < Q4 * 4; ++k) g[k] = 0.f;
+      g[KC] = gbo;
     }
 #pragma unroll
-    for (int q = 0; q < Q4; ++q) gslot[par][w][q][j] = make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+    for (int k = 0; k < KG; ++k) gslot[par][w][k][j] = g[k];
     if (j == 0) lslot[par][w] = lb;
-    __syncthreads();
-    // ---- batch gradient: rows summed in order 0..NW-1 (identical bits in every wave)
+    __syncthreads();  // barrier 1: every row's gradients are in LDS
+
+    // ---- batch gradient: rows summed in order 0..NW-1 (owned slots; all slots with XW > 0)
 #pragma unroll
-    for (int q = 0; q < Q4; ++q) {
-      float4 acc = gslot[par][0][q][j];
+    for (int k = 0; k < KG; ++k) {
+      if (owned(k)) {
+        float acc = gslot[par][0][k][j];
 #pragma unroll
-      for (int r = 1; r < NW; ++r) {
-        const float4 v = gslot[par][r][q][j];
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        for (int r = 1; r < NW; ++r) acc += gslot[par][r][k][j];
+        g[k] = acc;
       }
-      g[4 * q] = acc.x; g[4 * q + 1] = acc.y; g[4 * q + 2] = acc.z; g[4 * q + 3] = acc.w;
     }
     float bl = 0.f;
     if (w == 0) {
@@ -954,85 +979,88 @@ __global__ __launch_bounds__(64 * NW) void mlp_rows_kernel(WaveShape sh, MlpArgs
       for (int r = 0; r < NW; ++r) bl += lslot[par][r];
       bl *= inv;
     }
-    if (XG) {  // rank average of the batch gradients: wave 0 exchanges, LDS hands it to the rest
-      static_assert(!XG || KX >= KG, "granules cover the gradients");
+    if constexpr (XG) {  // rank average: wave 0 exchanges, LDS hands it to the rest
       if (w == 0) {
         float gv[KX];
 #pragma unroll
         for (int k = 0; k < KX; ++k) gv[k] = (k < KG) ? g[k] : 0.f;
-        // the bias slot carries the batch loss in lane 63 (lanes >= C own no bias)
-        gv[KG - 1] = (j < C) ? g[KG - 1] : (j == 63 ? bl : 0.f);
+        // the bout slot carries the batch loss in lane 63 (lanes >= C own no bias)
+        gv[KC] = (j < C) ? g[KC] : (j == 63 ? bl : 0.f);
         const bool ok = xg_allreduce<KX, XWN>(gv, a, prs, rrs, gstep, j);
 #pragma unroll
-        for (int q = 0; q < Q4; ++q) {
-          float4 o;
-          o.x = (4 * q + 0 < KG) ? gv[4 * q + 0] : 0.f;
-          o.y = (4 * q + 1 < KG) ? gv[4 * q + 1] : 0.f;
-          o.z = (4 * q + 2 < KG) ? gv[4 * q + 2] : 0.f;
-          o.w = (4 * q + 3 < KG) ? gv[4 * q + 3] : 0.f;
-          gavg[q][j] = o;
-        }
+        for (int k = 0; k < KG; ++k) gavg[k][j] = gv[k];
         if (j == 0) xabort = ok ? 0 : 1;
-        bl = rl(gv[KG - 1], 63);
+        bl = rl(gv[KC], 63);
       }
-      __syncthreads();
+      __syncthreads();  // barrier 2: the rank average (or the abort flag) is in LDS
       if (xabort) {
         done = s;
-        break;
+        return false;
       }
 #pragma unroll
-      for (int q = 0; q < Q4; ++q) {
-        const float4 v = gavg[q][j];
-        g[4 * q] = v.x; g[4 * q + 1] = v.y; g[4 * q + 2] = v.z; g[4 * q + 3] = v.w;
-      }
-      if (j >= C) g[KG - 1] = 0.f;  // lane 63's loss slot is not a gradient
+      for (int k = 0; k < KG; ++k) g[k] = gavg[k][j];
+      if (j >= C) g[KC] = 0.f;  // lane 63's loss slot is not a gradient
     }
     if (w == 0 && j == 0 && a.loss_out) a.loss_out[s] = bl;
 
-    // ---- Adam (every wave, identical inputs -> identical parameters)
+    // ---- Adam on the owned slots
     {
       const int t = t0 + s + 1;
       const float step_size = a.lr * __builtin_amdgcn_rcpf(1.f - pow_t(l2b1, (float)t));
       const float rbc2 = __builtin_amdgcn_rsqf(1.f - pow_t(l2b2, (float)t));
-      if (own1) {
 #pragma unroll
-        for (int k = 0; k < D0; ++k)
-          if (k < d0) adam1(w0[k], g[k], mw0[k], vw0[k], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
-        adam1(b0, g[D0], mb0, vb0, a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
-#pragma unroll
-        for (int c = 0; c < CM; ++c)
-          if (c < C) adam1(wo[c], g[D0 + 1 + c], mwo[c], vwo[c], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+      for (int k = 0; k < KG; ++k) {
+        if (owned(k) && slot_live(k)) adam1(pr[k], g[k], mr[k], vr[k], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
       }
-      if (j < C) adam1(bo, g[D0 + 1 + CM], mbo, vbo, a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
     }
-    cur = nxt;
-    ridx_a = ridx_b;
+    if constexpr (!XG) {  // publish owned slots; read the others after barrier 2
+#pragma unroll
+      for (int k = 0; k < KG; ++k)
+        if (owned(k)) pslot[k][j] = pr[k];
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < KG; ++k)
+        if (!owned(k)) pr[k] = pslot[k][j];
+    }
+    return true;
+  };
+  for (int s0 = 0; s0 < a.steps; s0 += PF) {
+    bool go = true;
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      if (go && s0 + i < a.steps) go = step(s0 + i, vr_ring[i], ir_ring[i]);
+    }
+    if (!go) break;
   }
-  if (w != 0) return;
-  if (a.step_counter && j == 0)
+  if (w == 0 && a.step_counter && j == 0)
     __hip_atomic_store(a.step_counter, t0 + done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // ---- write back params + moments (wave 0; every wave holds the same values)
+  // ---- write back: every wave holds the same parameters; each slot's moments live in its owner
 #pragma unroll
-  for (int k = 0; k < D0; ++k) {
-    if (own1 && k < d0) {
-      const int f = sh.woff[0] + j * d0 + k;
-      a.p[f] = w0[k]; a.m[f] = mw0[k]; a.v[f] = vw0[k];
+  for (int k = 0; k < KG; ++k) {
+    if (slot_live(k) && owned(k) && (!XG || w == 0)) {
+      const int f = slot_flat(k);
+      a.p[f] = pr[k]; a.m[f] = mr[k]; a.v[f] = vr[k];
     }
   }
-  if (own1) {
-    const int f = sh.boff[0] + j;
-    a.p[f] = b0; a.m[f] = mb0; a.v[f] = vb0;
-#pragma unroll
-    for (int c = 0; c < CM; ++c) {
-      if (c < C) {
-        const int f2 = sh.woff[1] + c * H1 + j;
-        a.p[f2] = wo[c]; a.m[f2] = mwo[c]; a.v[f2] = vwo[c];
+}
+
+template <int NW, int D0, int CM, bool EX, int XW>
+__global__ __launch_bounds__(64 * NW) void mlp_rows_kernel(WaveShape sh, MlpArgs a) {
+  __shared__ RowsLds<NW, D0 + CM + 2, (XW > 0)> lds;
+  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+    case 0: mlp_rows_wave<NW, 0, D0, CM, EX, XW>(sh, a, lds); break;
+    case 1: mlp_rows_wave<NW, 1, D0, CM, EX, XW>(sh, a, lds); break;
+    case 2: mlp_rows_wave<NW, 2, D0, CM, EX, XW>(sh, a, lds); break;
+    case 3: mlp_rows_wave<NW, 3, D0, CM, EX, XW>(sh, a, lds); break;
+    default:
+      if constexpr (NW == 8) {
+        switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+          case 4: mlp_rows_wave<NW, 4, D0, CM, EX, XW>(sh, a, lds); break;
+          case 5: mlp_rows_wave<NW, 5, D0, CM, EX, XW>(sh, a, lds); break;
+          case 6: mlp_rows_wave<NW, 6, D0, CM, EX, XW>(sh, a, lds); break;
+          default: mlp_rows_wave<NW, 7, D0, CM, EX, XW>(sh, a, lds); break;
+        }
       }
-    }
-  }
-  if (j < C) {
-    const int f = sh.boff[1] + j;
-    a.p[f] = bo; a.m[f] = mbo; a.v[f] = vbo;
   }
 }
 

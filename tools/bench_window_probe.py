@@ -20,7 +20,7 @@ from dct_amd.trainer.trainer import seed_everything  # noqa: E402
 
 
 def main():
-    steps, warmup, reps = 20, 5, 12
+    steps, warmup, reps = 20, 5, 6
     ctx = init_distributed("gpu")
     seed_everything(42)
     total = warmup + steps * reps
@@ -33,7 +33,12 @@ def main():
     eng.attach_data(X, Y, perm[:n_train], perm[n_train:])
     n_items = eng.upload_epoch_indices(0, shuffle=True)
     loss = torch.zeros(total, dtype=torch.float32, device=ctx.device)
-    eng.run_steps(n_items, warmup, loss, first_step=0)
+    split = int(os.environ.get("PROBE_WARMUP_CALLS", "1"))  # warmup steps spread over this many launches
+    per = [warmup // split + (1 if i < warmup % split else 0) for i in range(split)]
+    done = 0
+    for k in per:
+        eng.run_steps(n_items, k, loss, first_step=done)
+        done += k
     first = warmup
     for r in range(reps):
         torch.cuda.synchronize()
