@@ -70,9 +70,12 @@ def _timed(ctx, fn):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     fn()
-    torch.cuda.synchronize()
-    ctx.barrier()
-    torch.cuda.synchronize()
+    if ctx.backend == "nccl":
+        ctx.barrier()  # an RCCL op queued behind the timed steps: the synchronize below covers both
+        torch.cuda.synchronize()
+    else:
+        torch.cuda.synchronize()
+        ctx.barrier()  # host-side (gloo) or a no-op at world size 1
     dt = time.perf_counter() - t0
     dt_t = torch.tensor([dt], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
     if ctx.is_distributed:
