@@ -751,7 +751,7 @@ struct RowsLds {
 
 // The whole per-wave program with the wave id W as a compile-time constant, so slot ownership
 // (k % NW == W) folds away instead of becoming a branch per slot.
-template <int NW, int W, int D0, int CM, bool EX, int XW>
+template <int NW, int W, int D0, int CM, bool EX, int XW, bool REP>
 __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs& a,
                                               RowsLds<NW, D0 + CM + 2, (XW > 0)>& L) {
   constexpr int KG = D0 + 1 + CM + 1;  // per-lane parameter slots: W0 row, b0, Wout column, bout
@@ -782,7 +782,10 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
     if (k < KC) return sh.woff[1] + (k - KO) * H1 + j;
     return sh.boff[1] + j;
   };
-  auto owned = [](int k) constexpr -> bool { return XG || (k % NW) == W; };
+  // REP: every wave runs Adam on every slot (one barrier per step instead of two).  Measured on
+  // the weather step it loses to the owner split: 0.893 vs 0.732 us/step (MI355X, round 2), so
+  // only the XW > 0 path, which needs the full gradient in every wave anyway, replicates.
+  auto owned = [](int k) constexpr -> bool { return XG || REP || (k % NW) == W; };
 
   // ---------------------------------------------------------------- parameters -> registers
   float pr[KG], mr[KG], vr[KG];
@@ -1013,7 +1016,7 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
         if (owned(k) && slot_live(k)) adam1(pr[k], g[k], mr[k], vr[k], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
       }
     }
-    if constexpr (!XG) {  // publish owned slots; read the others after barrier 2
+    if constexpr (!XG && !REP) {  // publish owned slots; read the others after barrier 2
 #pragma unroll
       for (int k = 0; k < KG; ++k)
         if (owned(k)) pslot[k][j] = pr[k];
@@ -1037,28 +1040,28 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
   // ---- write back: every wave holds the same parameters; each slot's moments live in its owner
 #pragma unroll
   for (int k = 0; k < KG; ++k) {
-    if (slot_live(k) && owned(k) && (!XG || w == 0)) {
+    if (slot_live(k) && owned(k) && (!(XG || REP) || w == 0)) {
       const int f = slot_flat(k);
       a.p[f] = pr[k]; a.m[f] = mr[k]; a.v[f] = vr[k];
     }
   }
 }
 
-template <int NW, int D0, int CM, bool EX, int XW>
+template <int NW, int D0, int CM, bool EX, int XW, bool REP = false>
 __global__ __launch_bounds__(64 * NW) void mlp_rows_kernel(WaveShape sh, MlpArgs a) {
   __shared__ RowsLds<NW, D0 + CM + 2, (XW > 0)> lds;
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: mlp_rows_wave<NW, 0, D0, CM, EX, XW>(sh, a, lds); break;
-    case 1: mlp_rows_wave<NW, 1, D0, CM, EX, XW>(sh, a, lds); break;
-    case 2: mlp_rows_wave<NW, 2, D0, CM, EX, XW>(sh, a, lds); break;
-    case 3: mlp_rows_wave<NW, 3, D0, CM, EX, XW>(sh, a, lds); break;
+    case 0: mlp_rows_wave<NW, 0, D0, CM, EX, XW, REP>(sh, a, lds); break;
+    case 1: mlp_rows_wave<NW, 1, D0, CM, EX, XW, REP>(sh, a, lds); break;
+    case 2: mlp_rows_wave<NW, 2, D0, CM, EX, XW, REP>(sh, a, lds); break;
+    case 3: mlp_rows_wave<NW, 3, D0, CM, EX, XW, REP>(sh, a, lds); break;
     default:
       if constexpr (NW == 8) {
         switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-          case 4: mlp_rows_wave<NW, 4, D0, CM, EX, XW>(sh, a, lds); break;
-          case 5: mlp_rows_wave<NW, 5, D0, CM, EX, XW>(sh, a, lds); break;
-          case 6: mlp_rows_wave<NW, 6, D0, CM, EX, XW>(sh, a, lds); break;
-          default: mlp_rows_wave<NW, 7, D0, CM, EX, XW>(sh, a, lds); break;
+          case 4: mlp_rows_wave<NW, 4, D0, CM, EX, XW, REP>(sh, a, lds); break;
+          case 5: mlp_rows_wave<NW, 5, D0, CM, EX, XW, REP>(sh, a, lds); break;
+          case 6: mlp_rows_wave<NW, 6, D0, CM, EX, XW, REP>(sh, a, lds); break;
+          default: mlp_rows_wave<NW, 7, D0, CM, EX, XW, REP>(sh, a, lds); break;
         }
       }
   }
