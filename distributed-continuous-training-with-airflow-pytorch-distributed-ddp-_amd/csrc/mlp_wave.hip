@@ -728,23 +728,23 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
 // The single-wave kernel above is issue-bound: one wave64 issues every VALU instruction over
 // 4 cycles on ONE SIMD16 of the CU, and a step is ~650 instructions (~3k cycles, 1.35 us).
 // Here wave w (NW = 4 or 8 waves spread over the CU's 4 SIMDs; rows >= B idle) runs the
-// forward, loss and backward of batch row w only, then the per-row gradients meet in LDS:
-//   * XW == 0: parameter slot k (lane j owns W0[j][:], b0[j], Wout[:, j], bout[j < C] as
-//     slots 0..KG-1) belongs to wave k % NW.  After barrier 1 the owner sums slot k over the
-//     rows (order 0..NW-1), runs Adam on it (moments live only in the owner) and publishes the
-//     new value; after barrier 2 every wave reads the parameters it does not own.  Adam's
-//     ~12 VALU ops and 2 quarter-rate transcendentals per slot are spread over the SIMDs.
-//   * XW > 0: every wave sums all slots; wave 0 runs the in-kernel xGMI exchange of the batch
-//     gradients (same protocol and granule layout as xg_allreduce above) and hands the rank
-//     average (plus a timeout flag, so all waves leave the loop together) to the others
-//     through LDS behind barrier 2; every wave then applies the identical Adam update to its
-//     own register copy.
+// forward, loss and backward of batch row w only, then the per-row gradients meet in LDS.
+// Parameter slot k (lane j owns W0[j][:], b0[j], Wout[:, j], bout[j < C] as slots 0..KG-1)
+// belongs to wave k % NW: the owner runs Adam on it (its moments live only in the owner) and
+// publishes the new value through LDS; after the step's last barrier every wave reads the
+// parameters it does not own.  Adam's ~12 VALU ops and 2 quarter-rate transcendentals per
+// slot are spread over the SIMDs.
+//   * XW == 0: after barrier 1 the owner sums slot k over the rows (order 0..NW-1).
+//   * XW > 0: wave 0 sums every slot and runs the in-kernel xGMI exchange of the batch
+//     gradients (same protocol and granule layout as xg_allreduce above); the rank average
+//     (plus a timeout flag, so all waves leave the loop together) reaches the owners through
+//     LDS behind barrier 2.
 // Row sums run in a fixed order, so the result is bit-identical across waves and ranks.
 template <int NW, int KG, bool XG>
 struct RowsLds {
   float gslot[2][NW][KG][64];    // [step parity][row][slot][lane] per-row gradients
   float lslot[2][NW];            // per-row losses
-  float pslot[XG ? 1 : KG][64];  // parameters published by their owner (XW == 0)
+  float pslot[KG][64];           // parameters published by their owner
   float gavg[XG ? KG : 1][64];   // rank-averaged gradients (XW > 0)
   int xabort;
 };
@@ -783,9 +783,8 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
     return sh.boff[1] + j;
   };
   // REP: every wave runs Adam on every slot (one barrier per step instead of two).  Measured on
-  // the weather step it loses to the owner split: 0.893 vs 0.732 us/step (MI355X, round 2), so
-  // only the XW > 0 path, which needs the full gradient in every wave anyway, replicates.
-  auto owned = [](int k) constexpr -> bool { return XG || REP || (k % NW) == W; };
+  // the weather step it loses to the owner split: 0.893 vs 0.732 us/step (MI355X, round 2).
+  auto owned = [](int k) constexpr -> bool { return REP || (k % NW) == W; };
 
   // ---------------------------------------------------------------- parameters -> registers
   float pr[KG], mr[KG], vr[KG];
@@ -966,10 +965,11 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
     if (j == 0) lslot[par][w] = lb;
     __syncthreads();  // barrier 1: every row's gradients are in LDS
 
-    // ---- batch gradient: rows summed in order 0..NW-1 (owned slots; all slots with XW > 0)
+    // ---- batch gradient: rows summed in order 0..NW-1 (owned slots; with XW > 0 wave 0 sums
+    // every slot for the exchange)
 #pragma unroll
     for (int k = 0; k < KG; ++k) {
-      if (owned(k)) {
+      if (XG ? (W == 0) : owned(k)) {
         float acc = gslot[par][0][k][j];
 #pragma unroll
         for (int r = 1; r < NW; ++r) acc += gslot[par][r][k][j];
@@ -1001,8 +1001,9 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
         return false;
       }
 #pragma unroll
-      for (int k = 0; k < KG; ++k) g[k] = gavg[k][j];
-      if (j >= C) g[KC] = 0.f;  // lane 63's loss slot is not a gradient
+      for (int k = 0; k < KG; ++k)
+        if (owned(k)) g[k] = gavg[k][j];
+      if (owned(KC) && j >= C) g[KC] = 0.f;  // lane 63's loss slot is not a gradient
     }
     if (w == 0 && j == 0 && a.loss_out) a.loss_out[s] = bl;
 
@@ -1016,7 +1017,7 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
         if (owned(k) && slot_live(k)) adam1(pr[k], g[k], mr[k], vr[k], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
       }
     }
-    if constexpr (!XG && !REP) {  // publish owned slots; read the others after barrier 2
+    if constexpr (!REP) {  // publish owned slots; read the others after the next barrier
 #pragma unroll
       for (int k = 0; k < KG; ++k)
         if (owned(k)) pslot[k][j] = pr[k];
@@ -1040,7 +1041,7 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
   // ---- write back: every wave holds the same parameters; each slot's moments live in its owner
 #pragma unroll
   for (int k = 0; k < KG; ++k) {
-    if (slot_live(k) && owned(k) && (!(XG || REP) || w == 0)) {
+    if (slot_live(k) && owned(k) && (!REP || w == 0)) {
       const int f = slot_flat(k);
       a.p[f] = pr[k]; a.m[f] = mr[k]; a.v[f] = vr[k];
     }
