@@ -864,6 +864,15 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
     const uint32_t cur = vslot;
     vslot = load_val(islot);       // values of step s + PF (index loaded PF steps ago)
     islot = load_idx(s + 2 * PF);  // index of step s + 2 PF
+    // step-only quantities first, branch-free: they share the basic block of the forward's
+    // latency chains, so the scheduler fills its bubbles with them (a branch or the barrier
+    // would fence them onto the critical path)
+    const uint32_t hkey = (a.seed * 0x9E3779B1u) ^ (gstep * 0x85EBCA77u);
+    const uint32_t hrnd = wave_hash(hkey ^ ((uint32_t)(w * 64 + j) * 0xC2B2AE3Du));
+    const bool dropped = hrnd < drop_thr;  // drop_thr == 0: never
+    const int t_adam = t0 + s + 1;
+    const float step_size = a.lr * __builtin_amdgcn_rcpf(1.f - pow_t(l2b1, (float)t_adam));
+    const float rbc2 = __builtin_amdgcn_rsqf(1.f - pow_t(l2b2, (float)t_adam));
 
     float x[D0];
 #pragma unroll
@@ -879,13 +888,8 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
       float z = pr[KB];
 #pragma unroll
       for (int k = 0; k < D0; ++k) z = fmaf(pr[k], x[k], z);
-      z = fmaxf(z, 0.f);
-      if (drop_thr) {
-        const uint32_t hkey = (a.seed * 0x9E3779B1u) ^ (gstep * 0x85EBCA77u);
-        const uint32_t r = wave_hash(hkey ^ ((uint32_t)(w * 64 + j) * 0xC2B2AE3Du));
-        z = (r < drop_thr) ? 0.f : z * keep_scale;
-      }
-      h = own1 ? z : 0.f;
+      z = fmaxf(z, 0.f) * keep_scale;  // keep_scale == 1 without dropout
+      h = (own1 && !dropped) ? z : 0.f;
     }
     // ---- output layer: logits[c] = sum_j Wout[c][j] h_j + bout[c]  (cross-lane, wave-uniform)
     float zc[CM];
@@ -1009,9 +1013,6 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
 
     // ---- Adam on the owned slots
     {
-      const int t = t0 + s + 1;
-      const float step_size = a.lr * __builtin_amdgcn_rcpf(1.f - pow_t(l2b1, (float)t));
-      const float rbc2 = __builtin_amdgcn_rsqf(1.f - pow_t(l2b2, (float)t));
 #pragma unroll
       for (int k = 0; k < KG; ++k) {
         if (owned(k) && slot_live(k)) adam1(pr[k], g[k], mr[k], vr[k], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
