@@ -325,7 +325,10 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
     store_tile<DM * 2, AS_LD * 2>(a.a2 + (size_t)row0 * DM, AS);
   }
   {
-    f32x4 acc[4][4];  // [row tile][column tile of this wave]
+    // Operands swapped (A = W1 rows, B = a2 rows): the C tile is [column][token], so each lane
+    // holds 4 CONSECUTIVE columns of one token and the pre-activation / GELU outputs leave as
+    // 8-byte stores (16 per lane instead of 64 two-byte ones, 8.6 -> see BASELINE.md)
+    f32x4 acc[4][4];  // [token tile][column tile of this wave]
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -341,21 +344,29 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[i][t] = mfma32(af[i], bw[t], acc[i][t]);
+        for (int t = 0; t < 4; ++t) acc[i][t] = mfma32(bw[t], af[i], acc[i][t]);
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int col = 64 * wv + 16 * t + c;
-      const float bv = a.b1[col];
+      const int col0 = 64 * wv + 16 * t + 4 * g;
+      const float4 bv = *reinterpret_cast<const float4*>(a.b1 + col0);
+      const float bvs[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
+        const int row = 16 * i + c;
+        uint16_t zp[4], fp[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = 16 * i + 4 * g + r;
-          const float z = acc[i][t][r] + bv;
-          if (a.save) a.pre[(size_t)(row0 + row) * FF + col] = f32_to_bf16(z);
-          RS[row * F_LD + col] = f32_to_bf16(gelu_f(z));
+          const float z = acc[i][t][r] + bvs[r];
+          zp[r] = f32_to_bf16(z);
+          fp[r] = f32_to_bf16(gelu_f(z));
         }
+        if (a.save)
+          *reinterpret_cast<uint2*>(a.pre + (size_t)(row0 + row) * FF + col0) =
+              make_uint2(zp[0] | ((uint32_t)zp[1] << 16), zp[2] | ((uint32_t)zp[3] << 16));
+        *reinterpret_cast<uint2*>(RS + row * F_LD + col0) =
+            make_uint2(fp[0] | ((uint32_t)fp[1] << 16), fp[2] | ((uint32_t)fp[3] << 16));
+      }
     }
   }
   __syncthreads();
@@ -579,17 +590,22 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[i][t] = mfma32(af[i], bw[t], acc[i][t]);
+        for (int t = 0; t < 4; ++t) acc[i][t] = mfma32(bw[t], af[i], acc[i][t]);  // C = [column][token]
     }
+    // each lane: 4 consecutive columns of one token -> one 8-byte LDS read-modify-write per tile
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < 4; ++t) {
+        uint2* pp = reinterpret_cast<uint2*>(R + (16 * i + c) * F_LD + 64 * wv + 16 * t + 4 * g);
+        const uint2 pv = *pp;
+        const uint16_t pr[4] = {(uint16_t)(pv.x & 0xFFFF), (uint16_t)(pv.x >> 16), (uint16_t)(pv.y & 0xFFFF),
+                                (uint16_t)(pv.y >> 16)};
+        uint16_t dp[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          uint16_t* pp = R + (16 * i + 4 * g + r) * F_LD + 64 * wv + 16 * t + c;
-          *pp = f32_to_bf16(acc[i][t][r] * gelu_grad_f(bf16_to_f32(*pp)));
-        }
+        for (int r = 0; r < 4; ++r) dp[r] = f32_to_bf16(acc[i][t][r] * gelu_grad_f(bf16_to_f32(pr[r])));
+        *pp = make_uint2(dp[0] | ((uint32_t)dp[1] << 16), dp[2] | ((uint32_t)dp[3] << 16));
+      }
     // dpre out: this wave's 64-column block of all 64 rows (128 B per row, 16-byte chunks)
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
