@@ -12,6 +12,8 @@ the sync_dist train_loss.  Other BASELINE.json configs:
   --model tabtransformer       4-layer TabTransformer over 64 feature tokens (d 64, 4 heads), CE,
                                Adam(1e-3), batch 512 per rank, HIP GEMM/LayerNorm/attention kernels,
                                autograd step captured in a HIP graph
+  --device cpu                 BASELINE config 1 (CPU plumbing: single process or gloo DDP, the
+                               reference's own execution model) with the autograd engine
 Data: synthetic rows (no network), random-init weights.
 
 Timed region: exactly K optimizer steps, bracketed by barrier + device synchronize on both
@@ -48,6 +50,8 @@ def parse():
     p.add_argument("--batch", type=int, default=None, help="per-rank batch (reference: 4; tabular: 4096)")
     p.add_argument("--rows", type=int, default=0,
                    help="synthetic dataset rows (0 = sized to the run; tabular: 100M per BASELINE config 4)")
+    p.add_argument("--device", default="gpu", choices=("gpu", "cpu"),
+                   help="cpu: BASELINE config 1 (autograd engine, gloo) - the plumbing path")
     p.add_argument("--epoch-rows", type=int, default=None,
                    help="dataset size used for the reported epoch wall-clock (weather 100k, tabular 100M)")
     a = p.parse_args()
@@ -65,6 +69,15 @@ def _timed(ctx, fn):
     import torch
     import torch.distributed as dist
 
+    if ctx.device.type != "cuda":  # CPU plumbing config: steps are synchronous
+        ctx.barrier()
+        t0 = time.perf_counter()
+        fn()
+        ctx.barrier()
+        dt_t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        if ctx.is_distributed:
+            dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+        return float(dt_t.item())
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()
@@ -182,6 +195,54 @@ class _StepLoop:
         return float(loss), float(acc)
 
 
+class _CpuLoop:
+    """BASELINE config 1: the reference's execution model (CPU, batch 4, per-step autograd, gloo
+    bucket all-reduce when distributed) on the AutogradEngine; batches sliced from the epoch's
+    DistributedSampler shard like the Trainer does."""
+
+    def __init__(self, eng):
+        self.eng = eng
+
+    def upload_epoch_indices(self, epoch, shuffle=True):
+        self.rows = self.eng.train_rows[self.eng.epoch_local_indices(len(self.eng.train_rows), epoch, shuffle)]
+        return self.rows.numel()
+
+    def run_steps(self, n_items, steps, loss_out, first_step=0):
+        B = self.eng.B
+        for s in range(first_step, first_step + steps):
+            loss_out[s] = self.eng.train_step(self.rows[s * B:(s + 1) * B], s)
+
+    def validate(self, limit=None):
+        import torch
+
+        eng = self.eng
+        rows = eng.val_rows[: (limit or len(eng.val_rows))]
+        with torch.no_grad():
+            eng.model.eval()
+            logits = eng.model(eng.X[rows])
+            loss = eng.model.compute_loss(logits, eng.Y[rows])
+            acc = (logits.argmax(1) == eng.Y[rows]).float().mean()
+            eng.model.train()
+        return float(loss), float(acc)
+
+
+def setup_cpu(a, ctx):
+    import torch
+
+    from dct_amd.data.synthetic import weather_tensors
+    from dct_amd.models.mlp import build_mlp
+    from dct_amd.trainer.engines import AutogradEngine
+
+    rows = a.rows or int(math.ceil((a.warmup + a.steps + 8) * a.batch * ctx.world_size / 0.8)) + 1024
+    X, Y = weather_tensors(rows, seed=0, dim=5)
+    model = build_mlp(a.model, 5)
+    eng = AutogradEngine(model, ctx, a.batch, seed=42)
+    n_train = int(0.8 * rows)
+    perm = torch.randperm(rows, generator=torch.Generator().manual_seed(42))
+    eng.attach_data(X, Y, perm[:n_train], perm[n_train:])
+    return eng, 5
+
+
 def setup_transformer(a, ctx):
     import torch
 
@@ -211,11 +272,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus and a.gpus > 1 and world == 1:
         raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    ctx = init_distributed("gpu")
+    cpu = a.device == "cpu"
+    ctx = init_distributed("cpu" if cpu else "gpu")
     seed_everything(42)
     tab = a.model in TABULAR
     tt = a.model in TRANSFORMER
-    if tt:
+    if cpu:
+        if tab or tt:
+            raise SystemExit("--device cpu runs the weather configs (BASELINE config 1)")
+        eng, feats = setup_cpu(a, ctx)
+        loop = _CpuLoop(eng)
+    elif tt:
         eng, feats = setup_transformer(a, ctx)
         loop = _StepLoop(eng, ctx)
     else:
@@ -240,12 +307,14 @@ def main():
             ok = False
         if not ok:
             _warmup(eng, n_items, a.warmup, loss)  # re-warm on the RCCL path
-    if not (tab or tt) and eng.ddp and eng.xg is None and eng.use_graph:
+    if not (tab or tt or cpu) and eng.ddp and eng.xg is None and eng.use_graph:
         eng._get_graph(n_items, min(eng.graph_chunk, a.steps), loss)
     dt = _timed(ctx, lambda: loop.run_steps(n_items, a.steps, loss, first_step=a.warmup))
 
     xg_ok = eng.xg_verify(fallback=True) if getattr(eng, "xg", None) is not None else None
-    if tt:
+    if cpu:
+        engine_desc = "autograd(cpu)" + ("+gloo-bucket-allreduce" if ctx.is_distributed else "")
+    elif tt:
         engine_desc = ("autograd(hip gemm/layernorm/attention)" + ("+rccl-bucket-allreduce" if ctx.is_distributed
                                                                     else "") + ("+hipgraph" if eng.graph_used else ""))
     elif tab:
@@ -257,7 +326,7 @@ def main():
             + ("+hipgraph" if eng.graph_used else ""))
     else:
         engine_desc = "fused-persistent"
-    in_sync = _params_in_sync(ctx, eng.flat_p if tt else eng.p)
+    in_sync = _params_in_sync(ctx, eng.flat_p if (tt or cpu) else eng.p)
     losses = loss.cpu()
     finite = bool(torch.isfinite(losses).all())
     first_l = float(losses[: max(1, a.warmup // 10)].mean())
@@ -278,7 +347,7 @@ def main():
         "metric": "samples/sec (whole node) for weather-MLP DDP",
         "value": round(sps, 1),
         "unit": "samples/s",
-        "n_gpus": ctx.world_size,
+        "n_gpus": 0 if cpu else ctx.world_size,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(ms_step, 6),
@@ -292,9 +361,9 @@ def main():
             "global_batch": a.batch * ctx.world_size,
             "per_rank_batch": a.batch,
             "seq_len": None,
-            "parallelism": f"dp{ctx.world_size}",
-            "optimizer": f"adam lr={(eng.optimizer.lr if tt else eng.adam['lr']):g}",
-            "loss": "ce" if tt else eng.loss,
+            "parallelism": f"dp{ctx.world_size}" + ("-cpu-gloo" if cpu else ""),
+            "optimizer": f"adam lr={(eng.optimizer.lr if (tt or cpu) else eng.adam['lr']):g}",
+            "loss": "ce" if tt else (eng.model.loss_kind if cpu else eng.loss),
             "engine": engine_desc,
             "dataset_rows": int(eng.X.shape[0]),
             "seq_len_tokens": feats if tt else None,
@@ -312,7 +381,7 @@ def main():
             "losses_finite": finite,
             "params_in_sync": in_sync,
             "xgmi_exchange_ok": xg_ok,
-            "device": torch.cuda.get_device_name(ctx.device),
+            "device": torch.cuda.get_device_name(ctx.device) if not cpu else "cpu",
         },
     }
     if tab:
