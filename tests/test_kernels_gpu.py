@@ -41,7 +41,7 @@ def test_native_loaded_and_arch():
 @pytest.mark.parametrize("loss", ["ce", "mse"])
 @pytest.mark.parametrize("dims,B", [([5, 64, 2], 4), ([5, 128, 128, 2], 4), ([5, 64, 2], 3), ([9, 48, 64, 3], 4),
                                     ([16, 32, 48, 32, 3], 16), ([5, 128, 128, 2], 16), ([7, 20, 2], 9),
-                                    ([7, 20, 2], 8)])
+                                    ([7, 20, 2], 8), ([12, 40, 4], 6), ([16, 64, 3], 2), ([5, 64, 2], 1)])
 def test_fused_train_matches_torch_adam(dims, B, loss, kernel, cuda, monkeypatch):
     monkeypatch.setenv("DCT_MLP_KERNEL", kernel.split("-")[0])
     monkeypatch.setenv("DCT_MLP_BLOCK", "0" if kernel.endswith("noblock") else "1")
