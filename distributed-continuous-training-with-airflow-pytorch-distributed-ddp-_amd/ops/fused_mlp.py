@@ -214,6 +214,17 @@ class FusedMLPKernel:
                             stream if stream is not None else stream_handle())
 
 
+# the current stream's raw handle without building a torch.cuda.Stream object (one C call); the
+# public API is the fallback should the private binding go away
+_raw_stream_fn = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _raw_stream(device_index: int) -> int:
+    if _raw_stream_fn is not None:
+        return _raw_stream_fn(device_index)
+    return torch.cuda.current_stream(device_index).cuda_stream
+
+
 class BoundTrain:
     """A prepared persistent train launch (see ``FusedMLPKernel.prepare_train``).  Holds the
     bound tensors so their storage outlives every launch enqueued through it."""
@@ -228,8 +239,7 @@ class BoundTrain:
         self.loss_len = int(launch.loss_len)
 
     def run(self, first_step: int, steps: int, stream: Optional[int] = None):
-        self._launch.run(first_step, steps,
-                         torch._C._cuda_getCurrentRawStream(self._dev) if stream is None else stream)
+        self._launch.run(first_step, steps, _raw_stream(self._dev) if stream is None else stream)
 
 
 # ---------------------------------------------------------------------------- reference
