@@ -191,6 +191,78 @@ __device__ __forceinline__ bool xg_allreduce(float (&g)[KX], const MlpArgs& a,
   return true;
 }
 
+// Per-wave exchange of the row-parallel kernel: wave w of every rank owns one region of the
+// receive buffer, [2 parity][W src][NW waves][XV/2 pairs][64 lanes] x 16 B {value, tag, value, tag},
+// and pushes / polls only that region - the waves of a CU exchange their owned parameter slots in
+// parallel instead of one wave moving everything.  Same tag protocol as xg_allreduce (the data is
+// the flag; parity slabs make reuse safe; sums in rank order; bounded spins).
+template <int XV, int XW>
+__device__ __forceinline__ bool xg_exchange_wave(float (&g)[XV], const MlpArgs& a,
+                                                 const __amdgpu_buffer_rsrc_t (&prs)[XW], __amdgpu_buffer_rsrc_t rrs,
+                                                 uint32_t gstep, int j, int w, int nw) {
+  static_assert(XV % 2 == 0, "granule pairs");
+  constexpr int P2 = XV / 2;
+  const int W = a.xg_world, rank = a.xg_rank;
+  const uint32_t tag = gstep + 1u;
+  const int par = (int)(gstep & 1u);
+  auto off = [&](int src, int p) { return ((((par * W + src) * nw + w) * P2 + p) * 64 + j) * 16; };
+#pragma unroll
+  for (int q = 0; q < XW; ++q) {
+    if (q < W && q != rank) {
+#pragma unroll
+      for (int p = 0; p < P2; ++p) {
+        xg_v4u d;
+        d.x = __float_as_uint(g[2 * p]);
+        d.y = tag;
+        d.z = __float_as_uint(g[2 * p + 1]);
+        d.w = tag;
+        __builtin_amdgcn_raw_buffer_store_b128(d, prs[q], off(rank, p), 0, XG_SYS);
+      }
+    }
+  }
+  float v[XW][XV];
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  int spin = 0;
+  for (;;) {  // sweep every source per pass (one round trip per pass)
+    bool ok = true;
+#pragma unroll
+    for (int q = 0; q < XW; ++q) {
+      const int qq = (q < W && q != rank) ? q : (rank == 0 ? 1 : 0);
+#pragma unroll
+      for (int p = 0; p < P2; ++p) {
+        const xg_v4u d = __builtin_amdgcn_raw_buffer_load_b128(rrs, off(qq, p), 0, XG_SYS);
+        v[q][2 * p] = __uint_as_float(d.x);
+        v[q][2 * p + 1] = __uint_as_float(d.z);
+        ok &= ((d.y == tag) & (d.w == tag)) | (q >= W) | (q == rank);
+      }
+    }
+    if (__all(ok)) break;
+    if ((++spin & 15) == 0 && (long long)(__builtin_amdgcn_s_memrealtime() - t_start) > a.xg_timeout) {
+      if (j == 0) __hip_atomic_store(a.xg_status, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  float acc[XV];
+#pragma unroll
+  for (int i = 0; i < XV; ++i) acc[i] = 0.f;
+#pragma unroll
+  for (int q = 0; q < XW; ++q) {
+    if (q < W) {
+#pragma unroll
+      for (int i = 0; i < XV; ++i) acc[i] += (q == rank) ? g[i] : v[q][i];
+    }
+  }
+  const float invw = 1.0f / (float)W;
+#pragma unroll
+  for (int i = 0; i < XV; ++i) g[i] = acc[i] * invw;
+  return true;
+}
+
+// receive-buffer granules per (parity, source rank) of the row-parallel kernel's per-wave regions:
+// NW x XV x 64 with XV = even(ceil(KG / NW) + 1), at most 2048 over its instantiations
+constexpr int XG_ROWS_GRANULES = 2048;
+
 // EX: the shape equals the template bounds (d0 == D0, C == CM) -> every guard folds away.
 // XW > 0: in-kernel gradient all-reduce across up to XW ranks (train mode, 2 layers).
 template <int L, int BMAX, int D0, int CM, bool EX, int XW>
@@ -735,18 +807,17 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
 // parameters it does not own.  Adam's ~12 VALU ops and 2 quarter-rate transcendentals per
 // slot are spread over the SIMDs.
 //   * XW == 0: after barrier 1 the owner sums slot k over the rows (order 0..NW-1).
-//   * XW > 0: wave 0 sums every slot and runs the in-kernel xGMI exchange of the batch
-//     gradients (same protocol and granule layout as xg_allreduce above); the rank average
-//     (plus a timeout flag, so all waves leave the loop together) reaches the owners through
-//     LDS behind barrier 2.
+//   * XW > 0: every wave runs the in-kernel xGMI exchange of ITS owned slots (and wave 0 of the
+//     batch loss) in its own region of the receive buffer (xg_exchange_wave), so the waves push
+//     and poll in parallel; Adam on the rank average is tentative until barrier 2 has shown
+//     that no wave's exchange timed out (then all waves undo the step and leave together).
 // Row sums run in a fixed order, so the result is bit-identical across waves and ranks.
 template <int NW, int KG, bool XG>
 struct RowsLds {
-  float gslot[2][NW][KG][64];    // [step parity][row][slot][lane] per-row gradients
-  float lslot[2][NW];            // per-row losses
-  float pslot[KG][64];           // parameters published by their owner
-  float gavg[XG ? KG : 1][64];   // rank-averaged gradients (XW > 0)
-  int xabort;
+  float gslot[2][NW][KG][64];  // [step parity][row][slot][lane] per-row gradients
+  float lslot[2][NW];          // per-row losses
+  float pslot[KG][64];         // parameters published by their owner
+  int xab[NW];                 // per-wave exchange timeout flags (XW > 0)
 };
 
 // The whole per-wave program with the wave id W as a compile-time constant, so slot ownership
@@ -762,8 +833,7 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
   auto& gslot = L.gslot;
   auto& lslot = L.lslot;
   auto& pslot = L.pslot;
-  auto& gavg = L.gavg;
-  auto& xabort = L.xabort;
+  auto& xab = L.xab;
   const int j = threadIdx.x & 63;
   constexpr int w = W;  // wave = batch row
   const int d0 = EX ? D0 : sh.d0, H1 = sh.h1, C = EX ? CM : sh.C;
@@ -842,10 +912,12 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
   constexpr int XWN = XW > 0 ? XW : 1;
   __amdgpu_buffer_rsrc_t prs[XWN];
   __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(a.xg_recv, 0, 0, 0x00020000);
-  constexpr int KX = D0 + CM + 2 + ((D0 + CM) & 1);  // exchange granules per lane (even)
-  static_assert(KX >= KG, "exchange granules cover the gradients");
-  if (XG && w == 0) {
-    const int nbytes = 2 * a.xg_world * KX * 64 * 8;
+  // exchange values per lane of this wave: its owned slots (k = w, w + NW, ...) then the batch loss
+  constexpr int NOWN = (KG + NW - 1) / NW;
+  constexpr int XV = (NOWN + 1 + 1) / 2 * 2;
+  static_assert(NW * XV * 64 <= XG_ROWS_GRANULES, "exchange region exceeds the allocated slab");
+  if (XG) {
+    const int nbytes = 2 * a.xg_world * NW * XV * 64 * 8;
     rrs = __builtin_amdgcn_make_buffer_rsrc(a.xg_recv, 0, nbytes, 0x00020000);
 #pragma unroll
     for (int q = 0; q < XWN; ++q) {
@@ -969,11 +1041,10 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
     if (j == 0) lslot[par][w] = lb;
     __syncthreads();  // barrier 1: every row's gradients are in LDS
 
-    // ---- batch gradient: rows summed in order 0..NW-1 (owned slots; with XW > 0 wave 0 sums
-    // every slot for the exchange)
+    // ---- batch gradient of the owned slots: rows summed in order 0..NW-1
 #pragma unroll
     for (int k = 0; k < KG; ++k) {
-      if (XG ? (W == 0) : owned(k)) {
+      if (owned(k)) {
         float acc = gslot[par][0][k][j];
 #pragma unroll
         for (int r = 1; r < NW; ++r) acc += gslot[par][r][k][j];
@@ -986,47 +1057,56 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
       for (int r = 0; r < NW; ++r) bl += lslot[par][r];
       bl *= inv;
     }
-    if constexpr (XG) {  // rank average: wave 0 exchanges, LDS hands it to the rest
-      if (w == 0) {
-        float gv[KX];
+    bool xg_ok = true;
+    if constexpr (XG) {  // rank average of the owned slots (and of the batch loss, wave 0)
+      float xv[XV];
 #pragma unroll
-        for (int k = 0; k < KX; ++k) gv[k] = (k < KG) ? g[k] : 0.f;
-        // the bout slot carries the batch loss in lane 63 (lanes >= C own no bias)
-        gv[KC] = (j < C) ? g[KC] : (j == 63 ? bl : 0.f);
-        const bool ok = xg_allreduce<KX, XWN>(gv, a, prs, rrs, gstep, j);
-#pragma unroll
-        for (int k = 0; k < KG; ++k) gavg[k][j] = gv[k];
-        if (j == 0) xabort = ok ? 0 : 1;
-        bl = rl(gv[KC], 63);
-      }
-      __syncthreads();  // barrier 2: the rank average (or the abort flag) is in LDS
-      if (xabort) {
-        done = s;
-        return false;
-      }
+      for (int i = 0; i < XV; ++i) xv[i] = 0.f;
 #pragma unroll
       for (int k = 0; k < KG; ++k)
-        if (owned(k)) g[k] = gavg[k][j];
-      if (owned(KC) && j >= C) g[KC] = 0.f;  // lane 63's loss slot is not a gradient
-    }
-    if (w == 0 && j == 0 && a.loss_out) a.loss_out[s] = bl;
-
-    // ---- Adam on the owned slots
-    {
+        if (owned(k)) xv[k / NW] = g[k];
+      xv[XV - 1] = bl;  // wave 0's batch loss (0 in the other waves)
+      xg_ok = xg_exchange_wave<XV, XWN>(xv, a, prs, rrs, gstep, j, w, NW);
 #pragma unroll
-      for (int k = 0; k < KG; ++k) {
-        if (owned(k) && slot_live(k)) adam1(pr[k], g[k], mr[k], vr[k], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
-      }
+      for (int k = 0; k < KG; ++k)
+        if (owned(k)) g[k] = xv[k / NW];
+      bl = xv[XV - 1];
+    }
+
+    // ---- Adam on the owned slots (tentative with XW > 0: undone if any wave's exchange timed out)
+    float bkp[KG], bkm[KG], bkv[KG];
+    if constexpr (XG) {
+#pragma unroll
+      for (int k = 0; k < KG; ++k)
+        if (owned(k)) { bkp[k] = pr[k]; bkm[k] = mr[k]; bkv[k] = vr[k]; }
+    }
+#pragma unroll
+    for (int k = 0; k < KG; ++k) {
+      if (owned(k) && slot_live(k)) adam1(pr[k], g[k], mr[k], vr[k], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
     }
     if constexpr (!REP) {  // publish owned slots; read the others after the next barrier
 #pragma unroll
       for (int k = 0; k < KG; ++k)
         if (owned(k)) pslot[k][j] = pr[k];
+      if (XG && j == 0) xab[w] = xg_ok ? 0 : 1;
       __syncthreads();
+      if constexpr (XG) {
+        bool abort = false;
+#pragma unroll
+        for (int r = 0; r < NW; ++r) abort |= (xab[r] != 0);
+        if (abort) {  // every wave sees the same flags: all leave before this step
+#pragma unroll
+          for (int k = 0; k < KG; ++k)
+            if (owned(k)) { pr[k] = bkp[k]; mr[k] = bkm[k]; vr[k] = bkv[k]; }
+          done = s;
+          return false;
+        }
+      }
 #pragma unroll
       for (int k = 0; k < KG; ++k)
         if (!owned(k)) pr[k] = pslot[k][j];
     }
+    if (w == 0 && j == 0 && a.loss_out) a.loss_out[s] = bl;
     return true;
   };
   for (int s0 = 0; s0 < a.steps; s0 += PF) {
@@ -1143,7 +1223,9 @@ size_t dct_mlp_xg_slab_granules(const int* dims, int L) {
   if (L != 2 || !dct_mlp_wave_supported(dims, L, 1)) return 0;
   const int D0 = (dims[0] == 5 && dims[2] == 2) ? 5 : (dims[0] <= 8 ? 8 : 16);
   const int CM = (dims[0] == 5 && dims[2] == 2) ? 2 : 4;
-  return (size_t)(D0 + CM + 2 + ((D0 + CM) & 1)) * 64;
+  // the single-wave kernel's [KX][64] layout or the row-parallel kernel's per-wave regions
+  const size_t wave_kernel = (size_t)(D0 + CM + 2 + ((D0 + CM) & 1)) * 64;
+  return wave_kernel > (size_t)dct::XG_ROWS_GRANULES ? wave_kernel : (size_t)dct::XG_ROWS_GRANULES;
 }
 
 int dct_mlp_wave_train(const int* dims, int L, const dct::MlpArgs* a, void* stream) {
