@@ -81,6 +81,7 @@ def _timed(ctx, fn):
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()
+    _release_together(ctx)
     t0 = time.perf_counter()
     fn()
     if ctx.backend == "nccl":
@@ -94,6 +95,21 @@ def _timed(ctx, fn):
     if ctx.is_distributed:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     return float(dt_t.item())
+
+
+def _release_together(ctx, margin_s: float = 0.002):
+    """Leave the start barrier at one shared wall-clock instant on every rank.
+
+    A barrier's release jitter (host wake-ups after the collective, a TCP round for gloo) puts
+    ranks' first launches tens of microseconds apart, and the early ranks' first step then waits
+    inside the timed window for the late one.  Rank 0 publishes a start time a couple of
+    milliseconds ahead (longer than that jitter) and every rank spins on the node's shared clock
+    until it: the window still contains all K steps of every rank, started together."""
+    if not ctx.is_distributed:
+        return
+    t_go = ctx.broadcast_object(time.time() + margin_s if ctx.rank == 0 else None, src=0)
+    while time.time() < t_go:
+        pass
 
 
 def _warmup(loop, n_items, warmup, loss):
