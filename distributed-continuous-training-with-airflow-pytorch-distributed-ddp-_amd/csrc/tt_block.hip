@@ -114,14 +114,22 @@ __device__ __forceinline__ void transpose_weights(const Args& a) {
   }
 }
 
-// 64-row LDS tile -> contiguous global rows, 16-byte chunks over the whole workgroup
+// 64-row LDS tile -> contiguous global rows, 16-byte chunks over the whole workgroup.  All of a
+// thread's LDS reads are issued before its stores (a rolled loop paid one LDS round trip each).
 template <int ROW_BYTES, int LD_BYTES>
 __device__ __forceinline__ void store_tile(void* g, const void* s) {
-  constexpr int CPR = ROW_BYTES / 16;
-  for (int idx = threadIdx.x; idx < T * CPR; idx += 256) {
-    const int r = idx / CPR, c = idx - r * CPR;
-    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(g) + r * ROW_BYTES + c * 16) =
-        *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(s) + r * LD_BYTES + c * 16);
+  constexpr int CPR = ROW_BYTES / 16, N = T * CPR / 256;
+  static_assert(T * CPR % 256 == 0, "whole 16-byte chunks per thread");
+  uint4 v[N];
+#pragma unroll
+  for (int it = 0; it < N; ++it) {
+    const int idx = it * 256 + threadIdx.x, r = idx / CPR, c = idx - r * CPR;
+    v[it] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(s) + r * LD_BYTES + c * 16);
+  }
+#pragma unroll
+  for (int it = 0; it < N; ++it) {
+    const int idx = it * 256 + threadIdx.x, r = idx / CPR, c = idx - r * CPR;
+    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(g) + r * ROW_BYTES + c * 16) = v[it];
   }
 }
 
@@ -448,14 +456,23 @@ __device__ __forceinline__ void store_rows16(void* gdst, const void* s, int wv, 
         *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(s) + r * LD_BYTES + c * 16);
   }
 }
-// global rows -> LDS tile (all 64 rows, whole workgroup)
+// global rows -> LDS tile (all 64 rows, whole workgroup).  Every global load of a thread is in
+// flight before the first LDS write: the rolled loop was partly unrolled by the compiler and ran its
+// remainder one HBM round trip per iteration (~2 us of a 3.5 us staging phase).
 template <int ROW_BYTES, int LD_BYTES>
 __device__ __forceinline__ void load_tile(void* s, const void* gsrc) {
-  constexpr int CPR = ROW_BYTES / 16;
-  for (int idx = threadIdx.x; idx < T * CPR; idx += 256) {
-    const int r = idx / CPR, c = idx - r * CPR;
-    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(s) + r * LD_BYTES + c * 16) =
-        *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(gsrc) + r * ROW_BYTES + c * 16);
+  constexpr int CPR = ROW_BYTES / 16, N = T * CPR / 256;
+  static_assert(T * CPR % 256 == 0, "whole 16-byte chunks per thread");
+  uint4 v[N];
+#pragma unroll
+  for (int it = 0; it < N; ++it) {
+    const int idx = it * 256 + threadIdx.x, r = idx / CPR, c = idx - r * CPR;
+    v[it] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(gsrc) + r * ROW_BYTES + c * 16);
+  }
+#pragma unroll
+  for (int it = 0; it < N; ++it) {
+    const int idx = it * 256 + threadIdx.x, r = idx / CPR, c = idx - r * CPR;
+    *reinterpret_cast<uint4*>(reinterpret_cast<char*>(s) + r * LD_BYTES + c * 16) = v[it];
   }
 }
 
