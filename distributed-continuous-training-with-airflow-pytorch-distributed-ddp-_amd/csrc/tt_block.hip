@@ -573,17 +573,29 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
 
   TT_MARK(0);
   // ---- P0: pre -> R (whole tile); dout rows -> G (fp32) and X (bf16); zero the LN partials
-  load_tile<FF * 2, F_LD * 2>(R, a.pre + (size_t)row0 * FF);
-  red[threadIdx.x] = 0.f;
+  {
+    // dout in row layout (lane -> row 16wv + (lane & 15), columns 16g..16g+15): 4 x 16-B loads
+    // per lane issued with the pre tile's, then 16-B LDS writes (was 16 scalar loads + 32 stores)
+    const int rl = 16 * wv + (lane & 15);
+    const float4* dp = reinterpret_cast<const float4*>(a.dout + (size_t)(row0 + rl) * DM + 16 * g);
+    float4 dv[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+    for (int q = 0; q < 4; ++q) dv[q] = dp[q];
+    load_tile<FF * 2, F_LD * 2>(R, a.pre + (size_t)row0 * FF);
+    red[threadIdx.x] = 0.f;
+    float4* gp = reinterpret_cast<float4*>(G + rl * HS_LD + 16 * g);
+    bf16x8 o[2];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int rl = 16 * wv + 4 * g + r, col = 16 * t + c;
-      const float v = a.dout[(size_t)(row0 + rl) * DM + col];
-      G[rl * HS_LD + col] = v;
-      X[rl * XB_LD + col] = f32_to_bf16(v);
+    for (int q = 0; q < 4; ++q) {
+      gp[q] = dv[q];
+      o[q >> 1][4 * (q & 1)] = (short)f32_to_bf16(dv[q].x);
+      o[q >> 1][4 * (q & 1) + 1] = (short)f32_to_bf16(dv[q].y);
+      o[q >> 1][4 * (q & 1) + 2] = (short)f32_to_bf16(dv[q].z);
+      o[q >> 1][4 * (q & 1) + 3] = (short)f32_to_bf16(dv[q].w);
     }
+    *reinterpret_cast<bf16x8*>(X + rl * XB_LD + 16 * g) = o[0];
+    *reinterpret_cast<bf16x8*>(X + rl * XB_LD + 16 * g + 8) = o[1];
+  }
   __syncthreads();
 
   TT_MARK(1);
