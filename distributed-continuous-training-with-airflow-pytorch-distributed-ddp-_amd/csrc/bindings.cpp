@@ -193,11 +193,12 @@ PYBIND11_MODULE(_dct_native, m) {
              uintptr_t idx, int n_items, int B, float lr, float b1, float b2, float eps, float wd, float dropout,
              uint32_t seed, uintptr_t loss_out, int64_t loss_len, int loss_kind, uintptr_t step_counter,
              uintptr_t xg_recv, uintptr_t xg_peers, int xg_world, int xg_rank, uintptr_t xg_status,
-             int64_t xg_timeout, int xg_poll) {
+             int64_t xg_timeout, int xg_poll, uintptr_t xg_ticks) {
             auto l = std::make_unique<MlpLaunch>(MlpLaunch{plan});
             l->base = make_train_args(plan, p, mo, vo, 0, X, ldx, Y, idx, n_items, B, 1, 0, lr, b1, b2, eps, wd,
                                       dropout, seed, 0, loss_out, 0, loss_kind, step_counter, 0, 0, 0, 0, xg_recv,
                                       xg_peers, xg_world, xg_rank, xg_status, xg_timeout, xg_poll);
+            l->base.xg_ticks = P<unsigned long long>(xg_ticks);
             l->n_items = n_items;
             l->loss_len = loss_out ? loss_len : 0;
             return l;
@@ -207,7 +208,7 @@ PYBIND11_MODULE(_dct_native, m) {
           py::arg("dropout"), py::arg("seed"), py::arg("loss_out"), py::arg("loss_len"), py::arg("loss_kind"),
           py::arg("step_counter"), py::arg("xg_recv") = 0, py::arg("xg_peers") = 0, py::arg("xg_world") = 0,
           py::arg("xg_rank") = 0, py::arg("xg_status") = 0, py::arg("xg_timeout") = 200000000LL,
-          py::arg("xg_poll") = 0)
+          py::arg("xg_poll") = 0, py::arg("xg_ticks") = 0)
       .def(
           "eval",
           [](const MlpPlan& plan, uintptr_t p, uintptr_t X, int ldx, uintptr_t Y, uintptr_t idx, int n_items,

@@ -99,6 +99,9 @@ struct MlpArgs {
   unsigned int* xg_status;                  // [0]: 0 ok, else (global step + 1) of a timeout
   long long xg_timeout;                     // spin limit in s_memrealtime ticks (100 MHz)
   int xg_poll;                              // 0 full sweeps, 1 probe-then-sweep, 2 sequential
+  // optional (row-parallel kernel): wave 0 adds the s_memrealtime ticks (100 MHz) its exchange
+  // took over the launch - the allreduce_ms metric of the fused DDP step
+  unsigned long long* xg_ticks;
 };
 
 constexpr int XG_MAXW = 8;  // ranks of the in-kernel exchange (one node)

@@ -926,6 +926,7 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
     }
   }
   int done = a.steps;
+  unsigned long long xg_ticks_acc = 0;
 
   // one optimizer step; returns false when the launch must stop (exchange timeout)
   auto step = [&](const int s, uint32_t& vslot, int& islot) -> bool {
@@ -1066,7 +1067,10 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
       for (int k = 0; k < KG; ++k)
         if (owned(k)) xv[k / NW] = g[k];
       xv[XV - 1] = bl;  // wave 0's batch loss (0 in the other waves)
+      const bool timing = (w == 0) && (a.xg_ticks != nullptr);
+      const unsigned long long tx = timing ? __builtin_amdgcn_s_memrealtime() : 0ull;
       xg_ok = xg_exchange_wave<XV, XWN>(xv, a, prs, rrs, gstep, j, w, NW);
+      if (timing) xg_ticks_acc += __builtin_amdgcn_s_memrealtime() - tx;
 #pragma unroll
       for (int k = 0; k < KG; ++k)
         if (owned(k)) g[k] = xv[k / NW];
@@ -1119,6 +1123,8 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
   }
   if (w == 0 && a.step_counter && j == 0)
     __hip_atomic_store(a.step_counter, t0 + done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (XG && w == 0 && j == 0 && a.xg_ticks)
+    __hip_atomic_fetch_add(a.xg_ticks, xg_ticks_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // ---- write back: every wave holds the same parameters; each slot's moments live in its owner
 #pragma unroll
   for (int k = 0; k < KG; ++k) {

@@ -152,7 +152,8 @@ class FusedMLPKernel:
     def prepare_train(self, p, m, v, X, Y, idx, n_items: int, batch: int, lr: float, betas=(0.9, 0.999),
                       eps: float = 1e-8, weight_decay: float = 0.0, dropout: float = 0.0, seed: int = 0,
                       loss_out: Optional[torch.Tensor] = None, loss: str = "ce",
-                      step_counter: Optional[torch.Tensor] = None, xg=None, xg_timeout_s: float = 2.0) -> "BoundTrain":
+                      step_counter: Optional[torch.Tensor] = None, xg=None, xg_timeout_s: float = 2.0,
+                      xg_ticks: Optional[torch.Tensor] = None) -> "BoundTrain":
         """Validate the operands of persistent train-mode launches ONCE and bind them natively.
 
         ``BoundTrain.run(first_step, steps)`` then launches steps [first_step, first_step+steps)
@@ -178,12 +179,16 @@ class FusedMLPKernel:
             xg_args = dict(xg_recv=xg.recv, xg_peers=xg.peers, xg_world=xg.world, xg_rank=xg.rank,
                            xg_status=xg.status, xg_timeout=int(xg_timeout_s * 1e8),
                            xg_poll=int(os.environ.get("DCT_XG_POLL", "0")))
+            if xg_ticks is not None:
+                if not (xg_ticks.is_cuda and xg_ticks.dtype == torch.int64 and xg_ticks.numel() >= 1):
+                    raise ValueError("xg_ticks must be a cuda int64 counter")
+                xg_args["xg_ticks"] = ptr(xg_ticks)
         launch = self.plan.prepare_train(
             ptr(p), ptr(m), ptr(v), ptr(X), X.stride(0), ptr(Y), ptr(idx), int(n_items), int(batch), float(lr),
             float(betas[0]), float(betas[1]), float(eps), float(weight_decay), float(dropout),
             int(seed) & 0xFFFFFFFF, ptr(loss_out), 0 if loss_out is None else loss_out.numel(), LOSS_KINDS[loss],
             ptr(step_counter), **xg_args)
-        return BoundTrain(launch, (p, m, v, X, Y, idx, loss_out, step_counter, xg), p.device.index or 0)
+        return BoundTrain(launch, (p, m, v, X, Y, idx, loss_out, step_counter, xg, xg_ticks), p.device.index or 0)
 
     # ------------------------------------------------------------ in-kernel all-reduce
     def xg_slab_granules(self) -> int:

@@ -23,6 +23,7 @@ Two executors with one interface:
 """
 from __future__ import annotations
 
+import time
 from dataclasses import dataclass
 from typing import List, Sequence, Tuple
 
@@ -74,6 +75,7 @@ class TorchBucketReducer:
         self.plan = plan
         self.world = world_size
         self.host_staging = bool(host_staging)
+        self.wait_s = 0.0  # exposed all-reduce wait, accumulated (the Trainer's allreduce_ms)
         self.expected = [0] * len(plan.offsets)
         for b in plan.param_bucket:
             self.expected[b] += 1
@@ -107,12 +109,14 @@ class TorchBucketReducer:
         while self.next < len(self.expected):
             self._launch(self.next)
             self.next += 1
+        t0 = time.perf_counter()
         for w, view, buf in self.works:
             w.wait()
             buf.div_(self.world)
             if buf is not view:
                 view.copy_(buf)
         self.works = []
+        self.wait_s += time.perf_counter() - t0  # all-reduce time NOT hidden behind the backward
 
     @property
     def num_buckets(self):

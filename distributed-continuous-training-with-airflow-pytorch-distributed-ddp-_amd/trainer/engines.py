@@ -129,9 +129,12 @@ class FusedMLPEngine(_EngineBase):
 
             self.xg = setup_peer_exchange(self.kernel, ctx, self.B)
             self.xg_timeout_s = timeout_s()
+            # exchange time of the launches (s_memrealtime ticks, 100 MHz) -> allreduce_ms per epoch
+            self.xg_ticks = torch.zeros(1, dtype=torch.int64, device=dev) if self.xg is not None else None
             if self.xg is None and self.comm is None:
                 raise RuntimeError("distributed fused engine needs RCCL (backend nccl) or the in-kernel "
                                    "xGMI exchange; neither is available")
+        self.last_allreduce_ms = None
 
     # ------------------------------------------------------------------ params
     def _linear_params(self):
@@ -231,7 +234,8 @@ class FusedMLPEngine(_EngineBase):
                                            batch=self.B, lr=a["lr"], betas=a["betas"], eps=a["eps"],
                                            weight_decay=a["weight_decay"], dropout=self.dropout, seed=self.rank_seed,
                                            loss_out=loss_out, loss=self.loss, step_counter=self.step_counter,
-                                           xg=self.xg, xg_timeout_s=getattr(self, "xg_timeout_s", 20.0))
+                                           xg=self.xg, xg_timeout_s=getattr(self, "xg_timeout_s", 20.0),
+                                           xg_ticks=getattr(self, "xg_ticks", None) if self.xg is not None else None)
             self._bound, self._bound_key = bl, key
         return bl
 
@@ -358,6 +362,9 @@ class FusedMLPEngine(_EngineBase):
         check_device("fused epoch")
         if self.xg is not None:
             self.xg_verify(fallback=False)
+            # wave 0's exchange time over the epoch (the in-kernel all-reduce: X5 + X6 of SURVEY 2.6)
+            self.last_allreduce_ms = float(self.xg_ticks.item()) / 1e5
+            self.xg_ticks.zero_()
         self.global_step += steps
         return loss_out[:steps]
 

@@ -310,6 +310,9 @@ class Trainer:
                 extra = {"epoch_time_s": epoch_t, "train_time_s": train_t,
                          "samples_per_sec": samples / max(train_t, 1e-9),
                          "step_time_ms": 1e3 * train_t / max(n_steps, 1)}
+                ar_ms = self._epoch_allreduce_ms()
+                if ar_ms is not None:
+                    extra["allreduce_ms"] = ar_ms
                 self._log_metrics(extra, self.global_step)
                 with trace_range(f"epoch{epoch}/checkpoint"):
                     self._run_checkpoint_callbacks(n_steps)
@@ -336,6 +339,20 @@ class Trainer:
     def teardown(self):
         if self.ctx is not None:
             shutdown(self.ctx)
+
+    def _epoch_allreduce_ms(self) -> Optional[float]:
+        """Gradient all-reduce time of the epoch (SURVEY 5.5 extra key): the in-kernel exchange's
+        own clock on the fused engine, the exposed (not overlapped) wait of the torch reducer on
+        the gloo path; None where it is not measured (the RCCL comm-stream reducers)."""
+        eng = self.engine
+        if getattr(eng, "last_allreduce_ms", None) is not None:
+            return float(eng.last_allreduce_ms)
+        red = getattr(eng, "reducer", None)
+        if red is not None and hasattr(red, "wait_s"):
+            ms = red.wait_s * 1e3
+            red.wait_s = 0.0
+            return ms
+        return None
 
     # ------------------------------------------------------------------ loops
     def _maybe_fault(self, step: int):

@@ -21,7 +21,8 @@ from dct_amd.trainer import DDPStrategy, Trainer, seed_everything  # noqa: E402
 
 def main():
     out_dir, epochs, rows = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
-    resume = len(sys.argv) > 4 and sys.argv[4] == "resume"
+    resume = "resume" in sys.argv[4:]
+    accel = "gpu" if "gpu" in sys.argv[4:] else "cpu"  # gpu: fused engine (+ in-kernel exchange)
     seed_everything(42)
     x, y = weather_tensors(rows, seed=0)
     ds = TensorPairDataset(x, y)
@@ -32,16 +33,18 @@ def main():
                          monitor="val_loss", mode="min", save_top_k=1, save_last=True)
     logger = MLFlowLogger(experiment_name="weather_forecasting", tracking_uri="file://" + os.path.join(out_dir, "mlruns"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    trainer = Trainer(max_epochs=epochs, accelerator="cpu", num_nodes=world,
+    trainer = Trainer(max_epochs=epochs, accelerator=accel, num_nodes=world,
                       strategy=DDPStrategy(find_unused_parameters=False) if world > 1 else "auto", logger=logger,
-                      callbacks=[ck], log_every_n_steps=5, engine="autograd", verbose=False)
+                      callbacks=[ck], log_every_n_steps=5, engine="autograd" if accel == "cpu" else "auto",
+                      verbose=False)
     ckpt_path = os.path.join(out_dir, "models", "last.ckpt") if resume else None
     trainer.fit(model, DataLoader(tr, batch_size=4, shuffle=True), DataLoader(va, batch_size=4), ckpt_path=ckpt_path)
     flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).tolist()
     rank = int(os.environ.get("RANK", "0"))
     with open(os.path.join(out_dir, f"params_rank{rank}.json"), "w") as f:
         json.dump({"params": flat, "global_step": trainer.global_step, "val_loss": trainer.callback_metrics.get("val_loss"),
-                   "best": ck.best_model_path}, f)
+                   "best": ck.best_model_path, "engine": trainer.engine.name,
+                   "xg": getattr(trainer.engine, "xg", None) is not None}, f)
 
 
 if __name__ == "__main__":

@@ -75,7 +75,7 @@ def test_two_rank_gloo_ddp_matches_emulation_and_rank0_io(tmp_path):
     assert len(runs) == 1  # rank 0 only
     logged = set(os.listdir(tmp_path / "mlruns" / exp_dirs[0] / runs[0] / "metrics"))
     # reference keys plus the throughput extras
-    assert {"train_loss", "val_loss", "val_acc", "epoch", "samples_per_sec", "step_time_ms"} <= logged, logged
+    assert {"train_loss", "val_loss", "val_acc", "epoch", "samples_per_sec", "step_time_ms", "allreduce_ms"} <= logged, logged
 
 
 @pytest.mark.slow

@@ -139,3 +139,24 @@ def test_autograd_engine_logs_train_loss_after_graph_replays(monkeypatch):
     ve = torch.tensor([v for _, v in hist_e])
     assert torch.isfinite(vg).all() and torch.allclose(vg, ve, atol=1e-4), (vg - ve).abs().max()
     assert abs(last_g - last_e) < 1e-4
+
+
+def test_two_rank_trainer_on_one_gpu_in_kernel_exchange(tmp_path):
+    """Two ranks sharing the GPU (gloo control plane): the Trainer picks the fused engine with the
+    in-kernel exchange over IPC mappings; replicas stay bit-identical, rank 0 alone writes the
+    checkpoints / MLflow run, and the exchange time is logged as allreduce_ms."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29671", os.path.join(ROOT, "tests", "ddp_worker.py"),
+           str(tmp_path), "2", "600", "gpu"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    p0 = json.loads((tmp_path / "params_rank0.json").read_text())
+    p1 = json.loads((tmp_path / "params_rank1.json").read_text())
+    assert p0["engine"] == "fused" and p0["xg"] and p0["params"] == p1["params"]
+    exp = [d for d in os.listdir(tmp_path / "mlruns") if d.isdigit() and d != "0"][0]
+    run = [d for d in os.listdir(tmp_path / "mlruns" / exp) if len(d) == 32][0]
+    mdir = tmp_path / "mlruns" / exp / run / "metrics"
+    assert {"train_loss", "val_loss", "allreduce_ms", "samples_per_sec"} <= set(os.listdir(mdir))
+    ar = [float(ln.split()[1]) for ln in (mdir / "allreduce_ms").read_text().splitlines()]
+    assert len(ar) == 2 and all(v > 0 for v in ar)
