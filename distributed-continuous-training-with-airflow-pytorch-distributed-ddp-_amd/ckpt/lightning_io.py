@@ -109,3 +109,24 @@ def save_checkpoint(ckpt: Dict[str, Any], path: str) -> str:
 def load_checkpoint(path: str, map_location="cpu") -> Dict[str, Any]:
     """Safe load: never unpickles arbitrary objects (weights_only=True)."""
     return torch.load(path, map_location=map_location, weights_only=True)
+
+
+def elastic_restart_count() -> int:
+    """How many times torchrun has restarted this job's workers (0 on the first attempt)."""
+    try:
+        return int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+    except ValueError:
+        return 0
+
+
+def resume_checkpoint(model_dir: str, requested: bool = False, name: str = "last.ckpt") -> Optional[str]:
+    """The checkpoint ``Trainer.fit(ckpt_path=...)`` should resume from, or None.
+
+    The reference always starts from scratch (train_lightning_ddp.py:143), so a fresh launch resumes
+    only when asked (``--resume``).  A torchrun elastic RESTART (``--max-restarts``, after a rank
+    failed) resumes from ``last.ckpt`` when one exists: the restarted workers continue the run at
+    the epoch after the last completed one instead of silently retraining from epoch 0."""
+    path = os.path.join(model_dir, name)
+    if (requested or elastic_restart_count() > 0) and os.path.exists(path):
+        return path
+    return None

@@ -158,7 +158,10 @@ def init_distributed(accelerator: str = "auto", backend: str = "auto", timeout_s
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", e["master_addr"])
             os.environ.setdefault("MASTER_PORT", str(e["master_port"]))
-            kwargs = dict(backend=backend, init_method="env://", world_size=e["world_size"], rank=e["rank"],
+            # no explicit init_method: torch then takes its env:// path AND, under torchrun, the
+            # agent's store with a per-attempt key prefix - an explicit "env://" skips that prefix, so
+            # workers restarted by --max-restarts read the dead attempt's gloo addresses and fail
+            kwargs = dict(backend=backend, world_size=e["world_size"], rank=e["rank"],
                           timeout=datetime.timedelta(seconds=timeout_s))
             if backend == "nccl":
                 kwargs["device_id"] = device

@@ -356,6 +356,10 @@ class Trainer:
 
     # ------------------------------------------------------------------ loops
     def _maybe_fault(self, step: int):
+        # an injected fault fires on the first attempt only: the workers torchrun restarts after it
+        # (--max-restarts) are the recovery being tested, not new victims
+        if self.fault_inject and int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or 0) > 0:
+            return
         if self.fault_inject and self.global_rank == self.fault_inject[0] and step >= self.fault_inject[1]:
             print(f"[dct] fault injection: rank {self.global_rank} exits at step {step}", flush=True)
             sys.stdout.flush()

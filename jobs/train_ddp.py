@@ -20,7 +20,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import dct_amd  # noqa: E402
-from dct_amd.ckpt import ModelCheckpoint  # noqa: E402
+from dct_amd.ckpt import ModelCheckpoint, resume_checkpoint  # noqa: E402
 from dct_amd.config import default_config  # noqa: E402
 from dct_amd.data.dataset import TensorPairDataset, WeatherDataset  # noqa: E402
 from dct_amd.models import build_model  # noqa: E402
@@ -93,10 +93,9 @@ def main(argv=None) -> int:
         log_every_n_steps=a.log_every_n_steps,
         engine=a.engine,
     )
-    ckpt_path = None
     last = os.path.join(a.model_dir, "last.ckpt")
-    if a.resume and os.path.exists(last):
-        ckpt_path = last
+    # --resume, or a torchrun elastic restart after a failed rank: continue from last.ckpt
+    ckpt_path = resume_checkpoint(a.model_dir, a.resume)
     trainer.fit(model, train_loader, val_loader, ckpt_path=ckpt_path)
 
     if trainer.global_rank == 0:

@@ -11,7 +11,7 @@ import torch  # noqa: E402
 from torch.utils.data import DataLoader, random_split  # noqa: E402
 
 import dct_amd  # noqa: E402,F401
-from dct_amd.ckpt import ModelCheckpoint  # noqa: E402
+from dct_amd.ckpt import ModelCheckpoint, resume_checkpoint  # noqa: E402
 from dct_amd.data.dataset import TensorPairDataset  # noqa: E402
 from dct_amd.data.synthetic import weather_tensors  # noqa: E402
 from dct_amd.models.mlp import MLPClassifier  # noqa: E402
@@ -37,12 +37,13 @@ def main():
                       strategy=DDPStrategy(find_unused_parameters=False) if world > 1 else "auto", logger=logger,
                       callbacks=[ck], log_every_n_steps=5, engine="autograd" if accel == "cpu" else "auto",
                       verbose=False)
-    ckpt_path = os.path.join(out_dir, "models", "last.ckpt") if resume else None
+    ckpt_path = resume_checkpoint(os.path.join(out_dir, "models"), resume)  # --resume or an elastic restart
     trainer.fit(model, DataLoader(tr, batch_size=4, shuffle=True), DataLoader(va, batch_size=4), ckpt_path=ckpt_path)
     flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).tolist()
     rank = int(os.environ.get("RANK", "0"))
     with open(os.path.join(out_dir, f"params_rank{rank}.json"), "w") as f:
-        json.dump({"params": flat, "global_step": trainer.global_step, "val_loss": trainer.callback_metrics.get("val_loss"),
+        json.dump({"params": flat, "global_step": trainer.global_step,
+                   "restart": int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")), "val_loss": trainer.callback_metrics.get("val_loss"),
                    "best": ck.best_model_path, "engine": trainer.engine.name,
                    "xg": getattr(trainer.engine, "xg", None) is not None}, f)
 

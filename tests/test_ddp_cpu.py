@@ -20,12 +20,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKER = os.path.join(ROOT, "tests", "ddp_worker.py")
 
 
-def _torchrun(nproc, port, args, env=None, timeout=600):
+def _torchrun(nproc, port, args, env=None, timeout=600, max_restarts=0):
     e = dict(os.environ)
     e.update(env or {})
     e.pop("CUDA_VISIBLE_DEVICES", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr=127.0.0.1", f"--master-port={port}", WORKER] + [str(a) for a in args]
+           "--master-addr=127.0.0.1", f"--master-port={port}", f"--max-restarts={max_restarts}",
+           WORKER] + [str(a) for a in args]
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=e)
 
 
@@ -106,3 +107,40 @@ def test_fault_injection_kills_the_chosen_rank(tmp_path):
     r = _torchrun(2, 29636, [tmp_path, 2, 400], env={"DCT_FAULT_RANK": "1", "DCT_FAULT_STEP": "7"}, timeout=300)
     assert r.returncode != 0
     assert "fault injection: rank 1 exits at step 7" in (r.stdout + r.stderr)
+
+
+@pytest.mark.slow
+def test_crash_then_relaunch_resumes_from_last_checkpoint(tmp_path):
+    """Rank 1 killed mid-epoch 2; the relaunched job (--resume: what an Airflow retry or a torchrun
+    elastic restart does - ckpt.resume_checkpoint) continues from last.ckpt written at the end of
+    epoch 1 and finishes with exactly the uninterrupted run's parameters and step count
+    (failure detection + checkpoint resume)."""
+    full, faulty = tmp_path / "full", tmp_path / "faulty"
+    full.mkdir()
+    faulty.mkdir()
+    rows, epochs = 400, 3  # 320 train rows / 2 ranks / batch 4 = 40 steps per epoch
+    assert _torchrun(2, 29637, [full, epochs, rows]).returncode == 0
+    r = _torchrun(2, 29638, [faulty, epochs, rows], env={"DCT_FAULT_RANK": "1", "DCT_FAULT_STEP": "60"})
+    assert r.returncode != 0 and "fault injection: rank 1 exits at step 60" in (r.stdout + r.stderr)
+    assert (faulty / "models" / "last.ckpt").exists()
+    r = _torchrun(2, 29639, [faulty, epochs, rows, "resume"])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    a = json.loads((full / "params_rank0.json").read_text())
+    b = json.loads((faulty / "params_rank0.json").read_text())
+    assert a["global_step"] == b["global_step"] == 120
+    assert torch.allclose(torch.tensor(a["params"]), torch.tensor(b["params"]), atol=1e-6)
+
+
+def test_resume_checkpoint_policy(tmp_path, monkeypatch):
+    """Fresh launches start from scratch unless --resume (the reference never resumes); a torchrun
+    elastic restart (TORCHELASTIC_RESTART_COUNT > 0) resumes from last.ckpt when it exists."""
+    from dct_amd.ckpt import resume_checkpoint
+
+    monkeypatch.delenv("TORCHELASTIC_RESTART_COUNT", raising=False)
+    assert resume_checkpoint(str(tmp_path), False) is None
+    assert resume_checkpoint(str(tmp_path), True) is None  # nothing to resume from
+    (tmp_path / "last.ckpt").write_bytes(b"x")
+    assert resume_checkpoint(str(tmp_path), False) is None
+    assert resume_checkpoint(str(tmp_path), True) == str(tmp_path / "last.ckpt")
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "1")
+    assert resume_checkpoint(str(tmp_path), False) == str(tmp_path / "last.ckpt")
