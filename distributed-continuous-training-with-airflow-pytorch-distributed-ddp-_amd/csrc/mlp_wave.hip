@@ -854,7 +854,9 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
   };
   // REP: every wave runs Adam on every slot (one barrier per step instead of two).  Measured on
   // the weather step it loses to the owner split: 0.893 vs 0.732 us/step (MI355X, round 2).
-  auto owned = [](int k) constexpr -> bool { return REP || (k % NW) == W; };
+  // slot k -> wave (k + 1) % NW: the wave that owns an extra slot is not wave 0, which also sums
+  // the batch loss
+  auto owned = [](int k) constexpr -> bool { return REP || ((k + 1) % NW) == W; };
 
   // ---------------------------------------------------------------- parameters -> registers
   float pr[KG], mr[KG], vr[KG];
@@ -928,8 +930,23 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
   int done = a.steps;
   unsigned long long xg_ticks_acc = 0;
 
+  // diagnostic phase stamps (profiling build, tools/prof_rows.py): shader-clock deltas of wave W
+  // accumulated per phase; never compiled into production launches
+#ifdef DCT_WAVE_PROF
+  unsigned long long rpt[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, rprev = 0;
+#define RSTAMP(k)                                                                            \
+  if (a.prof) {                                                                              \
+    unsigned long long t_;                                                                   \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");              \
+    if ((k) >= 0) rpt[(k) < 0 ? 0 : (k)] += t_ - rprev;                                      \
+    rprev = t_;                                                                              \
+  }
+#else
+#define RSTAMP(k)
+#endif
   // one optimizer step; returns false when the launch must stop (exchange timeout)
   auto step = [&](const int s, uint32_t& vslot, int& islot) -> bool {
+    RSTAMP(-1)
     const int bs = min(B, a.n_items - s * B);
     const bool live = w < bs;
     const uint32_t gstep = step_base + (uint32_t)s;
@@ -943,9 +960,6 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
     const uint32_t hkey = (a.seed * 0x9E3779B1u) ^ (gstep * 0x85EBCA77u);
     const uint32_t hrnd = wave_hash(hkey ^ ((uint32_t)(w * 64 + j) * 0xC2B2AE3Du));
     const bool dropped = hrnd < drop_thr;  // drop_thr == 0: never
-    const int t_adam = t0 + s + 1;
-    const float step_size = a.lr * __builtin_amdgcn_rcpf(1.f - pow_t(l2b1, (float)t_adam));
-    const float rbc2 = __builtin_amdgcn_rsqf(1.f - pow_t(l2b2, (float)t_adam));
 
     float x[D0];
 #pragma unroll
@@ -955,92 +969,113 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
     }
     const int y = live ? __builtin_amdgcn_readlane((int)cur, D0) : 0;
 
-    // ---- layer 0 for this row: h = dropout(relu(W0[j] . x + b0))
-    float h;
-    {
-      float z = pr[KB];
-#pragma unroll
-      for (int k = 0; k < D0; ++k) z = fmaf(pr[k], x[k], z);
-      z = fmaxf(z, 0.f) * keep_scale;  // keep_scale == 1 without dropout
-      h = (own1 && !dropped) ? z : 0.f;
-    }
-    // ---- output layer: logits[c] = sum_j Wout[c][j] h_j + bout[c]  (cross-lane, wave-uniform)
-    float zc[CM];
-#pragma unroll
-    for (int c = 0; c < CM; ++c) zc[c] = pr[KO + c] * h;
-    wave_sum_n(zc);
-#pragma unroll
-    for (int c = 0; c < CM; ++c) zc[c] += rl(pr[KC], c);
-
-    // ---- loss + dlogits of this row (wave-uniform)
-    float dz[CM];
+    RSTAMP(0)
+    float g[KG];
     float lb = 0.f;
+    // two-class CE: the loss VALUE (a log) is not on the gradient's path - it is formed after the
+    // gradient stores, where it overlaps their LDS latency
+    float ce_se = 1.f, ce_off = 0.f;
     const float inv = __builtin_amdgcn_rcpf((float)(bs > 0 ? bs : 1));  // bs <= 8: exact
-    if (a.loss_kind == 0) {
-      if constexpr (EX && CM == 2) {
-        // two classes: softmax = logistic of the margin; one exp, one log, one rcp
-        const float d = zc[1] - zc[0];
-        const float t = __builtin_amdgcn_exp2f(-fabsf(d) * 1.4426950408889634f);  // exp(-|d|)
-        const float se = 1.f + t;
-        const float rs = __builtin_amdgcn_rcpf(se);
-        const float mx = fmaxf(zc[0], zc[1]);
-        const float lse = mx + __builtin_amdgcn_logf(se) * 0.69314718055994531f;
-        const float p1 = d >= 0.f ? rs : t * rs;  // softmax prob of class 1
-        lb = lse - (y == 1 ? zc[1] : zc[0]);
-        dz[1] = (p1 - (y == 1 ? 1.f : 0.f)) * inv;
-        dz[0] = -dz[1];
-      } else {
-        float mx = -3.402823466e+38f;
+    if (NW == 4 || w < B) {  // waves beyond the batch (NW = 8, B <= 4) only own Adam slots
+      // ---- layer 0 for this row: h = dropout(relu(W0[j] . x + b0))
+      float h;
+      {
+        float z = pr[KB];
 #pragma unroll
-        for (int c = 0; c < CM; ++c)
-          if (c < C) mx = fmaxf(mx, zc[c]);
-        float e[CM], se = 0.f, zy = 0.f;
+        for (int k = 0; k < D0; ++k) z = fmaf(pr[k], x[k], z);
+        z = fmaxf(z, 0.f) * keep_scale;  // keep_scale == 1 without dropout
+        h = (own1 && !dropped) ? z : 0.f;
+      }
+      RSTAMP(1)
+      // ---- output layer: logits[c] = sum_j Wout[c][j] h_j + bout[c]  (cross-lane, wave-uniform)
+      float zc[CM];
+#pragma unroll
+      for (int c = 0; c < CM; ++c) zc[c] = pr[KO + c] * h;
+      wave_sum_n(zc);
+#pragma unroll
+      for (int c = 0; c < CM; ++c) zc[c] += rl(pr[KC], c);
+
+      RSTAMP(2)
+      // ---- loss + dlogits of this row (wave-uniform)
+      float dz[CM];
+      if (a.loss_kind == 0) {
+        if constexpr (EX && CM == 2) {
+          // two classes: softmax = logistic of the margin; one exp, one rcp (+ the deferred log)
+          const float d = zc[1] - zc[0];
+          const float t = __builtin_amdgcn_exp2f(-fabsf(d) * 1.4426950408889634f);  // exp(-|d|)
+          const float se = 1.f + t;
+          const float rs = __builtin_amdgcn_rcpf(se);
+          const float p1 = d >= 0.f ? rs : t * rs;  // softmax prob of class 1
+          ce_se = se;
+          ce_off = fmaxf(zc[0], zc[1]) - (y == 1 ? zc[1] : zc[0]);  // lb = ce_off + log(se)
+          dz[1] = (p1 - (y == 1 ? 1.f : 0.f)) * inv;
+          dz[0] = -dz[1];
+        } else {
+          float mx = -3.402823466e+38f;
+#pragma unroll
+          for (int c = 0; c < CM; ++c)
+            if (c < C) mx = fmaxf(mx, zc[c]);
+          float e[CM], se = 0.f, zy = 0.f;
+#pragma unroll
+          for (int c = 0; c < CM; ++c) {
+            e[c] = (c < C) ? __builtin_amdgcn_exp2f((zc[c] - mx) * 1.4426950408889634f) : 0.f;
+            se += e[c];
+            zy = (c == y) ? zc[c] : zy;
+          }
+          lb = mx + __builtin_amdgcn_logf(se) * 0.69314718055994531f - zy;
+          const float rs = __builtin_amdgcn_rcpf(se);
+#pragma unroll
+          for (int c = 0; c < CM; ++c) dz[c] = (e[c] * rs - (c == y ? 1.f : 0.f)) * inv;
+        }
+      } else {
+        const float sc = 2.f / (float)C;
 #pragma unroll
         for (int c = 0; c < CM; ++c) {
-          e[c] = (c < C) ? __builtin_amdgcn_exp2f((zc[c] - mx) * 1.4426950408889634f) : 0.f;
-          se += e[c];
-          zy = (c == y) ? zc[c] : zy;
+          const float d = (c < C) ? zc[c] - (c == y ? 1.f : 0.f) : 0.f;
+          lb += d * d;
+          dz[c] = d * sc * inv;
         }
-        lb = mx + __builtin_amdgcn_logf(se) * 0.69314718055994531f - zy;
-        const float rs = __builtin_amdgcn_rcpf(se);
+        lb *= 1.f / (float)C;
+      }
 #pragma unroll
-        for (int c = 0; c < CM; ++c) dz[c] = (e[c] * rs - (c == y ? 1.f : 0.f)) * inv;
+      for (int c = 0; c < CM; ++c) dz[c] = live ? dz[c] : 0.f;
+      lb = live ? lb : 0.f;
+
+      RSTAMP(3)
+      // ---- backward of this row (lane-local) -> per-row gradient of every slot
+      {
+        float gsum = 0.f;
+#pragma unroll
+        for (int c = 0; c < CM; ++c) gsum = fmaf(dz[c], pr[KO + c], gsum);
+        const float dh = (h > 0.f) ? gsum * keep_scale : 0.f;
+#pragma unroll
+        for (int k = 0; k < D0; ++k) g[k] = dh * x[k];
+        g[KB] = dh;
+#pragma unroll
+        for (int c = 0; c < CM; ++c) g[KO + c] = dz[c] * h;
+        float gbo = 0.f;
+#pragma unroll
+        for (int c = 0; c < CM; ++c) gbo = (c == j) ? dz[c] : gbo;
+        g[KC] = gbo;
       }
     } else {
-      const float sc = 2.f / (float)C;
 #pragma unroll
-      for (int c = 0; c < CM; ++c) {
-        const float d = (c < C) ? zc[c] - (c == y ? 1.f : 0.f) : 0.f;
-        lb += d * d;
-        dz[c] = d * sc * inv;
-      }
-      lb *= 1.f / (float)C;
-    }
-#pragma unroll
-    for (int c = 0; c < CM; ++c) dz[c] = live ? dz[c] : 0.f;
-    lb = live ? lb : 0.f;
-
-    // ---- backward of this row (lane-local) -> per-row gradient of every slot
-    float g[KG];
-    {
-      float gsum = 0.f;
-#pragma unroll
-      for (int c = 0; c < CM; ++c) gsum = fmaf(dz[c], pr[KO + c], gsum);
-      const float dh = (h > 0.f) ? gsum * keep_scale : 0.f;
-#pragma unroll
-      for (int k = 0; k < D0; ++k) g[k] = dh * x[k];
-      g[KB] = dh;
-#pragma unroll
-      for (int c = 0; c < CM; ++c) g[KO + c] = dz[c] * h;
-      float gbo = 0.f;
-#pragma unroll
-      for (int c = 0; c < CM; ++c) gbo = (c == j) ? dz[c] : gbo;
-      g[KC] = gbo;
+      for (int k = 0; k < KG; ++k) g[k] = 0.f;
     }
 #pragma unroll
     for (int k = 0; k < KG; ++k) gslot[par][w][k][j] = g[k];
+    // off the gradient path, overlapping the stores' LDS latency: the deferred CE value and the
+    // step's Adam bias-correction scalars
+    if constexpr (EX && CM == 2) {
+      if (a.loss_kind == 0) lb = live ? ce_off + __builtin_amdgcn_logf(ce_se) * 0.69314718055994531f : 0.f;
+    }
     if (j == 0) lslot[par][w] = lb;
+    const int t_adam = t0 + s + 1;
+    const float step_size = a.lr * __builtin_amdgcn_rcpf(1.f - pow_t(l2b1, (float)t_adam));
+    const float rbc2 = __builtin_amdgcn_rsqf(1.f - pow_t(l2b2, (float)t_adam));
+    RSTAMP(4)
     __syncthreads();  // barrier 1: every row's gradients are in LDS
+    RSTAMP(5)
 
     // ---- batch gradient of the owned slots: rows summed in order 0..NW-1
 #pragma unroll
@@ -1077,6 +1112,7 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
       bl = xv[XV - 1];
     }
 
+    RSTAMP(6)
     // ---- Adam on the owned slots (tentative with XW > 0: undone if any wave's exchange timed out)
     float bkp[KG], bkm[KG], bkv[KG];
     if constexpr (XG) {
@@ -1088,6 +1124,7 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
     for (int k = 0; k < KG; ++k) {
       if (owned(k) && slot_live(k)) adam1(pr[k], g[k], mr[k], vr[k], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
     }
+    RSTAMP(7)
     if constexpr (!REP) {  // publish owned slots; read the others after the next barrier
 #pragma unroll
       for (int k = 0; k < KG; ++k)
@@ -1111,6 +1148,7 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
         if (!owned(k)) pr[k] = pslot[k][j];
     }
     if (w == 0 && j == 0 && a.loss_out) a.loss_out[s] = bl;
+    RSTAMP(8)
     return true;
   };
   for (int s0 = 0; s0 < a.steps; s0 += PF) {
@@ -1121,6 +1159,13 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
     }
     if (!go) break;
   }
+#ifdef DCT_WAVE_PROF
+  if (a.prof && j == 0) {  // wave W's phase sums at prof[16 W + k]
+#pragma unroll
+    for (int k = 0; k < 10; ++k) a.prof[16 * W + k] = rpt[k];
+  }
+#endif
+#undef RSTAMP
   if (w == 0 && a.step_counter && j == 0)
     __hip_atomic_store(a.step_counter, t0 + done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (XG && w == 0 && j == 0 && a.xg_ticks)
@@ -1179,6 +1224,8 @@ hipError_t launch_wave_d0(const WaveShape& sh, const MlpArgs& a, hipStream_t st)
 
 template <int D0, int CM, bool EX, int XW>
 hipError_t launch_rows(const WaveShape& sh, const MlpArgs& a, hipStream_t st) {
+  // B <= 4 runs 4 waves: 8 (the extra ones owning only Adam slots, two waves per SIMD) measured
+  // 0.727-0.730 vs 0.710 us/step on the weather step (MI355X, round 2)
   if (a.B <= 4)
     hipLaunchKernelGGL((dct::mlp_rows_kernel<4, D0, CM, EX, XW>), dim3(1), dim3(64 * 4), 0, st, sh, a);
   else
@@ -1201,7 +1248,12 @@ bool rows_eligible(int L, const MlpArgs& a) {
     const char* e = std::getenv("DCT_MLP_ROWS");
     return !(e && e[0] == '0');
   }();
-  return enabled && L == 2 && a.mode == 0 && !a.cursor && !a.pending && !a.stage && !a.prof && a.B >= 1 &&
+#ifdef DCT_WAVE_PROF
+  const bool prof_ok = true;  // profiling build: the rows kernel stamps its phases into a.prof
+#else
+  const bool prof_ok = !a.prof;
+#endif
+  return enabled && L == 2 && a.mode == 0 && !a.cursor && !a.pending && !a.stage && prof_ok && a.B >= 1 &&
          a.B <= 8 && a.m && a.v;
 }
 
