@@ -79,6 +79,51 @@ __device__ __forceinline__ void wave_sum_n(float (&v)[N]) {
   for (int i = 0; i < N; ++i) v[i] = (rl(v[i], 0) + rl(v[i], 16)) + (rl(v[i], 32) + rl(v[i], 48));
 }
 
+// wave_sum_n for the row-parallel kernel: each stage is ONE v_add_f32_dpp (mov_dpp with no live
+// "old" operand folds into the add; update_dpp(v, v) above costs a copy + mov + add), and the
+// cross-row part runs in DPP too (row_bcast:15 / row_bcast:31 accumulate rows into lane 63), so a
+// value needs one v_readlane instead of four readlanes and three adds.
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+  return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+template <int N>
+__device__ __forceinline__ void wave_sum_bcast(float (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = dpp_add<0xB1>(v[i]);   // quad_perm [1,0,3,2]
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = dpp_add<0x4E>(v[i]);   // quad_perm [2,3,0,1]
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = dpp_add<0x124>(v[i]);  // row_ror:4
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = dpp_add<0x128>(v[i]);  // row_ror:8 -> every lane: its row's sum
+  // row_bcast:15 (rows 1, 3 += rows 0, 2), then row_bcast:31 (rows 2, 3 += row 1). Written as
+  // v_add_f32_dpp with the destination tied to the source: rows outside row_mask keep their value,
+  // which no builtin expresses (update_dpp needs a zero "old" plus a separate add). The s_nops give
+  // the two wait states a DPP read needs after a VALU write of its source.
+  if constexpr (N == 2) {
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "v_add_f32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+        "s_nop 0\n\t"
+        "v_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+        "v_add_f32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf"
+        : "+v"(v[0]), "+v"(v[1]));
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      asm volatile(
+          "s_nop 1\n\t"
+          "v_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+          "s_nop 1\n\t"
+          "v_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+          : "+v"(v[i]));
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = rl(v[i], 63);
+}
+
 __device__ __forceinline__ void adam1(float& p, float g, float& m, float& v, float b1, float b2, float wd,
                                       float step_size, float rbc2, float eps) {
   g += wd * p;
@@ -991,7 +1036,7 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
       float zc[CM];
 #pragma unroll
       for (int c = 0; c < CM; ++c) zc[c] = pr[KO + c] * h;
-      wave_sum_n(zc);
+      wave_sum_bcast(zc);
 #pragma unroll
       for (int c = 0; c < CM; ++c) zc[c] += rl(pr[KC], c);
 
