@@ -996,7 +996,18 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
     const bool live = w < bs;
     const uint32_t gstep = step_base + (uint32_t)s;
     const int par = s & 1;
+    // this step's row leaves the ring register (readlanes) BEFORE that register is reloaded with
+    // step s + PF's values: with the reload first, the old and the new value are live together,
+    // the ring needs a fifth register, and the unrolled loop's back-edge rotates it with moves
+    // that wait for every load in flight
     const uint32_t cur = vslot;
+    float x[D0];
+#pragma unroll
+    for (int k = 0; k < D0; ++k) {
+      const float xv = __int_as_float(__builtin_amdgcn_readlane((int)cur, k));
+      x[k] = (live && k < d0) ? xv : 0.f;  // dead rows: zeros, never a stale NaN
+    }
+    const int y = live ? __builtin_amdgcn_readlane((int)cur, D0) : 0;
     vslot = load_val(islot);       // values of step s + PF (index loaded PF steps ago)
     islot = load_idx(s + 2 * PF);  // index of step s + 2 PF
     // step-only quantities first, branch-free: they share the basic block of the forward's
@@ -1005,14 +1016,6 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
     const uint32_t hkey = (a.seed * 0x9E3779B1u) ^ (gstep * 0x85EBCA77u);
     const uint32_t hrnd = wave_hash(hkey ^ ((uint32_t)(w * 64 + j) * 0xC2B2AE3Du));
     const bool dropped = hrnd < drop_thr;  // drop_thr == 0: never
-
-    float x[D0];
-#pragma unroll
-    for (int k = 0; k < D0; ++k) {
-      const float xv = __int_as_float(__builtin_amdgcn_readlane((int)cur, k));
-      x[k] = (live && k < d0) ? xv : 0.f;  // dead rows: zeros, never a stale NaN
-    }
-    const int y = live ? __builtin_amdgcn_readlane((int)cur, D0) : 0;
 
     RSTAMP(0)
     float g[KG];
@@ -1196,14 +1199,20 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
     RSTAMP(8)
     return true;
   };
-  for (int s0 = 0; s0 < a.steps; s0 += PF) {
-    bool go = true;
+  // Whole PF-step groups run unconditionally, the remainder after the loop: a per-step "s < steps"
+  // guard inside the loop gives the back-edge a path that skips the later steps' loads, and the
+  // wait-count pass, merging that path at the loop header, then drains every load in flight
+  // (vmcnt(0)) once per group.  A failed exchange leaves both loops directly (no back-edge path).
+  int s0 = 0;
+  for (; s0 + PF <= a.steps; s0 += PF) {
 #pragma unroll
-    for (int i = 0; i < PF; ++i) {
-      if (go && s0 + i < a.steps) go = step(s0 + i, vr_ring[i], ir_ring[i]);
-    }
-    if (!go) break;
+    for (int i = 0; i < PF; ++i)
+      if (!step(s0 + i, vr_ring[i], ir_ring[i])) goto steps_done;
   }
+#pragma unroll
+  for (int i = 0; i < PF - 1; ++i)
+    if (s0 + i < a.steps && !step(s0 + i, vr_ring[i], ir_ring[i])) goto steps_done;
+steps_done:
 #ifdef DCT_WAVE_PROF
   if (a.prof && j == 0) {  // wave W's phase sums at prof[16 W + k]
 #pragma unroll

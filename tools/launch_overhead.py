@@ -55,6 +55,20 @@ def main():
         torch.cuda.synchronize()
         out[f"kw_launch_sync_s{steps}"] = best(lambda: (kw(steps), torch.cuda.synchronize()))
         out[f"bound_launch_sync_s{steps}"] = best(lambda: (bl.run(0, steps), torch.cuda.synchronize()))
+    tiny = torch.zeros(1, device=dev)
+    out["torch_tiny_launch_sync"] = best(lambda: (tiny.add_(1.0), torch.cuda.synchronize()))
+    # GPU-side duration of the launch itself (prologue + steps), from events around it.
+    for steps in (1, 20):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ts = []
+        for _ in range(200):
+            e0.record()
+            bl.run(0, steps)
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        ts.sort()
+        out[f"bound_gpu_events_s{steps}"] = (ts[len(ts) // 2], ts[0])
     for name, (med, lo) in out.items():
         print(f"{name:24s} median {med:8.2f} us   min {lo:8.2f} us", flush=True)
 
