@@ -124,6 +124,11 @@ def _warmup(loop, n_items, warmup, loss):
         if k:
             loop.run_steps(n_items, k, loss, first_step=first)
             first += k
+            if i == 0 and getattr(loop, "xg", None) is not None:
+                # the in-kernel exchange is checked after its FIRST launch: if peers cannot see
+                # each other's writes, only that launch pays the spin timeout before the RCCL
+                # fallback, not every warmup launch
+                loop.xg_verify(fallback=True)
 
 
 def _params_in_sync(ctx, p):

@@ -135,6 +135,8 @@ class FusedMLPEngine(_EngineBase):
                 raise RuntimeError("distributed fused engine needs RCCL (backend nccl) or the in-kernel "
                                    "xGMI exchange; neither is available")
         self.last_allreduce_ms = None
+        self._bound = None
+        self._fast_run = None  # (loss_out, n_items, step limit, bound launch, loss ptr) of the last run
 
     # ------------------------------------------------------------------ params
     def _linear_params(self):
@@ -252,12 +254,21 @@ class FusedMLPEngine(_EngineBase):
 
         loss_out is indexed by the absolute batch index (loss_out[first_step + s]) and must hold
         first_step + steps entries (with DDP: the cross-rank mean loss).  No host synchronisation."""
+        fr = self._fast_run
+        if (fr is not None and loss_out is fr[0] and n_items == fr[1] and 0 < steps and 0 <= first_step
+                and first_step + steps <= fr[2] and fr[3] is self._bound and loss_out.data_ptr() == fr[4]):
+            # repeat call on the same bound launch (the driver's timed window): checks already done
+            fr[3].run(first_step, steps)
+            return
         if steps <= 0:
             return
         if (first_step + steps - 1) * self.B >= n_items or loss_out.numel() < first_step + steps:
             raise ValueError("step range exceeds the epoch's batches / loss buffer")
         if not self.ddp or self.xg is not None:
             bl = self._bound_launch(n_items, loss_out)
+            if not self.steps_per_launch:
+                self._fast_run = (loss_out, n_items, min(loss_out.numel(), -(-n_items // self.B)), bl,
+                                  loss_out.data_ptr())
             chunk = self.steps_per_launch or steps
             s = 0
             while s < steps:
