@@ -91,7 +91,7 @@ struct MlpArgs {
   // across GPUs.  Every rank pushes its step gradients as 8-byte {tag, value} granules
   // straight into each peer's receive buffer (peer-mapped over xGMI via IPC) and sums the
   // peers' granules in rank order, so all ranks apply bit-identical Adam updates with no
-  // host round trip, no RCCL launch and no kernel boundary per step.  See mlp_wave.hip.
+  // host round trip, no RCCL launch and no kernel boundary per step.  See mlp_wave_impl.h.
   unsigned long long* xg_recv;              // own receive buffer, [2][W][KX][64] granules
   unsigned long long* const* xg_peers;      // device array [W]: every rank's receive buffer
   int xg_world;                             // 0/1 = off

@@ -1,4 +1,4 @@
-"""In-kernel data-parallel all-reduce (parallel/xgmi.py, csrc/mlp_wave.hip XG path).
+"""In-kernel data-parallel all-reduce (parallel/xgmi.py, csrc/mlp_wave_impl.h XG path).
 
 Reference semantics: DDP averages every rank's gradients before an identical Adam step on each
 rank (jobs/train_lightning_ddp.py:136), and ``sync_dist`` logs the mean loss.

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-phase shader cycles of the row-parallel weather step (profiling build only:
-DCT_PROF_BUILD=1 python -m dct_amd._build; csrc/mlp_wave.hip RSTAMP).  Prints each wave's cycles per
+DCT_PROF_BUILD=1 python -m dct_amd._build; csrc/mlp_wave_impl.h RSTAMP).  Prints each wave's cycles per
 step in every phase; the stamps themselves cost cycles, so compare shares, not totals."""
 import os
 import sys
