@@ -65,7 +65,14 @@ def parse():
     return a
 
 
-def _timed(ctx, fn):
+def _timed(ctx, fn, device_barrier=None):
+    """Seconds for fn() (the K timed steps), max over ranks, bracketed by barrier + synchronize.
+
+    End bracket on GPU ranks: with the in-kernel xGMI exchange active, ``device_barrier`` enqueues
+    the exchange's own barrier (one wave per rank writes a tag into every peer's slot over xGMI
+    and polls its own) right behind the steps, then the device is synchronized: no rank's clock
+    stops before every rank finished its K steps.  Otherwise the process-group barrier (an RCCL
+    4-byte all-reduce, or gloo on the host) brackets them."""
     import torch
     import torch.distributed as dist
 
@@ -84,7 +91,9 @@ def _timed(ctx, fn):
     _release_together(ctx)
     t0 = time.perf_counter()
     fn()
-    if ctx.backend == "nccl":
+    if device_barrier is not None and device_barrier():
+        torch.cuda.synchronize()  # the xGMI barrier queued behind the steps on every rank
+    elif ctx.backend == "nccl":
         ctx.barrier()  # an RCCL op queued behind the timed steps: the synchronize below covers both
         torch.cuda.synchronize()
     else:
@@ -330,7 +339,10 @@ def main():
             _warmup(eng, n_items, a.warmup, loss)  # re-warm on the RCCL path
     if not (tab or tt or cpu) and eng.ddp and eng.xg is None and eng.use_graph:
         eng._get_graph(n_items, min(eng.graph_chunk, a.steps), loss)
-    dt = _timed(ctx, lambda: loop.run_steps(n_items, a.steps, loss, first_step=a.warmup))
+    dbar = getattr(eng, "device_barrier", None) if (ctx.is_distributed and not cpu) else None
+    if dbar is not None and dbar():  # first launch of the barrier kernel (code-object load) untimed
+        torch.cuda.synchronize()
+    dt = _timed(ctx, lambda: loop.run_steps(n_items, a.steps, loss, first_step=a.warmup), device_barrier=dbar)
 
     xg_ok = eng.xg_verify(fallback=True) if getattr(eng, "xg", None) is not None else None
     if cpu:

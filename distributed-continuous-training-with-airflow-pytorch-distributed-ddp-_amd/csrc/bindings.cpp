@@ -479,6 +479,7 @@ PYBIND11_MODULE(_dct_native, m) {
            })
       .def("set_peers", &dct::PeerExchange::set_peers)
       .def("reset", &dct::PeerExchange::reset, py::arg("stream") = 0)
+      .def("barrier", &dct::PeerExchange::barrier, py::arg("stream"), py::arg("timeout_s") = 20.0)
       .def("read_status", &dct::PeerExchange::read_status)
       .def_property_readonly("recv", &dct::PeerExchange::recv)
       .def_property_readonly("peers", &dct::PeerExchange::peers)

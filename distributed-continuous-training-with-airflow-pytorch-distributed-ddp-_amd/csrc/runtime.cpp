@@ -19,6 +19,7 @@
 #include <string>
 #include <vector>
 
+#include "kernels.h"
 #include "runtime.h"
 
 namespace dct {
@@ -218,10 +219,12 @@ size_t StreamGraph::num_nodes() const {
 // ------------------------------------------------------------------------ PeerExchange
 PeerExchange::PeerExchange(int world, int rank, int64_t bytes) : world_(world), rank_(rank), bytes_(bytes) {
   if (world < 1 || rank < 0 || rank >= world || bytes <= 0) throw std::invalid_argument("PeerExchange: bad arguments");
-  hip_check(hipExtMallocWithFlags(&recv_, (size_t)bytes, hipDeviceMallocUncached), "hipExtMallocWithFlags(uncached)");
+  // exchange slabs, then the barrier region (BARRIER_BYTES: one 16-B slot per source rank)
+  hip_check(hipExtMallocWithFlags(&recv_, (size_t)(bytes + BARRIER_BYTES), hipDeviceMallocUncached),
+            "hipExtMallocWithFlags(uncached)");
   hip_check(hipMalloc(reinterpret_cast<void**>(&d_peers_), sizeof(void*) * world), "hipMalloc(peers)");
   hip_check(hipMalloc(reinterpret_cast<void**>(&status_), 64), "hipMalloc(status)");
-  hip_check(hipMemset(recv_, 0, (size_t)bytes), "hipMemset(recv)");
+  hip_check(hipMemset(recv_, 0, (size_t)(bytes + BARRIER_BYTES)), "hipMemset(recv)");
   hip_check(hipMemset(status_, 0, 64), "hipMemset(status)");
   std::vector<void*> self(world, nullptr);
   self[rank] = recv_;
@@ -272,6 +275,16 @@ void PeerExchange::set_peers(const std::vector<uintptr_t>& addrs) {
   upload(ptrs);
 }
 
+void PeerExchange::barrier(uintptr_t stream, double timeout_s) {
+  // every rank calls barrier() the same number of times (a collective), so the call count is a
+  // tag no earlier barrier wrote; reset() zeroes the region and tags keep counting from here
+  const unsigned tag = ++bar_count_;
+  const long long ticks = (long long)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
+  hip_check((hipError_t)dct_xg_barrier(recv_, reinterpret_cast<void* const*>(d_peers_), bytes_, status_, world_, rank_,
+                                       tag, ticks, reinterpret_cast<void*>(stream)),
+            "xg_barrier");
+}
+
 unsigned int PeerExchange::read_status() const {
   unsigned int v = 0;
   hip_check(hipMemcpy(&v, status_, sizeof(v), hipMemcpyDeviceToHost), "hipMemcpy(status)");
@@ -280,7 +293,7 @@ unsigned int PeerExchange::read_status() const {
 
 void PeerExchange::reset(uintptr_t stream) {
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hip_check(hipMemsetAsync(recv_, 0, (size_t)bytes_, st), "hipMemsetAsync(recv)");
+  hip_check(hipMemsetAsync(recv_, 0, (size_t)(bytes_ + BARRIER_BYTES), st), "hipMemsetAsync(recv)");
   hip_check(hipMemsetAsync(status_, 0, 64, st), "hipMemsetAsync(status)");
 }
 

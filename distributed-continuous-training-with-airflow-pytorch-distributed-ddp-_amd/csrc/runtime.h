@@ -70,6 +70,7 @@ class PeerExchange {
   void open_peers(const std::vector<std::string>& handles);  // all ranks' handles, rank order
   void set_peers(const std::vector<uintptr_t>& ptrs);        // same process (tests): raw addresses
   void reset(uintptr_t stream);                              // zero receive buffer + status
+  void barrier(uintptr_t stream, double timeout_s);          // device-side barrier over the peer mappings
   unsigned int read_status() const;                          // synchronous D2H of status[0]
   uintptr_t recv() const { return reinterpret_cast<uintptr_t>(recv_); }
   uintptr_t peers() const { return reinterpret_cast<uintptr_t>(d_peers_); }
@@ -86,6 +87,8 @@ class PeerExchange {
   void** d_peers_ = nullptr;
   unsigned int* status_ = nullptr;
   std::vector<void*> opened_;
+  unsigned bar_count_ = 0;
+  static constexpr int64_t BARRIER_BYTES = 16 * 64;
 };
 
 class StreamGraph {

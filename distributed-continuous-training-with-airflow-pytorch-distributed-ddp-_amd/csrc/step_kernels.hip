@@ -101,6 +101,34 @@ __global__ void step_end_kernel(int* cursor, const float* slot, float* loss_out,
   }
 }
 
+// Device-side barrier over the xGMI peer mappings of the in-kernel exchange (runtime.cpp
+// PeerExchange::barrier).  Lane q < W (q != rank) writes this barrier's tag into slot `rank` of
+// peer q's barrier region (system-scope store across xGMI), then every lane polls slot q of its
+// own uncached region until peer q's tag arrived.  One wave, no host round trip and no RCCL
+// launch: it replaces the RCCL barrier where the bench brackets the timed steps (a 4-byte
+// all-reduce + host wait) with one peer-write latency.  Bounded spin: a timeout writes
+// 0x80000000 | tag into the exchange status word (xg_verify then reports the exchange failed).
+__global__ __launch_bounds__(64) void xg_barrier_kernel(char* recv, char* const* __restrict__ peers, int64_t off,
+                                                        unsigned* status, int W, int rank, unsigned tag,
+                                                        long long timeout_ticks) {
+  const int q = threadIdx.x;
+  if (q < W && q != rank) {
+    unsigned* dst = reinterpret_cast<unsigned*>(peers[q] + off) + rank * 4;
+    __hip_atomic_store(dst, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  const unsigned* src = reinterpret_cast<const unsigned*>(recv + off) + (q < W ? q : 0) * 4;
+  bool ok = q >= W || q == rank;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (!__all(ok)) {
+    if (!ok) ok = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == tag;
+    if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout_ticks) {
+      if (q == 0) __hip_atomic_store(status, 0x80000000u | tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 }  // namespace dct
 
 extern "C" {
@@ -171,6 +199,15 @@ int dct_loss_to_slot(const float* stats, float* slot, float inv_rows, void* stre
 int dct_step_end(int* cursor, const float* slot, float* loss_out, int loss_cap, void* stream) {
   hipLaunchKernelGGL(dct::step_end_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), cursor, slot,
                      loss_out, loss_cap);
+  return (int)hipGetLastError();
+}
+
+int dct_xg_barrier(void* recv, void* const* peers, int64_t off, unsigned* status, int world, int rank, unsigned tag,
+                   long long timeout_ticks, void* stream) {
+  if (world < 2 || world > 64 || rank < 0 || rank >= world || !recv || !peers || !status) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(dct::xg_barrier_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<char*>(recv), reinterpret_cast<char* const*>(peers), off, status, world, rank, tag,
+                     timeout_ticks);
   return (int)hipGetLastError();
 }
 

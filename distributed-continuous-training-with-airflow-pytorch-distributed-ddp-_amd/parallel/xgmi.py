@@ -78,6 +78,16 @@ def setup_peer_exchange(kernel, ctx: DistContext, batch: int):
     return xg
 
 
+def device_barrier(xg, stream: int, timeout: Optional[float] = None):
+    """Enqueue a barrier over the peer mappings on ``stream`` (collective: every rank calls it).
+
+    One wave writes a tag into every peer's barrier slot over xGMI and polls its own slots - no
+    RCCL launch, no host round trip.  Followed by a device synchronize it is a full barrier: no
+    rank's synchronize returns before every rank's stream reached the barrier.  A timeout is
+    recorded in the status word (:func:`check` then reports the exchange as failed)."""
+    xg.barrier(stream, timeout_s() if timeout is None else float(timeout))
+
+
 def status(xg) -> int:
     """This rank's exchange status word (0 = ok, else the step + 1 that timed out); syncs."""
     return int(xg.read_status())

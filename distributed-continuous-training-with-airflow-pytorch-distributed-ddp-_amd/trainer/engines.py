@@ -398,6 +398,16 @@ class FusedMLPEngine(_EngineBase):
         self.xg_disable()
         return False
 
+    def device_barrier(self) -> bool:
+        """Enqueue the in-kernel exchange's device-side barrier on the current stream (collective).
+        False when the exchange is not active (the caller then uses the process-group barrier)."""
+        if self.xg is None:
+            return False
+        from ..parallel.xgmi import device_barrier
+
+        device_barrier(self.xg, torch.cuda.current_stream(self.device).cuda_stream, self.xg_timeout_s)
+        return True
+
     def xg_disable(self):
         """Leave the in-kernel exchange: replicas re-synced from rank 0, RCCL step path from now on."""
         self.xg = None

@@ -142,6 +142,9 @@ def test_multi_process_ipc_exchange(W, tmp_path, cuda):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     res = json.loads(out.read_text())
     assert res["status"] == 0 and res["step_counter"] == steps
+    for i in range(3):  # device barrier: every rank left after the last rank arrived
+        last_arrival = max(res["barrier"][r][i][0] for r in range(W))
+        assert all(res["barrier"][r][i][1] >= last_arrival for r in range(W)), res["barrier"]
     ps = [torch.tensor(p) for p in res["params"]]
     p0 = ps[0]
     assert all(torch.equal(p, p0) for p in ps)
@@ -151,3 +154,35 @@ def test_multi_process_ipc_exchange(W, tmp_path, cuda):
     err = (p0 - want).abs()
     assert err.median() < 1e-5 and err.max() < 2e-3, (err.median(), err.max())
     assert torch.allclose(torch.tensor(res["losses"][0]), want_l, atol=2e-4, rtol=1e-3)
+
+
+
+def _barrier_run(out_path):
+    nat = native()
+    cuda = torch.device("cuda", 0)
+    xs = [nat.PeerExchange(2, r, 4096) for r in range(2)]
+    for x in xs:
+        x.set_peers([y.recv for y in xs])
+    streams = [torch.cuda.Stream(cuda) for _ in range(2)]
+    for _ in range(4):
+        for r in range(2):
+            xs[r].barrier(streams[r].cuda_stream, 5.0)
+    torch.cuda.synchronize()
+    met = [x.read_status() for x in xs]
+    xs[0].barrier(streams[0].cuda_stream, 0.1)  # the peer never comes
+    torch.cuda.synchronize()
+    json.dump({"met": met, "timeout": xs[0].read_status()}, open(out_path, "w"))
+
+
+def test_device_barrier_in_process_and_timeout(tmp_path, cuda):
+    """Two 'ranks' on two streams of a fresh process meet in the device barrier four times (status
+    stays 0); a rank whose peer never arrives gives up after the timeout and records
+    0x80000000 | tag (tag = its 5th barrier)."""
+    out = tmp_path / "bar.json"
+    code = (f"import sys; sys.path.insert(0, {ROOT!r}); sys.path.insert(0, {os.path.join(ROOT, 'tests')!r}); "
+            f"import test_xgmi_gpu as t; t._barrier_run({str(out)!r})")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    res = json.loads(out.read_text())
+    assert res["met"] == [0, 0]
+    assert res["timeout"] == (0x80000000 | 5)

@@ -38,12 +38,26 @@ def main():
                n_items=n_items, batch=B, steps=steps, t0=0, lr=0.01, loss_out=loss, step_counter=sc, xg=xg,
                xg_timeout_s=10.0)
     torch.cuda.synchronize()
+    # device-side barrier: rank r arrives r x 30 ms late; nobody may leave before the last arrival
+    import time
+
+    from dct_amd.parallel.xgmi import device_barrier
+
+    bar = []
+    for _ in range(3):
+        ctx.barrier()
+        time.sleep(0.03 * ctx.rank)
+        t_arrive = time.time()
+        device_barrier(xg, torch.cuda.current_stream().cuda_stream, 10.0)
+        torch.cuda.synchronize()
+        bar.append((t_arrive, time.time()))
     st = check(xg, ctx)
+    allbar = ctx.all_gather_object(bar)
     allp = ctx.all_gather_object(p.cpu().tolist())
     alll = ctx.all_gather_object(loss.cpu().tolist())
     if ctx.rank == 0:
         with open(out_path, "w") as f:
-            json.dump({"status": st, "params": allp, "losses": alll, "step_counter": int(sc.item())}, f)
+            json.dump({"status": st, "barrier": allbar, "params": allp, "losses": alll, "step_counter": int(sc.item())}, f)
     ctx.barrier()
     del xg
     shutdown(ctx)
