@@ -6,8 +6,9 @@ on global rank 0 only, hyper-parameters become params, metrics are logged with t
 step, and with ``log_model=True`` every checkpoint the ``ModelCheckpoint`` produced is uploaded
 under ``model/checkpoints/<stem>/`` when the run is finalized.  ``experiment.log_artifact``
 is exposed so the reference's explicit ``best_checkpoints`` upload (:157-161) works unchanged.
-Metric calls are buffered and flushed as ``runs/log-batch`` requests (one HTTP round trip per
-flush instead of one per metric).
+Metric calls are buffered and flushed as ``runs/log-batch`` requests of up to 1,000 metrics (MLflow's
+cap; one HTTP round trip per flush instead of one per metric); the trainer also flushes at the end
+of every epoch, so a run's metrics are visible epoch by epoch.
 """
 from __future__ import annotations
 
@@ -54,7 +55,7 @@ class InMemoryLogger(Logger):
 class MLFlowLogger(Logger):
     def __init__(self, experiment_name: str = "lightning_logs", tracking_uri: Optional[str] = None,
                  log_model: bool = False, run_name: Optional[str] = None, tags: Optional[Dict[str, str]] = None,
-                 flush_every: int = 64):
+                 flush_every: int = 1000):
         self.experiment_name = experiment_name
         self.tracking_uri = tracking_uri or os.environ.get("MLFLOW_TRACKING_URI")
         self.log_model = log_model
@@ -105,6 +106,22 @@ class MLFlowLogger(Logger):
         for k, v in metrics.items():
             self._buffer.append({"key": k, "value": float(v), "step": int(step), "timestamp": ts})
         if len(self._buffer) >= self.flush_every:
+            self.flush()
+
+    def log_metric_series(self, key: str, points, extra: Optional[Dict[str, float]] = None):
+        """log_metrics({key: v, **extra}, step) for every (step, v) of points, in one call."""
+        if not self.rank_zero:
+            return
+        import time
+
+        ts = int(time.time() * 1000)
+        ex = [(k, float(v)) for k, v in (extra or {}).items()]
+        buf = self._buffer
+        for step, v in points:
+            buf.append({"key": key, "value": float(v), "step": int(step), "timestamp": ts})
+            for k, xv in ex:
+                buf.append({"key": k, "value": xv, "step": int(step), "timestamp": ts})
+        if len(buf) >= self.flush_every:
             self.flush()
 
     def flush(self):

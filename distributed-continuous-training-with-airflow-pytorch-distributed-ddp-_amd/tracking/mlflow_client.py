@@ -244,9 +244,24 @@ class FileStore:
             f.write(str(value))
 
     def log_batch(self, run_id: str, metrics=(), params=(), tags=()):
-        self._run_dir(run_id)  # validates the id and that the run exists, even for an empty batch
+        d = self._run_dir(run_id)  # validates the id and that the run exists, even for an empty batch
+        # one append per metric KEY (lines in the batch's order), not an open + run lookup per value:
+        # a 20k-step epoch logs 8k values (train_loss every 5 steps + epoch)
+        lines: Dict[str, List[str]] = {}
+        now = None
         for m in metrics:
-            self.log_metric(run_id, m["key"], m["value"], m.get("timestamp"), m.get("step", 0))
+            ts = m.get("timestamp")
+            if not ts:
+                now = now or _now_ms()
+                ts = now
+            lines.setdefault(self._safe_key(m["key"]), []).append(
+                f"{ts} {float(m['value'])} {int(m.get('step', 0))}\n")
+        for key, ls in lines.items():
+            p = os.path.join(d, "metrics", key)
+            if "/" in key:
+                os.makedirs(os.path.dirname(p), exist_ok=True)
+            with open(p, "a") as f:
+                f.write("".join(ls))
         for p in params:
             self.log_param(run_id, p["key"], p["value"])
         for t in tags:

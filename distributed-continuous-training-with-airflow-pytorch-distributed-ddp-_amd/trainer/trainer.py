@@ -154,6 +154,18 @@ class Trainer:
         self._epoch_logs = {}
         return out
 
+    def _log_series(self, key: str, points):
+        """_log_metrics({key: v}, step) for every (step, v) in points, in one logger call."""
+        if not points:
+            return
+        self.logged_metrics.update({key: points[-1][1], "epoch": self.current_epoch})
+        if self.logger is not None and self.is_global_zero:
+            if hasattr(self.logger, "log_metric_series"):
+                self.logger.log_metric_series(key, points, extra={"epoch": self.current_epoch})
+            else:
+                for step, v in points:
+                    self.logger.log_metrics({key: v, "epoch": self.current_epoch}, step)
+
     def _log_metrics(self, metrics: Dict[str, float], step: int):
         metrics = dict(metrics)
         metrics.setdefault("epoch", self.current_epoch)
@@ -314,6 +326,8 @@ class Trainer:
                 if ar_ms is not None:
                     extra["allreduce_ms"] = ar_ms
                 self._log_metrics(extra, self.global_step)
+                if self.logger is not None and self.is_global_zero:
+                    self.logger.flush()  # the epoch's metrics reach the tracking store now
                 with trace_range(f"epoch{epoch}/checkpoint"):
                     self._run_checkpoint_callbacks(n_steps)
                 if self.verbose and self.is_global_zero:
@@ -375,14 +389,12 @@ class Trainer:
             self.global_step += n
             self._maybe_fault(self.global_step)
             lv = losses.cpu().tolist()
-            last = None
-            for k in range(1, n + 1):
-                gk = first + k
-                if gk % self.log_every_n_steps == 0:
-                    self._log_metrics({"train_loss": lv[k - 1]}, gk - 1)
-                last = lv[k - 1]
-            if last is not None:
-                self.callback_metrics["train_loss"] = last
+            # every log_every_n_steps-th step's loss, as ONE series call (a 20k-step epoch has 4k)
+            ev = self.log_every_n_steps
+            k0 = (-first) % ev or ev  # first k in 1..n with (first + k) % ev == 0
+            self._log_series("train_loss", [(first + k - 1, lv[k - 1]) for k in range(k0, n + 1, ev)])
+            if n:
+                self.callback_metrics["train_loss"] = lv[-1]
             return n
         local = eng.epoch_local_indices(len(eng.train_rows), epoch, shuffle)
         rows_all = eng.train_rows[local]
