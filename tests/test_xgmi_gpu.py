@@ -129,9 +129,10 @@ def test_exchange_timeout_is_bounded_and_reported(cuda):
     assert torch.equal(p.cpu(), _flat(_net()))
 
 
-@pytest.mark.parametrize("W", [2, 4])
+@pytest.mark.parametrize("W", [2, 4, 8])
 def test_multi_process_ipc_exchange(W, tmp_path, cuda):
-    """Real IPC path: W processes, receive buffers exported/imported with hipIpc handles."""
+    """Real IPC path: W processes, receive buffers exported/imported with hipIpc handles (W = 8:
+    the exchange width of a full MI355X node, XW = 8 kernel variant)."""
     out = tmp_path / "xg.json"
     steps, B = 80, 4
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")

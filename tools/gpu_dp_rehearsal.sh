@@ -1,11 +1,11 @@
 #!/bin/bash
-# DDP rehearsal: 2 and 4 ranks sharing ONE GPU (gloo control plane, in-kernel exchange over IPC
+# DDP rehearsal: 2, 4 and 8 ranks sharing ONE GPU (gloo control plane, in-kernel exchange over IPC
 # mappings of the same device - no xGMI links involved), long run and driver-shaped window.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for w in 2 4; do
+for w in ${WS:-2 4 8}; do
   for s in "20000 2000" "20 5"; do
     set -- $s
     timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=$w --master-addr 127.0.0.1 \
