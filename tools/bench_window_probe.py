@@ -54,7 +54,8 @@ def main():
         ctx.barrier()
         torch.cuda.synchronize()
         t3 = time.perf_counter()
-        first += steps
+        if os.environ.get("PROBE_SAME_ROWS", "0") != "1":  # 1: every rep re-runs the same (L2-warm) batches
+            first += steps
         print(f"rep {r:2d}: window {1e6 * (t3 - t0):7.1f} us  enqueue {1e6 * (t1 - t0):6.1f}  "
               f"wait {1e6 * (t2 - t1):6.1f}  tail {1e6 * (t3 - t2):5.1f}"
               + ("  (after 50 ms idle)" if r == reps - 1 else ""), flush=True)
