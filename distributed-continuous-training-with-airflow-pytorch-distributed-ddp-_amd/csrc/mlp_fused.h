@@ -98,7 +98,8 @@ struct MlpArgs {
   int xg_rank;
   unsigned int* xg_status;                  // [0]: 0 ok, else (global step + 1) of a timeout
   long long xg_timeout;                     // spin limit in s_memrealtime ticks (100 MHz)
-  int xg_poll;                              // 0 full sweeps, 1 probe-then-sweep, 2 sequential
+  int xg_poll;                              // 0 full sweeps, 1 probe-then-sweep, 2 sequential; rows kernel:
+                                            // 3 | stagger << 8 = two pipelined sweeps in flight
   // optional (row-parallel kernel): wave 0 adds the s_memrealtime ticks (100 MHz) its exchange
   // took over the launch - the allreduce_ms metric of the fused DDP step
   unsigned long long* xg_ticks;

@@ -275,6 +275,56 @@ __device__ __forceinline__ bool xg_exchange_wave(float (&g)[XV], const MlpArgs& 
   float v[XW][XV];
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   int spin = 0;
+  auto timed_out = [&]() -> bool {
+    if ((++spin & 15) == 0 && (long long)(__builtin_amdgcn_s_memrealtime() - t_start) > a.xg_timeout) {
+      if (j == 0) __hip_atomic_store(a.xg_status, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return true;
+    }
+    return false;
+  };
+  if ((a.xg_poll & 0xff) == 3) {
+    // Pipelined polls (DCT_XG_POLL=3, stagger = xg_poll >> 8 sleeps of 64 cycles): two sweeps in
+    // flight, issued half a round trip apart, so a granule that lands just after one sweep read
+    // its slot is seen by the other half a round trip later instead of a whole one.
+    xg_v4u dA[XW][P2], dB[XW][P2];
+    auto issue = [&](xg_v4u (&d)[XW][P2]) {
+#pragma unroll
+      for (int q = 0; q < XW; ++q) {
+        const int qq = (q < W && q != rank) ? q : (rank == 0 ? 1 : 0);
+#pragma unroll
+        for (int p = 0; p < P2; ++p) d[q][p] = __builtin_amdgcn_raw_buffer_load_b128(rrs, off(qq, p), 0, XG_SYS);
+      }
+    };
+    auto ready = [&](const xg_v4u (&d)[XW][P2]) -> bool {
+      bool ok = true;
+#pragma unroll
+      for (int q = 0; q < XW; ++q)
+#pragma unroll
+        for (int p = 0; p < P2; ++p) ok &= ((d[q][p].y == tag) & (d[q][p].w == tag)) | (q >= W) | (q == rank);
+      return __all(ok);
+    };
+    auto take = [&](const xg_v4u (&d)[XW][P2]) {
+#pragma unroll
+      for (int q = 0; q < XW; ++q)
+#pragma unroll
+        for (int p = 0; p < P2; ++p) {
+          v[q][2 * p] = __uint_as_float(d[q][p].x);
+          v[q][2 * p + 1] = __uint_as_float(d[q][p].z);
+        }
+    };
+    issue(dA);
+    for (int k = a.xg_poll >> 8; k > 0; --k) __builtin_amdgcn_s_sleep(1);
+    for (;;) {
+      issue(dB);
+      if (ready(dA)) { take(dA); break; }
+      if (timed_out()) return false;
+      __builtin_amdgcn_s_sleep(1);  // also keeps the re-issued loads from being merged with the last ones
+      issue(dA);
+      if (ready(dB)) { take(dB); break; }
+      if (timed_out()) return false;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  } else {
   for (;;) {  // sweep every source per pass (one round trip per pass)
     bool ok = true;
 #pragma unroll
@@ -289,11 +339,9 @@ __device__ __forceinline__ bool xg_exchange_wave(float (&g)[XV], const MlpArgs& 
       }
     }
     if (__all(ok)) break;
-    if ((++spin & 15) == 0 && (long long)(__builtin_amdgcn_s_memrealtime() - t_start) > a.xg_timeout) {
-      if (j == 0) __hip_atomic_store(a.xg_status, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return false;
-    }
+    if (timed_out()) return false;
     __builtin_amdgcn_s_sleep(1);
+  }
   }
   float acc[XV];
 #pragma unroll

@@ -137,7 +137,7 @@ class FusedMLPKernel:
                 raise ValueError(f"exchange buffer too small ({xg.bytes} < {need} bytes)")
             xg_args = dict(xg_recv=xg.recv, xg_peers=xg.peers, xg_world=xg.world, xg_rank=xg.rank,
                            xg_status=xg.status, xg_timeout=int(xg_timeout_s * 1e8),
-                           xg_poll=int(os.environ.get("DCT_XG_POLL", "0")))
+                           xg_poll=int(os.environ.get("DCT_XG_POLL", "3")))
         self.plan.train(
             ptr(p), ptr(m) if need_mv else 0, ptr(v) if need_mv else 0, ptr(grad_out),
             ptr(X), X.stride(0), ptr(Y), ptr(idx), int(n_items), int(batch), int(steps), int(t0),
@@ -178,7 +178,7 @@ class FusedMLPKernel:
                 raise ValueError(f"exchange buffer too small ({xg.bytes} < {need} bytes)")
             xg_args = dict(xg_recv=xg.recv, xg_peers=xg.peers, xg_world=xg.world, xg_rank=xg.rank,
                            xg_status=xg.status, xg_timeout=int(xg_timeout_s * 1e8),
-                           xg_poll=int(os.environ.get("DCT_XG_POLL", "0")))
+                           xg_poll=int(os.environ.get("DCT_XG_POLL", "3")))
             if xg_ticks is not None:
                 if not (xg_ticks.is_cuda and xg_ticks.dtype == torch.int64 and xg_ticks.numel() >= 1):
                     raise ValueError("xg_ticks must be a cuda int64 counter")
