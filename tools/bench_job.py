@@ -17,6 +17,7 @@ import argparse
 import json
 import os
 import re
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -32,12 +33,21 @@ def main():
     p.add_argument("--epochs", type=int, default=10)
     p.add_argument("--accelerator", default="gpu")
     p.add_argument("--no-mlflow", action="store_true")
+    p.add_argument("--keep", action="store_true", help="keep the work directory (data, checkpoints, mlruns)")
     a = p.parse_args()
 
     from dct_amd.data.etl import run_arrow_etl
     from dct_amd.data.synthetic import make_weather_csv
 
     work = tempfile.mkdtemp(prefix="dct_job_")
+    try:
+        return _run(a, work, run_arrow_etl, make_weather_csv)
+    finally:
+        if not a.keep:
+            shutil.rmtree(work, ignore_errors=True)
+
+
+def _run(a, work, run_arrow_etl, make_weather_csv):
     raw = os.path.join(work, "raw", "weather.csv")
     make_weather_csv(raw, n=a.rows, seed=0)
     t0 = time.perf_counter()
