@@ -46,11 +46,18 @@ def main():
     ctr = torch.zeros(1, dtype=torch.int32, device=dev)
     bl = k.prepare_train(p, m, v, X, Y, idx, n_items=N, batch=4, lr=1e-3, loss_out=loss, step_counter=ctr)
     tiny = torch.zeros(1, device=dev)
+    from dct_amd.ops._native import native
+
+    nat = native()
+    stream = torch.cuda.current_stream().cuda_stream
     torch.cuda.synchronize()
     out = {
         "sync_only": best(torch.cuda.synchronize),
         "tiny_launch_sync": best(lambda: (tiny.add_(1.0), torch.cuda.synchronize())),
         "tiny_launch_stream_sync": best(lambda: (tiny.add_(1.0), torch.cuda.current_stream().synchronize())),
+        # a one-thread native kernel through the same pybind + hipLaunchKernelGGL path: the floor
+        # the weather launch's own prologue / epilogue sit on top of
+        "native_null_launch_sync": best(lambda: (nat.zero_f32(tiny.data_ptr(), 1, stream), torch.cuda.synchronize())),
         "bound_s1_launch_sync": best(lambda: (bl.run(0, 1), torch.cuda.synchronize())),
         "bound_s20_launch_sync": best(lambda: (bl.run(0, 20), torch.cuda.synchronize())),
     }
