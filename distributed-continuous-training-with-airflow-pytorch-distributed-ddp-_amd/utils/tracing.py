@@ -1,6 +1,6 @@
 """Tracing / timing (the reference has none).
 
-* ``trace_range(name)`` - a roctx range (``libroctx64``) around a phase, so rocprofv3
+* ``trace_range(name)`` - a roctx range (rocprofiler-sdk's roctx) around a phase, so rocprofv3
   ``--marker-trace`` timelines show epoch / train / validate / checkpoint / all-reduce phases
   next to the kernels; a no-op when the library is missing or ``DCT_ROCTX=0``.
 * ``PhaseTimer`` - wall-clock accumulation per phase (device-synchronised on demand), reported
@@ -26,8 +26,12 @@ def _lib():
     _roctx_tried = True
     if os.environ.get("DCT_ROCTX", "1") == "0":
         return None
-    for name in ("libroctx64.so", "libroctx64.so.4", os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"),
-                                                                   "lib", "libroctx64.so")):
+    rocm_lib = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib")
+    # rocprofiler-sdk's roctx first: rocprofv3 (--marker-trace) intercepts that one; the legacy
+    # roctracer libroctx64 is only seen by the old rocprof
+    for name in ("librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so",
+                 os.path.join(rocm_lib, "librocprofiler-sdk-roctx.so"), "libroctx64.so", "libroctx64.so.4",
+                 os.path.join(rocm_lib, "libroctx64.so")):
         try:
             lib = ctypes.CDLL(name)
             lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
