@@ -315,6 +315,15 @@ PYBIND11_MODULE(_dct_native, m) {
                         reinterpret_cast<void*>(stream)),
           "skinny_dw");
   });
+  m.def("skinny_head_supported", [](int K, int C) { return dct_skinny_head_supported(K, C) != 0; });
+  m.def("skinny_head", [](uintptr_t H, uintptr_t W, uintptr_t bias, uintptr_t labels, uintptr_t dH, uintptr_t dW,
+                          uintptr_t db, uintptr_t loss_sum, int B, int K, int C, float grad_scale, int loss_kind,
+                          float loss_scale, int relu_mask, uintptr_t stream) {
+    check(dct_skinny_head(P<const uint16_t>(H), P<const uint16_t>(W), P<const float>(bias), P<const int>(labels),
+                          P<uint16_t>(dH), P<float>(dW), P<float>(db), P<float>(loss_sum), B, K, C, grad_scale,
+                          loss_kind, loss_scale, relu_mask, reinterpret_cast<void*>(stream)),
+          "skinny_head");
+  });
   m.attr("EPI_RELU_MASK") = 4;
   m.attr("EPI_GELU_GRAD") = 5;
   m.def(

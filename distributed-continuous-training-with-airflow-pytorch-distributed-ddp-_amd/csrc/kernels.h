@@ -49,6 +49,10 @@ int dct_skinny_fwd(const uint16_t* X, const uint16_t* W, const float* bias, uint
 int dct_skinny_dx(const uint16_t* dZ, const uint16_t* W, const uint16_t* aux, uint16_t* dX, int B, int K, int C,
                   void* stream);
 int dct_skinny_dw(const uint16_t* dZ, const uint16_t* X, float* dW, float* db, int B, int K, int C, void* stream);
+int dct_skinny_head_supported(int K, int C);
+int dct_skinny_head(const uint16_t* H, const uint16_t* W, const float* bias, const int* labels, uint16_t* dH,
+                    float* dW, float* db, float* loss_sum, int B, int K, int C, float grad_scale, int loss_kind,
+                    float loss_scale, int relu_mask, void* stream);
 // dZ = dY * act'(aux) (bf16 out); dbias[n] (+)= sum_m dZ[m][n]. dY is bf16. For RELU aux is
 // the activation OUTPUT (bf16), for GELU the pre-activation (bf16), for NONE unused.
 int dct_bias_act_bwd(const void* dY, const void* act_aux, uint16_t* dZ, float* dbias, int M, int N, int ldy, int act,

@@ -11,6 +11,8 @@
 //   L x gemm_bf16         A_{l+1} = act(A_l W_l^T + b_l): MFMA GEMM, bias+ReLU/GELU epilogue, bf16 out
 //   loss_fwd_bwd          CE / MSE + dlogits (scaled 1/rows); the batch-mean loss is accumulated
 //                         straight into g[P] (all-reduced with the grads: sync_dist for free)
+//                         [ReLU MLPs with a <= 8-class head: head forward, loss, head dW/db and the
+//                          layer below's dZ are ONE kernel, skinny_head (csrc/skinny.hip)]
 //   for l = L-1 .. 0:     bias_act_bwd (dZ = dA * act', db = colsum) ; dW_l = dZ^T A_l (fp32 straight
 //                         into the flat gradient buffer = the DDP bucket views) ; mark params ready
 //                         (the reducer launches each full bucket's ncclAvg on its comm stream while
@@ -92,8 +94,18 @@ void MlpStepExecutor::set_adam(float lr, float b1, float b2, float eps, float wd
   lr_ = lr; b1_ = b1; b2_ = b2; eps_ = eps; wd_ = wd; decoupled_ = decoupled;
 }
 
-void MlpStepExecutor::forward(int rows, hipStream_t st) {
-  for (int l = 0; l < L_; ++l) {
+bool MlpStepExecutor::fused_head() const {
+  // ReLU hidden layers only (GELU' needs the pre-activation: the unfused GEMM path); a skinny head
+  // whose width fits the kernel's register budget; DCT_FUSED_HEAD=0 keeps the four-kernel chain
+  const char* e = getenv("DCT_FUSED_HEAD");  // host side, once per issued (or captured) step
+  const bool off = e && e[0] == '0';
+  const int l = L_ - 1;
+  return !off && act_ == ACT_RELU && skinny(l) && dct_skinny_head_supported(dims_[l], dims_[L_]);
+}
+
+void MlpStepExecutor::forward(int rows, hipStream_t st, int layers) {
+  if (layers < 0) layers = L_;
+  for (int l = 0; l < layers; ++l) {
     const int din = dims_[l], dout = dims_[l + 1];
     const bool last = l == L_ - 1;
     int epi = EPI_BIAS;
@@ -123,16 +135,35 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
   ck(dct_gather_batch_step(reinterpret_cast<const void*>(X), row_bytes, reinterpret_cast<const int*>(Y),
                            reinterpret_cast<const int*>(idx), cur, B_, rows, n_items, acts_[0], y_, sc, g_, P_ + 1, st),
      "gather_batch");
-  forward(rows, st);
   const int C = dims_[L_];
   int ci = 0;  // dz_[ci] holds dL/d(output of the current layer)
-  ck(dct_loss_fwd_bwd_ex(acts_[L_], 1, y_, dz_[ci], g_ + P_, nullptr, rows, C, 1.0f / (float)rows, loss_kind_,
-                         1.0f / (float)rows, st),
-     "loss");
-  if (reducer_) reducer_->mark_ready(2 * L_, stream);  // the loss slot rides in the last-layer bucket
+  int top = L_ - 1;  // highest layer the backward loop below still has to run
+  if (fused_head()) {
+    // classifier head fused (csrc/skinny.hip skinny_head_kernel): logits, loss (into the loss
+    // slot g[P]), dlogits, dW/db of the head and the layer below's dZ in one pass over its input
+    forward(rows, st, L_ - 1);
+    const int l = L_ - 1;
+    ck(dct_skinny_head(acts_[l], pb_ + woff_[l], p_ + boff_[l], y_, l > 0 ? dz_[1] : nullptr, g_ + woff_[l],
+                       g_ + boff_[l], g_ + P_, rows, dims_[l], C, 1.0f / (float)rows, loss_kind_, 1.0f / (float)rows,
+                       /*relu_mask*/ 1, st),
+       "fused head");
+    if (reducer_) {
+      reducer_->mark_ready(2 * L_, stream);
+      reducer_->mark_ready(2 * l + 1, stream);
+      reducer_->mark_ready(2 * l, stream);
+    }
+    ci = 1;
+    top = L_ - 2;
+  } else {
+    forward(rows, st);
+    ck(dct_loss_fwd_bwd_ex(acts_[L_], 1, y_, dz_[ci], g_ + P_, nullptr, rows, C, 1.0f / (float)rows, loss_kind_,
+                           1.0f / (float)rows, st),
+       "loss");
+    if (reducer_) reducer_->mark_ready(2 * L_, stream);  // the loss slot rides in the last-layer bucket
+  }
   // dz_[ci] = dL/dZ_l (pre-activation gradient of layer l): the loss kernel's dlogits for the
   // head, then each dX GEMM's activation-derivative epilogue (ReLU mask / GELU') for the layer below.
-  for (int l = L_ - 1; l >= 0; --l) {
+  for (int l = top; l >= 0; --l) {
     const int din = dims_[l], dout = dims_[l + 1];
     const int mask_epi = act_ == ACT_GELU ? EPI_GELU_GRAD : EPI_RELU_MASK;
     const void* mask_aux = act_ == ACT_GELU ? (const void*)(l > 0 ? pre_[l] : nullptr) : (const void*)acts_[l];

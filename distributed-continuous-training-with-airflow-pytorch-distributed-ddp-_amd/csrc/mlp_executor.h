@@ -30,7 +30,8 @@ class MlpStepExecutor {
   int64_t num_params() const { return P_; }
 
  private:
-  void forward(int rows, hipStream_t st);
+  void forward(int rows, hipStream_t st, int layers = -1);  // layers 0 .. layers-1 (default all)
+  bool fused_head() const;
   // layers with <= 8 outputs run as bandwidth kernels (csrc/skinny.hip)
   bool skinny(int l) const { return dims_[l + 1] <= 8 && dims_[l] % 8 == 0 && woff_[l] % 8 == 0; }
   std::vector<int> dims_;

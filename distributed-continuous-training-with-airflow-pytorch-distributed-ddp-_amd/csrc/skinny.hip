@@ -203,6 +203,192 @@ __global__ __launch_bounds__(256) void skinny_dw_kernel(const uint16_t* __restri
   }
 }
 
+// The whole classifier head of a training step in one kernel (the executor's skinny fwd -> loss
+// -> skinny dW -> skinny dX chain, four launches and three extra passes over H, fused):
+//   z[b]   = bf16(H[b] . W^T + bias)                      (rounded like the unfused bf16 logits)
+//   loss  += CE(z[b], y[b]) or MSE(z[b], onehot(y[b]))     (summed, * loss_scale, one atomic/block)
+//   dz[b]  = bf16(dL/dz * grad_scale)                      (rounded like the unfused bf16 dlogits)
+//   dH[b]  = (dz[b] . W) * (H[b] > 0 if relu_mask)         (the layer below's pre-activation grad)
+//   dW    += dz^T H,  db += colsum(dz)                     (block partials folded in LDS, fp32 atomics)
+// One wave per RPW rows: the wave loads its W panel (CT x K bf16) and all RPW rows of H up front
+// (loads unconditional; rows past B re-read row B-1 and are masked), then each row's logits are a
+// butterfly sum per class, the loss math runs redundantly in every lane (no LDS round trip) and the
+// row's dH chunk is stored while its H chunk is still in registers.  NJ = K / 512 chunks per lane.
+// The head's H is read once instead of three times and dz never goes through memory.
+template <int CT, int NJ, int RPW, int NWV>
+__global__ __launch_bounds__(64 * NWV) void skinny_head_kernel(const uint16_t* __restrict__ H,
+                                                          const uint16_t* __restrict__ W,
+                                                          const float* __restrict__ bias,
+                                                          const int* __restrict__ labels, uint16_t* __restrict__ dH,
+                                                          float* __restrict__ dW, float* __restrict__ db,
+                                                          float* __restrict__ loss_sum, int B, int K, int C,
+                                                          float grad_scale, int loss_kind, float loss_scale,
+                                                          int relu_mask) {
+  __shared__ float4 red4[NWV][CT][NJ * 128];  // per-wave dW partials, [wave][c][k / 4]
+  __shared__ float red_s[NWV][CT + 1];        // per-wave db partials and loss
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r0 = (blockIdx.x * NWV + wv) * RPW;
+  uint4 wraw[CT][NJ];
+#pragma unroll
+  for (int c = 0; c < CT; ++c)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      wraw[c][j] = *reinterpret_cast<const uint4*>(W + (size_t)(c < C ? c : C - 1) * K + j * 512 + lane * 8);
+  uint4 hraw[RPW][NJ];
+  int ys[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int r = min(r0 + i, B - 1);
+    ys[i] = labels[r];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) hraw[i][j] = *reinterpret_cast<const uint4*>(H + (size_t)r * K + j * 512 + lane * 8);
+  }
+  float bs[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) bs[c] = bias ? bias[c < C ? c : C - 1] : 0.f;
+  float acc[CT][NJ][8];
+  float dbs[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    dbs[c] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[c][j][e] = 0.f;
+  }
+  float lsum = 0.f;
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const bool ok = r0 + i < B;
+    float h[NJ][8];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) unpack8(hraw[i][j], h[j]);
+    float z[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        float w[8];
+        unpack8(wraw[c][j], w);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += h[j][e] * w[e];
+      }
+      z[c] = bf16_to_f32(f32_to_bf16(wave_sum(s) + bs[c]));
+    }
+    // loss + dlogits of the row, as dct::loss_kernel computes them (same formulas, fp32)
+    const int y = ys[i];
+    float dz[CT];
+    float rl;
+    if (loss_kind == 0) {
+      float mx = z[0], zy = z[0];
+#pragma unroll
+      for (int c = 1; c < CT; ++c) {
+        if (c < C && z[c] > mx) mx = z[c];
+        if (c == y) zy = z[c];
+      }
+      float ex[CT], s = 0.f;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        ex[c] = c < C ? __expf(z[c] - mx) : 0.f;
+        s += ex[c];
+      }
+      rl = mx + __logf(s) - zy;
+      const float rs = 1.f / s;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) dz[c] = (ex[c] * rs - (c == y ? 1.f : 0.f)) * grad_scale;
+    } else {
+      rl = 0.f;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        const float d = c < C ? z[c] - (c == y ? 1.f : 0.f) : 0.f;
+        rl += d * d;
+        dz[c] = 2.f * d * grad_scale / (float)C;
+      }
+      rl /= (float)C;
+    }
+#pragma unroll
+    for (int c = 0; c < CT; ++c) dz[c] = (ok && c < C) ? bf16_to_f32(f32_to_bf16(dz[c])) : 0.f;
+    lsum += ok ? rl : 0.f;
+    // dH chunk of the row, then the dW / db contributions
+    if (dH && ok) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = 0.f;
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          float w[8];
+          unpack8(wraw[c][j], w);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] += dz[c] * w[e];
+        }
+        if (relu_mask) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = h[j][e] > 0.f ? o[e] : 0.f;
+        }
+        uint4 v;
+        v.x = f32_to_bf16(o[0]) | ((uint32_t)f32_to_bf16(o[1]) << 16);
+        v.y = f32_to_bf16(o[2]) | ((uint32_t)f32_to_bf16(o[3]) << 16);
+        v.z = f32_to_bf16(o[4]) | ((uint32_t)f32_to_bf16(o[5]) << 16);
+        v.w = f32_to_bf16(o[6]) | ((uint32_t)f32_to_bf16(o[7]) << 16);
+        *reinterpret_cast<uint4*>(dH + (size_t)(r0 + i) * K + j * 512 + lane * 8) = v;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      dbs[c] += dz[c];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[c][j][e] += dz[c] * h[j][e];
+    }
+  }
+  // fold the NWV waves' partials in column order, one atomic per (class, column) per block
+#pragma unroll
+  for (int c = 0; c < CT; ++c)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      red4[wv][c][j * 128 + 2 * lane] = make_float4(acc[c][j][0], acc[c][j][1], acc[c][j][2], acc[c][j][3]);
+      red4[wv][c][j * 128 + 2 * lane + 1] = make_float4(acc[c][j][4], acc[c][j][5], acc[c][j][6], acc[c][j][7]);
+    }
+  if (lane == 0) {
+#pragma unroll
+    for (int c = 0; c < CT; ++c) red_s[wv][c] = dbs[c];
+    red_s[wv][CT] = lsum;
+  }
+  __syncthreads();
+  const float* red = reinterpret_cast<const float*>(red4);
+  constexpr int PER_WAVE = CT * NJ * 512;
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    if (c >= C) break;
+#pragma unroll
+    for (int q = 0; q < 8 * NJ / NWV; ++q) {
+      const int col = threadIdx.x + 64 * NWV * q;
+      const int o = c * NJ * 512 + col;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) v += red[w * PER_WAVE + o];
+      atomicAdd(dW + (size_t)c * K + col, v);
+    }
+  }
+  if (threadIdx.x < C && db) {
+    const int c = threadIdx.x;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) v += red_s[w][c];
+    atomicAdd(db + c, v);
+  }
+  if (threadIdx.x == 64 && loss_sum) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) v += red_s[w][CT];
+    atomicAdd(loss_sum, v * loss_scale);
+  }
+}
+
 }  // namespace dct
 
 extern "C" {
@@ -233,6 +419,56 @@ int dct_skinny_dx(const uint16_t* dZ, const uint16_t* W, const uint16_t* aux, ui
   else if (C == 2) hipLaunchKernelGGL(dct::skinny_dx_kernel<2>, dim3(grid), dim3(256), 0, st, dZ, W, aux, dX, B, K, C);
   else if (C <= 4) hipLaunchKernelGGL(dct::skinny_dx_kernel<4>, dim3(grid), dim3(256), 0, st, dZ, W, aux, dX, B, K, C);
   else hipLaunchKernelGGL(dct::skinny_dx_kernel<8>, dim3(grid), dim3(256), 0, st, dZ, W, aux, dX, B, K, C);
+  return (int)hipGetLastError();
+}
+
+// Shapes the fused head covers (register budget: W panel + RPW rows of H + the dW partials stay
+// resident): K a multiple of 512 with C <= 2 and K <= 2048, C <= 4 and K <= 1024, or C <= 8 and K = 512.
+int dct_skinny_head_supported(int K, int C) {
+  if (C < 1 || K < 512 || K % 512) return 0;
+  return (C <= 2 && K <= 2048) || (C <= 4 && K <= 1024) || (C <= 8 && K == 512);
+}
+
+int dct_skinny_head(const uint16_t* H, const uint16_t* W, const float* bias, const int* labels, uint16_t* dH,
+                    float* dW, float* db, float* loss_sum, int B, int K, int C, float grad_scale, int loss_kind,
+                    float loss_scale, int relu_mask, void* stream) {
+  if (!dct_skinny_head_supported(K, C) || !H || !W || !labels || !dW ||
+      (((uintptr_t)H | (uintptr_t)W | (uintptr_t)dH) & 15))
+    return (int)hipErrorInvalidValue;
+  if (B <= 0) return 0;
+  // two-class heads up to K = 1024: 8 waves x 4 rows (32 rows per block, 2 waves per SIMD) once
+  // that still gives >= 128 blocks; otherwise 4 waves x 4 rows
+  const bool w8 = C <= 2 && K <= 1024;  // 8-wave blocks: LDS partials 8 x C x K fp32 <= 64 KB
+  int nwv = (w8 && B >= 128 * 32) ? 8 : 4, rpw = 4;
+  if (const char* f = getenv("DCT_SKINNY_HEAD_RPW")) rpw = (atoi(f) == 8 && C <= 2) ? 8 : (atoi(f) == 2 ? 2 : 4);
+  if (const char* f = getenv("DCT_SKINNY_HEAD_WAVES")) nwv = (atoi(f) == 8 && w8) ? 8 : 4;  // debug / A-B
+  if (nwv == 8 && rpw == 8) rpw = 4;  // 8-wave blocks come with 2 or 4 rows per wave (the grid must match)
+  const dim3 grid((B + nwv * rpw - 1) / (nwv * rpw));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int NJ = K / 512;
+#define DCT_HEAD(CT_, NJ_, R_, W_)                                                                           \
+  hipLaunchKernelGGL((dct::skinny_head_kernel<CT_, NJ_, R_, W_>), grid, dim3(64 * W_), 0, st, H, W, bias, labels, \
+                     dH, dW, db, loss_sum, B, K, C, grad_scale, loss_kind, loss_scale, relu_mask)
+#define DCT_HEAD_R4(CT_, NJ_) \
+  if (rpw == 8) DCT_HEAD(CT_, NJ_, 8, 4); else if (rpw == 2) DCT_HEAD(CT_, NJ_, 2, 4); else DCT_HEAD(CT_, NJ_, 4, 4)
+#define DCT_HEAD_R(CT_, NJ_)                                                     \
+  if (nwv == 8) {                                                                \
+    if (rpw == 2) DCT_HEAD(CT_, NJ_, 2, 8); else DCT_HEAD(CT_, NJ_, 4, 8);        \
+  } else DCT_HEAD_R4(CT_, NJ_)
+  if (C == 1) {
+    switch (NJ) { case 1: DCT_HEAD_R(1, 1); break; case 2: DCT_HEAD_R(1, 2); break;
+                  case 3: DCT_HEAD_R4(1, 3); break; default: DCT_HEAD_R4(1, 4); break; }
+  } else if (C == 2) {
+    switch (NJ) { case 1: DCT_HEAD_R(2, 1); break; case 2: DCT_HEAD_R(2, 2); break;
+                  case 3: DCT_HEAD_R4(2, 3); break; default: DCT_HEAD_R4(2, 4); break; }
+  } else if (C <= 4) {
+    if (NJ == 1) DCT_HEAD(4, 1, 4, 4); else DCT_HEAD(4, 2, 4, 4);
+  } else {
+    DCT_HEAD(8, 1, 4, 4);
+  }
+#undef DCT_HEAD_R
+#undef DCT_HEAD_R4
+#undef DCT_HEAD
   return (int)hipGetLastError();
 }
 

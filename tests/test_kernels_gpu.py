@@ -505,6 +505,87 @@ def test_skinny_head_kernels(C, cuda):
     assert torch.allclose(db, dZ.float().sum(0), atol=1e-2, rtol=1e-3)
 
 
+@pytest.mark.parametrize("B,K,C,kind,rpw", [(4096, 1024, 2, 0, "8"), (4096, 1024, 2, 1, "4"), (777, 1024, 2, 0, "8"),
+                                             (333, 512, 1, 1, "4"), (100, 2048, 2, 0, "4"), (130, 1024, 3, 0, "4"),
+                                             (65, 512, 8, 0, "4"), (4096, 1536, 2, 1, "8")])
+def test_fused_skinny_head_matches_fp32_reference_and_chain(B, K, C, kind, rpw, cuda, monkeypatch):
+    """csrc/skinny.hip skinny_head_kernel (head fwd + CE/MSE + dlogits + dW/db + masked dH in one
+    launch) against (a) a plain torch fp32 reference of the same op and (b) the unfused chain
+    skinny_fwd -> loss -> skinny_dw -> skinny_dx it replaces in the tabular step executor."""
+    monkeypatch.setenv("DCT_SKINNY_HEAD_RPW", rpw)
+    torch.manual_seed(B + K + C)
+    nat = native()
+    st = torch.cuda.current_stream().cuda_stream
+    assert nat.skinny_head_supported(K, C)
+    H = _bf(torch.relu(torch.randn(B, K, device=cuda)))
+    W = _bf(torch.randn(C, K, device=cuda) * 0.03)
+    b = torch.randn(C, device=cuda) * 0.1
+    y = torch.randint(0, C, (B,), device=cuda).to(torch.int32)
+    dH = torch.empty(B, K, device=cuda, dtype=torch.bfloat16)
+    dW = torch.zeros(C, K, device=cuda)
+    db = torch.zeros(C, device=cuda)
+    ls = torch.zeros(1, device=cuda)
+    nat.skinny_head(H.data_ptr(), W.data_ptr(), b.data_ptr(), y.data_ptr(), dH.data_ptr(), dW.data_ptr(),
+                    db.data_ptr(), ls.data_ptr(), B, K, C, 1.0 / B, kind, 1.0 / B, 1, st)
+    # (b) the unfused chain on the same operands
+    Z = torch.empty(B, C, device=cuda, dtype=torch.bfloat16)
+    nat.skinny_fwd(H.data_ptr(), W.data_ptr(), b.data_ptr(), Z.data_ptr(), B, K, C, st)
+    dZ = torch.empty(B, C, device=cuda, dtype=torch.bfloat16)
+    ls2 = torch.zeros(1, device=cuda)
+    nat.cross_entropy_fwd_bwd(Z.data_ptr(), 1, y.data_ptr(), dZ.data_ptr(), ls2.data_ptr(), 0, B, C, 1.0 / B, kind, st)
+    dW2 = torch.zeros(C, K, device=cuda)
+    db2 = torch.zeros(C, device=cuda)
+    nat.skinny_dw(dZ.data_ptr(), H.data_ptr(), dW2.data_ptr(), db2.data_ptr(), B, K, C, st)
+    dH2 = torch.empty(B, K, device=cuda, dtype=torch.bfloat16)
+    nat.skinny_dx(dZ.data_ptr(), W.data_ptr(), H.data_ptr(), dH2.data_ptr(), B, K, C, st)
+    # (a) fp32 reference
+    z = (H.float() @ W.float().t() + b).requires_grad_(True)
+    loss = _ref_loss(z, y.long(), "ce" if kind == 0 else "mse")
+    loss.backward()
+    dz = z.grad
+    torch.cuda.synchronize()
+    assert abs(ls.item() - loss.item()) < 2e-3 * max(1.0, abs(loss.item()))
+    assert abs(ls.item() - ls2.item() / B) < 1e-5 * max(1.0, abs(loss.item()))  # same bf16 logits, same math
+    assert torch.allclose(dW, dz.t() @ H.float(), atol=2e-3, rtol=2e-2)
+    assert torch.allclose(db, dz.sum(0), atol=2e-3, rtol=2e-2)
+    ref_dH = (dz @ W.float()) * (H.float() > 0)
+    assert torch.allclose(dH.float(), ref_dH, atol=1e-4, rtol=2e-2)
+    # chain parity: bf16 logits / dlogits rounded identically, only atomic summation order differs
+    assert torch.equal(dH, dH2)
+    assert torch.allclose(dW, dW2, atol=1e-6, rtol=1e-5)
+    assert torch.allclose(db, db2, atol=1e-6, rtol=1e-5)
+
+
+def test_fused_head_executor_step_matches_unfused(cuda, monkeypatch):
+    """The wide-MLP step executor with the fused head (default) and with DCT_FUSED_HEAD=0 (the
+    four-kernel chain) train the same trajectory (eager steps and captured graphs alike)."""
+    from dct_amd.models.mlp import MLPClassifier
+    from dct_amd.parallel.dist import init_distributed
+    from dct_amd.trainer.engines import adam_hparams_from
+    from dct_amd.trainer.graph_engine import GraphMLPEngine
+
+    ctx = init_distributed("gpu")
+    dims, B = [256, 1024, 1024, 2], 512
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(12 * B, dims[0], generator=g)
+    Y = ((X @ torch.randn(dims[0], generator=g)) > 0).long()
+    rows = torch.arange(X.shape[0])
+    res = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DCT_FUSED_HEAD", fused)
+        torch.manual_seed(0)
+        model = MLPClassifier(dims[0], hidden=tuple(dims[1:-1]), num_classes=2, dropout=0.0, loss="ce", lr=1e-3)
+        eng = GraphMLPEngine(model, ctx, B, seed=42, adam=adam_hparams_from(model.configure_optimizers()))
+        eng.attach_data(X, Y, rows, rows[:B])
+        losses = torch.cat([eng.train_epoch(ep).cpu() for ep in range(2)])
+        torch.cuda.synchronize()
+        res[fused] = (losses, eng.p.cpu())
+    (l1, p1), (l0, p0) = res["1"], res["0"]
+    assert torch.isfinite(l1).all() and l1[-4:].mean() < l1[:4].mean()
+    assert torch.allclose(l1, l0, atol=1e-3), (l1 - l0).abs().max()
+    assert (p1 - p0).norm() / p0.norm() < 1e-2
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,d,n", [(4096, 64, 256), (1000, 64, 128)])
 def test_ffn_residual_matches_fp32_reference(cuda, M, d, n):
