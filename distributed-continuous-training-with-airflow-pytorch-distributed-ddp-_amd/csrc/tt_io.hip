@@ -10,6 +10,7 @@
 // backward is a batch reduction split over (feature, batch-chunk) workgroups with fp32 atomics.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -126,9 +127,16 @@ __device__ __forceinline__ HeadFwd head_chain(const HeadArgs& a, int b, int d) {
   return r;
 }
 
-__global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6), d = threadIdx.x & 63;
-  if (b >= a.B) return;
+// NW samples per workgroup (one wave each).  The per-sample losses meet in LDS and each block adds
+// ONE value to the loss: the loss is a single address, and 512 same-address float atomics (one per
+// sample) serialised this kernel.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void head_fwd_kernel(HeadArgs a) {
+  __shared__ float lsum[NW];
+  const int w = threadIdx.x >> 6, d = threadIdx.x & 63;
+  const int b = blockIdx.x * NW + w;
+  if (d == 0) lsum[w] = 0.f;
+  if (b < a.B) {
   const int yb = (int)a.y[b];
   const HeadFwd r = head_chain(a, b, d);
   if (d == 0) {
@@ -141,15 +149,24 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(HeadArgs a) {
     float ly = 0.f;
 #pragma unroll
     for (int k = 0; k < CMAX; ++k) ly = (k == yb) ? r.logit[k] : ly;
-    atomicAdd(a.loss, (m + __logf(se) - ly) / a.B);
+    lsum[w] = (m + __logf(se) - ly) / a.B;
+  }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) v += lsum[i];
+    atomicAdd(a.loss, v);
   }
 }
 
-__global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
-  __shared__ float red[4][2 + CMAX][D];  // per wave: dln_w, dln_b, dW[C]
-  __shared__ float rbias[4][CMAX];
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void head_bwd_kernel(HeadArgs a) {
+  __shared__ float red[NW][2 + CMAX][D];  // per wave: dln_w, dln_b, dW[C]
+  __shared__ float rbias[NW][CMAX];
   const int w = threadIdx.x >> 6, d = threadIdx.x & 63;
-  const int b = blockIdx.x * 4 + w;
+  const int b = blockIdx.x * NW + w;
   const bool live = b < a.B;
   float gw = 0.f, gb = 0.f, gW[CMAX], gbias[CMAX];
 #pragma unroll
@@ -204,16 +221,30 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(HeadArgs a) {
     if (d < CMAX) rbias[w][d] = v;
   }
   __syncthreads();
-  // workgroup reduction over its 4 samples, then one atomic per parameter element
-  for (int i = threadIdx.x; i < (2 + a.C) * D; i += 256) {
+  // workgroup reduction over its NW samples, then one atomic per parameter element
+  for (int i = threadIdx.x; i < (2 + a.C) * D; i += 64 * NW) {
     const int row = i / D, dd = i - row * D;
-    const float v = red[0][row][dd] + red[1][row][dd] + red[2][row][dd] + red[3][row][dd];
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) v += red[q][row][dd];
     float* dst = row == 0 ? a.dln_w + dd : row == 1 ? a.dln_b + dd : a.dW + (row - 2) * D + dd;
     atomicAdd(dst, v);
   }
-  if (threadIdx.x < a.C)
-    atomicAdd(a.dbias + threadIdx.x,
-              rbias[0][threadIdx.x] + rbias[1][threadIdx.x] + rbias[2][threadIdx.x] + rbias[3][threadIdx.x]);
+  if (threadIdx.x < a.C) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) v += rbias[q][threadIdx.x];
+    atomicAdd(a.dbias + threadIdx.x, v);
+  }
+}
+
+// samples per workgroup (one wave each): 4.  16-sample (1024-thread) blocks quarter the
+// parameter-gradient atomics but measured no faster on the TabTransformer step (0.4195-0.4240 vs
+// 0.4184-0.4221 ms, profiles/tt_head_spb_side_dw_ab_r2.log); DCT_TT_HEAD_SPB=16 selects them.
+static inline int head_spb(int B) {
+  (void)B;
+  if (const char* f = getenv("DCT_TT_HEAD_SPB")) return atoi(f) == 16 ? 16 : 4;
+  return 4;
 }
 
 }  // namespace ttio
@@ -252,8 +283,10 @@ int dct_tt_head_fwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C,
   a.h = (const float*)p[0]; a.y = (const int64_t*)p[1]; a.ln_w = (const float*)p[2]; a.ln_b = (const float*)p[3];
   a.W = (const float*)p[4]; a.bias = (const float*)p[5]; a.loss = (float*)p[6];
   a.B = B; a.T = T; a.C = C; a.eps = eps;
-  hipLaunchKernelGGL(dct::ttio::head_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     a);
+  const int nw = dct::ttio::head_spb(B);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (nw == 16) hipLaunchKernelGGL(dct::ttio::head_fwd_kernel<16>, dim3((B + 15) / 16), dim3(1024), 0, st, a);
+  else hipLaunchKernelGGL(dct::ttio::head_fwd_kernel<4>, dim3((B + 3) / 4), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 
@@ -268,8 +301,10 @@ int dct_tt_head_bwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C,
   a.dh = (float*)p[7]; a.dh16 = (uint16_t*)p[8]; a.dln_w = (float*)p[9]; a.dln_b = (float*)p[10];
   a.dW = (float*)p[11]; a.dbias = (float*)p[12];
   a.B = B; a.T = T; a.C = C; a.eps = eps;
-  hipLaunchKernelGGL(dct::ttio::head_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     a);
+  const int nw = dct::ttio::head_spb(B);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (nw == 16) hipLaunchKernelGGL(dct::ttio::head_bwd_kernel<16>, dim3((B + 15) / 16), dim3(1024), 0, st, a);
+  else hipLaunchKernelGGL(dct::ttio::head_bwd_kernel<4>, dim3((B + 3) / 4), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 

@@ -36,16 +36,19 @@ def _stream():
 
 # ----------------------------------------------------------------------------- engine binding
 class _Binding:
-    def __init__(self, params: Iterable[torch.Tensor], shadows: Optional[Dict[int, torch.Tensor]]):
+    def __init__(self, params: Iterable[torch.Tensor], shadows: Optional[Dict[int, torch.Tensor]],
+                 side_dw: bool = False):
         self.direct = {id(p) for p in params}
         self.shadows = shadows or {}
+        self.side_dw = side_dw
 
 
 _BOUND: Optional[_Binding] = None
 
 
 @contextlib.contextmanager
-def bound_params(params: Iterable[torch.Tensor], bf16_shadows: Optional[Dict[int, torch.Tensor]] = None):
+def bound_params(params: Iterable[torch.Tensor], bf16_shadows: Optional[Dict[int, torch.Tensor]] = None,
+                 side_dw: bool = False):
     """Engine-scoped fast paths for the ops below (trainer/engines.py AutogradEngine):
 
     * gradient accumulation fusion - the weight-gradient GEMMs / LayerNorm column sums of a
@@ -54,14 +57,40 @@ def bound_params(params: Iterable[torch.Tensor], bf16_shadows: Optional[Dict[int
       parameter gradient tensor, fill or AccumulateGrad add.  Post-accumulate-grad hooks still
       fire (autograd runs them for undefined gradients too), so bucket all-reduces launch as before;
     * bf16 shadow weights - ``bf16_shadows[id(p)]`` (kept current by the fused Adam) replaces
-      the per-step fp32->bf16 weight conversion.
+      the per-step fp32->bf16 weight conversion;
+    * ``side_dw`` - the fused transformer block's weight-gradient GEMMs go to a side stream and
+      overlap the next (earlier) block's backward kernel; the caller joins them with
+      :func:`join_side_work` after backward.  Only for callers with no gradient hooks reading the
+      buffers during backward (no DDP bucket reducer): the grads land after the hooks fired.
     """
     global _BOUND
-    prev, _BOUND = _BOUND, _Binding(params, bf16_shadows)
+    prev, _BOUND = _BOUND, _Binding(params, bf16_shadows, side_dw)
     try:
         yield
     finally:
         _BOUND = prev
+
+
+# side-stream weight-gradient work (bound_params(side_dw=True)): the stream, and per launch the
+# completion event plus the operand tensors it reads (kept referenced until the join, so the
+# caching allocator cannot hand their memory to later main-stream work while the side stream
+# still reads it)
+_SIDE = {"stream": None, "pending": []}
+
+
+def _side_stream(dev) -> "torch.cuda.Stream":
+    s = _SIDE["stream"]
+    if s is None or s.device != dev:
+        s = _SIDE["stream"] = torch.cuda.Stream(dev)
+    return s
+
+
+def join_side_work():
+    """Current stream waits for every weight-gradient launch issued on the side stream."""
+    pend = _SIDE["pending"]
+    if pend:
+        torch.cuda.current_stream().wait_event(pend[-1][0])
+        pend.clear()
 
 
 def _w16(w: torch.Tensor) -> torch.Tensor:
@@ -73,13 +102,19 @@ def _w16(w: torch.Tensor) -> torch.Tensor:
     return w.detach().to(torch.bfloat16).contiguous()
 
 
+def _is_direct(p: torch.Tensor) -> bool:
+    """True when p's gradient accumulates straight into the bound p.grad (see bound_params)."""
+    b = _BOUND
+    if b is None or id(p) not in b.direct:
+        return False
+    g = p.grad
+    return g is not None and g.dtype == torch.float32 and g.is_contiguous() and g.shape == p.shape
+
+
 def _grad_dst(p: torch.Tensor, zero: bool = False):
     """(buffer, direct): p.grad itself when accumulation into it is bound, else a new tensor."""
-    b = _BOUND
-    if b is not None and id(p) in b.direct:
-        g = p.grad
-        if g is not None and g.dtype == torch.float32 and g.is_contiguous() and g.shape == p.shape:
-            return g, True
+    if _is_direct(p):
+        return p.grad, True
     alloc = torch.zeros if zero else torch.empty
     return alloc(p.shape, dtype=torch.float32, device=p.device), False
 
@@ -567,8 +602,20 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
         ptrs.append(_tt_prof_buf("bwd", B, dev))
     nat.tt_block_bwd([t.data_ptr() for t in ptrs], B, T, dm, H, FF, scale, st)
     dout16 = _bf16_of(dout)
-    (dw2, db2), (dw1, db1), (dwo, dbo), (dwqkv, dbqkv) = _dw_gemm_grouped(
-        nat, [(dout16, f, w2, b2), (dpre, a2, w1, b1), (dh1_16, o, wo, bo), (dqkv, a1, wqkv, bqkv)], st)
+    items = [(dout16, f, w2, b2), (dpre, a2, w1, b1), (dh1_16, o, wo, bo), (dqkv, a1, wqkv, bqkv)]
+    b = _BOUND
+    if b is not None and b.side_dw and all(_is_direct(t) for t in (w2, b2, w1, b1, wo, bo, wqkv, bqkv)):
+        # the four dW GEMMs accumulate straight into the bound grads: run them on the side stream,
+        # behind this block's dX chain, while the main stream goes on to the earlier block
+        side = _side_stream(dev)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            (dw2, db2), (dw1, db1), (dwo, dbo), (dwqkv, dbqkv) = _dw_gemm_grouped(nat, items, side.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        _SIDE["pending"].append((ev, items))
+    else:
+        (dw2, db2), (dw1, db1), (dwo, dbo), (dwqkv, dbqkv) = _dw_gemm_grouped(nat, items, st)
     _remember_bf16(dh, dh16)
     (dl1w, d1), (dl1b, d2), (dl2w, d3), (dl2b, d4) = lg
     return (dh, None if d1 else dl1w, None if d2 else dl1b, dwqkv, dbqkv, dwo, dbo, None if d3 else dl2w,

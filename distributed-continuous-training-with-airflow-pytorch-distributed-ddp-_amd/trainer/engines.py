@@ -30,7 +30,7 @@ import torch
 
 from ..data.sampler import distributed_indices
 from ..ops.fused_mlp import FusedMLPKernel, mlp_num_params
-from ..ops.nn import bound_params
+from ..ops.nn import bound_params, join_side_work
 from ..ops.optim import FlatAdam, adam_flat_
 from ..parallel.dist import DistContext, init_native_comm
 from ..parallel.reducer import NativeBucketReducer, TorchBucketReducer, plan_buckets
@@ -539,6 +539,7 @@ class AutogradEngine(_EngineBase):
         if one is None or one.device != loss.device or one.dtype != loss.dtype or one.shape != loss.shape:
             one = self._one_seed = torch.ones_like(loss)
         loss.backward(one)
+        join_side_work()  # weight-gradient GEMMs issued on the side stream (ops/nn.py side_dw)
 
     def _step_body(self, x, y, batch_idx: int):
         self._zero_grads()
@@ -743,7 +744,12 @@ class AutogradEngine(_EngineBase):
     def _bound(self):
         if self._shadows is None:
             return contextlib.nullcontext()
-        return bound_params(self.params, self._shadows)
+        # DCT_TT_DW_SIDE=1: transformer-block dW GEMMs on a side stream (ops/nn.py), only without a
+        # bucket reducer (its grad hooks launch all-reduces that must see the finished gradients).
+        # Off by default: the overlap slowed both kernels, TabTransformer step 0.420 -> 0.445 ms
+        # (profiles/tt_head_spb_side_dw_ab_r2.log)
+        side = self.reducer is None and os.environ.get("DCT_TT_DW_SIDE", "0") == "1"
+        return bound_params(self.params, self._shadows, side_dw=side)
 
     def sync_to_model(self):
         pass  # parameters ARE views of the flat buffer

@@ -781,10 +781,15 @@ def test_tt_block_fused_matches_fp32_reference_and_unfused(cuda, B, monkeypatch)
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,C", [(1, 2), (37, 2), (512, 2), (64, 5)])
-def test_tt_embed_and_head_loss_match_fp32_reference(cuda, B, C):
+@pytest.mark.parametrize("spb", ["auto", "4", "16"])
+def test_tt_embed_and_head_loss_match_fp32_reference(cuda, B, C, spb, monkeypatch):
     """csrc/tt_io.hip: feature-token embedding fwd/bwd and the pooled LN -> Linear -> mean-CE head
-    (loss forward, recomputing backward) vs fp32 torch, every gradient including dh."""
+    (loss forward, recomputing backward) vs fp32 torch, every gradient including dh; both block
+    shapes of the head kernels (4 / 16 samples per workgroup)."""
     from dct_amd.ops.nn import tt_embed, tt_head_loss
+
+    if spb != "auto":
+        monkeypatch.setenv("DCT_TT_HEAD_SPB", spb)
 
     F_, d = 64, 64
     g = torch.Generator(device="cpu").manual_seed(5)

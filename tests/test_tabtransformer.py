@@ -118,3 +118,38 @@ def test_device_loop_matches_host_loop(cuda, F_):
     noise = float((p0 - ph).norm() / p0.norm())
     diff = float((p0 - p1).norm() / p0.norm())
     assert diff < max(3 * noise, 1e-4), (diff, noise)
+
+
+@pytest.mark.gpu
+def test_side_stream_dw_matches_in_stream(cuda, monkeypatch):
+    """Fused-block dW GEMMs on the side stream (DCT_TT_DW_SIDE=1, joined after backward) train the
+    same trajectory as on the compute stream, eager steps and captured step graphs alike."""
+    from dct_amd.parallel.dist import init_distributed
+    from dct_amd.trainer.engines import AutogradEngine
+    from dct_amd.trainer.trainer import seed_everything
+
+    ctx = init_distributed("gpu")
+    F_ = 64
+    X, Y = _data(4096, F_, seed=4)
+    rows = torch.randperm(4096, generator=torch.Generator().manual_seed(2))
+    B, steps = 128, 12
+    res = {}
+    for side in ("1", "0", "0"):
+        monkeypatch.setenv("DCT_TT_DW_SIDE", side)
+        seed_everything(7)
+        m = TabTransformer(num_features=F_, d_model=64, heads=4, layers=3, lr=3e-3)
+        eng = AutogradEngine(m, ctx, B, seed=7)
+        eng.attach_data(X.to(cuda), Y.to(cuda), rows[:3584], rows[3584:])
+        rows_dev = eng.train_rows.to(cuda)
+        loss = torch.zeros(steps, device=cuda)
+        eng.run_device_steps(rows_dev, 0, steps, loss)  # eager warm-up steps, capture, replays
+        torch.cuda.synchronize()
+        assert eng.graph_used
+        res.setdefault(side, []).append((loss.cpu(), eng.flat_p.detach().cpu().clone()))
+    (l1, p1), = res["1"]
+    (l0, p0), (lh, ph) = res["0"]
+    assert torch.isfinite(l1).all() and (l1 != 0).all()
+    assert torch.allclose(l0, l1, rtol=2e-3, atol=2e-4), (l0, l1)
+    noise = float((p0 - ph).norm() / p0.norm())
+    diff = float((p0 - p1).norm() / p0.norm())
+    assert diff < max(3 * noise, 1e-4), (diff, noise)

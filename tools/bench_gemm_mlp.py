@@ -64,6 +64,12 @@ if os.environ.get("AB_SET") == "probe":  # split-K: atomics vs plain stores (tim
     VARIANTS = {f"{e}_sp{sp}": ({"DCT_GEMM_SPLIT_PROBE": "1"} if e == "plain" else {}) | {"DCT_GEMM_SPLITS": str(sp)}
                 for e in ("atom", "plain") for sp in (4, 16, 64, 128, 256, 512)}
 
+if os.environ.get("AB_SET") == "layout":  # transformer dW shapes in every operand layout (what would a
+    # feature-major copy of the activations buy?): (1,0) = today's dZ^T X on token-major storage
+    SHAPES = [(f"{n}_ta{ta}tb{tb}", M, N, K, ta, tb, 1) for n, M, N, K, *_ in SHAPES if n.startswith("tt_dw")
+              for ta, tb in ((1, 0), (0, 1), (0, 0), (1, 1))]
+    VARIANTS = {"default": {}}
+
 
 def main():
     ap = argparse.ArgumentParser()
