@@ -70,6 +70,10 @@ if os.environ.get("AB_SET") == "layout":  # transformer dW shapes in every opera
               for ta, tb in ((1, 0), (0, 1), (0, 0), (1, 1))]
     VARIANTS = {"default": {}}
 
+if os.environ.get("AB_SET") == "dwcmp":  # the tabular dW shapes: default launch vs hipBLASLt
+    SHAPES = [s for s in SHAPES if s[0] in ("dw_l1", "dw_l0", "fwd_l1", "dx_l1")]
+    VARIANTS = {"default": {}}
+
 
 def main():
     ap = argparse.ArgumentParser()
