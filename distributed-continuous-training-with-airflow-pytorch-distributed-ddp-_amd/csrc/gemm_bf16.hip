@@ -483,6 +483,23 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
       }
     return;
   }
+  if (SPLIT && g.split_part) {  // two-pass split-K: this slice's partial tile, plain stores
+    float* part = g.split_part + (size_t)split * g.M * g.N;
+    const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < IM; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wc * 64 + j * 16 + col_l;
+        if (col >= g.N) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wr * (BM / 2) + i * 16 + row_l + r;
+          if (row < g.M) part[(size_t)row * g.N + col] = acc[i][j][r];
+        }
+      }
+    return;
+  }
   if (SPLIT) {  // natural layout: col = lane&15, rows 4*(lane>>4) + r
     const int col_l = lane & 15, row_l = (lane >> 4) * 4;
 #pragma unroll
@@ -643,6 +660,73 @@ __global__ __launch_bounds__(256) void zero_panel_kernel(float* __restrict__ C, 
   }
 }
 
+// Second pass of the two-pass split-K: C[r][c] (+)= alpha * sum_s part[s][r][c], slices summed in
+// order (bit-reproducible), 4 columns per thread when N % 4 == 0.  Replaces `splits` fp32 atomics per
+// output element: on the 1024 x 1024 x 4096 dW each slice's 1 M atomics cost ~3.4 us
+// (profiles/gemm_splitk_sweep_*), the partials one streaming read.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int splits, float* C,
+                                                           int ldc, int M, int N, int accumulate, float alpha) {
+  const size_t MN = (size_t)M * N;
+  if ((N & 3) == 0) {
+    const int64_t total = (int64_t)(MN >> 2);
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+      float4 s = reinterpret_cast<const float4*>(part)[e];
+      for (int q = 1; q < splits; ++q) {
+        const float4 v = reinterpret_cast<const float4*>(part + (size_t)q * MN)[e];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+      const int64_t f = e * 4;
+      const int64_t r = f / N;
+      float* dst = C + r * ldc + (f - r * N);
+      if (accumulate) {
+        dst[0] += alpha * s.x; dst[1] += alpha * s.y; dst[2] += alpha * s.z; dst[3] += alpha * s.w;
+      } else {
+        dst[0] = alpha * s.x; dst[1] = alpha * s.y; dst[2] = alpha * s.z; dst[3] = alpha * s.w;
+      }
+    }
+    return;
+  }
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)MN; e += (int64_t)gridDim.x * blockDim.x) {
+    float s = part[e];
+    for (int q = 1; q < splits; ++q) s += part[(size_t)q * MN + e];
+    const int64_t r = e / N;
+    float* dst = C + r * ldc + (e - r * N);
+    *dst = accumulate ? *dst + alpha * s : alpha * s;
+  }
+}
+
+// the same second pass for a grouped launch: problem p owns float4 elements [start[p], start[p+1])
+struct SplitRedGroup {
+  const float* part[DW_GROUP];
+  float* C[DW_GROUP];
+  int N[DW_GROUP], splits[DW_GROUP];
+  int64_t MN[DW_GROUP];
+  int64_t start[DW_GROUP + 1];
+  int n, accumulate;
+};
+
+__global__ __launch_bounds__(256) void splitk_reduce_grouped_kernel(SplitRedGroup r) {
+  const int64_t total = r.start[r.n];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    int p = 0;
+#pragma unroll
+    for (int i = 1; i < DW_GROUP; ++i) p += (i < r.n && e >= r.start[i]) ? 1 : 0;
+    const int64_t q4 = e - r.start[p];
+    const float* part = r.part[p];
+    float4 s = reinterpret_cast<const float4*>(part)[q4];
+    for (int q = 1; q < r.splits[p]; ++q) {
+      const float4 v = reinterpret_cast<const float4*>(part + (size_t)q * r.MN[p])[q4];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    float4* dst = reinterpret_cast<float4*>(r.C[p]) + q4;  // C_i is [M_i][N_i] contiguous (ldc = N_i)
+    if (r.accumulate) {
+      const float4 c = *dst;
+      s.x += c.x; s.y += c.y; s.z += c.z; s.w += c.w;
+    }
+    *dst = s;
+  }
+}
+
 }  // namespace dct
 
 template <bool TA, bool TB>
@@ -703,6 +787,29 @@ static bool split_workspace(size_t bytes, int tiles, hipStream_t st, float** ws,
   return true;
 }
 
+// Two-pass split-K partials (DCT_GEMM_SPLIT_TWO_PASS=1): like the workspace above, one
+// buffer per process allocated outside stream capture and only ever superseded, never freed (a
+// captured graph keeps the pointer it recorded); the split GEMMs and their reduce run in stream
+// order on one compute stream, so one buffer serves them in turn.
+static float* g_part = nullptr;
+static size_t g_part_bytes = 0;
+static int g_part_dev = -1;
+static float* split_partials(size_t bytes, hipStream_t st) {
+  const char* f = getenv("DCT_GEMM_SPLIT_TWO_PASS");
+  if (!f || f[0] != '1') return nullptr;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (g_part && g_part_dev == dev && g_part_bytes >= bytes) return g_part;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  if (g_part_dev != -1 && g_part_dev != dev) return nullptr;  // one device per process
+  const size_t want = std::max<size_t>(bytes, (size_t)32 << 20);
+  float* w = nullptr;
+  if (hipMalloc(&w, want) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+  g_part = w; g_part_bytes = want; g_part_dev = dev;
+  return g_part;
+}
+
 static int device_cus() {
   static int cus = 0;
   if (cus == 0) {
@@ -748,8 +855,9 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
   if (splits > 1 && !g.split_probe) {
     const size_t bytes = (size_t)tiles * splits * dct::GBM * dct::GBN * sizeof(float);
     if (!split_workspace(bytes, tiles, st, &g.split_ws, &g.split_cnt)) g.split_ws = nullptr, g.split_cnt = nullptr;
+    if (!g.split_ws) g.split_part = split_partials((size_t)splits * g.M * g.N * sizeof(float), st);
   }
-  if (splits > 1 && !g.accumulate && !g.split_ws) {  // slices accumulate atomically into a zeroed C
+  if (splits > 1 && !g.accumulate && !g.split_ws && !g.split_part) {  // slices accumulate atomically into a zeroed C
     const int64_t total = (int64_t)g.M * g.N;
     const int zgrid = (int)std::min<int64_t>(2048, (total + 255) / 256);
     hipLaunchKernelGGL(dct::zero_panel_kernel, dim3(zgrid), dim3(256), 0, st, reinterpret_cast<float*>(g.C), g.ldc,
@@ -779,8 +887,14 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
   }
   if (splits > 1) {
     const int grid = tiles * splits;
-    if (gemm_stages(grid, nk_slice) == 4) return launch(dct::gemm2_kernel<TA, TB, true, 128, 4>, grid, 4);
-    return launch(dct::gemm2_kernel<TA, TB, true, 128, 2>, grid, 2);
+    e = gemm_stages(grid, nk_slice) == 4 ? launch(dct::gemm2_kernel<TA, TB, true, 128, 4>, grid, 4)
+                                         : launch(dct::gemm2_kernel<TA, TB, true, 128, 2>, grid, 2);
+    if (e != hipSuccess || !g.split_part) return e;
+    const int64_t n4 = ((int64_t)g.M * g.N + 3) / 4;
+    hipLaunchKernelGGL(dct::splitk_reduce_kernel, dim3((int)std::min<int64_t>(2048, (n4 + 255) / 256)), dim3(256), 0,
+                       st, g.split_part, splits, reinterpret_cast<float*>(g.C), g.ldc, g.M, g.N, g.accumulate,
+                       g.alpha);
+    return hipGetLastError();
   }
   if (gemm_stages(tiles, nk) == 4) return launch(dct::gemm2_kernel<TA, TB, false, 128, 4>, tiles, 4);
   return launch(dct::gemm2_kernel<TA, TB, false, 128, 2>, tiles, 2);
@@ -862,7 +976,28 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
   }
   gg.start[n] = total;
   hipError_t e;
-  if (!accumulate) {
+  // two-pass split-K (see split_partials): partial regions back to back, one grouped reduce after
+  dct::SplitRedGroup rg{};
+  size_t part_floats = 0;
+  bool two_pass = true;
+  for (int i = 0; i < n; ++i) two_pass = two_pass && N[i] % 4 == 0 && ((((uintptr_t)C[i]) & 15) == 0);
+  for (int i = 0; i < n; ++i) part_floats += (size_t)gg.splits[i] * M[i] * N[i];
+  float* part = two_pass ? split_partials(part_floats * sizeof(float), st) : nullptr;
+  if (part) {
+    rg.n = n; rg.accumulate = accumulate;
+    size_t off = 0;
+    int64_t s4 = 0;
+    for (int i = 0; i < n; ++i) {
+      gg.g[i].split_part = part + off;
+      rg.part[i] = part + off; rg.C[i] = C[i]; rg.N[i] = N[i]; rg.splits[i] = gg.splits[i];
+      rg.MN[i] = (int64_t)M[i] * N[i];
+      rg.start[i] = s4;
+      s4 += rg.MN[i] / 4;
+      off += (size_t)gg.splits[i] * M[i] * N[i];
+    }
+    rg.start[n] = s4;
+  }
+  if (!accumulate && !part) {
     for (int i = 0; i < n; ++i) {
       const int64_t tot = (int64_t)M[i] * N[i];
       hipLaunchKernelGGL(dct::zero_panel_kernel, dim3((int)std::min<int64_t>(2048, (tot + 255) / 256)), dim3(256), 0,
@@ -875,6 +1010,10 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
   e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(fn, dim3(total), dim3(dct::GNT), lds, st, gg);
+  e = hipGetLastError();
+  if (e != hipSuccess || !part) return (int)e;
+  hipLaunchKernelGGL(dct::splitk_reduce_grouped_kernel,
+                     dim3((int)std::min<int64_t>(2048, (rg.start[n] + 255) / 256)), dim3(256), 0, st, rg);
   return (int)hipGetLastError();
 }
 

@@ -25,6 +25,8 @@ struct GemmArgs {
   int split_probe;        // debug timing probe: split-K slices plain-store (wrong result) instead of atomics
   float* split_ws;        // optional split-K workspace [tiles][splits][BM*GBN]: slices store partials, the
   int* split_cnt;         // last slice of a tile (split_cnt[tile] arrival counter) sums them in slice order
+  float* split_part;      // optional two-pass split-K: slice s plain-stores its partial C into
+                          // split_part[s][M][N]; splitk_reduce_kernel sums the slices into C afterwards
 };
 
 }  // namespace dct

@@ -269,6 +269,42 @@ def test_gemm_pipeline_depths(M, N, K, ta, tb, out_f32, stages, cuda, monkeypatc
     assert (C.float() - ref).abs().max().item() < tol, (C.float() - ref).abs().max().item()
 
 
+@pytest.mark.parametrize("two_pass", ["1", "0"])
+@pytest.mark.parametrize("M,N,K,accumulate,colsum", [
+    (1024, 1024, 4096, 1, 1),  # tabular dW_l1: 64 tiles x 4 slices
+    (1024, 256, 4096, 1, 1),   # tabular dW_l0: 16 tiles x 16 slices
+    (192, 64, 32768, 0, 0),    # transformer dW (ungrouped): 2 tiles x 64 slices
+    (200, 72, 2048, 1, 0),     # ragged tile edges, N % 4 == 0
+    (136, 40, 1024, 0, 1),     # N % 8 == 0 only
+])
+def test_gemm_split_k_two_pass_and_atomic(M, N, K, accumulate, colsum, two_pass, cuda, monkeypatch):
+    """Split-K dW (fp32 out, few tiles): the two-pass mode (slices store partials, one reduce
+    kernel sums them in slice order) and the fp32-atomic mode against the fp32 torch reference,
+    accumulating into an existing C and with the fused bias column sums."""
+    monkeypatch.setenv("DCT_GEMM_SPLIT_TWO_PASS", two_pass)
+    torch.manual_seed(M + N)
+    A = _bf(torch.randn(K, M, device=cuda))  # dZ [rows][M]
+    B = _bf(torch.randn(K, N, device=cuda))  # X  [rows][N]
+    C0 = torch.randn(M, N, device=cuda)
+    C = C0.clone()
+    cs0 = torch.randn(M, device=cuda)
+    cs = cs0.clone()
+    native().gemm_bf16_ex(A.data_ptr(), B.data_ptr(), C.data_ptr(), 0, M, N, K, M, N, N, 1, 0, 0, 1, accumulate, 0,
+                          cs.data_ptr() if colsum else 0, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = A.float().t() @ B.float() + (C0 if accumulate else 0)
+    tol = 2e-3 * math.sqrt(K)
+    assert (C - ref).abs().max().item() < tol, (C - ref).abs().max().item()
+    if colsum:
+        assert torch.allclose(cs, cs0 + A.float().sum(0), atol=1e-2 * math.sqrt(K), rtol=1e-4)
+    if two_pass == "1":  # slices summed in a fixed order: bit-reproducible
+        C2 = C0.clone()
+        native().gemm_bf16_ex(A.data_ptr(), B.data_ptr(), C2.data_ptr(), 0, M, N, K, M, N, N, 1, 0, 0, 1, accumulate,
+                              0, 0, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(C, C2)
+
+
 @pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0)])
 def test_gemm_bf16_out_and_fast_path_match_generic(ta, tb, cuda, monkeypatch):
     """bf16 output; the fast path and the generic kernel agree."""

@@ -49,7 +49,8 @@ VARIANTS = {
     "s2_splits128": {"DCT_GEMM_STAGES": "2", "DCT_GEMM_SPLITS": "128"},
     "s4_splits128": {"DCT_GEMM_STAGES": "4", "DCT_GEMM_SPLITS": "128"},
 }
-ENV_KEYS = ("DCT_GEMM_STAGES", "DCT_GEMM_SPLIT_WG", "DCT_GEMM_SPLITS", "DCT_GEMM_SPLIT_PROBE", "DCT_GEMM_BM64_NK")
+ENV_KEYS = ("DCT_GEMM_STAGES", "DCT_GEMM_SPLIT_WG", "DCT_GEMM_SPLITS", "DCT_GEMM_SPLIT_PROBE", "DCT_GEMM_BM64_NK",
+            "DCT_GEMM_SPLIT_TWO_PASS")
 if os.environ.get("AB_SET") == "dw":  # split-K sweep on the transformer dW shapes only
     SHAPES = [s for s in SHAPES if s[0].startswith("tt_dw") or s[0] == "dw_l1"]
     VARIANTS = {f"{st}_sp{sp}": {"DCT_GEMM_STAGES": st[1], "DCT_GEMM_SPLITS": str(sp)}
@@ -73,6 +74,11 @@ if os.environ.get("AB_SET") == "layout":  # transformer dW shapes in every opera
 if os.environ.get("AB_SET") == "dwcmp":  # the tabular dW shapes: default launch vs hipBLASLt
     SHAPES = [s for s in SHAPES if s[0] in ("dw_l1", "dw_l0", "fwd_l1", "dx_l1")]
     VARIANTS = {"default": {}}
+if os.environ.get("AB_SET") == "twopass":  # split-K dW: two-pass partials + reduce vs fp32 atomics
+    SHAPES = [s for s in SHAPES if s[0] in ("dw_l1", "dw_l0") or s[0].startswith("tt_dw")]
+    VARIANTS = {"two_pass": {"DCT_GEMM_SPLIT_TWO_PASS": "1"}, "atomics": {"DCT_GEMM_SPLIT_TWO_PASS": "0"},
+                "two_pass_wg512": {"DCT_GEMM_SPLIT_TWO_PASS": "1", "DCT_GEMM_SPLIT_WG": "512"},
+                "two_pass_wg1024": {"DCT_GEMM_SPLIT_TWO_PASS": "1", "DCT_GEMM_SPLIT_WG": "1024"}}
 
 
 def main():
