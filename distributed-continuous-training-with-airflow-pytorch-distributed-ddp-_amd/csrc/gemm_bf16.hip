@@ -787,16 +787,21 @@ static bool split_workspace(size_t bytes, int tiles, hipStream_t st, float** ws,
   return true;
 }
 
-// Two-pass split-K partials (DCT_GEMM_SPLIT_TWO_PASS=1): like the workspace above, one
+// Two-pass split-K partials.  Auto mode takes it for <= 4 slices per tile: 1024 x 1024 x 4096 dW
+// (4 slices) 30.0 -> 23.3 us, tabular step 0.186 -> 0.1835 ms; with 16-64 slices (1024 x 256 x
+// 4096, the 32k-row transformer dW) the reduce pass costs more than the atomics it removes (15.9 ->
+// 16.7 us, 13-15 -> 28-29 us; profiles/gemm_splitk_two_pass_ab_r2.log).
+// DCT_GEMM_SPLIT_TWO_PASS=1 forces it, =0 disables it. like the workspace above, one
 // buffer per process allocated outside stream capture and only ever superseded, never freed (a
 // captured graph keeps the pointer it recorded); the split GEMMs and their reduce run in stream
 // order on one compute stream, so one buffer serves them in turn.
 static float* g_part = nullptr;
 static size_t g_part_bytes = 0;
 static int g_part_dev = -1;
-static float* split_partials(size_t bytes, hipStream_t st) {
-  const char* f = getenv("DCT_GEMM_SPLIT_TWO_PASS");
-  if (!f || f[0] != '1') return nullptr;
+static float* split_partials(size_t bytes, int max_splits, hipStream_t st) {
+  const char* f = getenv("DCT_GEMM_SPLIT_TWO_PASS");  // unset: auto; "1": always; "0": never
+  if (f && f[0] == '0') return nullptr;
+  if (!(f && f[0] == '1') && max_splits > 4) return nullptr;
   int dev = -1;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   if (g_part && g_part_dev == dev && g_part_bytes >= bytes) return g_part;
@@ -855,7 +860,7 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
   if (splits > 1 && !g.split_probe) {
     const size_t bytes = (size_t)tiles * splits * dct::GBM * dct::GBN * sizeof(float);
     if (!split_workspace(bytes, tiles, st, &g.split_ws, &g.split_cnt)) g.split_ws = nullptr, g.split_cnt = nullptr;
-    if (!g.split_ws) g.split_part = split_partials((size_t)splits * g.M * g.N * sizeof(float), st);
+    if (!g.split_ws) g.split_part = split_partials((size_t)splits * g.M * g.N * sizeof(float), splits, st);
   }
   if (splits > 1 && !g.accumulate && !g.split_ws && !g.split_part) {  // slices accumulate atomically into a zeroed C
     const int64_t total = (int64_t)g.M * g.N;
@@ -980,9 +985,11 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
   dct::SplitRedGroup rg{};
   size_t part_floats = 0;
   bool two_pass = true;
+  int max_splits = 1;
   for (int i = 0; i < n; ++i) two_pass = two_pass && N[i] % 4 == 0 && ((((uintptr_t)C[i]) & 15) == 0);
   for (int i = 0; i < n; ++i) part_floats += (size_t)gg.splits[i] * M[i] * N[i];
-  float* part = two_pass ? split_partials(part_floats * sizeof(float), st) : nullptr;
+  for (int i = 0; i < n; ++i) max_splits = std::max(max_splits, gg.splits[i]);
+  float* part = two_pass ? split_partials(part_floats * sizeof(float), max_splits, st) : nullptr;
   if (part) {
     rg.n = n; rg.accumulate = accumulate;
     size_t off = 0;
