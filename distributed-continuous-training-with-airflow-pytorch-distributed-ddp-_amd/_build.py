@@ -78,37 +78,63 @@ def _compile(src: str, flags, verbose: bool):
     if os.path.exists(obj):
         return obj, False
     lang = ["-x", "hip"] if src.endswith(".hip") else []
-    cmd = [os.path.join(ROCM, "bin", "hipcc")] + flags + lang + ["-c", src, "-o", obj + ".tmp"]
+    tmp = f"{obj}.{os.getpid()}.tmp"  # per-process: concurrent builds never share a temp file
+    cmd = [os.path.join(ROCM, "bin", "hipcc")] + flags + lang + ["-c", src, "-o", tmp]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {base}:\n{r.stdout}\n{r.stderr}")
-    os.replace(obj + ".tmp", obj)
+    os.replace(tmp, obj)
     return obj, True
 
 
+def _manifest_path() -> str:
+    return target_path() + ".objs"
+
+
 def build(force: bool = False, verbose: bool = False, jobs: int = 0, debug: bool = False) -> str:
-    flags = _flags(debug)
-    srcs = _sources()
-    jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 4)), 16)
-    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        results = list(ex.map(lambda s: _compile(s, flags, verbose), srcs))
-    objs = [o for o, _ in results]
-    rebuilt = any(b for _, b in results)
-    out = target_path()
-    if force or rebuilt or not os.path.exists(out):
-        cmd = (
-            [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"]
-            + objs
-            + [f"-L{ROCM}/lib", "-lrccl", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"]
-        )
-        if verbose:
-            print(" ".join(cmd), flush=True)
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
-        os.replace(out + ".tmp", out)
+    """Compile what changed and relink when the linked object set differs from the current one.
+
+    The object cache is keyed by source + header content and flags, so reverting a source finds
+    its old object already built: the relink decision compares the object list recorded next to
+    the .so (``<so>.objs``), not just "was anything recompiled".  Builds from several processes
+    (torchrun ranks finding a stale extension) are serialised by a lock file."""
+    import fcntl
+
+    os.makedirs(BUILD, exist_ok=True)
+    with open(os.path.join(BUILD, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        flags = _flags(debug)
+        srcs = _sources()
+        jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 4)), 16)
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            results = list(ex.map(lambda s: _compile(s, flags, verbose), srcs))
+        objs = [o for o, _ in results]
+        manifest = "\n".join(os.path.basename(o) for o in objs) + "\n"
+        out = target_path()
+        try:
+            with open(_manifest_path()) as f:
+                linked = f.read()
+        except OSError:
+            linked = None
+        if force or linked != manifest or not os.path.exists(out):
+            tmp = f"{out}.{os.getpid()}.tmp"
+            cmd = (
+                [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp]
+                + objs
+                + [f"-L{ROCM}/lib", "-lrccl", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"]
+            )
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+            os.replace(tmp, out)
+            with open(_manifest_path(), "w") as f:
+                f.write(manifest)
+        elif is_stale():  # same objects, but a source was touched after the link: refresh the stamp
+            os.utime(out, None)
     return out
 
 
