@@ -31,3 +31,42 @@ def test_debug_reducer_assertion(monkeypatch):
         debug.assert_reducer_complete(R())
     R.launched = 3
     debug.assert_reducer_complete(R())
+
+
+def test_native_build_relinks_when_the_object_set_changes(tmp_path, monkeypatch):
+    """_build.build() links when the object list differs from the one recorded next to the .so,
+    not only when something was recompiled: reverting a source finds its cached object, and the
+    previously linked .so (built from the other version) must not survive.  hipcc is faked."""
+    import subprocess
+
+    from dct_amd import _build
+
+    pkg, csrc, obj = tmp_path / "pkg", tmp_path / "pkg" / "csrc", tmp_path / "build" / "obj"
+    csrc.mkdir(parents=True)
+    (csrc / "a.hip").write_text("v1")
+    monkeypatch.setattr(_build, "PKG_DIR", str(pkg))
+    monkeypatch.setattr(_build, "CSRC", str(csrc))
+    monkeypatch.setattr(_build, "BUILD", str(obj))
+    monkeypatch.setattr(_build, "_flags", lambda debug=False: ["-O3"])
+    links = []
+
+    def fake_run(cmd, capture_output=True, text=True):
+        out = cmd[cmd.index("-o") + 1]
+        with open(out, "w") as f:
+            f.write(" ".join(cmd))
+        if "-shared" in cmd:
+            links.append([c for c in cmd if c.endswith(".o")])
+        return subprocess.CompletedProcess(cmd, 0, "", "")
+
+    monkeypatch.setattr(_build.subprocess, "run", fake_run)
+    _build.build()
+    assert len(links) == 1 and not _build.is_stale()
+    _build.build()
+    assert len(links) == 1  # nothing changed: no relink
+    (csrc / "a.hip").write_text("v2")
+    _build.build()
+    assert len(links) == 2  # recompiled -> relinked
+    (csrc / "a.hip").write_text("v1")  # revert: the v1 object is cached, no compile ...
+    _build.build()
+    assert len(links) == 3 and links[2] == links[0]  # ... but the .so is relinked from it
+    assert not _build.is_stale()
