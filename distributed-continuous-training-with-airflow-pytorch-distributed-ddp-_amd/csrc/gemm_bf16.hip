@@ -905,6 +905,44 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
   return launch(dct::gemm2_kernel<TA, TB, false, 128, 2>, tiles, 2);
 }
 
+// dW = dZ^T X as `splits` split-K slices stored to part[splits][M][N] (no reduce: the consumer -
+// the executor's Adam - sums them in slice order); colsum (+)= column sums of dZ by atomics.
+// dZ [K][M], X [K][N] bf16 row-major.  Returns hipErrorInvalidValue when the shape does not take the
+// LDS-DMA kernel or the slices would not each hold >= 1 k-tile.
+extern "C" int dct_gemm_bf16_dw_partials(const uint16_t* dZ, const uint16_t* X, float* part, float* colsum, int M,
+                                         int N, int K, int splits, void* stream) {
+  dct::GemmArgs g{};
+  g.A = dZ; g.B = X; g.C = part; g.M = M; g.N = N; g.K = K; g.lda = M; g.ldb = N; g.ldc = N;
+  g.epilogue = dct::EPI_NONE; g.out_f32 = 1; g.accumulate = 0; g.alpha = 1.0f;
+  g.vec_a = ((((uintptr_t)dZ) & 15) == 0) && (M % 8 == 0);
+  g.vec_b = ((((uintptr_t)X) & 15) == 0) && (N % 8 == 0);
+  g.colsum = colsum;
+  g.split_part = part;
+  const int nk = K / dct::GBK;
+  if (!part || M <= 0 || N <= 0 || !gemm_v2_ok(g, 1, 0) || splits < 1 || splits > nk) return (int)hipErrorInvalidValue;
+  const int tiles = ((M + dct::GBM - 1) / dct::GBM) * ((N + dct::GBN - 1) / dct::GBN);
+  const int nk_slice = (nk + splits - 1) / splits;
+  if ((splits - 1) * nk_slice >= nk) return (int)hipErrorInvalidValue;  // an empty slice would store zeros: fine, but keep it tight
+  auto fn = dct::gemm2_kernel<true, false, true, 128, 2>;
+  const size_t lds = (size_t)(nk_slice > 1 ? 4 : 2) * dct::G2_BYTES;
+  hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(fn, dim3(tiles * splits), dim3(dct::GNT), lds, reinterpret_cast<hipStream_t>(stream), g, splits);
+  return (int)hipGetLastError();
+}
+
+// the split count launch_gemm2 picks for an fp32-out dW of this shape (1 = not split)
+extern "C" int dct_gemm_dw_auto_splits(int M, int N, int K) {
+  const int tiles = ((M + dct::GBM - 1) / dct::GBM) * ((N + dct::GBN - 1) / dct::GBN);
+  const int nk = K / dct::GBK;
+  if (tiles >= 256 || nk < 8 || K % dct::GBK) return 1;
+  int target = device_cus();
+  if (const char* f = getenv("DCT_GEMM_SPLIT_WG")) target = std::max(1, atoi(f));
+  int splits = std::min(nk / 8, (target + tiles - 1) / tiles);
+  if (const char* f = getenv("DCT_GEMM_SPLITS")) splits = std::min(nk, atoi(f));
+  return splits < 1 ? 1 : splits;
+}
+
 extern "C" int dct_bias_act_bwd(const void* dY, const void* act_aux, uint16_t* dZ, float* dbias, int M, int N,
                                 int ldy, int act, int accumulate_bias, void* stream);
 

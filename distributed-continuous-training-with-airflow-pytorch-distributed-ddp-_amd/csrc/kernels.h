@@ -52,6 +52,9 @@ int dct_skinny_dx(const uint16_t* dZ, const uint16_t* W, const uint16_t* aux, ui
                   void* stream);
 int dct_skinny_dw(const uint16_t* dZ, const uint16_t* X, float* dW, float* db, int B, int K, int C, void* stream);
 int dct_skinny_head_supported(int K, int C);
+int dct_gemm_bf16_dw_partials(const uint16_t* dZ, const uint16_t* X, float* part, float* colsum, int M, int N, int K,
+                              int splits, void* stream);
+int dct_gemm_dw_auto_splits(int M, int N, int K);
 int dct_skinny_head(const uint16_t* H, const uint16_t* W, const float* bias, const int* labels, uint16_t* dH,
                     float* dW, float* db, float* loss_sum, int B, int K, int C, float grad_scale, int loss_kind,
                     float loss_scale, int relu_mask, void* stream);

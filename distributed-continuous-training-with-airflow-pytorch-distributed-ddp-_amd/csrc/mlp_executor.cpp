@@ -19,6 +19,8 @@
 //                         the earlier layers' backward GEMMs keep running) ; dA_l = dZ W_l
 //   finalize              compute stream waits for the last bucket
 //   adam_flat             fp32 master update + bf16 shadow weights for the next forward's GEMMs;
+//                         [no reducer: the 2-4-way split-K slices of up to two hidden layers' dW
+//                          are summed here, in slice order, instead of by a reduce pass into g]
 //                         its first thread writes loss_out[cursor] = reduced loss, cursor += 1
 // (the step prologue, gradient zeroing, loss slot and epilogue ride inside the gather, loss and
 // Adam kernels instead of a memset node and three single-thread launches)
@@ -49,6 +51,11 @@ int dct_adam_flat_step(float* p, const float* g, float* m, float* v, uint16_t* p
                        const int* step_counter, int* cursor, const float* loss_slot, float* loss_out, int loss_cap,
                        void* stream);
 int dct_step_end(int* cursor, const float* slot, float* loss_out, int loss_cap, void* stream);
+int dct_adam_flat_step_parts(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, float lr,
+                             float b1, float b2, float eps, float wd, float grad_scale, int decoupled,
+                             const int* step_counter, int* cursor, const float* loss_slot, float* loss_out,
+                             int loss_cap, int nparts, const int64_t* part_off, const int64_t* part_n,
+                             const float* const* part, const int* part_splits, void* stream);
 }
 
 namespace dct {
@@ -88,6 +95,7 @@ MlpStepExecutor::MlpStepExecutor(const std::vector<int>& dims, int batch, int ac
     off += dims[l + 1];
   }
   P_ = off;
+  plan_partials();
 }
 
 void MlpStepExecutor::set_adam(float lr, float b1, float b2, float eps, float wd, int decoupled) {
@@ -131,6 +139,7 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int* cur = reinterpret_cast<int*>(cursor);
   int* sc = reinterpret_cast<int*>(step_counter);
+  bool part_used[2] = {false, false};
   if (reducer_) reducer_->prepare();
   ck(dct_gather_batch_step(reinterpret_cast<const void*>(X), row_bytes, reinterpret_cast<const int*>(Y),
                            reinterpret_cast<const int*>(idx), cur, B_, rows, n_items, acts_[0], y_, sc, g_, P_ + 1, st),
@@ -187,11 +196,20 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
       continue;
     }
     // dW = dZ^T A_l (fp32 into the zeroed flat gradient buffer = a DDP bucket view), with the
-    // bias gradient db = colsum(dZ) fused into the same GEMM
-    ck(dct_gemm_bf16_ex(dz_[ci], acts_[l], g_ + woff_[l], nullptr, dout, din, rows, dout, din, din,
-                        /*trans_a*/ 1, /*trans_b*/ 0, EPI_NONE, /*out_f32*/ 1, /*accumulate*/ 1, nullptr,
-                        g_ + boff_[l], st),
-       "dW gemm");
+    // bias gradient db = colsum(dZ) fused into the same GEMM.  Without a reducer, a layer planned
+    // for it leaves its split-K slices in part_[r] for the Adam kernel to sum (no reduce pass, no
+    // gradient write + re-read); the weight range of g stays zero and is not read.
+    const int r = part_slot(l);
+    if (r >= 0 && dct_gemm_bf16_dw_partials(dz_[ci], acts_[l], part_[r], g_ + boff_[l], dout, din, rows,
+                                            part_splits_[r], st) == 0) {
+      part_used[r] = true;
+    } else {
+      if (r >= 0) (void)hipGetLastError();
+      ck(dct_gemm_bf16_ex(dz_[ci], acts_[l], g_ + woff_[l], nullptr, dout, din, rows, dout, din, din,
+                          /*trans_a*/ 1, /*trans_b*/ 0, EPI_NONE, /*out_f32*/ 1, /*accumulate*/ 1, nullptr,
+                          g_ + boff_[l], st),
+         "dW gemm");
+    }
     if (reducer_) {
       reducer_->mark_ready(2 * l + 1, stream);
       reducer_->mark_ready(2 * l, stream);
@@ -205,9 +223,55 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
     }
   }
   if (reducer_) reducer_->finalize(stream);
-  ck(dct_adam_flat_step(p_, g_, m_, v_, pb_, P_, lr_, b1_, b2_, eps_, wd_, 1, 1.0f, decoupled_, sc, cur, g_ + P_,
-                        reinterpret_cast<float*>(loss_out), loss_cap, st),
-     "adam");
+  int np = 0;
+  int64_t poff[2], pn[2];
+  const float* pp[2];
+  int psp[2];
+  for (int q = 0; q < nparts_; ++q) {
+    if (!part_used[q]) continue;
+    const int l = part_layer_[q];
+    poff[np] = woff_[l]; pn[np] = (int64_t)dims_[l] * dims_[l + 1]; pp[np] = part_[q]; psp[np] = part_splits_[q];
+    ++np;
+  }
+  if (np)
+    ck(dct_adam_flat_step_parts(p_, g_, m_, v_, pb_, P_, lr_, b1_, b2_, eps_, wd_, 1.0f, decoupled_, sc, cur, g_ + P_,
+                                reinterpret_cast<float*>(loss_out), loss_cap, np, poff, pn, pp, psp, st),
+       "adam");
+  else
+    ck(dct_adam_flat_step(p_, g_, m_, v_, pb_, P_, lr_, b1_, b2_, eps_, wd_, 1, 1.0f, decoupled_, sc, cur, g_ + P_,
+                          reinterpret_cast<float*>(loss_out), loss_cap, st),
+       "adam");
+}
+
+int MlpStepExecutor::part_slot(int l) const {
+  const char* e = getenv("DCT_DW_INTO_ADAM");  // "0": dW through g and the reduce pass
+  if (e && e[0] == '0') return -1;
+  for (int q = 0; q < nparts_; ++q)
+    if (part_layer_[q] == l) return q;
+  return -1;
+}
+
+void MlpStepExecutor::plan_partials() {
+  // up to two hidden layers whose dW the launcher would split 2..4 ways (the two-pass regime):
+  // their slices go straight to Adam.  Only without a DDP reducer (it must all-reduce g).
+  if (reducer_) return;
+  for (int l = L_ - 1; l >= 0 && nparts_ < 2; --l) {
+    if (skinny(l)) continue;
+    const int M = dims_[l + 1], N = dims_[l];
+    const int sp = dct_gemm_dw_auto_splits(M, N, B_);
+    if (sp < 2 || sp > 4 || (woff_[l] & 3) || (((int64_t)M * N) & 3)) continue;
+    float* buf = nullptr;
+    if (hipMalloc(&buf, (size_t)sp * M * N * sizeof(float)) != hipSuccess) {
+      (void)hipGetLastError();
+      return;
+    }
+    part_[nparts_] = buf; part_layer_[nparts_] = l; part_splits_[nparts_] = sp;
+    ++nparts_;
+  }
+}
+
+MlpStepExecutor::~MlpStepExecutor() {
+  for (int q = 0; q < nparts_; ++q) (void)hipFree(part_[q]);
 }
 
 void MlpStepExecutor::eval_batch(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t idx, int n_items,

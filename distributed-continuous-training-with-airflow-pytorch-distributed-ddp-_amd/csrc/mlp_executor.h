@@ -28,10 +28,15 @@ class MlpStepExecutor {
   void eval_batch(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t idx, int n_items, uintptr_t cursor, int rows,
                   uintptr_t stats, uintptr_t stream);
   int64_t num_params() const { return P_; }
+  ~MlpStepExecutor();
+  MlpStepExecutor(const MlpStepExecutor&) = delete;
+  MlpStepExecutor& operator=(const MlpStepExecutor&) = delete;
 
  private:
   void forward(int rows, hipStream_t st, int layers = -1);  // layers 0 .. layers-1 (default all)
   bool fused_head() const;
+  void plan_partials();
+  int part_slot(int l) const;  // partial-buffer slot of layer l's dW, or -1
   // layers with <= 8 outputs run as bandwidth kernels (csrc/skinny.hip)
   bool skinny(int l) const { return dims_[l + 1] <= 8 && dims_[l] % 8 == 0 && woff_[l] % 8 == 0; }
   std::vector<int> dims_;
@@ -50,6 +55,10 @@ class MlpStepExecutor {
   BucketReducer* reducer_ = nullptr;
   float lr_ = 1e-3f, b1_ = 0.9f, b2_ = 0.999f, eps_ = 1e-8f, wd_ = 0.f;
   int decoupled_ = 0;
+  // split-K dW slices handed to Adam (plan_partials): device buffers [splits][M][N]
+  float* part_[2] = {nullptr, nullptr};
+  int part_layer_[2] = {-1, -1}, part_splits_[2] = {1, 1};
+  int nparts_ = 0;
 };
 
 }  // namespace dct

@@ -119,3 +119,25 @@ def test_trainer_fit_graph_engine_writes_checkpoint(tmp_path, cuda):
     sd = load_checkpoint(str(tmp_path / "last.ckpt"))["state_dict"]
     assert set(sd) == set(model.state_dict())
     assert tr.callback_metrics["val_loss"] < 0.5
+
+
+@pytest.mark.parametrize("B", [1024, 4096])
+def test_dw_slices_into_adam_match_reduce_path(B, cuda, monkeypatch):
+    """Without a DDP reducer the executor hands the 2-4-way split-K dW slices of the hidden
+    1024x1024 layers to Adam (summed there in slice order) instead of reducing them into g: the
+    same trajectory as DCT_DW_INTO_ADAM=0 (same slices, same order -> the same gradients)."""
+    dims = [256, 1024, 1024, 1024, 2]
+    X, Y = _data(8 * B, dims[0], seed=5)
+    rows = torch.arange(X.shape[0])
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DCT_DW_INTO_ADAM", mode)
+        model, eng = _engine(dims, B, loss="ce", lr=1e-3)
+        eng.attach_data(X, Y, rows, rows[:B])
+        losses = torch.cat([eng.train_epoch(ep).cpu() for ep in range(2)])
+        torch.cuda.synchronize()
+        res[mode] = (losses, eng.p.cpu())
+    (l1, p1), (l0, p0) = res["1"], res["0"]
+    assert torch.isfinite(l1).all()
+    assert torch.allclose(l1, l0, atol=1e-3), (l1 - l0).abs().max()
+    assert (p1 - p0).norm() / p0.norm() < 1e-2
