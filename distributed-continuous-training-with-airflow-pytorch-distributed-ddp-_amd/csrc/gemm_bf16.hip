@@ -632,8 +632,9 @@ __global__ __launch_bounds__(GNT, BM == 64 ? 4 : 2) void gemm2_kernel(GemmArgs g
 }
 
 // Grouped split-K launch: up to DW_GROUP independent problems (the dW GEMMs of one transformer
-// block) in ONE grid, so the per-launch fixed cost (ramp, first-load latency, tail) is paid once.
-constexpr int DW_GROUP = 4;
+// block, or of every block when the backward defers them to its end) in ONE grid, so the
+// per-launch fixed cost (ramp, first-load latency, tail) is paid once.
+constexpr int DW_GROUP = 16;
 struct GemmGroup {
   GemmArgs g[DW_GROUP];
   int splits[DW_GROUP];

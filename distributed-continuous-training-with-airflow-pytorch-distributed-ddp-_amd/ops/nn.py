@@ -37,10 +37,11 @@ def _stream():
 # ----------------------------------------------------------------------------- engine binding
 class _Binding:
     def __init__(self, params: Iterable[torch.Tensor], shadows: Optional[Dict[int, torch.Tensor]],
-                 side_dw: bool = False):
+                 side_dw: bool = False, defer_dw: bool = False):
         self.direct = {id(p) for p in params}
         self.shadows = shadows or {}
         self.side_dw = side_dw
+        self.defer_dw = defer_dw
 
 
 _BOUND: Optional[_Binding] = None
@@ -48,7 +49,7 @@ _BOUND: Optional[_Binding] = None
 
 @contextlib.contextmanager
 def bound_params(params: Iterable[torch.Tensor], bf16_shadows: Optional[Dict[int, torch.Tensor]] = None,
-                 side_dw: bool = False):
+                 side_dw: bool = False, defer_dw: bool = False):
     """Engine-scoped fast paths for the ops below (trainer/engines.py AutogradEngine):
 
     * gradient accumulation fusion - the weight-gradient GEMMs / LayerNorm column sums of a
@@ -61,10 +62,12 @@ def bound_params(params: Iterable[torch.Tensor], bf16_shadows: Optional[Dict[int
     * ``side_dw`` - the fused transformer block's weight-gradient GEMMs go to a side stream and
       overlap the next (earlier) block's backward kernel; the caller joins them with
       :func:`join_side_work` after backward.  Only for callers with no gradient hooks reading the
-      buffers during backward (no DDP bucket reducer): the grads land after the hooks fired.
+      buffers during backward (no DDP bucket reducer): the grads land after the hooks fired;
+    * ``defer_dw`` - the same GEMMs are queued instead and issued by :func:`join_side_work` as
+      ONE grouped split-K launch for every block (same no-reducer condition).
     """
     global _BOUND
-    prev, _BOUND = _BOUND, _Binding(params, bf16_shadows, side_dw)
+    prev, _BOUND = _BOUND, _Binding(params, bf16_shadows, side_dw, defer_dw)
     try:
         yield
     finally:
@@ -75,7 +78,7 @@ def bound_params(params: Iterable[torch.Tensor], bf16_shadows: Optional[Dict[int
 # completion event plus the operand tensors it reads (kept referenced until the join, so the
 # caching allocator cannot hand their memory to later main-stream work while the side stream
 # still reads it)
-_SIDE = {"stream": None, "pending": []}
+_SIDE = {"stream": None, "pending": [], "deferred": []}
 
 
 def _side_stream(dev) -> "torch.cuda.Stream":
@@ -86,11 +89,18 @@ def _side_stream(dev) -> "torch.cuda.Stream":
 
 
 def join_side_work():
-    """Current stream waits for every weight-gradient launch issued on the side stream."""
+    """Current stream waits for every weight-gradient launch issued on the side stream, and
+    issues the deferred ones (bound_params(defer_dw=True)) as grouped launches of up to 16."""
     pend = _SIDE["pending"]
     if pend:
         torch.cuda.current_stream().wait_event(pend[-1][0])
         pend.clear()
+    dfr = _SIDE["deferred"]
+    if dfr:
+        nat, st = native(), _stream()
+        for i in range(0, len(dfr), 16):
+            _dw_gemm_grouped(nat, dfr[i:i + 16], st)
+        dfr.clear()
 
 
 def _w16(w: torch.Tensor) -> torch.Tensor:
@@ -604,7 +614,12 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
     dout16 = _bf16_of(dout)
     items = [(dout16, f, w2, b2), (dpre, a2, w1, b1), (dh1_16, o, wo, bo), (dqkv, a1, wqkv, bqkv)]
     b = _BOUND
-    if b is not None and b.side_dw and all(_is_direct(t) for t in (w2, b2, w1, b1, wo, bo, wqkv, bqkv)):
+    direct = b is not None and all(_is_direct(t) for t in (w2, b2, w1, b1, wo, bo, wqkv, bqkv))
+    if direct and b.defer_dw:
+        # accumulate straight into the bound grads at the end of backward, every block in one launch
+        _SIDE["deferred"].extend(items)
+        dw2 = db2 = dw1 = db1 = dwo = dbo = dwqkv = dbqkv = None
+    elif direct and b.side_dw:
         # the four dW GEMMs accumulate straight into the bound grads: run them on the side stream,
         # behind this block's dX chain, while the main stream goes on to the earlier block
         side = _side_stream(dev)

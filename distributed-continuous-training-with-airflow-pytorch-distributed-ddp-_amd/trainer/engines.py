@@ -749,7 +749,11 @@ class AutogradEngine(_EngineBase):
         # Off by default: the overlap slowed both kernels, TabTransformer step 0.420 -> 0.445 ms
         # (profiles/tt_head_spb_side_dw_ab_r2.log)
         side = self.reducer is None and os.environ.get("DCT_TT_DW_SIDE", "0") == "1"
-        return bound_params(self.params, self._shadows, side_dw=side)
+        # every transformer block's dW GEMMs as ONE grouped launch after backward (same no-reducer
+        # condition; DCT_TT_DW_DEFER=0 keeps one launch per block): TabTransformer step 0.421-0.426
+        # -> 0.407 ms (profiles/tt_dw_defer_ab_r2.log)
+        defer = self.reducer is None and os.environ.get("DCT_TT_DW_DEFER", "1") != "0"
+        return bound_params(self.params, self._shadows, side_dw=side, defer_dw=defer)
 
     def sync_to_model(self):
         pass  # parameters ARE views of the flat buffer

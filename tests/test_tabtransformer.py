@@ -121,9 +121,11 @@ def test_device_loop_matches_host_loop(cuda, F_):
 
 
 @pytest.mark.gpu
-def test_side_stream_dw_matches_in_stream(cuda, monkeypatch):
-    """Fused-block dW GEMMs on the side stream (DCT_TT_DW_SIDE=1, joined after backward) train the
-    same trajectory as on the compute stream, eager steps and captured step graphs alike."""
+@pytest.mark.parametrize("knob", ["DCT_TT_DW_SIDE", "DCT_TT_DW_DEFER"])
+def test_side_stream_dw_matches_in_stream(cuda, monkeypatch, knob):
+    """Fused-block dW GEMMs on the side stream (DCT_TT_DW_SIDE=1, joined after backward) or deferred
+    to one grouped launch after backward (DCT_TT_DW_DEFER=1) train the same trajectory as the
+    per-block launches on the compute stream, eager steps and captured step graphs alike."""
     from dct_amd.parallel.dist import init_distributed
     from dct_amd.trainer.engines import AutogradEngine
     from dct_amd.trainer.trainer import seed_everything
@@ -135,7 +137,7 @@ def test_side_stream_dw_matches_in_stream(cuda, monkeypatch):
     B, steps = 128, 12
     res = {}
     for side in ("1", "0", "0"):
-        monkeypatch.setenv("DCT_TT_DW_SIDE", side)
+        monkeypatch.setenv(knob, side)
         seed_everything(7)
         m = TabTransformer(num_features=F_, d_model=64, heads=4, layers=3, lr=3e-3)
         eng = AutogradEngine(m, ctx, B, seed=7)
