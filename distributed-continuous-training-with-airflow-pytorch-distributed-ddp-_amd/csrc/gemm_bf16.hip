@@ -999,16 +999,32 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
     const int tiles = ((g.M + dct::GBM - 1) / dct::GBM) * ((g.N + dct::GBN - 1) / dct::GBN);
     const int nk = g.K / dct::GBK;
     if (!gemm_v2_ok(g, 1, 0) || tiles >= 256 || nk < 8) { grouped = false; break; }
-    int target = device_cus();
-    if (const char* f = getenv("DCT_GEMM_SPLIT_WG")) target = std::max(1, atoi(f));
-    int min_kt = 8;  // k-tiles per split slice
-    if (const char* f = getenv("DCT_GEMM_DW_MINK")) min_kt = std::max(2, atoi(f));
-    int splits = std::min(nk / min_kt, (target + tiles - 1) / tiles);
-    if (splits < 1) splits = 1;
-    gg.splits[i] = splits;
-    gg.start[i] = total;
-    total += tiles * splits;
-    max_slice = std::max(max_slice, (nk + splits - 1) / splits);
+  }
+  // k-tiles per split slice: 8, doubled (up to 64) while the whole group would exceed two
+  // workgroups per CU.  One transformer block's four dW GEMMs (448 workgroups at 8) keep 8; the
+  // four blocks' sixteen deferred to one launch go to 32 (448 workgroups instead of 1792: a quarter
+  // of the fp32 atomics, four times the k-loop per slice): TabTransformer step 0.411 -> 0.368 ms
+  // (profiles/tt_dw_mink_ab_r2.log).  DCT_GEMM_DW_MINK pins it.
+  int target = device_cus();
+  if (const char* f = getenv("DCT_GEMM_SPLIT_WG")) target = std::max(1, atoi(f));
+  const char* mk_env = getenv("DCT_GEMM_DW_MINK");
+  int min_kt = mk_env ? std::max(2, atoi(mk_env)) : 8;
+  for (;;) {
+    total = 0;
+    max_slice = 1;
+    for (int i = 0; grouped && i < n; ++i) {
+      const dct::GemmArgs& g = gg.g[i];
+      const int tiles = ((g.M + dct::GBM - 1) / dct::GBM) * ((g.N + dct::GBN - 1) / dct::GBN);
+      const int nk = g.K / dct::GBK;
+      int splits = std::min(nk / min_kt, (target + tiles - 1) / tiles);
+      if (splits < 1) splits = 1;
+      gg.splits[i] = splits;
+      gg.start[i] = total;
+      total += tiles * splits;
+      max_slice = std::max(max_slice, (nk + splits - 1) / splits);
+    }
+    if (!grouped || mk_env || total <= 2 * device_cus() || min_kt >= 64) break;
+    min_kt *= 2;
   }
   if (!grouped) {
     for (int i = 0; i < n; ++i) {
