@@ -67,6 +67,12 @@ def bound_params(params: Iterable[torch.Tensor], bf16_shadows: Optional[Dict[int
       ONE grouped split-K launch for every block (same no-reducer condition).
     """
     global _BOUND
+    # leftovers of a backward that never reached join_side_work (an aborted graph capture) belong
+    # to that step: issuing them into this step's gradients would corrupt it
+    _SIDE["deferred"].clear()
+    if _SIDE["pending"]:  # side-stream launches of such a step: order them before this step's work
+        torch.cuda.current_stream().wait_event(_SIDE["pending"][-1][0])
+        _SIDE["pending"].clear()
     prev, _BOUND = _BOUND, _Binding(params, bf16_shadows, side_dw, defer_dw)
     try:
         yield
