@@ -67,7 +67,9 @@ struct HeadArgs {
   const float* h;  // [B][T][D] fp32 residual stream after the last block
   const int64_t* y;
   const float *ln_w, *ln_b, *W, *bias;  // LN (D), head W [C][D], bias [C]
-  float* loss;                          // forward: += mean CE
+  float* loss;                          // forward: mean CE (stored, no pre-zeroed output needed)
+  float* partial;                       // forward: one loss partial per workgroup
+  unsigned* ticket;                     // forward: finished-workgroup count, 0 between launches
   const float* dloss;                   // backward: upstream gradient of the loss (device scalar)
   float* dh; uint16_t* dh16;            // backward: d h (fp32 + bf16 copy)
   float *dln_w, *dln_b, *dW, *dbias;    // backward: accumulated
@@ -127,9 +129,10 @@ __device__ __forceinline__ HeadFwd head_chain(const HeadArgs& a, int b, int d) {
   return r;
 }
 
-// NW samples per workgroup (one wave each).  The per-sample losses meet in LDS and each block adds
-// ONE value to the loss: the loss is a single address, and 512 same-address float atomics (one per
-// sample) serialised this kernel.
+// NW samples per workgroup (one wave each).  The per-sample losses meet in LDS; each block stores ONE
+// partial, and the last block to finish (ticket count) sums the partials in block order and stores
+// the loss: deterministic, and the caller needs no zero-filled loss (a fill kernel per step before,
+// 512 same-address float atomics, one per sample, before that).  The last block resets the ticket.
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void head_fwd_kernel(HeadArgs a) {
   __shared__ float lsum[NW];
@@ -152,12 +155,28 @@ __global__ __launch_bounds__(64 * NW) void head_fwd_kernel(HeadArgs a) {
     lsum[w] = (m + __logf(se) - ly) / a.B;
   }
   }
+  __shared__ unsigned last;
   __syncthreads();
   if (threadIdx.x == 0) {
     float v = 0.f;
 #pragma unroll
     for (int i = 0; i < NW; ++i) v += lsum[i];
-    atomicAdd(a.loss, v);
+    __hip_atomic_store(a.partial + blockIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && threadIdx.x < 64) {
+    // wave 0 sums the partials: lane-strided loads all in flight at once, then the butterfly (a fixed
+    // order, so the loss is bit-identical run to run); a one-thread serial sum cost ~18 us per step
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    float s = 0.f;
+    for (unsigned i = threadIdx.x; i < gridDim.x; i += 64)
+      s += __hip_atomic_load(a.partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s = wsum(s);
+    if (threadIdx.x == 0) {
+      a.loss[0] = s;
+      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -275,13 +294,15 @@ int dct_tt_embed_bwd(const float* x, const float* dh, float* dE, float* dc, int 
   return (int)hipGetLastError();
 }
 
-// ptrs: h, y(int64), ln_w, ln_b, W, bias, loss  (forward)
+// ptrs: h, y(int64), ln_w, ln_b, W, bias, loss, partial (>= ceil(B / 4) floats), ticket
+// (uint32, zero before the first launch; every launch leaves it zero)  (forward)
 int dct_tt_head_fwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C, float eps, void* stream) {
-  if (n_ptrs != 7 || Dm != dct::ttio::D || C < 1 || C > dct::ttio::CMAX || B <= 0 || T <= 0 || (p[0] & 15))
+  if (n_ptrs != 9 || Dm != dct::ttio::D || C < 1 || C > dct::ttio::CMAX || B <= 0 || T <= 0 || (p[0] & 15))
     return (int)hipErrorInvalidValue;
   dct::ttio::HeadArgs a{};
   a.h = (const float*)p[0]; a.y = (const int64_t*)p[1]; a.ln_w = (const float*)p[2]; a.ln_b = (const float*)p[3];
   a.W = (const float*)p[4]; a.bias = (const float*)p[5]; a.loss = (float*)p[6];
+  a.partial = (float*)p[7]; a.ticket = (unsigned*)p[8];
   a.B = B; a.T = T; a.C = C; a.eps = eps;
   const int nw = dct::ttio::head_spb(B);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);

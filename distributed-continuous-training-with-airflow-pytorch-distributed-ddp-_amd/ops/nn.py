@@ -778,6 +778,23 @@ def tt_embed(x: torch.Tensor, E: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
     return (x.float()[:, :, None] * E + c).reshape(B * F_, E.shape[1])
 
 
+_HEAD_SCRATCH: Dict[Optional[int], torch.Tensor] = {}
+
+
+def _head_scratch(device: torch.device, B: int) -> torch.Tensor:
+    """Per-device head-loss scratch: [ticket (uint32 bits, left 0 by every launch) | ceil(B/4) fp32
+    partials].  Allocated zeroed by the eager warm-up steps, then reused by the captured step graph
+    (one key per device, not per stream: a stream-keyed buffer first met under capture would put its
+    zero fill back into every replay).  Head forwards on one device run in stream order."""
+    key = device.index
+    n = 1 + (B + 3) // 4
+    buf = _HEAD_SCRATCH.get(key)
+    if buf is None or buf.numel() < n:
+        buf = torch.zeros(max(n, 1 + 128), dtype=torch.float32, device=device)
+        _HEAD_SCRATCH[key] = buf
+    return buf
+
+
 class _TTHeadLossFn(torch.autograd.Function):
     """mean_b CE(Linear(LN(mean_t h[b, t, :])), y_b) in one kernel; the backward kernel recomputes the
     per-sample chain and writes dh (fp32 + the bf16 copy the last block's dW GEMM consumes)."""
@@ -787,8 +804,10 @@ class _TTHeadLossFn(torch.autograd.Function):
         h = h.contiguous().float()
         y = y.contiguous().long()
         vec = [t.contiguous() for t in (ln_w, ln_b, W, bias)]
-        loss = torch.zeros((), dtype=torch.float32, device=h.device)
-        native().tt_head_fwd([h.data_ptr(), y.data_ptr()] + [t.data_ptr() for t in vec] + [loss.data_ptr()], B, T,
+        loss = torch.empty((), dtype=torch.float32, device=h.device)  # stored by the kernel's last block
+        scratch = _head_scratch(h.device, B)
+        native().tt_head_fwd([h.data_ptr(), y.data_ptr()] + [t.data_ptr() for t in vec]
+                             + [loss.data_ptr(), scratch.data_ptr() + 4, scratch.data_ptr()], B, T,
                              h.shape[1], W.shape[0], float(eps), _stream())
         ctx.save_for_backward(h, y, *vec)
         ctx.params = (ln_w, ln_b, W, bias)

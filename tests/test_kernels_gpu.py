@@ -858,6 +858,32 @@ def test_tt_embed_and_head_loss_match_fp32_reference(cuda, B, C, spb, monkeypatc
 
 
 @pytest.mark.gpu
+def test_tt_head_loss_repeated_launches_deterministic(cuda):
+    """tt_io.hip head_fwd_kernel: the last workgroup (ticket count) sums the per-workgroup partials in
+    block order and stores the loss, leaving the ticket at zero - so back-to-back launches of any batch
+    size (the scratch grows past its first size) give the fp32 reference loss, bit-identical on
+    repeats, without a zero-filled loss tensor."""
+    from dct_amd.ops.nn import tt_head_loss
+
+    F_, d, C = 64, 64, 2
+    g = torch.Generator(device="cpu").manual_seed(11)
+    lw = (1 + 0.1 * torch.randn(d, generator=g)).to(cuda)
+    lb, W, bias = (0.1 * torch.randn(d, generator=g)).to(cuda), (0.3 * torch.randn(C, d, generator=g)).to(cuda), \
+        (0.1 * torch.randn(C, generator=g)).to(cuda)
+    for B in (512, 3, 1100, 512, 64):
+        h = torch.randn(B * F_, d, generator=g).to(cuda)
+        y = torch.randint(0, C, (B,), generator=g).to(cuda)
+        with torch.no_grad():
+            losses = [tt_head_loss(h, y, B, F_, lw, lb, W, bias) for _ in range(3)]
+            z = F.layer_norm(h.reshape(B, F_, d).mean(1), (d,), lw, lb, 1e-5)
+            ref = F.cross_entropy(F.linear(z, W, bias), y)
+        torch.cuda.synchronize()
+        vals = [float(t) for t in losses]
+        assert vals[0] == vals[1] == vals[2], (B, vals)
+        assert abs(vals[0] - ref.item()) < 1e-4 * max(1.0, abs(ref.item())), (B, vals[0], ref.item())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("accumulate", [0, 1])
 @pytest.mark.parametrize("grouped", [True, False])
 def test_gemm_dw_grouped(cuda, accumulate, grouped, monkeypatch):
