@@ -2,11 +2,14 @@
 """Headline benchmark: whole-node training samples/sec of the weather-MLP DDP job.
 
 BASELINE.json metric: "samples/sec (whole node) for weather-MLP DDP at 1/2/4/8 MI355X; epoch
-wall-clock".  Default workload = the reference training step exactly (jobs/train_lightning_ddp.py):
-WeatherClassifier 5->64->2 (ReLU, Dropout 0.2), cross-entropy, Adam(lr=0.01), batch 4 PER RANK
-(weak scaling), DistributedSampler sharding, per-step gradient all-reduce across ranks plus
-the sync_dist train_loss.  Other BASELINE.json configs:
-  --model weather-mlp-3x128    3-layer / 128-h weather MLP (fused single-CU kernel)
+wall-clock", on BASELINE.json's "Weather MLP (3-layer, 128-h)" (configs 0-2).  Default workload
+(--model weather-mlp-3x128): 5 -> 128 -> 128 -> 2 with ReLU + Dropout(0.2) after each hidden
+layer, cross-entropy, Adam(lr=0.01), batch 4 PER RANK (weak scaling) - the reference training step
+(jobs/train_lightning_ddp.py:57-62,66-71,88,122) with BASELINE's 3-layer 128-h model -
+DistributedSampler sharding, per-step gradient all-reduce across ranks plus the sync_dist
+train_loss.  At one rank the reference-exact WeatherClassifier 5->64->2 is measured too, with the
+same steps / warmup, and reported under extra.reference_model_*.  Other configs:
+  --model weather              the reference-exact WeatherClassifier 5-64-2 as the headline
   --model tabular-mlp-4x1024   100M x 256 synthetic rows (bf16, HBM-resident), 256-1024-1024-1024-2
                                MLP, MSE, Adam(1e-3), batch 4096 per rank, graph-captured MFMA step
   --model tabtransformer       4-layer TabTransformer over 64 feature tokens (d 64, 4 heads), CE,
@@ -36,7 +39,19 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 # BASELINE.md local probe (reference step shape, torch CPU, W=1): ~8,500 samples/s whole node.
 # The reference publishes no number (BASELINE.json "published": {}); this probe is the only one.
-BASELINE_SAMPLES_PER_SEC = {"weather": 8500.0}
+# BASELINE.md local probes (reference step shape, plain torch on CPU, W=1, tools/cpu_reference_probe.py);
+# the reference publishes no number (BASELINE.json "published": {}).  3x128: the 5-64-2 probe scaled by
+# the measured 3x128 / 5-64-2 probe ratio (0.52), an optimistic CPU ceiling.
+BASELINE_SAMPLES_PER_SEC = {"weather": 8500.0, "weather-mlp-3x128": 4400.0}
+BASELINE_REF = {"weather": "BASELINE.md CPU probe (reference step shape, torch CPU, W=1): 8500 samples/s; the "
+                           "reference publishes none",
+                "weather-mlp-3x128": "BASELINE.md CPU probe of the 3-layer 128-h step (torch CPU, W=1): 4400 "
+                                     "samples/s; the reference publishes none"}
+MODELS = {"weather": "WeatherClassifier 5-64-2 (reference jobs/train_lightning_ddp.py)",
+          "weather-mlp-3x128": "weather-mlp-3x128: Weather MLP (3-layer, 128-h) 5-128-128-2, ReLU+Dropout 0.2, CE "
+                               "(BASELINE.json configs 0-2)",
+          "tabular-mlp-4x1024": "tabular MLP 256-1024-1024-1024-2 (BASELINE config 4)",
+          "tabtransformer": "TabTransformer 4 layers, 64 feature tokens, d 64, 4 heads (BASELINE config 5)"}
 TABULAR = ("tabular-mlp-4x1024",)
 TRANSFORMER = ("tabtransformer",)
 
@@ -46,7 +61,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=None, help="timed steps (default 20000; tabular 200)")
     p.add_argument("--warmup", type=int, default=None, help="untimed steps (default 2000; tabular 20)")
-    p.add_argument("--model", default="weather", help="weather | weather-mlp-3x128 | tabular-mlp-4x1024")
+    p.add_argument("--model", default="weather-mlp-3x128",
+                   help="weather-mlp-3x128 (BASELINE) | weather (reference 5-64-2) | tabular-mlp-4x1024 | tabtransformer")
+    p.add_argument("--no-reference-model", action="store_true",
+                   help="skip the extra 5-64-2 measurement of a single-rank weather-mlp-3x128 run")
     p.add_argument("--batch", type=int, default=None, help="per-rank batch (reference: 4; tabular: 4096)")
     p.add_argument("--rows", type=int, default=0,
                    help="synthetic dataset rows (0 = sized to the run; tabular: 100M per BASELINE config 4)")
@@ -291,20 +309,11 @@ def setup_transformer(a, ctx):
     return eng, feats
 
 
-def main():
-    a = parse()
+def measure(a, ctx):
+    """Set up a.model, run the W warmup steps, time exactly K steps; returns (result dict, ok)."""
     import torch
 
-    import dct_amd  # noqa: F401
-    from dct_amd.parallel.dist import init_distributed, shutdown
-    from dct_amd.trainer.trainer import seed_everything
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != a.gpus and a.gpus > 1 and world == 1:
-        raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank per GPU)")
     cpu = a.device == "cpu"
-    ctx = init_distributed("cpu" if cpu else "gpu")
-    seed_everything(42)
     tab = a.model in TABULAR
     tt = a.model in TRANSFORMER
     if cpu:
@@ -373,14 +382,13 @@ def main():
     # epoch wall-clock for an --epoch-rows dataset at the measured step rate (train part)
     steps_per_epoch = math.ceil(math.ceil(int(0.8 * a.epoch_rows) / ctx.world_size) / a.batch)
     base = BASELINE_SAMPLES_PER_SEC.get(a.model)
-    models = {"weather": "WeatherClassifier 5-64-2 (reference jobs/train_lightning_ddp.py)",
-              "tabular-mlp-4x1024": "tabular MLP 256-1024-1024-1024-2 (BASELINE config 4)",
-              "tabtransformer": "TabTransformer 4 layers, 64 feature tokens, d 64, 4 heads (BASELINE config 5)"}
+    devices = _physical_devices(ctx)
+    n_dev = len(set(devices)) if devices else 0
     out = {
         "metric": "samples/sec (whole node) for weather-MLP DDP",
         "value": round(sps, 1),
         "unit": "samples/s",
-        "n_gpus": 0 if cpu else ctx.world_size,
+        "n_gpus": 0 if cpu else n_dev,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(ms_step, 6),
@@ -390,7 +398,7 @@ def main():
         "dtype": "bf16" if (tab or tt) else "fp32",
         "data": "synthetic",
         "config": {
-            "model": models.get(a.model, a.model),
+            "model": MODELS.get(a.model, a.model),
             "global_batch": a.batch * ctx.world_size,
             "per_rank_batch": a.batch,
             "seq_len": None,
@@ -401,9 +409,11 @@ def main():
             "dataset_rows": int(eng.X.shape[0]),
             "seq_len_tokens": feats if tt else None,
             "features": feats,
-            "baseline_ref": "BASELINE.md CPU probe, W=1, 8500 samples/s (reference publishes none)",
+            "baseline_ref": BASELINE_REF.get(a.model, "none (the reference publishes no number)"),
         },
         "extra": {
+            "ranks": ctx.world_size,
+            "ranks_per_device": (round(ctx.world_size / n_dev, 3) if n_dev else None),
             "us_per_step": round(ms_step * 1e3, 3),
             "epoch_wall_clock_s_train": round(steps_per_epoch * ms_step / 1e3, 6),
             "epoch_rows": a.epoch_rows,
@@ -420,10 +430,68 @@ def main():
     if tab:
         flops = 6.0 * sum(eng.dims[i] * eng.dims[i + 1] for i in range(len(eng.dims) - 1)) * a.batch
         out["extra"]["model_tflops_per_gpu"] = round(flops / (ms_step * 1e-3) / 1e12, 1)
+    if tt:
+        out["extra"]["dtypes"] = {"gemm_and_attention_operands": "bf16", "accumulation": "fp32",
+                                  "master_weights_and_adam": "fp32", "hbm_dataset": "fp32"}
+    elif tab:
+        out["extra"]["dtypes"] = {"gemm_operands": "bf16", "accumulation": "fp32",
+                                  "master_weights_and_adam": "fp32", "hbm_dataset": "bf16"}
+    return out, (finite and in_sync), eng
+
+
+def _physical_devices(ctx):
+    """PCI bus id of every rank's GPU (rank order): n_gpus counts DISTINCT physical devices, so a
+    rehearsal of several ranks on one GPU is never reported as a multi-GPU result."""
+    if ctx.device.type != "cuda":
+        return []
+    from dct_amd.ops._native import native
+
+    mine = native().pci_bus_id(ctx.device.index or 0)
+    return ctx.all_gather_object(mine) if ctx.is_distributed else [mine]
+
+
+def main():
+    a = parse()
+    import copy
+
+    import torch
+
+    import dct_amd  # noqa: F401
+    from dct_amd.parallel.dist import init_distributed, shutdown
+    from dct_amd.trainer.trainer import seed_everything
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus and a.gpus > 1 and world == 1:
+        raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    cpu = a.device == "cpu"
+    ctx = init_distributed("cpu" if cpu else "gpu")
+    seed_everything(42)
+    out, ok, eng = measure(a, ctx)
+    if not cpu and ctx.world_size > 1:
+        from dct_amd.parallel.xgmi import peer_report
+
+        bus, mat, peers_ok = peer_report(ctx)
+        out["extra"]["xgmi_peers"] = {"rank_devices": bus, "can_access_peer": mat, "all_rank_pairs_ok": peers_ok}
+    if (a.model == "weather-mlp-3x128" and not cpu and ctx.world_size == 1 and not a.no_reference_model):
+        # the reference-exact model (jobs/train_lightning_ddp.py:57-62) with the same K / W
+        del eng
+        seed_everything(42)
+        a_ref = copy.copy(a)
+        a_ref.model = "weather"
+        ref, ok_ref, _ = measure(a_ref, ctx)
+        out["extra"].update({
+            "reference_model": ref["config"]["model"],
+            "reference_model_value": ref["value"],
+            "reference_model_us_per_step": ref["extra"]["us_per_step"],
+            "reference_model_vs_baseline": ref["vs_baseline"],
+            "reference_model_engine": ref["config"]["engine"],
+            "reference_model_loss_last": ref["extra"]["loss_last"],
+        })
+        ok = ok and ok_ref
     if ctx.rank == 0:
         print(json.dumps(out), flush=True)
     shutdown(ctx)
-    return 0 if (finite and in_sync) else 3
+    return 0 if ok else 3
 
 
 if __name__ == "__main__":

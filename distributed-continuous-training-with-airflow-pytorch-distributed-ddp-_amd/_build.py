@@ -37,7 +37,7 @@ def _headers():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h"))
 
 
-def _flags(debug: bool = False):
+def _flags(debug: bool = False, sanitize: bool = None):
     import pybind11
 
     f = [
@@ -56,7 +56,9 @@ def _flags(debug: bool = False):
         f.append("-g")
     if os.environ.get("DCT_PROF_BUILD", "0") == "1":  # in-kernel phase stamps (tools/prof_fused.py)
         f.append("-DDCT_WAVE_PROF")
-    if os.environ.get("DCT_SANITIZE", "0") == "1":  # host-side ASan only (no GPU sanitizer on this pool)
+    if sanitize is None:
+        sanitize = os.environ.get("DCT_SANITIZE", "0") == "1"
+    if sanitize:  # host-side ASan only (no GPU sanitizer on this pool)
         f += ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
     return f
 
@@ -136,6 +138,35 @@ def build(force: bool = False, verbose: bool = False, jobs: int = 0, debug: bool
         elif is_stale():  # same objects, but a source was touched after the link: refresh the stamp
             os.utime(out, None)
     return out
+
+
+def build_sanitized(out_dir: str, verbose: bool = False) -> str:
+    """Host-ASan variant of the extension in ``out_dir`` (never the in-tree module): the host C++
+    runtime (``*.cpp``: bindings, RCCL communicator / bucket reducer / peer exchange, step
+    executor) is compiled with ``-Xarch_host -fsanitize=address`` and linked with the regular
+    objects of the HIP sources (their device code cannot be sanitized on this pool anyway).
+    Load it with the clang ASan runtime preloaded (``asan_runtime()``); tests/test_sanitize_cpu.py
+    drives it."""
+    os.makedirs(out_dir, exist_ok=True)
+    plain, asan = _flags(), _flags(sanitize=True)
+    objs = []
+    for src in _sources():
+        o, _ = _compile(src, asan if src.endswith(".cpp") else plain, verbose)
+        objs.append(o)
+    out = os.path.join(out_dir, MODULE + sysconfig.get_config_var("EXT_SUFFIX"))
+    cmd = ([os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-fsanitize=address",
+            "-shared-libsan", "-o", out] + objs + [f"-L{ROCM}/lib", "-lrccl", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"])
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"ASan link failed:\n{r.stdout}\n{r.stderr}")
+    return out
+
+
+def asan_runtime() -> str:
+    """Path of the clang ASan runtime hipcc links against (LD_PRELOAD it into a plain python)."""
+    r = subprocess.run([os.path.join(ROCM, "bin", "hipcc"), "-print-file-name=libclang_rt.asan-x86_64.so"],
+                       capture_output=True, text=True)
+    return r.stdout.strip()
 
 
 def is_stale() -> bool:

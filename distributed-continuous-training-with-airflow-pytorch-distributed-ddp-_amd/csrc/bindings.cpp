@@ -151,6 +151,27 @@ PYBIND11_MODULE(_dct_native, m) {
     return std::string(p.gcnArchName);
   });
   m.def("synchronize", []() { check((int)hipDeviceSynchronize(), "hipDeviceSynchronize"); });
+  // PCI bus id of a device: identifies the physical GPU behind a rank (ranks sharing one GPU in a
+  // rehearsal report the same id)
+  m.def("pci_bus_id", [](int dev) {
+    char buf[64] = {0};
+    check((int)hipDeviceGetPCIBusId(buf, (int)sizeof(buf), dev), "hipDeviceGetPCIBusId");
+    return std::string(buf);
+  });
+  // hipDeviceCanAccessPeer over every ordered pair of visible devices (1 on the diagonal): the
+  // xGMI peer matrix the in-kernel exchange depends on
+  m.def("peer_matrix", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    std::vector<std::vector<int>> mat(n, std::vector<int>(n, 0));
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        int ok = (i == j) ? 1 : 0;
+        if (i != j && hipDeviceCanAccessPeer(&ok, i, j) != hipSuccess) ok = 0;
+        mat[i][j] = ok;
+      }
+    return mat;
+  });
 
   // ------------------------------------------------------------------ fused MLP
   py::class_<MlpLaunch>(m, "MlpLaunch")
@@ -261,6 +282,13 @@ PYBIND11_MODULE(_dct_native, m) {
                                      P<int>(step_counter), P<float>(zero), zero_n, reinterpret_cast<void*>(stream)),
                 "ag_step_prologue");
         });
+  // device timestamps (s_memrealtime, 100 MHz) of step phases: graph-capturable one-thread kernels
+  m.def("phase_stamp", [](uintptr_t buf, int index, uintptr_t stream) {
+    check(dct_reducer_stamp(P<unsigned long long>(buf) + index, reinterpret_cast<void*>(stream)), "phase_stamp");
+  });
+  m.def("phase_accum", [](uintptr_t buf, int n, uintptr_t stream) {
+    check(dct_phase_accum(P<unsigned long long>(buf), n, reinterpret_cast<void*>(stream)), "phase_accum");
+  });
   m.def("zero_f32", [](uintptr_t p, int64_t n, uintptr_t stream) {
     check(dct_zero_f32(P<float>(p), n, reinterpret_cast<void*>(stream)), "zero_f32");
   });
@@ -476,7 +504,11 @@ PYBIND11_MODULE(_dct_native, m) {
       .def("finalize", &dct::BucketReducer::finalize)
       .def_property_readonly("num_buckets", &dct::BucketReducer::num_buckets)
       .def_property_readonly("launched", &dct::BucketReducer::launched)
-      .def_property_readonly("comm_stream", &dct::BucketReducer::comm_stream);
+      .def_property_readonly("launched_before_finalize", &dct::BucketReducer::launched_before_finalize)
+      .def_property_readonly("comm_stream", &dct::BucketReducer::comm_stream)
+      .def("enable_timing", &dct::BucketReducer::enable_timing, py::arg("check") = false)
+      .def("read_timing", &dct::BucketReducer::read_timing)
+      .def("reset_timing", &dct::BucketReducer::reset_timing);
   py::class_<dct::PeerExchange>(m, "PeerExchange")
       .def(py::init<int, int, int64_t>(), py::arg("world"), py::arg("rank"), py::arg("bytes"))
       .def("ipc_handle", [](const dct::PeerExchange& x) { return py::bytes(x.ipc_handle()); })

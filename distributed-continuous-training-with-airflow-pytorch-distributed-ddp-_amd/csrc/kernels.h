@@ -32,6 +32,11 @@ struct GemmArgs {
 }  // namespace dct
 
 extern "C" {
+// reducer instrumentation (step_kernels.hip)
+int dct_reducer_stamp(unsigned long long* dst, void* stream);
+int dct_reducer_close(unsigned long long* s, void* stream);
+int dct_reducer_check(unsigned long long* s, void* stream);
+int dct_phase_accum(unsigned long long* b, int n, void* stream);
 int dct_gemm_bf16(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K, int lda,
                   int ldb, int ldc, int trans_a, int trans_b, int epilogue, int out_f32, int accumulate, void* aux,
                   void* stream);

@@ -1,0 +1,556 @@
+// One-barrier register-resident trainer for 3-layer MLPs D0 -> 128 -> 128 -> C (C <= 4,
+// D0 <= 32, batch <= 4): BASELINE "Weather MLP (3-layer, 128-h)" (models/mlp.py preset
+// weather-mlp-3x128; the reference's WeatherClassifier with a second 128-wide hidden layer,
+// jobs/train_lightning_ddp.py:57-62,69,88,122).  Same contract as mlp_train_kernel /
+// mlp_block_kernel: one workgroup runs every step of a launch, identical dropout hash, loss and
+// Adam, so it is a drop-in replacement selected by dct_mlp_train.
+//
+// Design (8 waves = 2 per SIMD, the minimum that keeps VALU issue back to back):
+//   * wave w owns the k-slice [16w, 16w+16) of the 128x128 matrix W1, lane l the outputs
+//     o = l and l + 64: 32 weights + both Adam moments per lane, all in VGPRs;
+//   * layer 0 is computed by the wave that consumes it: lane (unit 16w + l/4, row l%4) forms
+//     h1 for its own k-slice (quad all-reduce over input slices), publishes it to a
+//     WAVE-PRIVATE LDS tile and reads it back as broadcast ds_read_b128 - no workgroup barrier;
+//   * the ONLY workgroup barrier of a step sits after the layer-1 k-slice partials
+//     ([o][wave][row], padded stride: conflict-free b128 stores and loads, double-buffered);
+//   * after it every wave sums the 8 partials of ITS lanes' outputs itself, so the layer-2
+//     logits, the loss, dlogits, dW2/db2/db1 and their Adam run redundantly (bit-identically)
+//     in every wave instead of behind more barriers and single-lane phases; the hidden-layer
+//     dropout keep bits come from one hash per lane, published as 64-bit ballots;
+//   * logits: 4*C per-lane partials reduce-scattered over the wave (v_permlane32_swap,
+//     v_permlane16_swap, DPP), so DPP row r holds row r's logits; the loss runs 16 lanes per
+//     row and v_readlane makes dlogits wave-uniform;
+//   * dX of W1 from the same registers: one 16-value reduce-scatter per batch row (permlane
+//     swaps + DPP, no LDS) leaves dZ1 in exactly the lane that computed the matching h1;
+//   * dW0/db0 via quad DPP broadcasts, dW1 from the wave-private h1 tile, Adam in registers.
+// The input tile is triple-buffered (the backward re-reads it after the barrier while faster
+// waves already publish the next batch); the next batch is gathered one step ahead.
+#include "mlp_fused_impl.h"
+
+namespace dct {
+
+namespace blk2 {
+constexpr int H = 128, NT = 512, NW = 8, KS = 16, DMAX = 32, B = 4;
+constexpr int XT = 0;                    // [3][DMAX][4] input tile, transposed (unit-major, 4 rows)
+constexpr int LAB = XT + 3 * DMAX * 4;   // [3][4] labels (int)
+constexpr int MSK = LAB + 12;            // [2][NW][2] hidden-2 dropout keep ballots (uint64 per wave)
+constexpr int H1W = MSK + 2 * NW * 2;    // [NW][KS][4] wave-private layer-1 inputs h1[k][row]
+constexpr int PSTR = 36;                 // partials: [o][wave][4] with a 36-float o stride
+constexpr int PART = H1W + NW * KS * 4;  // [2][H][PSTR]
+constexpr int TOTAL = PART + 2 * H * PSTR;
+static_assert((H1W % 4) == 0 && (PART % 4) == 0 && (MSK % 4) == 0 && (LAB % 4) == 0, "16-B aligned tiles");
+}  // namespace blk2
+
+namespace b2d {
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int QP_X1 = 0xB1;     // quad_perm [1,0,3,2]: lane ^ 1
+constexpr int QP_X2 = 0x4E;     // quad_perm [2,3,0,1]: lane ^ 2
+constexpr int ROR8 = 0x128;     // row_ror:8 == lane ^ 8 inside a 16-lane row
+constexpr int HMIRROR = 0x141;  // row_half_mirror: lane i <-> 7 - i inside each 8 lanes (lane ^ 7)
+
+__device__ __forceinline__ float swap32_sum(float lo, float hi) {
+  // lanes 0-31 get lo(own) + lo(partner), lanes 32-63 hi(partner) + hi(own)
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap16_sum(float lo, float hi) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(lo), __float_as_uint(hi), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// Wave reduce-scatter of N = 8 or 16 per-lane values: afterwards lane l holds the wave sum of
+// value l >> 3 (N = 8) or l >> 2 (N = 16), i.e. DPP row r holds values [N/4 r, N/4 (r+1)).
+// Levels: lane bit 5 (v_permlane32_swap), 4 (v_permlane16_swap), 3 (row_ror 8 = lane ^ 8),
+// [N = 16: bit 2 via row_half_mirror, partner lane ^ 7, which agrees on bits 5..3], then an
+// all-reduce over the remaining low bits; every partner agrees on the bits already decided, so
+// each kept value sums disjoint lane sets and the last one covers all 64 lanes.
+template <int N>
+__device__ __forceinline__ float rs_small(float (&P)[N], int lane) {
+  static_assert(N == 8 || N == 16, "");
+#pragma unroll
+  for (int i = 0; i < N / 2; ++i) P[i] = swap32_sum(P[i], P[i + N / 2]);
+#pragma unroll
+  for (int i = 0; i < N / 4; ++i) P[i] = swap16_sum(P[i], P[i + N / 4]);
+  const bool b3 = (lane >> 3) & 1;
+  float r;
+  if constexpr (N == 8) {
+    const float keep = b3 ? P[1] : P[0], send = b3 ? P[0] : P[1];
+    r = keep + dpp<ROR8>(send);
+    r += dpp<QP_X1>(r);
+    r += dpp<QP_X2>(r);
+    r += dpp<HMIRROR>(r);  // quads are uniform now: the mirror pairs quad 0 with quad 1
+  } else {
+    const bool b2 = (lane >> 2) & 1;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float keep = b3 ? P[i + 2] : P[i], send = b3 ? P[i] : P[i + 2];
+      P[i] = keep + dpp<ROR8>(send);
+    }
+    const float keep = b2 ? P[1] : P[0], send = b2 ? P[0] : P[1];
+    r = keep + dpp<HMIRROR>(send);
+    r += dpp<QP_X1>(r);
+    r += dpp<QP_X2>(r);
+  }
+  return r;
+}
+
+__device__ __forceinline__ float sel4(const float (&v)[4], int i) {
+  return i == 0 ? v[0] : (i == 1 ? v[1] : (i == 2 ? v[2] : v[3]));
+}
+
+__device__ __forceinline__ float rl(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+}  // namespace b2d
+
+// PROF (diagnostic instantiation, launched only when MlpArgs::prof is set): lane 0 of every wave
+// sums s_memtime deltas per phase into prof[wave * 16 + phase] (tools/prof_block.py)
+#define B2STAMP(k)                                                   \
+  if constexpr (PROF) {                                              \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();      \
+    pacc[(k)] += t_ - t_last;                                        \
+    t_last = t_;                                                     \
+  }
+
+// ND: input slices per lane (D0 <= 4 * ND); CM: class capacity (2 or 4); ADAM: train mode vs
+// grad mode (gradients + loss to grad_out).
+template <int ND, int CM, bool ADAM, bool PROF = false>
+__global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, MlpArgs a) {
+  using namespace blk2;
+  using namespace b2d;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int D0 = sh.dims[0], C = sh.dims[3];
+  const int r0 = l & 3;                 // layer-0 role: row r0, unit u = KS w + l / 4, input slice r0
+  const int u = KS * w + (l >> 2);
+  const int wo0 = sh.woff[0], bo0 = sh.boff[0], wo1 = sh.woff[1], bo1 = sh.boff[1];
+  const int wo2 = sh.woff[2], bo2 = sh.boff[2];
+  unsigned long long pacc[PROF ? 10 : 1] = {};
+  unsigned long long t_last = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
+
+  int cur0 = 0;
+  if (a.cursor) {
+    cur0 = __hip_atomic_load(a.cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0 && cur0 > 0 && a.loss_out) a.loss_out[cur0 - 1] = a.grad_out[sh.P];
+  }
+  int t0 = a.t0;
+  uint32_t step_base = a.step_base;
+  if (a.step_counter) {
+    t0 = __hip_atomic_load(a.step_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    step_base = (uint32_t)t0;
+  }
+
+  // ---- registers: W1 k-slice + moments; W0 slices; replicated W2 / b1 / b2 (+ moments)
+  float w1[2][KS], m1[2][KS], v1[2][KS];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int f = wo1 + (l + 64 * j) * H + KS * w + kk;
+      w1[j][kk] = a.p[f];
+      m1[j][kk] = ADAM ? a.m[f] : 0.f;
+      v1[j][kk] = ADAM ? a.v[f] : 0.f;
+    }
+  float w0[ND], m0[ND], v0[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) {
+    const int d = r0 + 4 * i;
+    const bool ok = d < D0;
+    const int f = wo0 + u * D0 + (ok ? d : 0);
+    w0[i] = ok ? a.p[f] : 0.f;
+    m0[i] = (ok && ADAM) ? a.m[f] : 0.f;
+    v0[i] = (ok && ADAM) ? a.v[f] : 0.f;
+  }
+  float pb0 = a.p[bo0 + u], mb0 = ADAM ? a.m[bo0 + u] : 0.f, vb0 = ADAM ? a.v[bo0 + u] : 0.f;
+  float pb1[2], mb1[2], vb1[2];
+  float pw2[CM][2], mw2[CM][2], vw2[CM][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int o = l + 64 * j;
+    pb1[j] = a.p[bo1 + o];
+    mb1[j] = ADAM ? a.m[bo1 + o] : 0.f;
+    vb1[j] = ADAM ? a.v[bo1 + o] : 0.f;
+#pragma unroll
+    for (int c = 0; c < CM; ++c) {
+      const bool ok = c < C;
+      const int f = wo2 + (ok ? c : 0) * H + o;
+      pw2[c][j] = ok ? a.p[f] : 0.f;
+      mw2[c][j] = (ok && ADAM) ? a.m[f] : 0.f;
+      vw2[c][j] = (ok && ADAM) ? a.v[f] : 0.f;
+    }
+  }
+  float pb2[CM], mb2[CM], vb2[CM];
+#pragma unroll
+  for (int c = 0; c < CM; ++c) {
+    const bool ok = c < C;
+    pb2[c] = ok ? a.p[bo2 + c] : 0.f;
+    mb2[c] = (ok && ADAM) ? a.m[bo2 + c] : 0.f;
+    vb2[c] = (ok && ADAM) ? a.v[bo2 + c] : 0.f;
+  }
+
+  // ---- LDS: first batch into input buffer 0
+  for (int e = tid; e < TOTAL; e += NT) lds[e] = 0.f;
+  __syncthreads();
+  const int Bsz = a.B;
+  {
+    const int bs0 = min(Bsz, a.n_items - cur0 * Bsz);
+    if (tid < B * DMAX) {
+      const int b = tid & 3, d = tid >> 2;
+      float x = 0.f;
+      if (b < bs0 && d < D0) x = a.X[(size_t)a.idx[cur0 * Bsz + b] * a.ldx + d];
+      lds[XT + d * 4 + b] = x;
+    }
+    if (tid < B) reinterpret_cast<int*>(lds + LAB)[tid] = (tid < bs0) ? a.Y[a.idx[cur0 * Bsz + tid]] : 0;
+  }
+  // prefetch roles: thread -> (row pb, feature pk) of the next batch, or (row pb, label)
+  const int nel = Bsz * D0;
+  int role = 0, pb = 0, pk = 0;
+  if (tid < nel) { role = 1; pb = tid / D0; pk = tid - pb * D0; }
+  else if (tid < nel + Bsz) { role = 2; pb = tid - nel; }
+  int ridx_next = 0;
+  if (role && (cur0 + 1) * Bsz + pb < a.n_items) ridx_next = a.idx[(cur0 + 1) * Bsz + pb];
+  __syncthreads();
+
+  const float p_drop = a.dropout;
+  const bool drop = p_drop > 0.f;
+  const float scale = drop ? 1.0f / (1.0f - p_drop) : 1.0f;
+  const float l2b1 = log2f(a.b1), l2b2 = log2f(a.b2);
+  float* h1w = lds + H1W + w * (KS * 4);
+  int xb = 0;
+  if constexpr (PROF) t_last = __builtin_amdgcn_s_memtime();
+  for (int s = 0; s < a.steps; ++s) {
+    const int sb = s + cur0;
+    const int bs = min(Bsz, a.n_items - sb * Bsz);
+    const uint32_t gstep = step_base + (uint32_t)s;
+    const int xbn = xb == 2 ? 0 : xb + 1;
+    const float* xT = lds + XT + xb * DMAX * 4;
+    const bool have_next = (s + 1 < a.steps);
+    const int bs_next = have_next ? min(Bsz, a.n_items - (sb + 1) * Bsz) : 0;
+    const uint32_t* src = (role == 1) ? reinterpret_cast<const uint32_t*>(a.X) + (size_t)ridx_next * a.ldx + pk
+                                      : reinterpret_cast<const uint32_t*>(a.Y) + ridx_next;
+    const uint32_t raw_next = *src;
+    const int nx2 = min((sb + 2) * Bsz + pb, a.n_items - 1);
+    const int ridx_next2 = a.idx[nx2 < 0 ? 0 : nx2];
+    const int4 labs = *reinterpret_cast<const int4*>(lds + LAB + xb * 4);
+
+    // ---- F1: h1[u][r0] (quad all-reduce over the input slices) -> wave-private tile
+    float h1;
+    {
+      // input slices d >= D0 hold zeros in the tile (and zero weights): no guards, no branches
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        const float4 x = *reinterpret_cast<const float4*>(xT + (r0 + 4 * i) * 4);
+        acc[0] += w0[i] * x.x; acc[1] += w0[i] * x.y; acc[2] += w0[i] * x.z; acc[3] += w0[i] * x.w;
+      }
+      // quad reduce-scatter over the input slices: lane r0 keeps row r0
+      const bool qb1 = (r0 >> 1) & 1, qb0 = r0 & 1;
+      const float k0 = qb1 ? acc[2] : acc[0], k1 = qb1 ? acc[3] : acc[1];
+      const float s0 = qb1 ? acc[0] : acc[2], s1 = qb1 ? acc[1] : acc[3];
+      const float e0 = k0 + dpp<QP_X2>(s0), e1 = k1 + dpp<QP_X2>(s1);
+      const float kq = qb0 ? e1 : e0, sq = qb0 ? e0 : e1;
+      float z = fmaxf(kq + dpp<QP_X1>(sq) + pb0, 0.f);
+      if (drop) {
+        const uint32_t hsh = mix_hash(a.seed, gstep, (uint32_t)((0 * 64 + r0) * 65536 + u));
+        z = (u01(hsh) < p_drop) ? 0.f : z * scale;
+      }
+      h1 = z;
+      h1w[l] = z;  // [k = l / 4][row = l % 4]
+    }
+    // keep bits of the layer-1 outputs: wave w hashes (row w / 2, unit 64 (w % 2) + l)
+    if (drop) {
+      const int rr = w >> 1, oo = 64 * (w & 1) + l;
+      const uint32_t hsh = mix_hash(a.seed, gstep, (uint32_t)((1 * 64 + rr) * 65536 + oo));
+      const unsigned long long bal = __ballot(u01(hsh) >= p_drop);
+      if (l == 0)
+        *reinterpret_cast<uint2*>(lds + MSK + (s & 1) * (NW * 2) + w * 2) =
+            make_uint2((uint32_t)bal, (uint32_t)(bal >> 32));
+    }
+    __builtin_amdgcn_wave_barrier();
+    B2STAMP(0)
+    // ---- F2: this wave's k-slice partials of all 128 outputs x 4 rows
+    {
+      float acc[2][4] = {};
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        if ((kk & 3) == 0) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted tile loads (VGPRs)
+        const float4 h = *reinterpret_cast<const float4*>(h1w + kk * 4);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[j][0] += w1[j][kk] * h.x; acc[j][1] += w1[j][kk] * h.y;
+          acc[j][2] += w1[j][kk] * h.z; acc[j][3] += w1[j][kk] * h.w;
+        }
+      }
+      float* part = lds + PART + (s & 1) * (H * PSTR);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        *reinterpret_cast<float4*>(part + (l + 64 * j) * PSTR + w * 4) =
+            make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+    }
+    // next batch into the next input buffer (its last readers finished before the previous barrier)
+    if (role) {
+      const uint32_t v = (have_next && pb < bs_next) ? raw_next : 0u;
+      uint32_t* dst = (role == 1) ? reinterpret_cast<uint32_t*>(lds + XT + xbn * DMAX * 4) + pk * 4 + pb
+                                  : reinterpret_cast<uint32_t*>(lds + LAB) + xbn * 4 + pb;
+      *dst = v;
+    }
+    ridx_next = role ? ridx_next2 : 0;
+    B2STAMP(1)
+    lds_barrier();  // the step's only workgroup barrier
+    B2STAMP(2)
+
+    // ---- F2r: h2 for this lane's outputs o = l, l + 64 (sum of the 8 wave partials)
+    float h2[2][4];
+    {
+      const float* part = lds + PART + (s & 1) * (H * PSTR);
+      uint32_t kw[2][4] = {};  // keep ballot word holding this lane's bit, per (j, row)
+      if (drop) {
+        const uint4* mk = reinterpret_cast<const uint4*>(lds + MSK + (s & 1) * (NW * 2));
+        const uint4 q0 = mk[0], q1 = mk[1], q2 = mk[2], q3 = mk[3];  // waves (0,1) (2,3) (4,5) (6,7)
+        const bool hi = l >= 32;
+        kw[0][0] = hi ? q0.y : q0.x; kw[1][0] = hi ? q0.w : q0.z;
+        kw[0][1] = hi ? q1.y : q1.x; kw[1][1] = hi ? q1.w : q1.z;
+        kw[0][2] = hi ? q2.y : q2.x; kw[1][2] = hi ? q2.w : q2.z;
+        kw[0][3] = hi ? q3.y : q3.x; kw[1][3] = hi ? q3.w : q3.z;
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        __builtin_amdgcn_sched_barrier(0);
+        const float* pr = part + (l + 64 * j) * PSTR;
+        float4 sum = *reinterpret_cast<const float4*>(pr);
+#pragma unroll
+        for (int ww = 1; ww < NW; ++ww) {
+          const float4 t = *reinterpret_cast<const float4*>(pr + ww * 4);
+          sum.x += t.x; sum.y += t.y; sum.z += t.z; sum.w += t.w;
+        }
+        const float zz[4] = {sum.x, sum.y, sum.z, sum.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float z = fmaxf(zz[r] + pb1[j], 0.f);
+          if (drop) z = ((kw[j][r] >> (l & 31)) & 1u) ? z * scale : 0.f;
+          h2[j][r] = z;
+        }
+      }
+    }
+    B2STAMP(3)
+    // ---- logits (reduce-scatter: DPP row r holds row r's C logits), loss, dlogits
+    float dz3[4][CM];
+    float bl;
+    {
+      float P[4 * CM];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < CM; ++c) P[r * CM + c] = pw2[c][0] * h2[0][r] + pw2[c][1] * h2[1][r];
+      const float zown = rs_small<4 * CM>(P, l);
+      const int rr = l >> 4;
+      float z[CM];
+      if constexpr (CM == 2) {
+        const int co = (l >> 3) & 1;
+        const float zx = dpp<ROR8>(zown);
+        z[0] = co ? zx : zown;
+        z[1] = co ? zown : zx;
+      } else {
+        const int co = (l >> 2) & 3;
+        float v[4];
+        v[0] = zown;
+        v[1] = dpp<HMIRROR>(zown);  // quad (l/4) ^ 1 -> class co ^ 1
+        v[2] = dpp<ROR8>(zown);     // class co ^ 2
+        v[3] = dpp<ROR8>(v[1]);     // class co ^ 3
+#pragma unroll
+        for (int c = 0; c < CM; ++c) z[c] = sel4(v, c ^ co);
+      }
+      float z4[4] = {0.f, 0.f, 0.f, 0.f}, dz[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < CM; ++c) z4[c] = z[c] + pb2[c];
+      const int lab = (rr & 2) ? ((rr & 1) ? labs.w : labs.z) : ((rr & 1) ? labs.y : labs.x);
+      const bool live = rr < bs;
+      const float inv = live ? 1.0f / (float)(bs > 0 ? bs : 1) : 0.f;
+      const LossAcc lr_ = row_loss4(z4, C, lab, a.loss_kind, inv, dz);
+      const float lv = live ? lr_.loss : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < CM; ++c) dz3[r][c] = (c < C) ? rl(dz[c], 16 * r) : 0.f;
+      const float ltot = rl(lv, 0) + rl(lv, 16) + rl(lv, 32) + rl(lv, 48);
+      bl = bs > 0 ? ltot / (float)bs : 0.f;
+      if (tid == 0) {
+        if (a.loss_out && !a.cursor) a.loss_out[s] = bl;
+        if (!ADAM) a.grad_out[sh.P] = bl;
+      }
+    }
+    B2STAMP(4)
+
+    const int t = t0 + s + 1;
+    const float step_size = a.lr / (1.f - pow_t(l2b1, (float)t));
+    const float rbc2 = __builtin_amdgcn_rsqf(1.f - pow_t(l2b2, (float)t));
+    // ---- dZ2 (old W2), then W2 / b2 / b1 gradients + Adam (replicated per wave)
+    float dz2[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float g = 0.f;
+#pragma unroll
+        for (int c = 0; c < CM; ++c) g += pw2[c][j] * dz3[r][c];
+        dz2[j][r] = h2[j][r] > 0.f ? g * scale : 0.f;
+      }
+#pragma unroll
+    for (int c = 0; c < CM; ++c) {
+      if (c < C) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float gw = dz3[0][c] * h2[j][0] + dz3[1][c] * h2[j][1] + dz3[2][c] * h2[j][2] + dz3[3][c] * h2[j][3];
+          if (ADAM) adam_elem(pw2[c][j], gw, mw2[c][j], vw2[c][j], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+          else if (w == 0) a.grad_out[wo2 + c * H + l + 64 * j] = gw;
+        }
+        const float gb = dz3[0][c] + dz3[1][c] + dz3[2][c] + dz3[3][c];
+        if (ADAM) adam_elem(pb2[c], gb, mb2[c], vb2[c], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+        else if (tid == 0) a.grad_out[bo2 + c] = gb;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float gb = dz2[j][0] + dz2[j][1] + dz2[j][2] + dz2[j][3];
+      if (ADAM) adam_elem(pb1[j], gb, mb1[j], vb1[j], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+      else if (w == 0) a.grad_out[bo1 + l + 64 * j] = gb;
+    }
+    B2STAMP(5)
+    // ---- dZ1 = W1^T dZ2 over this wave's k-slice: one 16-value reduce-scatter per batch row
+    // (pass p = row p leaves unit k's sum in lanes 4k..4k+3), lane l keeps pass l & 3 - exactly
+    // the (unit, row) whose h1 (and ReLU/dropout mask) it computed in F1
+    float dz1 = 0.f;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      float P[16];
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) P[kk] = w1[0][kk] * dz2[0][p] + w1[1][kk] * dz2[1][p];
+      const float tot = rs_small<16>(P, l);
+      if (r0 == p) dz1 = tot;
+    }
+    dz1 = h1 > 0.f ? dz1 * scale : 0.f;
+    B2STAMP(6)
+    // ---- dW0 / db0: the quad holds unit u's four rows
+    {
+      float dq[4];
+      dq[0] = dpp<0x00>(dz1); dq[1] = dpp<0x55>(dz1); dq[2] = dpp<0xAA>(dz1); dq[3] = dpp<0xFF>(dz1);
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        const int d = r0 + 4 * i;
+        const float4 x = *reinterpret_cast<const float4*>(xT + d * 4);
+        const float gw = dq[0] * x.x + dq[1] * x.y + dq[2] * x.z + dq[3] * x.w;
+        if (ADAM) adam_elem(w0[i], gw, m0[i], v0[i], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);  // d >= D0: stays 0
+        else if (d < D0) a.grad_out[wo0 + u * D0 + d] = gw;
+      }
+      const float gb = dq[0] + dq[1] + dq[2] + dq[3];
+      if (ADAM) adam_elem(pb0, gb, mb0, vb0, a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+      else if (r0 == 0) a.grad_out[bo0 + u] = gb;
+    }
+    B2STAMP(7)
+    // ---- dW1 + Adam in registers
+    int gb1 = wo1 + l * H + KS * w;  // grad mode: opaque per step, so 32 store addresses are not hoisted
+    if (!ADAM) asm volatile("" : "+v"(gb1));
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      if ((kk & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+      const float4 h = *reinterpret_cast<const float4*>(h1w + kk * 4);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float gw = dz2[j][0] * h.x + dz2[j][1] * h.y + dz2[j][2] * h.z + dz2[j][3] * h.w;
+        if (ADAM) adam_elem(w1[j][kk], gw, m1[j][kk], v1[j][kk], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+        else a.grad_out[gb1 + 64 * j * H + kk] = gw;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the next step rewrites this wave's h1 tile
+    B2STAMP(8)
+    xb = xbn;
+  }
+  if (a.cursor && tid == 0) __hip_atomic_store(a.cursor, cur0 + a.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.step_counter && tid == 0)
+    __hip_atomic_store(a.step_counter, t0 + a.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if constexpr (PROF) {
+    if (l == 0) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) atomicAdd(a.prof + w * 16 + i, pacc[i]);
+    }
+  }
+  if (!ADAM) return;
+
+  // ---- write back parameters and moments (flat torch order).  The base offset is made opaque so
+  // the compiler recomputes these addresses here instead of keeping the prologue's load addresses
+  // (3 x 32 pointers) live across the step loop - that alone cost ~90 spilled VGPRs.
+  int lo = l, uo = u;
+  asm volatile("" : "+v"(lo), "+v"(uo));
+  const int fb1 = wo1 + lo * H + KS * w;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int f = fb1 + 64 * j * H + kk;
+      a.p[f] = w1[j][kk];
+      a.m[f] = m1[j][kk];
+      a.v[f] = v1[j][kk];
+    }
+#pragma unroll
+  for (int i = 0; i < ND; ++i) {
+    const int d = r0 + 4 * i;
+    if (d < D0) {
+      const int f = wo0 + uo * D0 + d;
+      a.p[f] = w0[i];
+      a.m[f] = m0[i];
+      a.v[f] = v0[i];
+    }
+  }
+  if (r0 == 0) { a.p[bo0 + uo] = pb0; a.m[bo0 + uo] = mb0; a.v[bo0 + uo] = vb0; }
+  if (w == 0) {  // every wave holds the same W2 / b1 / b2
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int o = lo + 64 * j;
+      a.p[bo1 + o] = pb1[j]; a.m[bo1 + o] = mb1[j]; a.v[bo1 + o] = vb1[j];
+#pragma unroll
+      for (int c = 0; c < CM; ++c)
+        if (c < C) { const int f = wo2 + c * H + o; a.p[f] = pw2[c][j]; a.m[f] = mw2[c][j]; a.v[f] = vw2[c][j]; }
+    }
+    if (l < C) {
+#pragma unroll
+      for (int c = 0; c < CM; ++c)
+        if (c == l) { a.p[bo2 + c] = pb2[c]; a.m[bo2 + c] = mb2[c]; a.v[bo2 + c] = vb2[c]; }
+    }
+  }
+}
+#undef B2STAMP
+
+bool mlp_block2_ok(const MlpShape& sh, const MlpArgs& a) {
+  const char* env = getenv("DCT_MLP_BLOCK");  // "0": generic LDS kernel, "v1": mlp_block.hip (A/B, tests)
+  if (env && (env[0] == '0' || (env[0] == 'v' && env[1] == '1'))) return false;
+  // a profiling launch is served for the weather shape (D0 <= 8, C <= 2, train mode) only
+  const bool prof_ok = a.prof == nullptr || (sh.dims[0] <= 8 && sh.dims[3] <= 2 && a.mode == 0);
+  return prof_ok && sh.L == 3 && sh.dims[1] == blk2::H && sh.dims[2] == blk2::H && sh.dims[0] >= 1 &&
+         sh.dims[0] <= blk2::DMAX && sh.dims[3] >= 1 && sh.dims[3] <= 4 && a.B >= 1 && a.B <= blk2::B &&
+         a.pending == nullptr && a.stage == nullptr && a.xg_world <= 1 && (a.mode == 0 || a.mode == 1);
+}
+
+hipError_t mlp_launch_block2(const MlpShape& sh, const MlpArgs& a, hipStream_t st) {
+  const int d0 = sh.dims[0], C = sh.dims[3];
+  const bool tr = a.mode == 0;
+  const size_t bytes = (size_t)blk2::TOTAL * sizeof(float);
+#define B2K(ND, CM)                                                                                     \
+  do {                                                                                                  \
+    if (tr) hipLaunchKernelGGL((mlp_block2_kernel<ND, CM, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a); \
+    else hipLaunchKernelGGL((mlp_block2_kernel<ND, CM, false>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);  \
+  } while (0)
+  if (a.prof) {
+    hipLaunchKernelGGL((mlp_block2_kernel<2, 2, true, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);
+  } else if (d0 <= 8) {
+    if (C <= 2) B2K(2, 2); else B2K(2, 4);
+  } else {
+    if (C <= 2) B2K(8, 2); else B2K(8, 4);
+  }
+#undef B2K
+  return hipGetLastError();
+}
+
+}  // namespace dct

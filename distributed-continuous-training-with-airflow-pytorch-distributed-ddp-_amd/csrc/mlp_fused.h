@@ -113,6 +113,9 @@ hipError_t mlp_launch_train_L4(const MlpShape& sh, const MlpArgs& a, hipStream_t
 // register-resident multi-wave kernel for D0 -> 128 -> 128 -> C (mlp_block.hip)
 bool mlp_block_ok(const MlpShape& sh, const MlpArgs& a);
 hipError_t mlp_launch_block(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
+// one-barrier successor of mlp_block (mlp_block2.hip); DCT_MLP_BLOCK=v1 selects the old one
+bool mlp_block2_ok(const MlpShape& sh, const MlpArgs& a);
+hipError_t mlp_launch_block2(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
 hipError_t mlp_launch_eval_L2(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
 hipError_t mlp_launch_eval_L3(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
 hipError_t mlp_launch_eval_L4(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);

@@ -132,6 +132,8 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
 BucketReducer::~BucketReducer() {
   for (auto& e : ready_events_) hipEventDestroy(e);
   if (done_event_) hipEventDestroy(done_event_);
+  if (tail_event_) hipEventDestroy(tail_event_);
+  if (stamps_) hipFree(stamps_);
   if (comm_stream_) hipStreamDestroy(comm_stream_);
 }
 
@@ -142,10 +144,43 @@ void BucketReducer::prepare() {
   n_launched_ = 0;
 }
 
+void BucketReducer::enable_timing(bool check) {
+  if (!stamps_) {
+    hip_check(hipMalloc(&stamps_, 8 * sizeof(unsigned long long)), "hipMalloc stamps");
+    hip_check(hipMemset(stamps_, 0, 8 * sizeof(unsigned long long)), "hipMemset stamps");
+    hip_check(hipEventCreateWithFlags(&tail_event_, hipEventDisableTiming), "hipEventCreate");
+  }
+  timing_ = true;
+  check_ = check;
+}
+
+std::vector<double> BucketReducer::read_timing() const {
+  std::vector<double> out(4, 0.0);
+  if (!stamps_) return out;
+  unsigned long long h[8];
+  hip_check(hipMemcpy(h, stamps_, sizeof(h), hipMemcpyDeviceToHost), "read reducer stamps");
+  out[0] = (double)h[2] / 1e5;  // s_memrealtime ticks at 100 MHz -> ms
+  out[1] = (double)h[3] / 1e5;
+  out[2] = (double)h[7];
+  out[3] = (double)h[6];
+  return out;
+}
+
+void BucketReducer::reset_timing() {
+  if (!stamps_) return;
+  hip_check(hipDeviceSynchronize(), "reset_timing sync");
+  unsigned long long h[8];
+  hip_check(hipMemcpy(h, stamps_, sizeof(h), hipMemcpyDeviceToHost), "read reducer stamps");
+  h[2] = h[3] = h[6] = h[7] = 0;  // keep the close / check counters in step with each other
+  hip_check(hipMemcpy(stamps_, h, sizeof(h), hipMemcpyHostToDevice), "reset reducer stamps");
+}
+
 void BucketReducer::launch_bucket(int b, uintptr_t compute_stream) {
   hipStream_t cs = reinterpret_cast<hipStream_t>(compute_stream);
   hip_check(hipEventRecord(ready_events_[b], cs), "hipEventRecord");
   hip_check(hipStreamWaitEvent(comm_stream_, ready_events_[b], 0), "hipStreamWaitEvent");
+  if (timing_ && b == 0)
+    hip_check((hipError_t)dct_reducer_stamp(stamps_, reinterpret_cast<void*>(comm_stream_)), "reducer stamp");
   if (comm_) {
     comm_->allreduce(flat_ + (uintptr_t)(offsets_[b] * dsize_), counts_[b], dtype_, op_,
                      reinterpret_cast<uintptr_t>(comm_stream_));
@@ -172,6 +207,13 @@ int BucketReducer::mark_ready(int param_idx, uintptr_t compute_stream) {
 }
 
 void BucketReducer::finalize(uintptr_t compute_stream) {
+  hipStream_t cs = reinterpret_cast<hipStream_t>(compute_stream);
+  n_before_finalize_ = n_launched_;
+  if (timing_) {  // end of backward on the compute stream, ordered before the comm stream's close
+    hip_check((hipError_t)dct_reducer_stamp(stamps_ + 1, reinterpret_cast<void*>(cs)), "reducer stamp");
+    hip_check(hipEventRecord(tail_event_, cs), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(comm_stream_, tail_event_, 0), "hipStreamWaitEvent");
+  }
   // buckets whose params did not all receive a gradient (unused params): reduce anyway so
   // the collective sequence matches across ranks (find_unused_parameters=False semantics
   // would error; we zero-fill instead, which is what DDP's static graph does).
@@ -179,8 +221,10 @@ void BucketReducer::finalize(uintptr_t compute_stream) {
     launch_bucket(next_to_launch_, compute_stream);
     next_to_launch_++;
   }
+  if (timing_) hip_check((hipError_t)dct_reducer_close(stamps_, reinterpret_cast<void*>(comm_stream_)), "reducer close");
   hip_check(hipEventRecord(done_event_, comm_stream_), "hipEventRecord");
-  hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(compute_stream), done_event_, 0), "hipStreamWaitEvent");
+  hip_check(hipStreamWaitEvent(cs, done_event_, 0), "hipStreamWaitEvent");
+  if (timing_ && check_) hip_check((hipError_t)dct_reducer_check(stamps_, reinterpret_cast<void*>(cs)), "reducer check");
 }
 
 // ---------------------------------------------------------------------------- StreamGraph

@@ -40,7 +40,16 @@ class BucketReducer {
   void finalize(uintptr_t compute_stream);
   int num_buckets() const { return (int)offsets_.size(); }
   int launched() const { return n_launched_; }
+  // buckets the mark_ready hooks launched before finalize() in the last step: > 0 means the
+  // all-reduce really overlapped (part of) the backward
+  int launched_before_finalize() const { return n_before_finalize_; }
   uintptr_t comm_stream() const { return reinterpret_cast<uintptr_t>(comm_stream_); }
+  // device-side instrumentation (also inside captured graphs): span / exposed all-reduce time per
+  // step; with `check` a compute-stream kernel after the join verifies the stream ordering
+  void enable_timing(bool check);
+  // {span_ms, exposed_ms, steps, ordering_violations} accumulated since the last reset
+  std::vector<double> read_timing() const;
+  void reset_timing();
 
  private:
   void launch_bucket(int b, uintptr_t compute_stream);
@@ -50,10 +59,13 @@ class BucketReducer {
   std::vector<int> param_bucket_, expected_, pending_, launched_;
   int dtype_, op_;
   size_t dsize_ = 4;
-  int next_to_launch_ = 0, n_launched_ = 0;
+  int next_to_launch_ = 0, n_launched_ = 0, n_before_finalize_ = 0;
   hipStream_t comm_stream_ = nullptr;
   std::vector<hipEvent_t> ready_events_;
   hipEvent_t done_event_ = nullptr;
+  hipEvent_t tail_event_ = nullptr;
+  unsigned long long* stamps_ = nullptr;  // [8], see step_kernels.hip reducer_close_kernel
+  bool timing_ = false, check_ = false;
 };
 
 // Receive buffers of the in-kernel (xGMI) gradient exchange.  Each rank allocates an

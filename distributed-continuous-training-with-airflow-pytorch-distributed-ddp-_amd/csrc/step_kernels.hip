@@ -104,7 +104,7 @@ __global__ void step_end_kernel(int* cursor, const float* slot, float* loss_out,
 // Device-side barrier over the xGMI peer mappings of the in-kernel exchange (runtime.cpp
 // PeerExchange::barrier).  Lane q < W (q != rank) writes this barrier's tag into slot `rank` of
 // peer q's barrier region (system-scope store across xGMI), then every lane polls slot q of its
-// own uncached region until peer q's tag arrived.  One wave, no host round trip and no RCCL
+// own uncached region until peer q's tag (or a later one) arrived.  One wave, no host round trip and no RCCL
 // launch: it replaces the RCCL barrier where the bench brackets the timed steps (a 4-byte
 // all-reduce + host wait) with one peer-write latency.  Bounded spin: a timeout writes
 // 0x80000000 | tag into the exchange status word (xg_verify then reports the exchange failed).
@@ -120,7 +120,10 @@ __global__ __launch_bounds__(64) void xg_barrier_kernel(char* recv, char* const*
   bool ok = q >= W || q == rank;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (!__all(ok)) {
-    if (!ok) ok = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == tag;
+    // any tag at or past this barrier's: tags only grow (reset() zeroes the region), and a fast
+    // peer may already have left this barrier and written the NEXT one's tag into our slot
+    // before we polled - an exact compare would then spin to the timeout (wrap-safe compare)
+    if (!ok) ok = (int)(__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - tag) >= 0;
     if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > timeout_ticks) {
       if (q == 0) __hip_atomic_store(status, 0x80000000u | tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
@@ -129,9 +132,68 @@ __global__ __launch_bounds__(64) void xg_barrier_kernel(char* recv, char* const*
   }
 }
 
+// Reducer instrumentation (runtime.cpp BucketReducer, enable_timing): one-thread kernels, so the
+// stamps ride inside captured step graphs too (an event timing pair does not survive capture).
+// s[0] first bucket's all-reduce start (comm stream), s[1] end of backward (compute stream),
+// s[2] / s[3] accumulated span / exposed ticks of s_memrealtime (100 MHz), s[4] comm-stream
+// closes, s[5] compute-stream checks, s[6] ordering violations, s[7] steps.
+__global__ void reducer_stamp_kernel(unsigned long long* dst) {
+  if (threadIdx.x == 0) *dst = __builtin_amdgcn_s_memrealtime();
+}
+__global__ void reducer_close_kernel(unsigned long long* s) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long t0 = s[0], tb = s[1];
+    s[2] += t > t0 ? t - t0 : 0ull;   // all-reduce span: first bucket start -> last bucket done
+    s[3] += t > tb ? t - tb : 0ull;   // exposed: backward end -> last bucket done
+    __hip_atomic_store(&s[4], s[4] + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s[7] += 1ull;
+  }
+}
+// debug mode: runs on the compute stream right after it joined the comm stream - if that wait
+// were missing the comm stream's close for this step might not have run yet
+__global__ void reducer_check_kernel(unsigned long long* s) {
+  if (threadIdx.x == 0) {
+    const unsigned long long c = s[5] + 1ull;
+    s[5] = c;
+    if (__hip_atomic_load(&s[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != c) s[6] = 1ull;
+  }
+}
+
+// Step-phase timing (utils/tracing.py DevicePhaseTimer): b[0..n) stamps of the phase marks of
+// the current step (reducer_stamp_kernel writes them), b[n..2n-1) accumulated ticks per phase,
+// b[2n-1] step count.  One thread; captured into step graphs like any kernel.
+__global__ void phase_accum_kernel(unsigned long long* b, int n) {
+  if (threadIdx.x == 0) {
+    for (int i = 0; i + 1 < n; ++i) {
+      const unsigned long long a = b[i], c = b[i + 1];
+      b[n + i] += c > a ? c - a : 0ull;
+    }
+    b[2 * n - 1] += 1ull;
+  }
+}
+
 }  // namespace dct
 
 extern "C" {
+
+int dct_phase_accum(unsigned long long* b, int n, void* stream) {
+  hipLaunchKernelGGL(dct::phase_accum_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), b, n);
+  return (int)hipGetLastError();
+}
+
+int dct_reducer_stamp(unsigned long long* dst, void* stream) {
+  hipLaunchKernelGGL(dct::reducer_stamp_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), dst);
+  return (int)hipGetLastError();
+}
+int dct_reducer_close(unsigned long long* s, void* stream) {
+  hipLaunchKernelGGL(dct::reducer_close_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), s);
+  return (int)hipGetLastError();
+}
+int dct_reducer_check(unsigned long long* s, void* stream) {
+  hipLaunchKernelGGL(dct::reducer_check_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), s);
+  return (int)hipGetLastError();
+}
 
 int dct_gather_batch_step(const void* X, int row_bytes, const int* Y, const int* idx, const int* cursor, int stride,
                           int B, int n_items, void* xdst, int* ydst, int* step_counter, float* zero,

@@ -40,6 +40,10 @@ class _Block(nn.Module):
 
 
 class TabTransformer(TrainModule):
+    # its fused blocks may defer their weight-gradient GEMMs to one grouped launch after backward
+    # (ops/nn.py tt_block): a bucket reducer must then launch at finalize, not from the hooks
+    uses_fused_blocks = True
+
     def __init__(self, num_features: int = 64, d_model: int = 64, heads: int = 4, layers: int = 4, ffn_mult: int = 4,
                  num_classes: int = 2, lr: float = 1e-3):
         super().__init__()

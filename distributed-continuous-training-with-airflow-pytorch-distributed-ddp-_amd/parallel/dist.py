@@ -158,9 +158,10 @@ def init_distributed(accelerator: str = "auto", backend: str = "auto", timeout_s
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", e["master_addr"])
             os.environ.setdefault("MASTER_PORT", str(e["master_port"]))
-            # no explicit init_method: torch then takes its env:// path AND, under torchrun, the
-            # agent's store with a per-attempt key prefix - an explicit "env://" skips that prefix, so
-            # workers restarted by --max-restarts read the dead attempt's gloo addresses and fail
+            # env:// rendezvous (torch 2.10 maps init_method=None to "env://"; under torchrun that
+            # handler uses the agent's store with its per-attempt key prefix either way).  Elastic
+            # restarts recover because a restarted attempt skips the injected fault and resumes from
+            # last.ckpt (trainer fault_inject, ckpt.resume_checkpoint) - tests/test_ddp_cpu.py
             kwargs = dict(backend=backend, world_size=e["world_size"], rank=e["rank"],
                           timeout=datetime.timedelta(seconds=timeout_s))
             if backend == "nccl":

@@ -124,7 +124,16 @@ class TorchBucketReducer:
 
 
 class NativeBucketReducer:
-    def __init__(self, comm, flat_grad: torch.Tensor, plan: BucketPlan):
+    """The C++ ``BucketReducer`` (RCCL on a comm stream).  ``timing=True`` adds device-side stamps
+    (one-thread kernels, so they survive HIP graph capture): per step the all-reduce SPAN (first
+    bucket's start -> last bucket done, on the comm stream) and the EXPOSED part (end of backward
+    on the compute stream -> last bucket done), read as ``allreduce_ms()``; ``check=True``
+    (``DCT_DEBUG=1``) also verifies on the device that the compute stream joined the comm stream
+    before the optimizer (``ordering_violations``).  ``defer_launch``: mark_ready only counts and
+    every bucket launches at ``finalize`` - for backward passes whose weight gradients are issued
+    after the hooks fire (the TabTransformer's grouped deferred dW GEMMs)."""
+
+    def __init__(self, comm, flat_grad: torch.Tensor, plan: BucketPlan, timing: bool = False, check: bool = False):
         from ..ops._native import native
 
         nat = native()
@@ -134,18 +143,62 @@ class NativeBucketReducer:
         self.plan = plan
         self._r = nat.BucketReducer(comm, flat_grad.data_ptr(), list(plan.offsets), list(plan.counts),
                                     list(plan.param_bucket), nat.DT_F32, nat.OP_AVG)
+        self.timing = bool(timing or check)
+        if self.timing:
+            self._r.enable_timing(bool(check))
+        self.defer_launch = False
+        self._deferred: List[int] = []
+        self.hook_launches = 0  # buckets launched from backward hooks (before finalize), cumulative
 
     def prepare(self):
+        self._deferred = []
         self._r.prepare()
 
     def mark_ready(self, param_idx: int, stream=None) -> int:
+        if self.defer_launch:
+            self._deferred.append(param_idx)
+            return 0
         s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
-        return self._r.mark_ready(param_idx, s)
+        n = self._r.mark_ready(param_idx, s)
+        self.hook_launches += n
+        return n
 
     def finalize(self, stream=None):
         s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        for i in self._deferred:  # every gradient producer is enqueued by now (grouped dW included)
+            self._r.mark_ready(i, s)
+        self._deferred = []
         self._r.finalize(s)
+
+    @property
+    def launched(self) -> int:
+        return self._r.launched
+
+    @property
+    def launched_before_finalize(self) -> int:
+        return self._r.launched_before_finalize
 
     @property
     def num_buckets(self):
         return self._r.num_buckets
+
+    def allreduce_ms(self, reset: bool = True):
+        """(span_ms, exposed_ms, steps, ordering_violations) accumulated on the device since the
+        last reset (synchronising read); None without timing."""
+        if not self.timing:
+            return None
+        span, exposed, steps, bad = self._r.read_timing()
+        if reset:
+            self._r.reset_timing()
+        return span, exposed, int(steps), int(bad)
+
+    # the Trainer's allreduce_ms contract (seconds of exposed all-reduce wait, reset by assigning 0)
+    @property
+    def wait_s(self) -> float:
+        t = self.allreduce_ms(reset=False)
+        return 0.0 if t is None else t[1] / 1e3
+
+    @wait_s.setter
+    def wait_s(self, value: float):
+        if value == 0.0 and self.timing:
+            self._r.reset_timing()

@@ -41,12 +41,50 @@ def timeout_s() -> float:
     return float(os.environ.get("DCT_XG_TIMEOUT_S", "20"))
 
 
+def peer_report(ctx: DistContext):
+    """Collective: which physical GPU every rank drives and whether they can map each other.
+
+    Returns ``(bus_ids, matrix, ok)``: the PCI bus id of each rank's device (rank order), the
+    ``hipDeviceCanAccessPeer`` matrix over the devices visible to this process, and whether every
+    pair of distinct rank devices that this process can see is peer-accessible (ranks sharing one
+    GPU - a rehearsal - are trivially fine).  A peer outside this process's visible set cannot be
+    checked here; the exchange's first-launch verification (``check``) still covers it."""
+    from ..ops._native import native
+
+    nat, mine = None, ""
+    try:
+        nat = native()
+        mine = nat.pci_bus_id(ctx.device.index or 0) if ctx.device.type == "cuda" else ""
+    except Exception:  # noqa: BLE001 - still take part in the collective below
+        nat = None
+    bus = ctx.all_gather_object(mine) if ctx.is_distributed else [mine]
+    if ctx.device.type != "cuda" or nat is None or not mine:
+        return bus, [], False
+    mat = nat.peer_matrix()
+    local = {nat.pci_bus_id(i).lower(): i for i in range(len(mat))}
+    me = local.get(mine.lower(), ctx.device.index or 0)
+    ok = True
+    for b in bus:
+        j = local.get(b.lower())
+        if j is not None and j != me and not mat[me][j]:
+            ok = False
+    return bus, mat, ok
+
+
 def setup_peer_exchange(kernel, ctx: DistContext, batch: int):
-    """Collective: returns a native PeerExchange on every rank, or None on every rank."""
+    """Collective: returns a native PeerExchange on every rank, or None on every rank.
+
+    Before any buffer is exported every rank checks ``hipDeviceCanAccessPeer`` towards every
+    other rank's device (:func:`peer_report`); one failing pair sends all ranks to RCCL."""
     m = mode()
     W = ctx.world_size
     single_node = ctx.local_world_size == W
-    eligible = (m != "rccl" and ctx.device.type == "cuda" and 2 <= W <= 8 and single_node
+    peers_ok = True
+    if m != "rccl" and ctx.device.type == "cuda" and 2 <= W <= 8 and single_node:
+        peers_ok = peer_report(ctx)[2]
+        if not peers_ok and ctx.rank == 0:
+            print("[dct] some rank pair is not peer-accessible (hipDeviceCanAccessPeer)", flush=True)
+    eligible = (m != "rccl" and ctx.device.type == "cuda" and 2 <= W <= 8 and single_node and peers_ok
                 and kernel.xg_supported(batch))
     # every rank must take the same decision before any collective below diverges
     if not ctx.all_reduce_bool_and(eligible):

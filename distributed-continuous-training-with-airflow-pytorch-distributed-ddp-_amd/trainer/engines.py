@@ -35,6 +35,7 @@ from ..ops.optim import FlatAdam, adam_flat_
 from ..parallel.dist import DistContext, init_native_comm
 from ..parallel.reducer import NativeBucketReducer, TorchBucketReducer, plan_buckets
 from ..utils.debug import assert_reducer_complete, check_device
+from ..utils.debug import enabled as debug_enabled
 
 
 def adam_hparams_from(optimizer) -> Optional[Dict]:
@@ -467,10 +468,24 @@ class AutogradEngine(_EngineBase):
             ctx.broadcast_(self.flat_p, 0) if ctx.backend != "nccl" else self._bcast_nccl()
         self.plan = plan_buckets(numels, 4, bucket_cap_bytes, first_bucket_bytes)
         self.reducer = None
-        if ctx.is_distributed:
-            if dev.type == "cuda" and ctx.backend == "nccl":
-                comm = init_native_comm(ctx)
-                self.reducer = NativeBucketReducer(comm, self.flat_g, self.plan)
+        # DCT_FORCE_DDP=1 at world size 1 on a GPU: the full DDP path (RCCL communicator of one
+        # rank, bucket reducer on its comm stream, hooks, graph capture) - how its correctness,
+        # overlap and cost are tested and measured on one GPU
+        forced = (not ctx.is_distributed and dev.type == "cuda" and os.environ.get("DCT_FORCE_DDP", "0") == "1")
+        if ctx.is_distributed or forced:
+            if dev.type == "cuda" and (forced or ctx.backend == "nccl"):
+                if forced:
+                    from ..ops._native import native
+
+                    nat = native()
+                    self._own_comm = comm = nat.Comm(nat.comm_unique_id(), 1, 0, dev.index or 0)
+                else:
+                    comm = init_native_comm(ctx)
+                # device-side all-reduce timing (allreduce_ms) unless DCT_REDUCER_TIMING=0 (bench.py);
+                # DCT_DEBUG=1 adds the stream-ordering check
+                timing = os.environ.get("DCT_REDUCER_TIMING", "1") != "0"
+                self.reducer = NativeBucketReducer(comm, self.flat_g, self.plan, timing=timing,
+                                                   check=debug_enabled())
             else:
                 # gloo: the CPU plumbing config, or GPU ranks sharing one device (init_distributed
                 # falls back to gloo there because RCCL refuses it) - buckets staged through host
@@ -483,6 +498,13 @@ class AutogradEngine(_EngineBase):
             for i, p in enumerate(params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
         self.graph_used = False
+        # per-step GPU phase timing (device timestamps, works inside captured graphs): the Trainer
+        # logs time/{fwd,bwd,allreduce,opt}_s per epoch
+        self.phase_timer = None
+        if dev.type == "cuda" and os.environ.get("DCT_PHASE_TIMING", "0") == "1":
+            from ..utils.tracing import DevicePhaseTimer
+
+            self.phase_timer = DevicePhaseTimer(["fwd", "bwd", "allreduce", "opt"], dev)
         opt = model.configure_optimizers()
         hp = adam_hparams_from(opt)
         if hp is not None:
@@ -541,23 +563,36 @@ class AutogradEngine(_EngineBase):
         loss.backward(one)
         join_side_work()  # weight-gradient GEMMs issued on the side stream (ops/nn.py side_dw)
 
+    def _pm(self, i: int):
+        """Phase mark i of the step (DCT_PHASE_TIMING=1): 0 start, 1 forward done, 2 backward done,
+        3 all-reduce joined, 4 optimizer done."""
+        if self.phase_timer is not None:
+            self.phase_timer.mark(i)
+            if i == 4:
+                self.phase_timer.close()
+
     def _step_body(self, x, y, batch_idx: int):
         self._zero_grads()
         if self.reducer is not None:
             self.reducer.prepare()
+        self._pm(0)
         self.model.train()
         with self._bound():
             loss = self.model.training_step((x, y), batch_idx)
             if isinstance(loss, dict):
                 loss = loss["loss"]
+            self._pm(1)
             self._backward(loss)
+        self._pm(2)
         if self.reducer is not None:
             self.reducer.finalize()
             assert_reducer_complete(self.reducer)
+        self._pm(3)
         if self.optimizer is not None:
             self.optimizer.step()
         else:
             self.torch_optimizer.step()
+        self._pm(4)
         return loss
 
     def train_step(self, rows: torch.Tensor, batch_idx: int):
@@ -714,15 +749,20 @@ class AutogradEngine(_EngineBase):
                 self._prologue(nat, rows_dev)
                 if self.reducer is not None:
                     self.reducer.prepare()
+                self._pm(0)
                 self.model.train()
                 with self._bound():
                     loss = self.model.training_step((self._x_dev, self._y_dev), first)
                     if isinstance(loss, dict):
                         loss = loss["loss"]
+                    self._pm(1)
                     self._backward(loss)
+                self._pm(2)
                 if self.reducer is not None:
                     self.reducer.finalize()
+                self._pm(3)
                 self.optimizer.step(bump_counter=False, epilogue=(self._dcursor, loss.detach(), loss_out))
+                self._pm(4)
         torch.cuda.current_stream().wait_stream(s)
         self._dgraph = g
         self._dloss = loss
@@ -749,11 +789,22 @@ class AutogradEngine(_EngineBase):
         # Off by default: the overlap slowed both kernels, TabTransformer step 0.420 -> 0.445 ms
         # (profiles/tt_head_spb_side_dw_ab_r2.log)
         side = self.reducer is None and os.environ.get("DCT_TT_DW_SIDE", "0") == "1"
-        # every transformer block's dW GEMMs as ONE grouped launch after backward (same no-reducer
-        # condition; DCT_TT_DW_DEFER=0 keeps one launch per block): TabTransformer step 0.421-0.426
-        # -> 0.407 ms (profiles/tt_dw_defer_ab_r2.log)
-        defer = self.reducer is None and os.environ.get("DCT_TT_DW_DEFER", "1") != "0"
+        # every transformer block's dW GEMMs as ONE grouped launch after backward (DCT_TT_DW_DEFER=0
+        # keeps one launch per block): TabTransformer step 0.421-0.426 -> 0.407 ms
+        # (profiles/tt_dw_defer_ab_r2.log).  With the native bucket reducer too: its hooks then only
+        # count and every bucket launches at finalize, after the grouped launch - the model's
+        # gradients fit ONE bucket (<= first_bucket_bytes), which could only start after the last
+        # dW GEMM anyway, so deferring loses no overlap and keeps the grouped-dW win at W > 1
+        defer_ok = self.reducer is None or isinstance(self.reducer, NativeBucketReducer)
+        defer = defer_ok and os.environ.get("DCT_TT_DW_DEFER", "1") != "0"
+        if isinstance(self.reducer, NativeBucketReducer):
+            self.reducer.defer_launch = defer and self._has_deferrable_ops()
         return bound_params(self.params, self._shadows, side_dw=side, defer_dw=defer)
+
+    def _has_deferrable_ops(self) -> bool:
+        """True when the model routes weight gradients through the deferred grouped dW path
+        (the fused transformer blocks); plain MLP/linear models keep hook-driven bucket launches."""
+        return bool(getattr(self.model, "uses_fused_blocks", False))
 
     def sync_to_model(self):
         pass  # parameters ARE views of the flat buffer

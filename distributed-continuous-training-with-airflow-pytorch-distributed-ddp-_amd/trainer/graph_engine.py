@@ -26,7 +26,8 @@ from ..data.sampler import distributed_indices
 from ..ops._native import native
 from ..ops.optim import FlatAdam
 from ..parallel.dist import DistContext, init_native_comm
-from ..parallel.reducer import plan_buckets
+from ..parallel.reducer import NativeBucketReducer, plan_buckets
+from ..utils.debug import enabled as debug_enabled
 
 ACT_IDS = {"relu": 1, "gelu": 2}
 LOSS_IDS = {"ce": 0, "mse": 1}
@@ -80,23 +81,29 @@ class GraphMLPEngine:
         nat = native()
         self.comm = None
         self.reducer = None
-        if ctx.is_distributed:
-            if ctx.backend != "nccl":
+        # DCT_FORCE_DDP=1 at world size 1: the DDP step (one-rank RCCL communicator, bucket reducer,
+        # per-layer bucket launches, two-pass split-K dW into g) on one GPU - tested and measured
+        # against the no-reducer step (split-K slices summed inside Adam)
+        forced = not ctx.is_distributed and os.environ.get("DCT_FORCE_DDP", "0") == "1"
+        if ctx.is_distributed or forced:
+            if ctx.is_distributed and ctx.backend != "nccl":
                 raise RuntimeError("graph engine needs the RCCL (nccl) backend for multi-rank runs")
-            self.comm = init_native_comm(ctx)
+            self.comm = init_native_comm(ctx) if ctx.is_distributed else nat.Comm(nat.comm_unique_id(), 1, 0,
+                                                                                   dev.index or 0)
             s = torch.cuda.current_stream().cuda_stream
             self.comm.broadcast(self.p.data_ptr(), self.P, nat.DT_F32, 0, s)  # DDP _sync_module_states
             self.p_bf16.copy_(self.p)
             plan = plan_buckets(self.numels + [1], bucket_cap_bytes=bucket_cap_bytes,
                                 first_bucket_bytes=first_bucket_bytes)
             self.bucket_plan = plan
-            self.reducer = nat.BucketReducer(self.comm, self.g.data_ptr(), list(plan.offsets), list(plan.counts),
-                                             list(plan.param_bucket), nat.DT_F32, nat.OP_AVG)
+            self.reducer = NativeBucketReducer(self.comm, self.g, plan,
+                                               timing=os.environ.get("DCT_REDUCER_TIMING", "1") != "0",
+                                               check=debug_enabled())
         self.exe = nat.MlpStepExecutor(self.dims, B, ACT_IDS["relu"], LOSS_IDS[self.loss], self.p.data_ptr(),
                                        self.p_bf16.data_ptr(), self.g.data_ptr(), self.m.data_ptr(),
                                        self.v.data_ptr(), [a.data_ptr() for a in self.acts], [],
                                        self.dz[0].data_ptr(), self.dz[1].data_ptr(), self.ybuf.data_ptr(),
-                                       self.stats.data_ptr(), self.reducer)
+                                       self.stats.data_ptr(), self.reducer._r if self.reducer is not None else None)
         a = adam
         self.exe.set_adam(a["lr"], a["betas"][0], a["betas"][1], a["eps"], a["weight_decay"], 0)
         self._graph = None

@@ -32,7 +32,8 @@ from ..data.sampler import distributed_indices
 from ..parallel.dist import DistContext, init_distributed, shutdown
 from .engines import AutogradEngine, FusedMLPEngine, adam_hparams_from
 from .graph_engine import GraphMLPEngine
-from ..utils.tracing import trace_range
+from ..utils.debug import assert_reducer_ordering
+from ..utils.tracing import PhaseTimer, trace_range
 
 
 def seed_everything(seed: int = 42) -> int:
@@ -93,6 +94,7 @@ class Trainer:
         self.logged_metrics: Dict[str, float] = {}
         self.progress_bar_metrics: Dict[str, float] = {}
         self.epoch_times: List[float] = []
+        self.phase_times = PhaseTimer(sync_device=False)  # host phases of an epoch -> time/<phase>_s
         self.engine = None
         self._stage = "idle"
         self._step_logs: Dict[str, Tuple[torch.Tensor, bool]] = {}
@@ -311,7 +313,7 @@ class Trainer:
                 with trace_range(f"epoch{epoch}/train"):
                     n_steps = self._train_epoch(epoch, B, tinfo.get("shuffle", True))
                 train_t = time.perf_counter() - t0
-                with trace_range(f"epoch{epoch}/validate"):
+                with self.phase_times.phase("validate"):
                     val_metrics = self._validate(VB) if len(val_rows) else {}
                 epoch_t = time.perf_counter() - t0
                 self.epoch_times.append(epoch_t)
@@ -322,14 +324,25 @@ class Trainer:
                 extra = {"epoch_time_s": epoch_t, "train_time_s": train_t,
                          "samples_per_sec": samples / max(train_t, 1e-9),
                          "step_time_ms": 1e3 * train_t / max(n_steps, 1)}
+                assert_reducer_ordering(getattr(self.engine, "reducer", None), f"epoch {epoch}")
                 ar_ms = self._epoch_allreduce_ms()
                 if ar_ms is not None:
                     extra["allreduce_ms"] = ar_ms
+                pt = getattr(self.engine, "phase_timer", None)
+                if pt is not None:  # GPU time of the step phases (DCT_PHASE_TIMING=1)
+                    ph = pt.read()
+                    extra.update({f"time/{k}_s": v for k, v in ph.items() if k != "steps"})
+                extra.update(self.phase_times.metrics())
+                self.phase_times = PhaseTimer(sync_device=False)
                 self._log_metrics(extra, self.global_step)
                 if self.logger is not None and self.is_global_zero:
                     self.logger.flush()  # the epoch's metrics reach the tracking store now
                 with trace_range(f"epoch{epoch}/checkpoint"):
+                    t_ck = time.perf_counter()
                     self._run_checkpoint_callbacks(n_steps)
+                    t_ck = time.perf_counter() - t_ck
+                if self.logger is not None and self.is_global_zero:
+                    self._log_metrics({"time/checkpoint_s": t_ck}, self.global_step)
                 if self.verbose and self.is_global_zero:
                     vm = " ".join(f"{k}={v:.4f}" for k, v in val_metrics.items())
                     print(f"[dct] epoch {epoch} steps={n_steps} {vm} epoch_time={epoch_t:.3f}s "

@@ -5,7 +5,12 @@
     asynchronous HIP fault is reported at the phase that caused it (the HIP_LAUNCH_BLOCKING idea
     without serialising every launch of the runtime);
   * stream-ordering assertions of the bucketed reducer: every bucket must have been launched
-    before the optimizer reads the gradients (``assert_reducer_complete``).
+    before the optimizer reads the gradients (``assert_reducer_complete``), and - on the native
+    RCCL reducer - a device-side check that the optimizer's stream really waited for the comm
+    stream's done event: a one-thread kernel on the compute stream, right after the join,
+    compares the comm stream's per-step close counter with its own step count and latches a
+    violation flag (csrc/step_kernels.hip reducer_check_kernel; it runs inside replayed HIP
+    graphs too), read by ``assert_reducer_ordering`` at the end of every epoch.
 Host-side C++ can additionally be built with ASan (``DCT_SANITIZE=1 python -m dct_amd._build``,
 host code only: ``-Xarch_host -fsanitize=address``).
 """
@@ -41,3 +46,14 @@ def assert_reducer_complete(reducer):
     n = reducer.num_buckets
     if launched is not None and launched != n:
         raise AssertionError(f"[dct debug] optimizer step with {launched}/{n} gradient buckets all-reduced")
+
+
+def assert_reducer_ordering(reducer, where: str = "epoch end"):
+    """Debug mode: raise if the device-side ordering check of the native reducer latched a
+    violation (the compute stream ran the optimizer before the comm stream finished)."""
+    if not enabled() or reducer is None or not hasattr(reducer, "allreduce_ms"):
+        return
+    t = reducer.allreduce_ms(reset=False)
+    if t is not None and t[3] > 0:
+        raise AssertionError(f"[dct debug] {where}: the optimizer stream did not wait for the gradient "
+                             f"all-reduce ({t[3]} ordering violation(s) over {t[2]} steps)")

@@ -3,8 +3,14 @@
 * ``trace_range(name)`` - a roctx range (rocprofiler-sdk's roctx) around a phase, so rocprofv3
   ``--marker-trace`` timelines show epoch / train / validate / checkpoint / all-reduce phases
   next to the kernels; a no-op when the library is missing or ``DCT_ROCTX=0``.
-* ``PhaseTimer`` - wall-clock accumulation per phase (device-synchronised on demand), reported
-  by the Trainer as extra metrics (``time/<phase>_s``).
+* ``PhaseTimer`` - wall-clock accumulation per host phase (device-synchronised on demand): the
+  Trainer reports its epoch phases (train / validate / checkpoint / tracking flush) as
+  ``time/<phase>_s`` metrics.
+* ``DevicePhaseTimer`` - GPU time of the phases INSIDE a training step (forward, backward,
+  all-reduce, optimizer): one-thread kernels write ``s_memrealtime`` at each phase mark on the
+  compute stream and one more accumulates the deltas on the device, so it also works inside
+  captured / replayed HIP graphs (host timers and event pairs do not); ``DCT_PHASE_TIMING=1``
+  turns it on in the autograd engine and the Trainer logs ``time/<phase>_s`` per epoch.
 """
 from __future__ import annotations
 
@@ -89,3 +95,44 @@ class PhaseTimer:
 
     def metrics(self, prefix: str = "time/") -> Dict[str, float]:
         return {f"{prefix}{k}_s": v for k, v in self.totals.items()}
+
+
+class DevicePhaseTimer:
+    """Per-step GPU phase timing with device timestamps (see the module docstring).
+
+    ``mark(i)`` for i = 0 .. len(phases) on the current stream delimit the phases of one step,
+    ``close()`` after the last mark accumulates them; ``read()`` synchronises and returns seconds
+    per phase summed over the steps since the last reset."""
+
+    def __init__(self, phases, device):
+        import torch
+
+        self.phases = list(phases)
+        self.n = len(self.phases) + 1  # marks
+        self.buf = torch.zeros(2 * self.n, dtype=torch.int64, device=device)
+
+    def _nat(self):
+        from ..ops._native import native
+
+        return native()
+
+    def mark(self, i: int):
+        import torch
+
+        self._nat().phase_stamp(self.buf.data_ptr(), int(i), torch.cuda.current_stream().cuda_stream)
+
+    def close(self):
+        import torch
+
+        self._nat().phase_accum(self.buf.data_ptr(), self.n, torch.cuda.current_stream().cuda_stream)
+
+    def read(self, reset: bool = True) -> Dict[str, float]:
+        import torch
+
+        torch.cuda.synchronize(self.buf.device)
+        v = self.buf.cpu().tolist()
+        out = {name: v[self.n + i] / 1e8 for i, name in enumerate(self.phases)}  # 100 MHz ticks -> s
+        out["steps"] = v[2 * self.n - 1]
+        if reset:
+            self.buf[self.n:].zero_()
+        return out

@@ -47,6 +47,9 @@ def parse_args(argv=None):
                    help="train on N synthetic weather rows instead of the parquet (no data on the box)")
     p.add_argument("--log-every-n-steps", type=int, default=cfg.train.log_every_n_steps)
     p.add_argument("--no-mlflow", action="store_true", help="disable tracking (smoke tests)")
+    p.add_argument("--dump-params", default="",
+                   help="directory: every rank writes its final flat parameters to params_rank<R>.json "
+                        "(replica-consistency checks in tests)")
     return p.parse_args(argv)
 
 
@@ -97,6 +100,13 @@ def main(argv=None) -> int:
     # --resume, or a torchrun elastic restart after a failed rank: continue from last.ckpt
     ckpt_path = resume_checkpoint(a.model_dir, a.resume)
     trainer.fit(model, train_loader, val_loader, ckpt_path=ckpt_path)
+    if a.dump_params:
+        import json
+
+        os.makedirs(a.dump_params, exist_ok=True)
+        flat = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()]).tolist()
+        with open(os.path.join(a.dump_params, f"params_rank{trainer.global_rank}.json"), "w") as f:
+            json.dump({"params": flat, "global_step": trainer.global_step, "world_size": trainer.world_size}, f)
 
     if trainer.global_rank == 0:
         best_path = checkpoint_callback.best_model_path

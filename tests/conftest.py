@@ -12,6 +12,7 @@ os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP) device")
     config.addinivalue_line("markers", "slow: multi-process / long-running test")
+    config.addinivalue_line("markers", "multigpu: needs >= 2 MI355X devices on one node (self-skips below)")
 
 
 def pytest_collection_modifyitems(config, items):

@@ -21,24 +21,29 @@ from dct_amd.trainer import DDPStrategy, Trainer, seed_everything  # noqa: E402
 
 def main():
     out_dir, epochs, rows = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
-    resume = "resume" in sys.argv[4:]
-    accel = "gpu" if "gpu" in sys.argv[4:] else "cpu"  # gpu: fused engine (+ in-kernel exchange)
+    opts = sys.argv[4:]
+    resume = "resume" in opts
+    accel = "gpu" if "gpu" in opts else "cpu"  # gpu: fused engine (+ in-kernel exchange)
+    # engine=<auto|autograd|fused|graph>, hidden=<a,b,..> (default 64), batch=<B>
+    kv = dict(o.split("=", 1) for o in opts if "=" in o)
+    engine = kv.get("engine", "autograd" if accel == "cpu" else "auto")
+    hidden = tuple(int(h) for h in kv.get("hidden", "64").split(","))
+    B = int(kv.get("batch", "4"))
     seed_everything(42)
     x, y = weather_tensors(rows, seed=0)
     ds = TensorPairDataset(x, y)
     n_tr = int(0.8 * rows)
     tr, va = random_split(ds, [n_tr, rows - n_tr])
-    model = MLPClassifier(5, hidden=(64,), dropout=0.0)
+    model = MLPClassifier(5, hidden=hidden, dropout=0.0)
     ck = ModelCheckpoint(dirpath=os.path.join(out_dir, "models"), filename="weather-best-{epoch:02d}-{val_loss:.2f}",
                          monitor="val_loss", mode="min", save_top_k=1, save_last=True)
     logger = MLFlowLogger(experiment_name="weather_forecasting", tracking_uri="file://" + os.path.join(out_dir, "mlruns"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     trainer = Trainer(max_epochs=epochs, accelerator=accel, num_nodes=world,
                       strategy=DDPStrategy(find_unused_parameters=False) if world > 1 else "auto", logger=logger,
-                      callbacks=[ck], log_every_n_steps=5, engine="autograd" if accel == "cpu" else "auto",
-                      verbose=False)
+                      callbacks=[ck], log_every_n_steps=5, engine=engine, verbose=False)
     ckpt_path = resume_checkpoint(os.path.join(out_dir, "models"), resume)  # --resume or an elastic restart
-    trainer.fit(model, DataLoader(tr, batch_size=4, shuffle=True), DataLoader(va, batch_size=4), ckpt_path=ckpt_path)
+    trainer.fit(model, DataLoader(tr, batch_size=B, shuffle=True), DataLoader(va, batch_size=B), ckpt_path=ckpt_path)
     flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).tolist()
     rank = int(os.environ.get("RANK", "0"))
     with open(os.path.join(out_dir, f"params_rank{rank}.json"), "w") as f:

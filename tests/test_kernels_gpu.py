@@ -37,14 +37,14 @@ def test_native_loaded_and_arch():
     assert "gfx950" in nat.arch_name(0)
 
 
-@pytest.mark.parametrize("kernel", ["auto", "lds", "lds-noblock"])
+@pytest.mark.parametrize("kernel", ["auto", "lds", "lds-noblock", "lds-v1"])
 @pytest.mark.parametrize("loss", ["ce", "mse"])
 @pytest.mark.parametrize("dims,B", [([5, 64, 2], 4), ([5, 128, 128, 2], 4), ([5, 64, 2], 3), ([9, 48, 64, 3], 4),
                                     ([16, 32, 48, 32, 3], 16), ([5, 128, 128, 2], 16), ([7, 20, 2], 9),
                                     ([7, 20, 2], 8), ([12, 40, 4], 6), ([16, 64, 3], 2), ([5, 64, 2], 1)])
 def test_fused_train_matches_torch_adam(dims, B, loss, kernel, cuda, monkeypatch):
     monkeypatch.setenv("DCT_MLP_KERNEL", kernel.split("-")[0])
-    monkeypatch.setenv("DCT_MLP_BLOCK", "0" if kernel.endswith("noblock") else "1")
+    monkeypatch.setenv("DCT_MLP_BLOCK", "0" if kernel.endswith("noblock") else ("v1" if kernel.endswith("v1") else "1"))
     torch.manual_seed(1)
     N, n_items = 301, 50
     X = torch.randn(N, dims[0])
@@ -80,12 +80,12 @@ def test_fused_train_matches_torch_adam(dims, B, loss, kernel, cuda, monkeypatch
     assert torch.allclose(m.cpu(), ref_m, atol=1e-4, rtol=1e-2)
 
 
-@pytest.mark.parametrize("kernel", ["auto", "lds", "lds-noblock"])
+@pytest.mark.parametrize("kernel", ["auto", "lds", "lds-noblock", "lds-v1"])
 @pytest.mark.parametrize("dims,B", [([5, 64, 2], 4), ([5, 128, 128, 2], 4), ([12, 40, 40, 5], 13),
                                     ([9, 48, 64, 3], 4), ([20, 128, 128, 4], 3), ([32, 128, 128, 1], 4)])
 def test_fused_grad_mode_matches_autograd(dims, B, kernel, cuda, monkeypatch):
     monkeypatch.setenv("DCT_MLP_KERNEL", kernel.split("-")[0])
-    monkeypatch.setenv("DCT_MLP_BLOCK", "0" if kernel.endswith("noblock") else "1")
+    monkeypatch.setenv("DCT_MLP_BLOCK", "0" if kernel.endswith("noblock") else ("v1" if kernel.endswith("v1") else "1"))
     torch.manual_seed(2)
     N = 64
     X = torch.randn(N, dims[0])
@@ -107,8 +107,9 @@ def test_fused_grad_mode_matches_autograd(dims, B, kernel, cuda, monkeypatch):
 
 @pytest.mark.parametrize("dims,B,D0", [([7, 128, 128, 2], 4, 7), ([30, 128, 128, 3], 3, 30)])
 def test_block_kernel_matches_lds_kernel_with_dropout(dims, B, D0, cuda, monkeypatch):
-    """mlp_block.hip (register-resident 3-layer kernel) vs the generic LDS kernel: same dropout
-    hash, loss and Adam -> the same trajectory up to fp32 summation order."""
+    """mlp_block2.hip (one-barrier register-resident 3-layer kernel, the default) and mlp_block.hip
+    (its predecessor, DCT_MLP_BLOCK=v1) vs the generic LDS kernel: same dropout hash, loss and
+    Adam -> the same trajectory up to fp32 summation order."""
     monkeypatch.setenv("DCT_MLP_KERNEL", "lds")
     torch.manual_seed(4)
     N, n_items = 500, 203
@@ -118,7 +119,7 @@ def test_block_kernel_matches_lds_kernel_with_dropout(dims, B, D0, cuda, monkeyp
     p0 = _flat(_ref_net(dims)).to(cuda)
     steps = math.ceil(n_items / B)
     out = {}
-    for blk in ("1", "0"):
+    for blk in ("1", "v1", "0"):
         monkeypatch.setenv("DCT_MLP_BLOCK", blk)
         p, m, v = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
         losses = torch.zeros(steps, device=cuda)
@@ -127,9 +128,10 @@ def test_block_kernel_matches_lds_kernel_with_dropout(dims, B, D0, cuda, monkeyp
                 step_base=5, loss_out=losses)
         torch.cuda.synchronize()
         out[blk] = (p.cpu(), m.cpu(), v.cpu(), losses.cpu())
-    for a_, b_ in zip(out["1"], out["0"]):
-        assert torch.isfinite(a_).all()
-        assert (a_ - b_).abs().max() <= 1e-4 * (1 + b_.abs().max()), float((a_ - b_).abs().max())
+    for blk in ("1", "v1"):
+        for a_, b_ in zip(out[blk], out["0"]):
+            assert torch.isfinite(a_).all()
+            assert (a_ - b_).abs().max() <= 1e-4 * (1 + b_.abs().max()), (blk, float((a_ - b_).abs().max()))
 
 
 @pytest.mark.parametrize("kernel", ["auto", "lds"])

@@ -175,6 +175,36 @@ def _barrier_run(out_path):
     json.dump({"met": met, "timeout": xs[0].read_status()}, open(out_path, "w"))
 
 
+def _barrier_later_tag_run(out_path):
+    nat = native()
+    a, b, c = (nat.PeerExchange(2, r, 4096) for r in (0, 1, 1))
+    a.set_peers([a.recv, b.recv])
+    c.set_peers([a.recv, c.recv])  # an impostor rank 1 whose own slot nobody writes
+    st = torch.cuda.Stream(torch.device("cuda", 0))
+    # rank 1 "leaves" barrier 1 and enters barrier 2 before rank 0 ever polled: rank 0's slot of
+    # rank 1 already holds tag 2 when rank 0 runs barrier 1 (the impostor's own polls time out)
+    c.barrier(st.cuda_stream, 0.05)
+    c.barrier(st.cuda_stream, 0.05)
+    torch.cuda.synchronize()
+    a.barrier(st.cuda_stream, 2.0)
+    torch.cuda.synchronize()
+    json.dump({"a": a.read_status(), "c": c.read_status()}, open(out_path, "w"))
+
+
+def test_device_barrier_accepts_a_later_tag(tmp_path, cuda):
+    """ADVICE r2: a peer that already left barrier N may have overwritten its slot with tag N+1;
+    barrier N must accept any tag at or past its own (wrap-safe compare) instead of spinning to
+    the timeout and reporting a failure that did not happen."""
+    out = tmp_path / "bar2.json"
+    code = (f"import sys; sys.path.insert(0, {ROOT!r}); sys.path.insert(0, {os.path.join(ROOT, 'tests')!r}); "
+            f"import test_xgmi_gpu as t; t._barrier_later_tag_run({str(out)!r})")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    res = json.loads(out.read_text())
+    assert res["a"] == 0, hex(res["a"])
+    assert res["c"] & 0x80000000  # the impostor itself did time out
+
+
 def test_device_barrier_in_process_and_timeout(tmp_path, cuda):
     """Two 'ranks' on two streams of a fresh process meet in the device barrier four times (status
     stays 0); a rank whose peer never arrives gives up after the timeout and records
