@@ -27,6 +27,12 @@ def target_path() -> str:
     return os.path.join(PKG_DIR, MODULE + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
+# per-source extra flags.  mlp_block2.hip: the SLP vectorizer packs the trainer's independent fp32
+# FMAs into v_pk_fma_f32 plus the v_mov_b32 pairs that marshal their operands - on gfx950 a packed op
+# issues no faster than two plain ones, so the moves are pure overhead in an issue-bound kernel.
+FILE_FLAGS = {"mlp_block2.hip": ["-fno-slp-vectorize"]}
+
+
 def _sources():
     return sorted(
         os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp"))
@@ -64,6 +70,7 @@ def _flags(debug: bool = False, sanitize: bool = None):
 
 
 def _stamp(src: str, flags) -> str:
+    flags = list(flags) + FILE_FLAGS.get(os.path.basename(src), [])
     h = hashlib.sha1()
     h.update(" ".join(flags).encode())
     for p in [src] + _headers():
@@ -81,7 +88,7 @@ def _compile(src: str, flags, verbose: bool):
         return obj, False
     lang = ["-x", "hip"] if src.endswith(".hip") else []
     tmp = f"{obj}.{os.getpid()}.tmp"  # per-process: concurrent builds never share a temp file
-    cmd = [os.path.join(ROCM, "bin", "hipcc")] + flags + lang + ["-c", src, "-o", tmp]
+    cmd = [os.path.join(ROCM, "bin", "hipcc")] + flags + FILE_FLAGS.get(base, []) + lang + ["-c", src, "-o", tmp]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

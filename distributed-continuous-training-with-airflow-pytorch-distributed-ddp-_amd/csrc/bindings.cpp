@@ -546,7 +546,9 @@ PYBIND11_MODULE(_dct_native, m) {
       .def("eval_batch", &dct::MlpStepExecutor::eval_batch, py::arg("X"), py::arg("row_bytes"), py::arg("Y"),
            py::arg("idx"), py::arg("n_items"), py::arg("cursor"), py::arg("rows"), py::arg("stats"),
            py::arg("stream"))
-      .def_property_readonly("num_params", &dct::MlpStepExecutor::num_params);
+      .def_property_readonly("num_params", &dct::MlpStepExecutor::num_params)
+      .def_property_readonly("part_fallbacks", &dct::MlpStepExecutor::part_fallbacks)
+      .def_property_readonly("partial_layers", &dct::MlpStepExecutor::partial_layers);
   py::class_<dct::StreamGraph>(m, "StreamGraph")
       .def(py::init<>())
       .def("begin", &dct::StreamGraph::begin)

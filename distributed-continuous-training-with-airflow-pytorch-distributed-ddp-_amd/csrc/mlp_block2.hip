@@ -37,14 +37,31 @@ constexpr int MSK = LAB + 12;            // [2][NW][2] hidden-2 dropout keep bal
 constexpr int H1W = MSK + 2 * NW * 2;    // [NW][KS][4] wave-private layer-1 inputs h1[k][row]
 constexpr int PSTR = 36;                 // partials: [o][wave][4] with a 36-float o stride
 constexpr int PART = H1W + NW * KS * 4;  // [2][H][PSTR]
-constexpr int TOTAL = PART + 2 * H * PSTR;
-static_assert((H1W % 4) == 0 && (PART % 4) == 0 && (MSK % 4) == 0 && (LAB % 4) == 0, "16-B aligned tiles");
+constexpr int W2L = PART + 2 * H * PSTR; // [2][H][4] last-layer weights W2[c][o] (o-major), published by owners
+constexpr int B1L = W2L + 2 * H * 4;     // [2][H] b1
+constexpr int B2L = B1L + 2 * H;         // [2][4] b2
+constexpr int TOTAL = B2L + 8;
+static_assert((H1W % 4) == 0 && (PART % 4) == 0 && (MSK % 4) == 0 && (LAB % 4) == 0 && (W2L % 4) == 0 &&
+              (B1L % 4) == 0 && (B2L % 4) == 0, "16-B aligned tiles");
 }  // namespace blk2
 
 namespace b2d {
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
+  // every control used here reads a valid lane of the same row: bound_ctrl lets the compiler fold
+  // the move into the consuming VALU op (v_add_f32_dpp) instead of copying the operand first
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
+// Adam with the step size folded into the denominator: p -= m / (sqrt(v) * A + E), A = rbc2 / ss,
+// E = eps / ss (ss = lr / (1 - b1^t), rbc2 = 1 / sqrt(1 - b2^t)) - torch's update up to rounding,
+// 10 VALU ops (2 transcendental) per element; m moves like torch's lerp_(g, 1 - b1)
+__device__ __forceinline__ void adam_lean(float& p, float g, float& m, float& v, float c1, float b2, float c2,
+                                          float wd, float A, float E) {
+  g = fmaf(wd, p, g);
+  m = fmaf(c1, g - m, m);
+  v = fmaf(c2 * g, g, v * b2);
+  p = fmaf(-m, __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_sqrtf(v), A, E)), p);
 }
 constexpr int QP_X1 = 0xB1;     // quad_perm [1,0,3,2]: lane ^ 1
 constexpr int QP_X2 = 0x4E;     // quad_perm [2,3,0,1]: lane ^ 2
@@ -101,6 +118,14 @@ __device__ __forceinline__ float sel4(const float (&v)[4], int i) {
   return i == 0 ? v[0] : (i == 1 ? v[1] : (i == 2 ? v[2] : v[3]));
 }
 
+template <int N>
+__device__ __forceinline__ float sel4c(const float (&v)[N], int i) {
+  float r = v[0];
+#pragma unroll
+  for (int k = 1; k < N; ++k) r = i == k ? v[k] : r;
+  return r;
+}
+
 __device__ __forceinline__ float rl(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
@@ -128,8 +153,9 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
   const int u = KS * w + (l >> 2);
   const int wo0 = sh.woff[0], bo0 = sh.boff[0], wo1 = sh.woff[1], bo1 = sh.boff[1];
   const int wo2 = sh.woff[2], bo2 = sh.boff[2];
-  unsigned long long pacc[PROF ? 10 : 1] = {};
+  unsigned long long pacc[PROF ? 11 : 1] = {};
   unsigned long long t_last = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
+  const unsigned long long t_kstart = t_last;
 
   int cur0 = 0;
   if (a.cursor) {
@@ -144,15 +170,25 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
   }
 
   // ---- registers: W1 k-slice + moments; W0 slices; replicated W2 / b1 / b2 (+ moments)
+  // a lane's 16 weights of one output row are contiguous: 16-byte loads (mlp_block2_ok checks the
+  // alignment), all issued before the first use - the prologue is one memory round trip
   float w1[2][KS], m1[2][KS], v1[2][KS];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-      const int f = wo1 + (l + 64 * j) * H + KS * w + kk;
-      w1[j][kk] = a.p[f];
-      m1[j][kk] = ADAM ? a.m[f] : 0.f;
-      v1[j][kk] = ADAM ? a.v[f] : 0.f;
+    for (int q = 0; q < KS / 4; ++q) {
+      const int f = wo1 + (l + 64 * j) * H + KS * w + 4 * q;
+      const float4 tp = *reinterpret_cast<const float4*>(a.p + f);
+      w1[j][4 * q] = tp.x; w1[j][4 * q + 1] = tp.y; w1[j][4 * q + 2] = tp.z; w1[j][4 * q + 3] = tp.w;
+      if (ADAM) {
+        const float4 tm = *reinterpret_cast<const float4*>(a.m + f);
+        const float4 tv = *reinterpret_cast<const float4*>(a.v + f);
+        m1[j][4 * q] = tm.x; m1[j][4 * q + 1] = tm.y; m1[j][4 * q + 2] = tm.z; m1[j][4 * q + 3] = tm.w;
+        v1[j][4 * q] = tv.x; v1[j][4 * q + 1] = tv.y; v1[j][4 * q + 2] = tv.z; v1[j][4 * q + 3] = tv.w;
+      } else {
+        m1[j][4 * q] = m1[j][4 * q + 1] = m1[j][4 * q + 2] = m1[j][4 * q + 3] = 0.f;
+        v1[j][4 * q] = v1[j][4 * q + 1] = v1[j][4 * q + 2] = v1[j][4 * q + 3] = 0.f;
+      }
     }
   float w0[ND], m0[ND], v0[ND];
 #pragma unroll
@@ -165,31 +201,22 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
     v0[i] = (ok && ADAM) ? a.v[f] : 0.f;
   }
   float pb0 = a.p[bo0 + u], mb0 = ADAM ? a.m[bo0 + u] : 0.f, vb0 = ADAM ? a.v[bo0 + u] : 0.f;
-  float pb1[2], mb1[2], vb1[2];
-  float pw2[CM][2], mw2[CM][2], vw2[CM][2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int o = l + 64 * j;
-    pb1[j] = a.p[bo1 + o];
-    mb1[j] = ADAM ? a.m[bo1 + o] : 0.f;
-    vb1[j] = ADAM ? a.v[bo1 + o] : 0.f;
-#pragma unroll
-    for (int c = 0; c < CM; ++c) {
-      const bool ok = c < C;
-      const int f = wo2 + (ok ? c : 0) * H + o;
-      pw2[c][j] = ok ? a.p[f] : 0.f;
-      mw2[c][j] = (ok && ADAM) ? a.m[f] : 0.f;
-      vw2[c][j] = (ok && ADAM) ? a.v[f] : 0.f;
-    }
-  }
-  float pb2[CM], mb2[CM], vb2[CM];
-#pragma unroll
-  for (int c = 0; c < CM; ++c) {
-    const bool ok = c < C;
-    pb2[c] = ok ? a.p[bo2 + c] : 0.f;
-    mb2[c] = (ok && ADAM) ? a.m[bo2 + c] : 0.f;
-    vb2[c] = (ok && ADAM) ? a.v[bo2 + c] : 0.f;
-  }
+  // W2 / b1 / b2: every wave needs them (logits, dZ2), ONE owner lane per element updates it and
+  // publishes the new value to LDS for the next step (read after its barrier).  CM = 2: waves 0-3
+  // own W2[c = w / 2][o = l + 64 (w % 2)], waves 4-5 b1[o = l + 64 (w - 4)], wave 6 b2[l];
+  // CM = 4: all 8 waves own W2, waves 0-1 also b1, wave 2 b2.
+  const int cw = w >> 1, jw = w & 1;
+  const bool own_w2 = cw < C;
+  const int wb = CM == 2 ? 4 : 0;
+  const bool own_b1 = w == wb || w == wb + 1;
+  const int jb = w - wb;
+  const bool own_b2 = (w == (CM == 2 ? 6 : 2)) && l < C;
+  const int fw2 = wo2 + (own_w2 ? cw : 0) * H + l + 64 * jw;
+  const int fb1 = bo1 + l + 64 * (own_b1 ? jb : 0);
+  const int fb2 = bo2 + (own_b2 ? l : 0);
+  float pw2 = own_w2 ? a.p[fw2] : 0.f, mw2 = (own_w2 && ADAM) ? a.m[fw2] : 0.f, vw2 = (own_w2 && ADAM) ? a.v[fw2] : 0.f;
+  float pb1 = own_b1 ? a.p[fb1] : 0.f, mb1 = (own_b1 && ADAM) ? a.m[fb1] : 0.f, vb1 = (own_b1 && ADAM) ? a.v[fb1] : 0.f;
+  float pb2 = own_b2 ? a.p[fb2] : 0.f, mb2 = (own_b2 && ADAM) ? a.m[fb2] : 0.f, vb2 = (own_b2 && ADAM) ? a.v[fb2] : 0.f;
 
   // ---- LDS: first batch into input buffer 0
   for (int e = tid; e < TOTAL; e += NT) lds[e] = 0.f;
@@ -205,6 +232,9 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
     }
     if (tid < B) reinterpret_cast<int*>(lds + LAB)[tid] = (tid < bs0) ? a.Y[a.idx[cur0 * Bsz + tid]] : 0;
   }
+  if (own_w2) lds[W2L + (l + 64 * jw) * 4 + cw] = pw2;  // classes >= C stay 0 (zeroed above)
+  if (own_b1) lds[B1L + l + 64 * jb] = pb1;
+  if (own_b2) lds[B2L + l] = pb2;
   // prefetch roles: thread -> (row pb, feature pk) of the next batch, or (row pb, label)
   const int nel = Bsz * D0;
   int role = 0, pb = 0, pk = 0;
@@ -212,15 +242,22 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
   else if (tid < nel + Bsz) { role = 2; pb = tid - nel; }
   int ridx_next = 0;
   if (role && (cur0 + 1) * Bsz + pb < a.n_items) ridx_next = a.idx[(cur0 + 1) * Bsz + pb];
+  // per-thread source of its prefetch element: base + row index * stride (no per-step branch)
+  const uint32_t* pf_base = role == 1 ? reinterpret_cast<const uint32_t*>(a.X) + pk : reinterpret_cast<const uint32_t*>(a.Y);
+  const int pf_stride = role == 1 ? a.ldx : (role == 2 ? 1 : 0);
   __syncthreads();
 
   const float p_drop = a.dropout;
   const bool drop = p_drop > 0.f;
   const float scale = drop ? 1.0f / (1.0f - p_drop) : 1.0f;
   const float l2b1 = log2f(a.b1), l2b2 = log2f(a.b2);
+  const float c1 = 1.f - a.b1, c2 = 1.f - a.b2;
   float* h1w = lds + H1W + w * (KS * 4);
   int xb = 0;
-  if constexpr (PROF) t_last = __builtin_amdgcn_s_memtime();
+  if constexpr (PROF) {
+    t_last = __builtin_amdgcn_s_memtime();
+    pacc[9] = t_last - t_kstart;  // prologue: parameters + moments in, LDS init, first batch
+  }
   for (int s = 0; s < a.steps; ++s) {
     const int sb = s + cur0;
     const int bs = min(Bsz, a.n_items - sb * Bsz);
@@ -229,9 +266,7 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
     const float* xT = lds + XT + xb * DMAX * 4;
     const bool have_next = (s + 1 < a.steps);
     const int bs_next = have_next ? min(Bsz, a.n_items - (sb + 1) * Bsz) : 0;
-    const uint32_t* src = (role == 1) ? reinterpret_cast<const uint32_t*>(a.X) + (size_t)ridx_next * a.ldx + pk
-                                      : reinterpret_cast<const uint32_t*>(a.Y) + ridx_next;
-    const uint32_t raw_next = *src;
+    const uint32_t raw_next = pf_base[(size_t)ridx_next * pf_stride];
     const int nx2 = min((sb + 2) * Bsz + pb, a.n_items - 1);
     const int ridx_next2 = a.idx[nx2 < 0 ? 0 : nx2];
     const int4 labs = *reinterpret_cast<const int4*>(lds + LAB + xb * 4);
@@ -302,6 +337,27 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
     lds_barrier();  // the step's only workgroup barrier
     B2STAMP(2)
 
+    // ---- this step's W2 / b1 / b2 (published by their owners during the previous step)
+    float pw2v[CM][2], pb1v[2], pb2v[CM];
+    {
+      const int pbuf = s & 1;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float* wp = lds + W2L + pbuf * (H * 4) + (l + 64 * j) * 4;
+        if constexpr (CM == 2) {
+          const float2 t = *reinterpret_cast<const float2*>(wp);
+          pw2v[0][j] = t.x; pw2v[1][j] = t.y;
+        } else {
+          const float4 t = *reinterpret_cast<const float4*>(wp);
+          pw2v[0][j] = t.x; pw2v[1 % CM][j] = t.y; pw2v[2 % CM][j] = t.z; pw2v[3 % CM][j] = t.w;
+        }
+        pb1v[j] = lds[B1L + pbuf * H + l + 64 * j];
+      }
+      const float4 t2 = *reinterpret_cast<const float4*>(lds + B2L + pbuf * 4);
+      const float t2v[4] = {t2.x, t2.y, t2.z, t2.w};
+#pragma unroll
+      for (int c = 0; c < CM; ++c) pb2v[c] = t2v[c];
+    }
     // ---- F2r: h2 for this lane's outputs o = l, l + 64 (sum of the 8 wave partials)
     float h2[2][4];
     {
@@ -329,7 +385,7 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
         const float zz[4] = {sum.x, sum.y, sum.z, sum.w};
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float z = fmaxf(zz[r] + pb1[j], 0.f);
+          float z = fmaxf(zz[r] + pb1v[j], 0.f);
           if (drop) z = ((kw[j][r] >> (l & 31)) & 1u) ? z * scale : 0.f;
           h2[j][r] = z;
         }
@@ -344,7 +400,7 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int c = 0; c < CM; ++c) P[r * CM + c] = pw2[c][0] * h2[0][r] + pw2[c][1] * h2[1][r];
+        for (int c = 0; c < CM; ++c) P[r * CM + c] = pw2v[c][0] * h2[0][r] + pw2v[c][1] * h2[1][r];
       const float zown = rs_small<4 * CM>(P, l);
       const int rr = l >> 4;
       float z[CM];
@@ -365,7 +421,7 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
       }
       float z4[4] = {0.f, 0.f, 0.f, 0.f}, dz[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < CM; ++c) z4[c] = z[c] + pb2[c];
+      for (int c = 0; c < CM; ++c) z4[c] = z[c] + pb2v[c];
       const int lab = (rr & 2) ? ((rr & 1) ? labs.w : labs.z) : ((rr & 1) ? labs.y : labs.x);
       const bool live = rr < bs;
       const float inv = live ? 1.0f / (float)(bs > 0 ? bs : 1) : 0.f;
@@ -387,7 +443,9 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
     const int t = t0 + s + 1;
     const float step_size = a.lr / (1.f - pow_t(l2b1, (float)t));
     const float rbc2 = __builtin_amdgcn_rsqf(1.f - pow_t(l2b2, (float)t));
-    // ---- dZ2 (old W2), then W2 / b2 / b1 gradients + Adam (replicated per wave)
+    const float rss = __builtin_amdgcn_rcpf(step_size);
+    const float aA = rbc2 * rss, aE = a.eps * rss;  // adam_lean's folded denominator
+    // ---- dZ2 (old W2), then the owners' W2 / b2 / b1 gradients + Adam, published for step s + 1
     float dz2[2][4];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -395,28 +453,36 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
       for (int r = 0; r < 4; ++r) {
         float g = 0.f;
 #pragma unroll
-        for (int c = 0; c < CM; ++c) g += pw2[c][j] * dz3[r][c];
+        for (int c = 0; c < CM; ++c) g += pw2v[c][j] * dz3[r][c];
         dz2[j][r] = h2[j][r] > 0.f ? g * scale : 0.f;
       }
+    {
+      const int nbuf = (s + 1) & 1;
+      if (own_w2) {  // dW2[cw][o] = sum_r dz3[r][cw] h2[o][r]
+        float d3[4];
 #pragma unroll
-    for (int c = 0; c < CM; ++c) {
-      if (c < C) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const float gw = dz3[0][c] * h2[j][0] + dz3[1][c] * h2[j][1] + dz3[2][c] * h2[j][2] + dz3[3][c] * h2[j][3];
-          if (ADAM) adam_elem(pw2[c][j], gw, mw2[c][j], vw2[c][j], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
-          else if (w == 0) a.grad_out[wo2 + c * H + l + 64 * j] = gw;
-        }
-        const float gb = dz3[0][c] + dz3[1][c] + dz3[2][c] + dz3[3][c];
-        if (ADAM) adam_elem(pb2[c], gb, mb2[c], vb2[c], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
-        else if (tid == 0) a.grad_out[bo2 + c] = gb;
+        for (int r = 0; r < 4; ++r) d3[r] = CM == 2 ? (cw ? dz3[r][1 % CM] : dz3[r][0]) : sel4c<CM>(dz3[r], cw);
+        const float* hh = jw ? h2[1] : h2[0];
+        const float gw = d3[0] * hh[0] + d3[1] * hh[1] + d3[2] * hh[2] + d3[3] * hh[3];
+        if (ADAM) adam_lean(pw2, gw, mw2, vw2, c1, a.b2, c2, a.wd, aA, aE);
+        else if (s == 0) a.grad_out[fw2] = gw;
+        lds[W2L + nbuf * (H * 4) + (l + 64 * jw) * 4 + cw] = pw2;
       }
-    }
+      if (own_b1) {
+        const float* dd = jb ? dz2[1] : dz2[0];
+        const float gb = dd[0] + dd[1] + dd[2] + dd[3];
+        if (ADAM) adam_lean(pb1, gb, mb1, vb1, c1, a.b2, c2, a.wd, aA, aE);
+        else if (s == 0) a.grad_out[fb1] = gb;
+        lds[B1L + nbuf * H + l + 64 * jb] = pb1;
+      }
+      if (own_b2) {
+        float gb = 0.f;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const float gb = dz2[j][0] + dz2[j][1] + dz2[j][2] + dz2[j][3];
-      if (ADAM) adam_elem(pb1[j], gb, mb1[j], vb1[j], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
-      else if (w == 0) a.grad_out[bo1 + l + 64 * j] = gb;
+        for (int r = 0; r < 4; ++r) gb += CM == 2 ? (l ? dz3[r][1 % CM] : dz3[r][0]) : sel4c<CM>(dz3[r], l);
+        if (ADAM) adam_lean(pb2, gb, mb2, vb2, c1, a.b2, c2, a.wd, aA, aE);
+        else if (s == 0) a.grad_out[fb2] = gb;
+        lds[B2L + nbuf * 4 + l] = pb2;
+      }
     }
     B2STAMP(5)
     // ---- dZ1 = W1^T dZ2 over this wave's k-slice: one 16-value reduce-scatter per batch row
@@ -442,11 +508,11 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
         const int d = r0 + 4 * i;
         const float4 x = *reinterpret_cast<const float4*>(xT + d * 4);
         const float gw = dq[0] * x.x + dq[1] * x.y + dq[2] * x.z + dq[3] * x.w;
-        if (ADAM) adam_elem(w0[i], gw, m0[i], v0[i], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);  // d >= D0: stays 0
+        if (ADAM) adam_lean(w0[i], gw, m0[i], v0[i], c1, a.b2, c2, a.wd, aA, aE);  // d >= D0: stays 0
         else if (d < D0) a.grad_out[wo0 + u * D0 + d] = gw;
       }
       const float gb = dq[0] + dq[1] + dq[2] + dq[3];
-      if (ADAM) adam_elem(pb0, gb, mb0, vb0, a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+      if (ADAM) adam_lean(pb0, gb, mb0, vb0, c1, a.b2, c2, a.wd, aA, aE);
       else if (r0 == 0) a.grad_out[bo0 + u] = gb;
     }
     B2STAMP(7)
@@ -460,7 +526,7 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const float gw = dz2[j][0] * h.x + dz2[j][1] * h.y + dz2[j][2] * h.z + dz2[j][3] * h.w;
-        if (ADAM) adam_elem(w1[j][kk], gw, m1[j][kk], v1[j][kk], a.b1, a.b2, a.wd, step_size, rbc2, a.eps);
+        if (ADAM) adam_lean(w1[j][kk], gw, m1[j][kk], v1[j][kk], c1, a.b2, c2, a.wd, aA, aE);
         else a.grad_out[gb1 + 64 * j * H + kk] = gw;
       }
     }
@@ -471,12 +537,6 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
   if (a.cursor && tid == 0) __hip_atomic_store(a.cursor, cur0 + a.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (a.step_counter && tid == 0)
     __hip_atomic_store(a.step_counter, t0 + a.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if constexpr (PROF) {
-    if (l == 0) {
-#pragma unroll
-      for (int i = 0; i < 9; ++i) atomicAdd(a.prof + w * 16 + i, pacc[i]);
-    }
-  }
   if (!ADAM) return;
 
   // ---- write back parameters and moments (flat torch order).  The base offset is made opaque so
@@ -484,15 +544,15 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
   // (3 x 32 pointers) live across the step loop - that alone cost ~90 spilled VGPRs.
   int lo = l, uo = u;
   asm volatile("" : "+v"(lo), "+v"(uo));
-  const int fb1 = wo1 + lo * H + KS * w;
+  const int fw1 = wo1 + lo * H + KS * w;
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-      const int f = fb1 + 64 * j * H + kk;
-      a.p[f] = w1[j][kk];
-      a.m[f] = m1[j][kk];
-      a.v[f] = v1[j][kk];
+    for (int q = 0; q < KS / 4; ++q) {
+      const int f = fw1 + 64 * j * H + 4 * q;
+      *reinterpret_cast<float4*>(a.p + f) = make_float4(w1[j][4 * q], w1[j][4 * q + 1], w1[j][4 * q + 2], w1[j][4 * q + 3]);
+      *reinterpret_cast<float4*>(a.m + f) = make_float4(m1[j][4 * q], m1[j][4 * q + 1], m1[j][4 * q + 2], m1[j][4 * q + 3]);
+      *reinterpret_cast<float4*>(a.v + f) = make_float4(v1[j][4 * q], v1[j][4 * q + 1], v1[j][4 * q + 2], v1[j][4 * q + 3]);
     }
 #pragma unroll
   for (int i = 0; i < ND; ++i) {
@@ -505,19 +565,15 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
     }
   }
   if (r0 == 0) { a.p[bo0 + uo] = pb0; a.m[bo0 + uo] = mb0; a.v[bo0 + uo] = vb0; }
-  if (w == 0) {  // every wave holds the same W2 / b1 / b2
+  if (own_w2) { a.p[fw2] = pw2; a.m[fw2] = mw2; a.v[fw2] = vw2; }
+  if (own_b1) { a.p[fb1] = pb1; a.m[fb1] = mb1; a.v[fb1] = vb1; }
+  if (own_b2) { a.p[fb2] = pb2; a.m[fb2] = mb2; a.v[fb2] = vb2; }
+  if constexpr (PROF) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pacc[10] = __builtin_amdgcn_s_memtime() - t_last;  // epilogue: write-back issued and retired
+    if (l == 0) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int o = lo + 64 * j;
-      a.p[bo1 + o] = pb1[j]; a.m[bo1 + o] = mb1[j]; a.v[bo1 + o] = vb1[j];
-#pragma unroll
-      for (int c = 0; c < CM; ++c)
-        if (c < C) { const int f = wo2 + c * H + o; a.p[f] = pw2[c][j]; a.m[f] = mw2[c][j]; a.v[f] = vw2[c][j]; }
-    }
-    if (l < C) {
-#pragma unroll
-      for (int c = 0; c < CM; ++c)
-        if (c == l) { a.p[bo2 + c] = pb2[c]; a.m[bo2 + c] = mb2[c]; a.v[bo2 + c] = vb2[c]; }
+      for (int i = 0; i < 11; ++i) atomicAdd(a.prof + w * 16 + i, pacc[i]);
     }
   }
 }
@@ -528,7 +584,10 @@ bool mlp_block2_ok(const MlpShape& sh, const MlpArgs& a) {
   if (env && (env[0] == '0' || (env[0] == 'v' && env[1] == '1'))) return false;
   // a profiling launch is served for the weather shape (D0 <= 8, C <= 2, train mode) only
   const bool prof_ok = a.prof == nullptr || (sh.dims[0] <= 8 && sh.dims[3] <= 2 && a.mode == 0);
-  return prof_ok && sh.L == 3 && sh.dims[1] == blk2::H && sh.dims[2] == blk2::H && sh.dims[0] >= 1 &&
+  // 16-byte W1 row loads / stores
+  const bool aligned = (sh.woff[1] % 4) == 0 && ((uintptr_t)a.p & 15) == 0 &&
+                       (a.mode != 0 || (((uintptr_t)a.m | (uintptr_t)a.v) & 15) == 0);
+  return prof_ok && aligned && sh.L == 3 && sh.dims[1] == blk2::H && sh.dims[2] == blk2::H && sh.dims[0] >= 1 &&
          sh.dims[0] <= blk2::DMAX && sh.dims[3] >= 1 && sh.dims[3] <= 4 && a.B >= 1 && a.B <= blk2::B &&
          a.pending == nullptr && a.stage == nullptr && a.xg_world <= 1 && (a.mode == 0 || a.mode == 1);
 }

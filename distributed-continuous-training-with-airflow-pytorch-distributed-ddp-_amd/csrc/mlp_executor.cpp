@@ -204,7 +204,12 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
                                             part_splits_[r], st) == 0) {
       part_used[r] = true;
     } else {
-      if (r >= 0) (void)hipGetLastError();
+      if (r >= 0) {
+        // the slice plan was made for a full batch; a shorter one (the epoch's partial last batch)
+        // has too few k-tiles for it - the layer's dW then goes through g like with a reducer
+        (void)hipGetLastError();
+        ++part_fallbacks_;
+      }
       ck(dct_gemm_bf16_ex(dz_[ci], acts_[l], g_ + woff_[l], nullptr, dout, din, rows, dout, din, din,
                           /*trans_a*/ 1, /*trans_b*/ 0, EPI_NONE, /*out_f32*/ 1, /*accumulate*/ 1, nullptr,
                           g_ + boff_[l], st),

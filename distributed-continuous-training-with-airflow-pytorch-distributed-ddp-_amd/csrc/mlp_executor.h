@@ -28,6 +28,9 @@ class MlpStepExecutor {
   void eval_batch(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t idx, int n_items, uintptr_t cursor, int rows,
                   uintptr_t stats, uintptr_t stream);
   int64_t num_params() const { return P_; }
+  int part_fallbacks() const { return part_fallbacks_; }
+  // layers whose dW goes to Adam as split-K slices (no reducer): their weight range of g stays 0
+  int partial_layers() const { return nparts_; }
   ~MlpStepExecutor();
   MlpStepExecutor(const MlpStepExecutor&) = delete;
   MlpStepExecutor& operator=(const MlpStepExecutor&) = delete;
@@ -59,6 +62,7 @@ class MlpStepExecutor {
   float* part_[2] = {nullptr, nullptr};
   int part_layer_[2] = {-1, -1}, part_splits_[2] = {1, 1};
   int nparts_ = 0;
+  int part_fallbacks_ = 0;  // steps whose planned split-K slices went through g instead (short batch)
 };
 
 }  // namespace dct

@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import contextlib
 import math
-from typing import Dict, Iterable, Optional
+from typing import Dict, Iterable, List, Optional
 
 import torch
 import torch.nn.functional as F
@@ -779,17 +779,27 @@ def tt_embed(x: torch.Tensor, E: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
 
 
 _HEAD_SCRATCH: Dict[Optional[int], torch.Tensor] = {}
+# superseded scratch buffers stay referenced for the life of the process: a HIP graph captured
+# before a regrow still holds the old ticket / partials pointer, and replaying it must never write
+# into memory the caching allocator has handed to someone else
+_HEAD_SCRATCH_RETIRED: List[torch.Tensor] = []
 
 
 def _head_scratch(device: torch.device, B: int) -> torch.Tensor:
     """Per-device head-loss scratch: [ticket (uint32 bits, left 0 by every launch) | ceil(B/4) fp32
     partials].  Allocated zeroed by the eager warm-up steps, then reused by the captured step graph
     (one key per device, not per stream: a stream-keyed buffer first met under capture would put its
-    zero fill back into every replay).  Head forwards on one device run in stream order."""
+    zero fill back into every replay).  ONE ticket per device: head forwards must not run
+    concurrently on two streams of a device - the engines issue them in stream order on the
+    compute stream (a regrow under an active capture is refused for the same reason)."""
     key = device.index
     n = 1 + (B + 3) // 4
     buf = _HEAD_SCRATCH.get(key)
     if buf is None or buf.numel() < n:
+        if buf is not None and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("tt head scratch must be sized by an eager step before graph capture")
+        if buf is not None:
+            _HEAD_SCRATCH_RETIRED.append(buf)
         buf = torch.zeros(max(n, 1 + 128), dtype=torch.float32, device=device)
         _HEAD_SCRATCH[key] = buf
     return buf

@@ -10,6 +10,14 @@ Adam with bf16 shadow weights.  The batch cursor, Adam step and loss slot live i
 so the step is captured once and replayed for every full batch of an epoch; the partial last
 batch (reference ``drop_last=False``) runs eagerly with its real row count.
 
+Gradient buffer ``g`` (flat, parameter order + the loss slot): with a DDP reducer it holds every
+averaged gradient after a step.  WITHOUT one (world size 1), up to two hidden layers hand their
+split-K dW slices straight to the Adam kernel (``exe.partial_layers``), so those layers' weight
+ranges of ``g`` stay ZERO - read gradients through a reducer run (``DCT_FORCE_DDP=1``) or
+``DCT_DW_INTO_ADAM=0`` for debugging / grad-norm checks.  A batch too short for the planned
+slices (an epoch's partial last batch) falls back to ``g`` for that step
+(``exe.part_fallbacks`` counts those steps).
+
 Reference semantics kept: DistributedSampler sharding, batch-mean loss averaged over ranks
 (``sync_dist``), Adam(lr) on fp32 master weights, checkpoints in the Lightning layout (the flat
 buffers are copied back into the nn.Module for saving).

@@ -57,8 +57,9 @@ def test_tabular_forced_reducer_matches_no_reducer(cuda, monkeypatch):
     assert torch.isfinite(l1).all()
     assert torch.allclose(l0, l1, atol=1e-3), (l0 - l1).abs().max()
     assert (eng.p.cpu() - ref.p.cpu()).norm() / ref.p.cpu().norm() < 1e-2
-    # (b) the head buckets were launched from the per-layer mark_ready calls, before finalize
-    assert 1 <= red.launched_before_finalize < red.num_buckets, (red.launched_before_finalize, red.num_buckets)
+    # (b) buckets were launched from the per-layer mark_ready calls during backward, before finalize
+    # (every one of them, when the input layer's gradients complete the last bucket)
+    assert 1 <= red.launched_before_finalize <= red.num_buckets, (red.launched_before_finalize, red.num_buckets)
     # (c) device-measured all-reduce time of every step (graph replays included), no ordering fault
     span, exposed, steps, bad = red.allreduce_ms(reset=False)
     assert steps >= len(l1) and span > 0 and 0 <= exposed <= span + 1e-3, (span, exposed, steps)

@@ -121,13 +121,15 @@ def test_trainer_fit_graph_engine_writes_checkpoint(tmp_path, cuda):
     assert tr.callback_metrics["val_loss"] < 0.5
 
 
-@pytest.mark.parametrize("B", [1024, 4096])
-def test_dw_slices_into_adam_match_reduce_path(B, cuda, monkeypatch):
+@pytest.mark.parametrize("B,extra", [(1024, 0), (4096, 0), (1024, 300)])
+def test_dw_slices_into_adam_match_reduce_path(B, extra, cuda, monkeypatch):
     """Without a DDP reducer the executor hands the 2-4-way split-K dW slices of the hidden
     1024x1024 layers to Adam (summed there in slice order) instead of reducing them into g: the
-    same trajectory as DCT_DW_INTO_ADAM=0 (same slices, same order -> the same gradients)."""
+    same trajectory as DCT_DW_INTO_ADAM=0 (same slices, same order -> the same gradients).
+    ``extra`` rows make every epoch end with a partial batch: its dW falls back to g
+    for that step and the trajectories still agree."""
     dims = [256, 1024, 1024, 1024, 2]
-    X, Y = _data(8 * B, dims[0], seed=5)
+    X, Y = _data(8 * B + extra, dims[0], seed=5)
     rows = torch.arange(X.shape[0])
     res = {}
     for mode in ("1", "0"):
@@ -137,6 +139,9 @@ def test_dw_slices_into_adam_match_reduce_path(B, cuda, monkeypatch):
         losses = torch.cat([eng.train_epoch(ep).cpu() for ep in range(2)])
         torch.cuda.synchronize()
         res[mode] = (losses, eng.p.cpu())
+        if mode == "1":
+            assert eng.exe.partial_layers >= 1
+            assert (eng.exe.part_fallbacks > 0) == (extra > 0), eng.exe.part_fallbacks
     (l1, p1), (l0, p0) = res["1"], res["0"]
     assert torch.isfinite(l1).all()
     assert torch.allclose(l1, l0, atol=1e-3), (l1 - l0).abs().max()

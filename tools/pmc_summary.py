@@ -10,7 +10,9 @@ dispatches are counted too). Derived columns:
           SQ_VALU_MFMA_BUSY_CYCLES sums all 1024 SIMDs (checked: a 4096x1024x1024 bf16 GEMM
           reads 8.39M busy cycles = 2*M*N*K / 1024 flop per SIMD-cycle). Counter collection
           stretches the active cycles, so this is a lower bound.
-  TF      dense bf16 MFMA work implied by the busy cycles: busy * 1024 flop, per step (TFLOP)
+  GF/st   dense bf16 MFMA work implied by the busy cycles: busy * 1024 flop, per step (GFLOP)
+  TF/s    that work divided by the kernel's time per step in the same run (TFLOP/s; a lower
+          bound, counter collection stretches the kernels)
   ldsc%   SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE  (extra cycles lost to bank conflicts)
   GB/s    2 * FETCH_SIZE (KB) / kernel time  (gfx950 FETCH_SIZE counts half of a wide read)
 Kernel time comes from the same run's trace, which counter collection serialises, so it is an
@@ -42,19 +44,20 @@ def main():
         dur[r["Kernel_Name"]] += (float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
         calls[r["Kernel_Name"]] += 1
     names = sorted(set(ctr) | set(dur), key=lambda n: -dur.get(n, 0.0))[:top]
-    print(f"{'us/step':>9} {'calls':>6} {'mfma%':>6} {'TF':>7} {'ldsc%':>6} {'GB/s':>7}  kernel")
+    print(f"{'us/step':>9} {'calls':>6} {'mfma%':>6} {'GF/st':>7} {'TF/s':>7} {'ldsc%':>6} {'GB/s':>7}  kernel")
     for n in names:
         c = ctr.get(n, {})
         t_ns = dur.get(n, 0.0)
         mf = c.get("SQ_VALU_MFMA_BUSY_CYCLES")
         ga = c.get("GRBM_GUI_ACTIVE")
         mfma = f"{100 * mf * 8 / (ga * 1024):6.1f}" if mf is not None and ga else "     -"
-        tf = f"{mf * 1024 / 1e12 / steps:7.4f}" if mf is not None else "      -"
+        gf = f"{mf * 1024 / 1e9 / steps:7.2f}" if mf is not None else "      -"
+        tf = f"{mf * 1024 / t_ns / 1e3:7.1f}" if (mf is not None and t_ns) else "      -"
         bc, la = c.get("SQ_LDS_BANK_CONFLICT"), c.get("SQ_LDS_IDX_ACTIVE")
         ldsc = f"{100 * bc / la:6.1f}" if bc is not None and la else "     -"
         fs = c.get("FETCH_SIZE")
         bw = f"{2 * fs * 1024 / t_ns:7.0f}" if fs is not None and t_ns else "      -"
-        print(f"{t_ns / 1e3 / steps:9.1f} {calls[n] / steps:6.1f} {mfma} {tf} {ldsc} {bw}  {n[:100]}")
+        print(f"{t_ns / 1e3 / steps:9.1f} {calls[n] / steps:6.1f} {mfma} {gf} {tf} {ldsc} {bw}  {n[:100]}")
 
 
 if __name__ == "__main__":

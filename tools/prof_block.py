@@ -15,6 +15,7 @@ from dct_amd.ops.fused_mlp import FusedMLPKernel, mlp_num_params  # noqa: E402
 
 PHASES = ["F1 h1 + keep ballots", "F2 partials + prefetch", "barrier", "F2r h2 (8 partials)",
           "logits + loss", "dZ2, W2/b2/b1 Adam", "dX reduce-scatter", "dW0/db0 Adam", "dW1 + Adam"]
+ONCE = ["prologue (per launch)", "epilogue (per launch)"]
 
 
 def main():
@@ -38,12 +39,15 @@ def main():
     k.train(p, m, v, X, Y, idx, steps * 4, 4, steps, 0, 0.01, dropout=0.2, loss_out=loss, prof=prof)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    pr = prof.cpu().view(8, 16)[:, :len(PHASES)].double() / steps
+    raw = prof.cpu().view(8, 16).double()
+    pr = raw[:, :len(PHASES)] / steps
     print(f"stamped launch: {dt / steps * 1e6:.3f} us/step (stamps included)")
     print("cycles per step        " + "".join(f"  wave{w}" for w in range(8)))
     for i, name in enumerate(PHASES):
         print(f"{name:24s}" + "".join(f"{pr[w, i].item():7.0f}" for w in range(8)))
     print(f"{'total':24s}" + "".join(f"{pr[w].sum().item():7.0f}" for w in range(8)))
+    for i, name in enumerate(ONCE):
+        print(f"{name:24s}" + "".join(f"{raw[w, 9 + i].item():7.0f}" for w in range(8)))
 
 
 if __name__ == "__main__":
