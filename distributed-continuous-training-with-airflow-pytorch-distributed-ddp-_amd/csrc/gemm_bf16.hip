@@ -228,14 +228,16 @@ typedef __attribute__((address_space(3))) void lds_void;
 __device__ __forceinline__ int mc_swz(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
 
 // one ROWS x 64 operand tile -> LDS image (ROWS/32 glds per thread; the MC image is 128 wide)
-template <bool MC, int ROWS = 128>
+template <bool MC, int ROWS = 128, int NT = 256>
 __device__ __forceinline__ void g2_fill(const uint16_t* __restrict__ G, int ld, int R, int r0, int k0, char* img) {
   static_assert(ROWS == 128 || !MC, "k-major (MC) images are 128 columns wide");
+  constexpr int CH = (MC ? 1024 : ROWS * 8) / NT;  // 16-B chunks per thread
+  static_assert(CH >= 1 && CH * NT == (MC ? 1024 : ROWS * 8), "whole chunks per thread");
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
 #pragma unroll
-  for (int q = 0; q < ROWS / 32; ++q) {
-    const int L = q * 256 + wave * 64 + lane;  // linear 16-B chunk of the image
+  for (int q = 0; q < CH; ++q) {
+    const int L = q * NT + wave * 64 + lane;  // linear 16-B chunk of the image
     const uint16_t* src;
     if (!MC) {
       const int r = L >> 3, pc = L & 7;
@@ -254,7 +256,7 @@ __device__ __forceinline__ void g2_fill(const uint16_t* __restrict__ G, int ld, 
     // (it cannot prove the DMA does not alias them), serialising the prefetch with the MFMAs.
     // Completion is counted by hand: the k-loop's "s_waitcnt vmcnt(0)" before its barrier.
     const uint32_t dst = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(lds_void*)(img + (q * 256 + wave * 64) * 16));
+        (uint32_t)(uintptr_t)(lds_void*)(img + (q * NT + wave * 64) * 16));
     uint32_t keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -333,10 +335,14 @@ __device__ __forceinline__ int xcd_wgid() {
   return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
 }
 
-template <bool TA, bool TB, bool SPLIT, int BM, int S>
+// WM: waves along M (2: 256 threads, 2 x 2 waves; 4: 512 threads, 4 x 2 waves - two waves per SIMD
+// on a one-tile-per-CU grid, so one wave's LDS reads / waits overlap the other's MFMAs).
+template <bool TA, bool TB, bool SPLIT, int BM, int S, int WM = 2>
 __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wgid) {
   static_assert(BM == 128 || (BM == 64 && !TA), "BM = 64 needs a row-major (KC) A image");
-  constexpr int IM = BM / 32;  // 16-row MFMA tiles per wave (2 x 2 waves)
+  static_assert(WM == 2 || (WM == 4 && !SPLIT && BM == 128), "8-wave tiles: 128 x 128, no split-K");
+  constexpr int NT = 128 * WM;
+  constexpr int IM = BM / (16 * WM);  // 16-row MFMA tiles per wave (WM x 2 waves)
   extern __shared__ __attribute__((aligned(16))) char smem2[];
   // [buf][A,B] images of 16 KB each
   constexpr bool AMC = TA, BMC = !TB;
@@ -363,12 +369,13 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
   auto img = [&](int buf, int op) -> char* { return smem2 + (buf * 2 + op) * G2_BYTES; };
   auto fill = [&](int buf, int kt) {
     const int k0 = kt * GBK;
-    if (!TA) g2_fill<false, BM>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
-    else g2_fill<true>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
-    if (TB) g2_fill<false>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
-    else g2_fill<true>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
+    if (!TA) g2_fill<false, BM, NT>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
+    else g2_fill<true, 128, NT>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
+    if (TB) g2_fill<false, 128, NT>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
+    else g2_fill<true, 128, NT>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
   };
-  constexpr int FILL_OPS = (TA ? 4 : BM / 32) + 4;  // global_load_lds per thread per fill (A + B)
+  // global_load_lds per thread per fill (A + B)
+  constexpr int FILL_OPS = ((TA ? 1024 : BM * 8) + 1024) / NT;
   const int n = kt1 - kt0;
   if (n > 0) {
 #pragma unroll
@@ -385,7 +392,7 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
       for (int ks = 0; ks < GBK / 32; ++ks) {
         bf16x8 af[IM], bfr[4];
 #pragma unroll
-        for (int i = 0; i < IM; ++i) af[i] = g2_frag<AMC>(ai, wr * (BM / 2) + i * 16, ks, lane);
+        for (int i = 0; i < IM; ++i) af[i] = g2_frag<AMC>(ai, wr * (BM / WM) + i * 16, ks, lane);
 #pragma unroll
         for (int j = 0; j < 4; ++j) bfr[j] = g2_frag<BMC>(bi, wc * 64 + j * 16, ks, lane);
         if (do_cs) {  // fused bias gradient: row sums of the A fragments (lane: 8 k of row l&15)
@@ -409,7 +416,7 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
       float v = cs[i];
       v += __shfl_xor(v, 16);
       v += __shfl_xor(v, 32);
-      const int row = m0 + wr * (BM / 2) + i * 16 + (lane & 15);
+      const int row = m0 + wr * (BM / WM) + i * 16 + (lane & 15);
       if (lane < 16 && row < g.M) atomicAdd(g.colsum + row, v);
     }
   }
@@ -473,7 +480,7 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
         if (col >= g.N) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wr * (BM / 2) + i * 16 + row_l + r;
+          const int row = m0 + wr * (BM / WM) + i * 16 + row_l + r;
           if (row < g.M) {
             float* dst = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
             const float v = sum[(i * 4 + j) * 4 + r] * g.alpha;
@@ -494,7 +501,7 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
         if (col >= g.N) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wr * (BM / 2) + i * 16 + row_l + r;
+          const int row = m0 + wr * (BM / WM) + i * 16 + row_l + r;
           if (row < g.M) part[(size_t)row * g.N + col] = acc[i][j][r];
         }
       }
@@ -510,7 +517,7 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
         if (col >= g.N) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wr * (BM / 2) + i * 16 + row_l + r;
+          const int row = m0 + wr * (BM / WM) + i * 16 + row_l + r;
           if (row < g.M) {
             float* dst = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
             if (g.split_probe) *dst = acc[i][j][r] * g.alpha;
@@ -527,7 +534,7 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
                       (!g.aux || (((uintptr_t)g.aux) & 7) == 0);
 #pragma unroll
   for (int i = 0; i < IM; ++i) {
-    const int row = m0 + wr * (BM / 2) + i * 16 + c16;
+    const int row = m0 + wr * (BM / WM) + i * 16 + c16;
     if (row >= g.M) continue;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -626,9 +633,9 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
   }
 }
 
-template <bool TA, bool TB, bool SPLIT, int BM = 128, int S = 2>
-__global__ __launch_bounds__(GNT, BM == 64 ? 4 : 2) void gemm2_kernel(GemmArgs g, int splits) {
-  gemm2_body<TA, TB, SPLIT, BM, S>(g, splits, xcd_wgid());
+template <bool TA, bool TB, bool SPLIT, int BM = 128, int S = 2, int WM = 2>
+__global__ __launch_bounds__(128 * WM, WM == 4 ? 2 : (BM == 64 ? 4 : 2)) void gemm2_kernel(GemmArgs g, int splits) {
+  gemm2_body<TA, TB, SPLIT, BM, S, WM>(g, splits, xcd_wgid());
 }
 
 // Grouped split-K launch: up to DW_GROUP independent problems (the dW GEMMs of one transformer
@@ -872,14 +879,19 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
     if (e != hipSuccess) return e;
   }
   const int nk_slice = (nk + splits - 1) / splits;
-  auto launch = [&](auto fn, int grid, int stages) -> hipError_t {
+  auto launch = [&](auto fn, int grid, int stages, int threads = dct::GNT) -> hipError_t {
     // one k-tile -> one LDS stage; otherwise `stages` stages of A + B images
     const size_t lds = (size_t)(nk_slice > 1 ? 2 * stages : 2) * dct::G2_BYTES;
     hipError_t err = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (err != hipSuccess) return err;
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(dct::GNT), lds, st, g, splits);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(threads), lds, st, g, splits);
     return hipGetLastError();
   };
+  // DCT_GEMM_8W=1: one 128 x 128 tile per CU worked by 8 waves (two per SIMD) with three k-tiles in
+  // flight (4 LDS stages, 128 KB) for grids of at most one tile per CU
+  const char* w8e = getenv("DCT_GEMM_8W");
+  if (w8e && w8e[0] == '1' && splits == 1 && tiles <= device_cus() && nk >= 4)
+    return launch(dct::gemm2_kernel<TA, TB, false, 128, 4, 4>, tiles, 4, 512);
   if constexpr (!TA) {
     // small K and too few 128-row tiles to fill 256 CUs several times over: half-height tiles
     const bool force128 = getenv("DCT_GEMM_BM128") != nullptr;

@@ -35,14 +35,15 @@ constexpr int XT = 0;                    // [3][DMAX][4] input tile, transposed 
 constexpr int LAB = XT + 3 * DMAX * 4;   // [3][4] labels (int)
 constexpr int MSK = LAB + 12;            // [2][NW][2] hidden-2 dropout keep ballots (uint64 per wave)
 constexpr int H1W = MSK + 2 * NW * 2;    // [NW][KS][4] wave-private layer-1 inputs h1[k][row]
+constexpr int H1X = H1W + NW * KS * 4;   // [NW][4][KS] the same tile transposed (MFMA A operands)
 constexpr int PSTR = 36;                 // partials: [o][wave][4] with a 36-float o stride
-constexpr int PART = H1W + NW * KS * 4;  // [2][H][PSTR]
+constexpr int PART = H1X + NW * KS * 4;  // [2][H][PSTR]
 constexpr int W2L = PART + 2 * H * PSTR; // [2][H][4] last-layer weights W2[c][o] (o-major), published by owners
 constexpr int B1L = W2L + 2 * H * 4;     // [2][H] b1
 constexpr int B2L = B1L + 2 * H;         // [2][4] b2
 constexpr int TOTAL = B2L + 8;
 static_assert((H1W % 4) == 0 && (PART % 4) == 0 && (MSK % 4) == 0 && (LAB % 4) == 0 && (W2L % 4) == 0 &&
-              (B1L % 4) == 0 && (B2L % 4) == 0, "16-B aligned tiles");
+              (B1L % 4) == 0 && (B2L % 4) == 0 && (H1X % 4) == 0, "16-B aligned tiles");
 }  // namespace blk2
 
 namespace b2d {
@@ -118,6 +119,15 @@ __device__ __forceinline__ float sel4(const float (&v)[4], int i) {
   return i == 0 ? v[0] : (i == 1 ? v[1] : (i == 2 ? v[2] : v[3]));
 }
 
+// v_mfma_f32_4x4x1_16b_f32: 16 independent 4x4 outer products per wave, exact fp32 (an fmaf chain),
+// on the matrix pipe - beside the partner wave's VALU work.  Block b = lane / 4: A[b][m] comes from
+// lane 4b + m, B[b][n] from lane 4b + n, and lane 4b + n holds C[b][m = 0..3][n] in its 4 registers
+// (tools/probes/mfma4x4_probe.hip checks the maps).
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
+}
+
 template <int N>
 __device__ __forceinline__ float sel4c(const float (&v)[N], int i) {
   float r = v[0];
@@ -142,7 +152,7 @@ __device__ __forceinline__ float rl(float v, int lane) {
 
 // ND: input slices per lane (D0 <= 4 * ND); CM: class capacity (2 or 4); ADAM: train mode vs
 // grad mode (gradients + loss to grad_out).
-template <int ND, int CM, bool ADAM, bool PROF = false>
+template <int ND, int CM, bool ADAM, bool PROF = false, bool MF = false>
 __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, MlpArgs a) {
   using namespace blk2;
   using namespace b2d;
@@ -253,6 +263,7 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
   const float l2b1 = log2f(a.b1), l2b2 = log2f(a.b2);
   const float c1 = 1.f - a.b1, c2 = 1.f - a.b2;
   float* h1w = lds + H1W + w * (KS * 4);
+  float* h1x = lds + H1X + w * (KS * 4);
   int xb = 0;
   if constexpr (PROF) {
     t_last = __builtin_amdgcn_s_memtime();
@@ -294,6 +305,7 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
       }
       h1 = z;
       h1w[l] = z;  // [k = l / 4][row = l % 4]
+      if constexpr (MF) h1x[r0 * KS + (l >> 2)] = z;  // [row][k]
     }
     // keep bits of the layer-1 outputs: wave w hashes (row w / 2, unit 64 (w % 2) + l)
     if (drop) {
@@ -309,14 +321,33 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
     // ---- F2: this wave's k-slice partials of all 128 outputs x 4 rows
     {
       float acc[2][4] = {};
+      if constexpr (MF) {
+        // out[o = l + 64j][r] = sum_k h[k][r] W[o][k]: A = h[k][lane % 4] (the transposed tile),
+        // B = this lane's own weight, C lands as acc[j][r] of output o = l + 64j
+        f32x4_t cj[2] = {(f32x4_t){0.f, 0.f, 0.f, 0.f}, (f32x4_t){0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        if ((kk & 3) == 0) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted tile loads (VGPRs)
-        const float4 h = *reinterpret_cast<const float4*>(h1w + kk * 4);
+        for (int q = 0; q < KS / 4; ++q) {
+          const float4 hq = *reinterpret_cast<const float4*>(h1x + r0 * KS + 4 * q);
+          const float hv[4] = {hq.x, hq.y, hq.z, hq.w};
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc[j][0] += w1[j][kk] * h.x; acc[j][1] += w1[j][kk] * h.y;
-          acc[j][2] += w1[j][kk] * h.z; acc[j][3] += w1[j][kk] * h.w;
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) cj[j] = mfma4(hv[e], w1[j][4 * q + e], cj[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[j][r] = cj[j][r];
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+          if ((kk & 3) == 0) __builtin_amdgcn_sched_barrier(0);  // bound the hoisted tile loads (VGPRs)
+          const float4 h = *reinterpret_cast<const float4*>(h1w + kk * 4);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            acc[j][0] += w1[j][kk] * h.x; acc[j][1] += w1[j][kk] * h.y;
+            acc[j][2] += w1[j][kk] * h.z; acc[j][3] += w1[j][kk] * h.w;
+          }
         }
       }
       float* part = lds + PART + (s & 1) * (H * PSTR);
@@ -519,15 +550,37 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
     // ---- dW1 + Adam in registers
     int gb1 = wo1 + l * H + KS * w;  // grad mode: opaque per step, so 32 store addresses are not hoisted
     if (!ADAM) asm volatile("" : "+v"(gb1));
+    if constexpr (MF) {
+      // dW1[o = l + 64j][k = 4q + m] = sum_r h1[k][r] dZ2[o][r]: A = h1[4q + lane % 4][r] (one b128 of
+      // the tile per q), B = this lane's dZ2, C register m = the gradient of its own w1[j][4q + m]
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-      if ((kk & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-      const float4 h = *reinterpret_cast<const float4*>(h1w + kk * 4);
+      for (int q = 0; q < KS / 4; ++q) {
+        const float4 hq = *reinterpret_cast<const float4*>(h1w + (4 * q + r0) * 4);
+        const float hv[4] = {hq.x, hq.y, hq.z, hq.w};
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const float gw = dz2[j][0] * h.x + dz2[j][1] * h.y + dz2[j][2] * h.z + dz2[j][3] * h.w;
-        if (ADAM) adam_lean(w1[j][kk], gw, m1[j][kk], v1[j][kk], c1, a.b2, c2, a.wd, aA, aE);
-        else a.grad_out[gb1 + 64 * j * H + kk] = gw;
+        for (int j = 0; j < 2; ++j) {
+          f32x4_t g = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) g = mfma4(hv[r], dz2[j][r], g);
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const int kk = 4 * q + m;
+            if (ADAM) adam_lean(w1[j][kk], g[m], m1[j][kk], v1[j][kk], c1, a.b2, c2, a.wd, aA, aE);
+            else a.grad_out[gb1 + 64 * j * H + kk] = g[m];
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        if ((kk & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+        const float4 h = *reinterpret_cast<const float4*>(h1w + kk * 4);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float gw = dz2[j][0] * h.x + dz2[j][1] * h.y + dz2[j][2] * h.z + dz2[j][3] * h.w;
+          if (ADAM) adam_lean(w1[j][kk], gw, m1[j][kk], v1[j][kk], c1, a.b2, c2, a.wd, aA, aE);
+          else a.grad_out[gb1 + 64 * j * H + kk] = gw;
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();  // the next step rewrites this wave's h1 tile
@@ -601,8 +654,15 @@ hipError_t mlp_launch_block2(const MlpShape& sh, const MlpArgs& a, hipStream_t s
     if (tr) hipLaunchKernelGGL((mlp_block2_kernel<ND, CM, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a); \
     else hipLaunchKernelGGL((mlp_block2_kernel<ND, CM, false>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);  \
   } while (0)
+  // DCT_MLP_BLOCK_MF=1: F2 and dW1 on the 4x4x1 fp32 MFMA (weather shape D0 <= 8, C <= 2)
+  const char* mfe = getenv("DCT_MLP_BLOCK_MF");
+  const bool mf = mfe && mfe[0] == '1' && d0 <= 8 && C <= 2;
   if (a.prof) {
-    hipLaunchKernelGGL((mlp_block2_kernel<2, 2, true, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);
+    if (mf) hipLaunchKernelGGL((mlp_block2_kernel<2, 2, true, true, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);
+    else hipLaunchKernelGGL((mlp_block2_kernel<2, 2, true, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);
+  } else if (mf) {
+    if (tr) hipLaunchKernelGGL((mlp_block2_kernel<2, 2, true, false, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);
+    else hipLaunchKernelGGL((mlp_block2_kernel<2, 2, false, false, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);
   } else if (d0 <= 8) {
     if (C <= 2) B2K(2, 2); else B2K(2, 4);
   } else {

@@ -37,7 +37,7 @@ def test_native_loaded_and_arch():
     assert "gfx950" in nat.arch_name(0)
 
 
-@pytest.mark.parametrize("kernel", ["auto", "lds", "lds-noblock", "lds-v1"])
+@pytest.mark.parametrize("kernel", ["auto", "lds", "lds-noblock", "lds-v1", "lds-mf"])
 @pytest.mark.parametrize("loss", ["ce", "mse"])
 @pytest.mark.parametrize("dims,B", [([5, 64, 2], 4), ([5, 128, 128, 2], 4), ([5, 64, 2], 3), ([9, 48, 64, 3], 4),
                                     ([16, 32, 48, 32, 3], 16), ([5, 128, 128, 2], 16), ([7, 20, 2], 9),
@@ -45,6 +45,7 @@ def test_native_loaded_and_arch():
 def test_fused_train_matches_torch_adam(dims, B, loss, kernel, cuda, monkeypatch):
     monkeypatch.setenv("DCT_MLP_KERNEL", kernel.split("-")[0])
     monkeypatch.setenv("DCT_MLP_BLOCK", "0" if kernel.endswith("noblock") else ("v1" if kernel.endswith("v1") else "1"))
+    monkeypatch.setenv("DCT_MLP_BLOCK_MF", "1" if kernel.endswith("mf") else "0")
     torch.manual_seed(1)
     N, n_items = 301, 50
     X = torch.randn(N, dims[0])
@@ -80,12 +81,13 @@ def test_fused_train_matches_torch_adam(dims, B, loss, kernel, cuda, monkeypatch
     assert torch.allclose(m.cpu(), ref_m, atol=1e-4, rtol=1e-2)
 
 
-@pytest.mark.parametrize("kernel", ["auto", "lds", "lds-noblock", "lds-v1"])
+@pytest.mark.parametrize("kernel", ["auto", "lds", "lds-noblock", "lds-v1", "lds-mf"])
 @pytest.mark.parametrize("dims,B", [([5, 64, 2], 4), ([5, 128, 128, 2], 4), ([12, 40, 40, 5], 13),
                                     ([9, 48, 64, 3], 4), ([20, 128, 128, 4], 3), ([32, 128, 128, 1], 4)])
 def test_fused_grad_mode_matches_autograd(dims, B, kernel, cuda, monkeypatch):
     monkeypatch.setenv("DCT_MLP_KERNEL", kernel.split("-")[0])
     monkeypatch.setenv("DCT_MLP_BLOCK", "0" if kernel.endswith("noblock") else ("v1" if kernel.endswith("v1") else "1"))
+    monkeypatch.setenv("DCT_MLP_BLOCK_MF", "1" if kernel.endswith("mf") else "0")
     torch.manual_seed(2)
     N = 64
     X = torch.randn(N, dims[0])
@@ -119,8 +121,9 @@ def test_block_kernel_matches_lds_kernel_with_dropout(dims, B, D0, cuda, monkeyp
     p0 = _flat(_ref_net(dims)).to(cuda)
     steps = math.ceil(n_items / B)
     out = {}
-    for blk in ("1", "v1", "0"):
-        monkeypatch.setenv("DCT_MLP_BLOCK", blk)
+    for blk in ("1", "1mf", "v1", "0"):
+        monkeypatch.setenv("DCT_MLP_BLOCK", blk[:2] if blk != "1mf" else "1")
+        monkeypatch.setenv("DCT_MLP_BLOCK_MF", "1" if blk == "1mf" else "0")
         p, m, v = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
         losses = torch.zeros(steps, device=cuda)
         k = FusedMLPKernel(dims, bmax=4)
@@ -128,7 +131,7 @@ def test_block_kernel_matches_lds_kernel_with_dropout(dims, B, D0, cuda, monkeyp
                 step_base=5, loss_out=losses)
         torch.cuda.synchronize()
         out[blk] = (p.cpu(), m.cpu(), v.cpu(), losses.cpu())
-    for blk in ("1", "v1"):
+    for blk in ("1", "1mf", "v1"):
         for a_, b_ in zip(out[blk], out["0"]):
             assert torch.isfinite(a_).all()
             assert (a_ - b_).abs().max() <= 1e-4 * (1 + b_.abs().max()), (blk, float((a_ - b_).abs().max()))
@@ -269,6 +272,28 @@ def test_gemm_pipeline_depths(M, N, K, ta, tb, out_f32, stages, cuda, monkeypatc
     ref = (A.float().t() if ta else A.float()) @ (B.float().t() if tb else B.float())
     tol = 2e-3 * math.sqrt(K) if out_f32 else 0.02 * math.sqrt(K)
     assert (C.float() - ref).abs().max().item() < tol, (C.float() - ref).abs().max().item()
+
+
+@pytest.mark.parametrize("M,N,K,ta,tb", [
+    (4096, 1024, 1024, 0, 1),  # tabular forward layer: 256 tiles, one per CU
+    (4096, 1024, 1024, 0, 0),  # tabular dX layer (transposed-read B image)
+    (1024, 512, 256, 1, 0),    # transposed A image, 4 k-tiles (the prologue fills the whole loop)
+    (300, 200, 512, 0, 1),     # ragged tile edges
+])
+def test_gemm_8wave_tiles(M, N, K, ta, tb, cuda, monkeypatch):
+    """DCT_GEMM_8W=1: 128 x 128 tiles worked by 8 waves (4 x 2, two per SIMD) with 4 LDS stages, with
+    the bias + ReLU epilogue, bf16 out, against the fp32 torch reference of the same bf16 operands."""
+    monkeypatch.setenv("DCT_GEMM_8W", "1")
+    torch.manual_seed(13)
+    A = _bf(torch.randn(K, M, device=cuda) if ta else torch.randn(M, K, device=cuda))
+    B = _bf(torch.randn(N, K, device=cuda) if tb else torch.randn(K, N, device=cuda))
+    bias = torch.randn(N, device=cuda)
+    C = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    native().gemm_bf16(A.data_ptr(), B.data_ptr(), C.data_ptr(), bias.data_ptr(), M, N, K, A.stride(0), B.stride(0), N,
+                       ta, tb, 2, 0, 0, 0, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ref = torch.relu((A.float().t() if ta else A.float()) @ (B.float().t() if tb else B.float()) + bias)
+    assert (C.float() - ref).abs().max().item() < 0.02 * math.sqrt(K)
 
 
 @pytest.mark.parametrize("two_pass", ["1", "0", "auto"])
