@@ -42,6 +42,14 @@ constexpr int W2L = PART + 2 * H * PSTR; // [2][H][4] last-layer weights W2[c][o
 constexpr int B1L = W2L + 2 * H * 4;     // [2][H] b1
 constexpr int B2L = B1L + 2 * H;         // [2][4] b2
 constexpr int TOTAL = B2L + 8;
+// prologue / epilogue only: W1 (or a moment) staged as [128][128] with the 16-B slot of row r
+// XOR-swizzled by r % 16, so the per-lane row-segment reads/writes (16 lanes = 16 rows of one
+// column slot) hit 16 distinct slots - conflict-free ds_read/write_b128; aliases the step tiles
+constexpr int STG = H * H;
+constexpr int STG_LD = STG / 4 / NT;  // 16-B pieces per thread
+constexpr int LDS_FLOATS = TOTAL > STG ? TOTAL : STG;
+static_assert(LDS_FLOATS * 4 <= 65536, "fits the default dynamic-LDS limit");
+__device__ __forceinline__ int stg_slot(int r, int c) { return r * H + 4 * (c ^ (r & 15)); }
 static_assert((H1W % 4) == 0 && (PART % 4) == 0 && (MSK % 4) == 0 && (LAB % 4) == 0 && (W2L % 4) == 0 &&
               (B1L % 4) == 0 && (B2L % 4) == 0 && (H1X % 4) == 0, "16-B aligned tiles");
 }  // namespace blk2
@@ -179,27 +187,62 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
     step_base = (uint32_t)t0;
   }
 
-  // ---- registers: W1 k-slice + moments; W0 slices; replicated W2 / b1 / b2 (+ moments)
-  // a lane's 16 weights of one output row are contiguous: 16-byte loads (mlp_block2_ok checks the
-  // alignment), all issued before the first use - the prologue is one memory round trip
+  // ---- first batch: row index, then the values, into registers now (the LDS tile is written after
+  // the W1 staging below, which aliases it) - the dependent chain overlaps the W1 round trip
+  const int Bsz = a.B;
+  const int bs0 = min(Bsz, a.n_items - cur0 * Bsz);
+  float x_first = 0.f;
+  int lab_first = 0;
+  if (tid < B * DMAX) {
+    const int b = tid & 3, d = tid >> 2;
+    if (b < bs0 && d < D0) x_first = a.X[(size_t)a.idx[cur0 * Bsz + b] * a.ldx + d];
+  }
+  if (tid < B && tid < bs0) lab_first = a.Y[a.idx[cur0 * Bsz + tid]];
+
+  // ---- registers: W1 k-slice + moments; W0 slices; replicated W2 / b1 / b2 (+ moments).
+  // W1 comes in COALESCED (thread t: 16-byte pieces t, t + 512, ... of the flat [128][128] block)
+  // and is redistributed through LDS: a lane's own 16-float row segments are 512 B apart, so
+  // loading them directly costs one 64-B request per lane per load (4x the coalesced count;
+  // measured ~17k cycles of prologue).  All 24 loads are issued before the first use.
   float w1[2][KS], m1[2][KS], v1[2][KS];
+  {
+    int tq = tid;
+    float4 stg[3][STG_LD];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int q = 0; q < KS / 4; ++q) {
-      const int f = wo1 + (l + 64 * j) * H + KS * w + 4 * q;
-      const float4 tp = *reinterpret_cast<const float4*>(a.p + f);
-      w1[j][4 * q] = tp.x; w1[j][4 * q + 1] = tp.y; w1[j][4 * q + 2] = tp.z; w1[j][4 * q + 3] = tp.w;
+    for (int i = 0; i < STG_LD; ++i) {
+      const int f = wo1 + 4 * (i * NT + tq);
+      stg[0][i] = *reinterpret_cast<const float4*>(a.p + f);
       if (ADAM) {
-        const float4 tm = *reinterpret_cast<const float4*>(a.m + f);
-        const float4 tv = *reinterpret_cast<const float4*>(a.v + f);
-        m1[j][4 * q] = tm.x; m1[j][4 * q + 1] = tm.y; m1[j][4 * q + 2] = tm.z; m1[j][4 * q + 3] = tm.w;
-        v1[j][4 * q] = tv.x; v1[j][4 * q + 1] = tv.y; v1[j][4 * q + 2] = tv.z; v1[j][4 * q + 3] = tv.w;
-      } else {
-        m1[j][4 * q] = m1[j][4 * q + 1] = m1[j][4 * q + 2] = m1[j][4 * q + 3] = 0.f;
-        v1[j][4 * q] = v1[j][4 * q + 1] = v1[j][4 * q + 2] = v1[j][4 * q + 3] = 0.f;
+        stg[1][i] = *reinterpret_cast<const float4*>(a.m + f);
+        stg[2][i] = *reinterpret_cast<const float4*>(a.v + f);
       }
     }
+#pragma unroll
+    for (int arr = 0; arr < (ADAM ? 3 : 1); ++arr) {
+      if (arr) __syncthreads();  // the previous array's reads are done
+#pragma unroll
+      for (int i = 0; i < STG_LD; ++i) {
+        const int g = i * NT + tq;
+        *reinterpret_cast<float4*>(lds + stg_slot(g >> 5, g & 31)) = stg[arr][i];
+      }
+      __syncthreads();
+      float(&dst)[2][KS] = arr == 0 ? w1 : (arr == 1 ? m1 : v1);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < KS / 4; ++q) {
+          const float4 t4 = *reinterpret_cast<const float4*>(lds + stg_slot(l + 64 * j, 4 * w + q));
+          dst[j][4 * q] = t4.x; dst[j][4 * q + 1] = t4.y; dst[j][4 * q + 2] = t4.z; dst[j][4 * q + 3] = t4.w;
+        }
+    }
+    if (!ADAM) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int k = 0; k < KS; ++k) m1[j][k] = v1[j][k] = 0.f;
+    }
+    __syncthreads();  // staging reads done before the tiles (same LDS) are zeroed
+  }
   float w0[ND], m0[ND], v0[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) {
@@ -229,19 +272,10 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
   float pb2 = own_b2 ? a.p[fb2] : 0.f, mb2 = (own_b2 && ADAM) ? a.m[fb2] : 0.f, vb2 = (own_b2 && ADAM) ? a.v[fb2] : 0.f;
 
   // ---- LDS: first batch into input buffer 0
-  for (int e = tid; e < TOTAL; e += NT) lds[e] = 0.f;
+  for (int e = 4 * tid; e < TOTAL; e += 4 * NT) *reinterpret_cast<float4*>(lds + e) = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
-  const int Bsz = a.B;
-  {
-    const int bs0 = min(Bsz, a.n_items - cur0 * Bsz);
-    if (tid < B * DMAX) {
-      const int b = tid & 3, d = tid >> 2;
-      float x = 0.f;
-      if (b < bs0 && d < D0) x = a.X[(size_t)a.idx[cur0 * Bsz + b] * a.ldx + d];
-      lds[XT + d * 4 + b] = x;
-    }
-    if (tid < B) reinterpret_cast<int*>(lds + LAB)[tid] = (tid < bs0) ? a.Y[a.idx[cur0 * Bsz + tid]] : 0;
-  }
+  if (tid < B * DMAX) lds[XT + (tid >> 2) * 4 + (tid & 3)] = x_first;
+  if (tid < B) reinterpret_cast<int*>(lds + LAB)[tid] = lab_first;
   if (own_w2) lds[W2L + (l + 64 * jw) * 4 + cw] = pw2;  // classes >= C stay 0 (zeroed above)
   if (own_b1) lds[B1L + l + 64 * jb] = pb1;
   if (own_b2) lds[B2L + l] = pb2;
@@ -595,18 +629,28 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
   // ---- write back parameters and moments (flat torch order).  The base offset is made opaque so
   // the compiler recomputes these addresses here instead of keeping the prologue's load addresses
   // (3 x 32 pointers) live across the step loop - that alone cost ~90 spilled VGPRs.
-  int lo = l, uo = u;
-  asm volatile("" : "+v"(lo), "+v"(uo));
-  const int fw1 = wo1 + lo * H + KS * w;
+  int lo = l, uo = u, to = tid;
+  asm volatile("" : "+v"(lo), "+v"(uo), "+v"(to));
+  // W1 + moments leave through the same LDS staging as they came in: coalesced 16-byte stores
+  __syncthreads();  // every wave is past its last use of the step tiles (the staging aliases them)
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int arr = 0; arr < 3; ++arr) {
+    if (arr) __syncthreads();  // the previous array's reads are done
+    const float(&src)[2][KS] = arr == 0 ? w1 : (arr == 1 ? m1 : v1);
 #pragma unroll
-    for (int q = 0; q < KS / 4; ++q) {
-      const int f = fw1 + 64 * j * H + 4 * q;
-      *reinterpret_cast<float4*>(a.p + f) = make_float4(w1[j][4 * q], w1[j][4 * q + 1], w1[j][4 * q + 2], w1[j][4 * q + 3]);
-      *reinterpret_cast<float4*>(a.m + f) = make_float4(m1[j][4 * q], m1[j][4 * q + 1], m1[j][4 * q + 2], m1[j][4 * q + 3]);
-      *reinterpret_cast<float4*>(a.v + f) = make_float4(v1[j][4 * q], v1[j][4 * q + 1], v1[j][4 * q + 2], v1[j][4 * q + 3]);
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < KS / 4; ++q)
+        *reinterpret_cast<float4*>(lds + stg_slot(lo + 64 * j, 4 * w + q)) =
+            make_float4(src[j][4 * q], src[j][4 * q + 1], src[j][4 * q + 2], src[j][4 * q + 3]);
+    __syncthreads();
+    float* dst = arr == 0 ? a.p : (arr == 1 ? a.m : a.v);
+#pragma unroll
+    for (int i = 0; i < STG_LD; ++i) {
+      const int g = i * NT + to;
+      *reinterpret_cast<float4*>(dst + wo1 + 4 * g) = *reinterpret_cast<const float4*>(lds + stg_slot(g >> 5, g & 31));
     }
+  }
 #pragma unroll
   for (int i = 0; i < ND; ++i) {
     const int d = r0 + 4 * i;
@@ -648,15 +692,16 @@ bool mlp_block2_ok(const MlpShape& sh, const MlpArgs& a) {
 hipError_t mlp_launch_block2(const MlpShape& sh, const MlpArgs& a, hipStream_t st) {
   const int d0 = sh.dims[0], C = sh.dims[3];
   const bool tr = a.mode == 0;
-  const size_t bytes = (size_t)blk2::TOTAL * sizeof(float);
+  const size_t bytes = (size_t)blk2::LDS_FLOATS * sizeof(float);
 #define B2K(ND, CM)                                                                                     \
   do {                                                                                                  \
     if (tr) hipLaunchKernelGGL((mlp_block2_kernel<ND, CM, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a); \
     else hipLaunchKernelGGL((mlp_block2_kernel<ND, CM, false>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);  \
   } while (0)
-  // DCT_MLP_BLOCK_MF=1: F2 and dW1 on the 4x4x1 fp32 MFMA (weather shape D0 <= 8, C <= 2)
+  // weather shape (D0 <= 8, C <= 2): F2 and dW1 on the 4x4x1 fp32 MFMA by default (5.09 vs 5.25
+  // us/step on MI355X, profiles/block2_mf_ab_r3.log); DCT_MLP_BLOCK_MF=0 selects the VALU variant
   const char* mfe = getenv("DCT_MLP_BLOCK_MF");
-  const bool mf = mfe && mfe[0] == '1' && d0 <= 8 && C <= 2;
+  const bool mf = !(mfe && mfe[0] == '0') && d0 <= 8 && C <= 2;
   if (a.prof) {
     if (mf) hipLaunchKernelGGL((mlp_block2_kernel<2, 2, true, true, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);
     else hipLaunchKernelGGL((mlp_block2_kernel<2, 2, true, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);

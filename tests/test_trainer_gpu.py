@@ -77,11 +77,14 @@ def test_bench_contract_single_gpu():
     assert out["extra"]["losses_finite"]
 
 
+@pytest.mark.parametrize("hidden", [(64,), (128, 128)])
 @pytest.mark.parametrize("fused_update", ["1", "0"])
 @pytest.mark.parametrize("graph", ["1", "0"])
-def test_ddp_step_path_world1_matches_persistent(fused_update, graph, monkeypatch):
+def test_ddp_step_path_world1_matches_persistent(fused_update, graph, hidden, monkeypatch):
     """The DDP step loop (native RCCL comm, graph chunks, device cursor/step counter,
-    update-then-grad) at world size 1 must reproduce the persistent single-launch path."""
+    update-then-grad) at world size 1 must reproduce the persistent single-launch path - for the
+    reference 5-64-2 and for BASELINE's 3-layer 128-h MLP (grad-mode block kernel + flat Adam,
+    the path its DDP=8 run takes)."""
     from dct_amd.parallel.dist import init_distributed
     from dct_amd.trainer.engines import FusedMLPEngine, adam_hparams_from
 
@@ -94,7 +97,7 @@ def test_ddp_step_path_world1_matches_persistent(fused_update, graph, monkeypatc
         monkeypatch.setenv("DCT_GRAPH_CHUNK", "7")
         monkeypatch.setenv("DCT_FUSED_UPDATE", fused_update)
         torch.manual_seed(0)
-        model = MLPClassifier(5, hidden=(64,), dropout=0.0)
+        model = MLPClassifier(5, hidden=hidden, dropout=0.0)
         ctx = init_distributed("gpu")
         eng = FusedMLPEngine(model, ctx, 4, seed=42, adam=adam_hparams_from(model.configure_optimizers()))
         eng.attach_data(x, y, rows[:2400], rows[2400:])
@@ -110,9 +113,12 @@ def test_ddp_step_path_world1_matches_persistent(fused_update, graph, monkeypatc
     p1, m1, l1, e1 = run("1")
     assert e1.ddp and e1.comm is not None
     assert e1.graph_used == (graph == "1")
-    assert torch.allclose(l0, l1, atol=1e-5), (l0 - l1).abs().max()
-    assert (p0 - p1).abs().max() < 1e-3 and (p0 - p1).abs().median() < 1e-6
-    assert torch.allclose(m0, m1, atol=1e-5)
+    # 3x128: the persistent kernel's Adam (step size folded into the denominator) and the flat Adam
+    # kernel round differently - trajectories agree to fp32 noise, not bit for bit
+    med = 1e-6 if hidden == (64,) else 1e-5
+    assert torch.allclose(l0, l1, atol=1e-5 if hidden == (64,) else 1e-4), (l0 - l1).abs().max()
+    assert (p0 - p1).abs().max() < 1e-3 and (p0 - p1).abs().median() < med
+    assert torch.allclose(m0, m1, atol=1e-5 if hidden == (64,) else 1e-4)
 
 
 def test_autograd_engine_logs_train_loss_after_graph_replays(monkeypatch):
