@@ -47,9 +47,47 @@ constexpr int TOTAL = B2L + 8;
 // column slot) hit 16 distinct slots - conflict-free ds_read/write_b128; aliases the step tiles
 constexpr int STG = H * H;
 constexpr int STG_LD = STG / 4 / NT;  // 16-B pieces per thread
-constexpr int LDS_FLOATS = TOTAL > STG ? TOTAL : STG;
-static_assert(LDS_FLOATS * 4 <= 65536, "fits the default dynamic-LDS limit");
+constexpr int LDS_FLOATS = TOTAL > 2 * STG ? TOTAL : 2 * STG;  // two staging tiles (p and m at once)
+static_assert(LDS_FLOATS * 4 <= 160 * 1024, "fits the CU");
 __device__ __forceinline__ int stg_slot(int r, int c) { return r * H + 4 * (c ^ (r & 15)); }
+// coalesced piece g = i * NT + t of the flat block <-> staging slot (row g / 32, 16-B column g % 32)
+typedef float v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void stg_put(float* lds, const v4f (&s)[STG_LD], int t) {
+#pragma unroll
+  for (int i = 0; i < STG_LD; ++i) {
+    const int g = i * NT + t;
+    *reinterpret_cast<v4f*>(lds + stg_slot(g >> 5, g & 31)) = s[i];
+  }
+}
+__device__ __forceinline__ void stg_store(float* dst, const float* lds, int t) {
+#pragma unroll
+  for (int i = 0; i < STG_LD; ++i) {
+    const int g = i * NT + t;
+    *reinterpret_cast<float4*>(dst + 4 * g) = *reinterpret_cast<const float4*>(lds + stg_slot(g >> 5, g & 31));
+  }
+}
+// a lane's own k-slice [16w, 16w + 16) of rows l and l + 64
+__device__ __forceinline__ void stg_get(const float* lds, float (&d)[2][KS], int l, int w) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int q = 0; q < KS / 4; ++q) {
+      const float4 t4 = *reinterpret_cast<const float4*>(lds + stg_slot(l + 64 * j, 4 * w + q));
+      d[j][4 * q] = t4.x; d[j][4 * q + 1] = t4.y; d[j][4 * q + 2] = t4.z; d[j][4 * q + 3] = t4.w;
+    }
+}
+__device__ __forceinline__ void stg_own(float* lds, const float (&s)[2][KS], int l, int w) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int q = 0; q < KS / 4; ++q)
+      *reinterpret_cast<float4*>(lds + stg_slot(l + 64 * j, 4 * w + q)) =
+          make_float4(s[j][4 * q], s[j][4 * q + 1], s[j][4 * q + 2], s[j][4 * q + 3]);
+}
+// uniform int read through the scalar cache (a constant-address-space load is an s_load)
+__device__ __forceinline__ int sload(const int* p) {
+  return *(const __attribute__((address_space(4))) int*)p;
+}
 static_assert((H1W % 4) == 0 && (PART % 4) == 0 && (MSK % 4) == 0 && (LAB % 4) == 0 && (W2L % 4) == 0 &&
               (B1L % 4) == 0 && (B2L % 4) == 0 && (H1X % 4) == 0, "16-B aligned tiles");
 }  // namespace blk2
@@ -123,8 +161,15 @@ __device__ __forceinline__ float rs_small(float (&P)[N], int lane) {
   return r;
 }
 
+// Selects among register values.  The operands pass an empty asm first: otherwise InstCombine
+// folds the select chain into a dynamically indexed load, which pins the array in scratch.
+__device__ __forceinline__ float opq(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
 __device__ __forceinline__ float sel4(const float (&v)[4], int i) {
-  return i == 0 ? v[0] : (i == 1 ? v[1] : (i == 2 ? v[2] : v[3]));
+  const float a0 = opq(v[0]), a1 = opq(v[1]), a2 = opq(v[2]), a3 = opq(v[3]);
+  return i == 0 ? a0 : (i == 1 ? a1 : (i == 2 ? a2 : a3));
 }
 
 // v_mfma_f32_4x4x1_16b_f32: 16 independent 4x4 outer products per wave, exact fp32 (an fmaf chain),
@@ -138,9 +183,9 @@ __device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
 
 template <int N>
 __device__ __forceinline__ float sel4c(const float (&v)[N], int i) {
-  float r = v[0];
+  float r = opq(v[0]);
 #pragma unroll
-  for (int k = 1; k < N; ++k) r = i == k ? v[k] : r;
+  for (int k = 1; k < N; ++k) r = i == k ? opq(v[k]) : r;
   return r;
 }
 
@@ -175,74 +220,20 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
   unsigned long long t_last = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
   const unsigned long long t_kstart = t_last;
 
-  int cur0 = 0;
-  if (a.cursor) {
-    cur0 = __hip_atomic_load(a.cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tid == 0 && cur0 > 0 && a.loss_out) a.loss_out[cur0 - 1] = a.grad_out[sh.P];
-  }
-  int t0 = a.t0;
-  uint32_t step_base = a.step_base;
-  if (a.step_counter) {
-    t0 = __hip_atomic_load(a.step_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    step_base = (uint32_t)t0;
+  // ---- W1 + moments: issued first, COALESCED (thread t: 16-byte pieces t, t + 512, ... of the
+  // flat [128][128] block), redistributed through LDS below
+  // native vector type: a float4 (struct) copy becomes a memcpy that SROA left in scratch
+  v4f sp[STG_LD], sm[STG_LD], sv[STG_LD];
+#pragma unroll
+  for (int i = 0; i < STG_LD; ++i) {
+    const int f = wo1 + 4 * (i * NT + tid);
+    sp[i] = *reinterpret_cast<const v4f*>(a.p + f);
+    if (ADAM) {
+      sm[i] = *reinterpret_cast<const v4f*>(a.m + f);
+      sv[i] = *reinterpret_cast<const v4f*>(a.v + f);
+    }
   }
 
-  // ---- first batch: row index, then the values, into registers now (the LDS tile is written after
-  // the W1 staging below, which aliases it) - the dependent chain overlaps the W1 round trip
-  const int Bsz = a.B;
-  const int bs0 = min(Bsz, a.n_items - cur0 * Bsz);
-  float x_first = 0.f;
-  int lab_first = 0;
-  if (tid < B * DMAX) {
-    const int b = tid & 3, d = tid >> 2;
-    if (b < bs0 && d < D0) x_first = a.X[(size_t)a.idx[cur0 * Bsz + b] * a.ldx + d];
-  }
-  if (tid < B && tid < bs0) lab_first = a.Y[a.idx[cur0 * Bsz + tid]];
-
-  // ---- registers: W1 k-slice + moments; W0 slices; replicated W2 / b1 / b2 (+ moments).
-  // W1 comes in COALESCED (thread t: 16-byte pieces t, t + 512, ... of the flat [128][128] block)
-  // and is redistributed through LDS: a lane's own 16-float row segments are 512 B apart, so
-  // loading them directly costs one 64-B request per lane per load (4x the coalesced count;
-  // measured ~17k cycles of prologue).  All 24 loads are issued before the first use.
-  float w1[2][KS], m1[2][KS], v1[2][KS];
-  {
-    int tq = tid;
-    float4 stg[3][STG_LD];
-#pragma unroll
-    for (int i = 0; i < STG_LD; ++i) {
-      const int f = wo1 + 4 * (i * NT + tq);
-      stg[0][i] = *reinterpret_cast<const float4*>(a.p + f);
-      if (ADAM) {
-        stg[1][i] = *reinterpret_cast<const float4*>(a.m + f);
-        stg[2][i] = *reinterpret_cast<const float4*>(a.v + f);
-      }
-    }
-#pragma unroll
-    for (int arr = 0; arr < (ADAM ? 3 : 1); ++arr) {
-      if (arr) __syncthreads();  // the previous array's reads are done
-#pragma unroll
-      for (int i = 0; i < STG_LD; ++i) {
-        const int g = i * NT + tq;
-        *reinterpret_cast<float4*>(lds + stg_slot(g >> 5, g & 31)) = stg[arr][i];
-      }
-      __syncthreads();
-      float(&dst)[2][KS] = arr == 0 ? w1 : (arr == 1 ? m1 : v1);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int q = 0; q < KS / 4; ++q) {
-          const float4 t4 = *reinterpret_cast<const float4*>(lds + stg_slot(l + 64 * j, 4 * w + q));
-          dst[j][4 * q] = t4.x; dst[j][4 * q + 1] = t4.y; dst[j][4 * q + 2] = t4.z; dst[j][4 * q + 3] = t4.w;
-        }
-    }
-    if (!ADAM) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int k = 0; k < KS; ++k) m1[j][k] = v1[j][k] = 0.f;
-    }
-    __syncthreads();  // staging reads done before the tiles (same LDS) are zeroed
-  }
   float w0[ND], m0[ND], v0[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) {
@@ -270,6 +261,51 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
   float pw2 = own_w2 ? a.p[fw2] : 0.f, mw2 = (own_w2 && ADAM) ? a.m[fw2] : 0.f, vw2 = (own_w2 && ADAM) ? a.v[fw2] : 0.f;
   float pb1 = own_b1 ? a.p[fb1] : 0.f, mb1 = (own_b1 && ADAM) ? a.m[fb1] : 0.f, vb1 = (own_b1 && ADAM) ? a.v[fb1] : 0.f;
   float pb2 = own_b2 ? a.p[fb2] : 0.f, mb2 = (own_b2 && ADAM) ? a.m[fb2] : 0.f, vb2 = (own_b2 && ADAM) ? a.v[fb2] : 0.f;
+
+  // cursor, step counter and the first batch's row indices through the scalar cache (uniform
+  // addresses): their round trips overlap the W1 loads instead of queueing behind them in vmcnt
+  int cur0 = a.cursor ? sload(a.cursor) : 0;
+  int t0 = a.t0;
+  uint32_t step_base = a.step_base;
+  if (a.step_counter) {
+    t0 = sload(a.step_counter);
+    step_base = (uint32_t)t0;
+  }
+  const int Bsz = a.B;
+  const int bs0 = min(Bsz, a.n_items - cur0 * Bsz);
+  int ridx[B];
+#pragma unroll
+  for (int b = 0; b < B; ++b) ridx[b] = b < bs0 ? sload(a.idx + cur0 * Bsz + b) : 0;
+  float x_first = 0.f;
+  int lab_first = 0;
+  {
+    const int b = tid & 3, d = tid >> 2;
+    const int rb = ridx[0] * (b == 0) + ridx[1] * (b == 1) + ridx[2] * (b == 2) + ridx[3] * (b == 3);
+    if (tid < B * DMAX && b < bs0 && d < D0) x_first = a.X[(size_t)rb * a.ldx + d];
+    if (tid < B && tid < bs0) lab_first = a.Y[rb];
+  }
+
+  // ---- registers: W1 k-slice + moments (through the swizzled staging tile: a lane's own 16-float
+  // row segments are 512 B apart); W0 slices; replicated W2 / b1 / b2 (+ moments)
+  float w1[2][KS], m1[2][KS], v1[2][KS];
+  stg_put(lds, sp, tid);
+  if (ADAM) stg_put(lds + STG, sm, tid);
+  __syncthreads();
+  stg_get(lds, w1, l, w);
+  if (ADAM) {
+    stg_get(lds + STG, m1, l, w);
+    __syncthreads();
+    stg_put(lds, sv, tid);
+    __syncthreads();
+    stg_get(lds, v1, l, w);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int k = 0; k < KS; ++k) m1[j][k] = v1[j][k] = 0.f;
+  }
+  __syncthreads();  // staging reads done before the tiles (same LDS) are zeroed
+  if (tid == 0 && cur0 > 0 && a.loss_out) a.loss_out[cur0 - 1] = a.grad_out[sh.P];
 
   // ---- LDS: first batch into input buffer 0
   for (int e = 4 * tid; e < TOTAL; e += 4 * NT) *reinterpret_cast<float4*>(lds + e) = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -527,15 +563,19 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
         float d3[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) d3[r] = CM == 2 ? (cw ? dz3[r][1 % CM] : dz3[r][0]) : sel4c<CM>(dz3[r], cw);
-        const float* hh = jw ? h2[1] : h2[0];
-        const float gw = d3[0] * hh[0] + d3[1] * hh[1] + d3[2] * hh[2] + d3[3] * hh[3];
+        // both candidates, then a select: indexing h2 by jw (or selecting its elements, which
+        // InstCombine turns back into an indexed load) demotes h2 to scratch
+        const float g0 = d3[0] * h2[0][0] + d3[1] * h2[0][1] + d3[2] * h2[0][2] + d3[3] * h2[0][3];
+        const float g1 = d3[0] * h2[1][0] + d3[1] * h2[1][1] + d3[2] * h2[1][2] + d3[3] * h2[1][3];
+        const float gw = jw ? g1 : g0;
         if (ADAM) adam_lean(pw2, gw, mw2, vw2, c1, a.b2, c2, a.wd, aA, aE);
         else if (s == 0) a.grad_out[fw2] = gw;
         lds[W2L + nbuf * (H * 4) + (l + 64 * jw) * 4 + cw] = pw2;
       }
       if (own_b1) {
-        const float* dd = jb ? dz2[1] : dz2[0];
-        const float gb = dd[0] + dd[1] + dd[2] + dd[3];
+        const float g0 = dz2[0][0] + dz2[0][1] + dz2[0][2] + dz2[0][3];
+        const float g1 = dz2[1][0] + dz2[1][1] + dz2[1][2] + dz2[1][3];
+        const float gb = jb ? g1 : g0;
         if (ADAM) adam_lean(pb1, gb, mb1, vb1, c1, a.b2, c2, a.wd, aA, aE);
         else if (s == 0) a.grad_out[fb1] = gb;
         lds[B1L + nbuf * H + l + 64 * jb] = pb1;
@@ -633,24 +673,17 @@ __global__ __launch_bounds__(blk2::NT, 1) void mlp_block2_kernel(MlpShape sh, Ml
   asm volatile("" : "+v"(lo), "+v"(uo), "+v"(to));
   // W1 + moments leave through the same LDS staging as they came in: coalesced 16-byte stores
   __syncthreads();  // every wave is past its last use of the step tiles (the staging aliases them)
-#pragma unroll
-  for (int arr = 0; arr < 3; ++arr) {
-    if (arr) __syncthreads();  // the previous array's reads are done
-    const float(&src)[2][KS] = arr == 0 ? w1 : (arr == 1 ? m1 : v1);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int q = 0; q < KS / 4; ++q)
-        *reinterpret_cast<float4*>(lds + stg_slot(lo + 64 * j, 4 * w + q)) =
-            make_float4(src[j][4 * q], src[j][4 * q + 1], src[j][4 * q + 2], src[j][4 * q + 3]);
-    __syncthreads();
-    float* dst = arr == 0 ? a.p : (arr == 1 ? a.m : a.v);
-#pragma unroll
-    for (int i = 0; i < STG_LD; ++i) {
-      const int g = i * NT + to;
-      *reinterpret_cast<float4*>(dst + wo1 + 4 * g) = *reinterpret_cast<const float4*>(lds + stg_slot(g >> 5, g & 31));
-    }
-  }
+  stg_own(lds, w1, lo, w);
+  __syncthreads();
+  stg_store(a.p + wo1, lds, to);
+  __syncthreads();
+  stg_own(lds, m1, lo, w);
+  __syncthreads();
+  stg_store(a.m + wo1, lds, to);
+  __syncthreads();
+  stg_own(lds, v1, lo, w);
+  __syncthreads();
+  stg_store(a.v + wo1, lds, to);
 #pragma unroll
   for (int i = 0; i < ND; ++i) {
     const int d = r0 + 4 * i;
@@ -689,31 +722,46 @@ bool mlp_block2_ok(const MlpShape& sh, const MlpArgs& a) {
          a.pending == nullptr && a.stage == nullptr && a.xg_world <= 1 && (a.mode == 0 || a.mode == 1);
 }
 
+// one launch of an instantiation; its dynamic-LDS limit (two 64-KB staging tiles) is raised once
+template <int ND, int CM, bool ADAM, bool PROF = false, bool MF = false>
+static void b2_launch(dim3 grid, size_t bytes, hipStream_t st, const MlpShape& sh, const MlpArgs& a) {
+  static const hipError_t attr = hipFuncSetAttribute((const void*)mlp_block2_kernel<ND, CM, ADAM, PROF, MF>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  (void)attr;
+  hipLaunchKernelGGL((mlp_block2_kernel<ND, CM, ADAM, PROF, MF>), grid, dim3(blk2::NT), bytes, st, sh, a);
+}
+
 hipError_t mlp_launch_block2(const MlpShape& sh, const MlpArgs& a, hipStream_t st) {
   const int d0 = sh.dims[0], C = sh.dims[3];
   const bool tr = a.mode == 0;
   const size_t bytes = (size_t)blk2::LDS_FLOATS * sizeof(float);
-#define B2K(ND, CM)                                                                                     \
-  do {                                                                                                  \
-    if (tr) hipLaunchKernelGGL((mlp_block2_kernel<ND, CM, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a); \
-    else hipLaunchKernelGGL((mlp_block2_kernel<ND, CM, false>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);  \
-  } while (0)
-  // weather shape (D0 <= 8, C <= 2): F2 and dW1 on the 4x4x1 fp32 MFMA by default (5.09 vs 5.25
+  // one workgroup.  (Measured and not kept: 24 helper workgroups on the trainer's XCD touching
+  // every line of W1 and its moments first, so the prologue hits L2 - prologue 10.5k -> 11.5k
+  // cycles, 20-step window 6.53 -> 6.57 us/step; profiles/block2_prologue_r3.log)
+  const dim3 grid(1);
+  // weather shape (D0 <= 8, C <= 2): F2 and dW1 on the 4x4x1 fp32 MFMA by default (5.09 vs 5.17
   // us/step on MI355X, profiles/block2_mf_ab_r3.log); DCT_MLP_BLOCK_MF=0 selects the VALU variant
   const char* mfe = getenv("DCT_MLP_BLOCK_MF");
   const bool mf = !(mfe && mfe[0] == '0') && d0 <= 8 && C <= 2;
   if (a.prof) {
-    if (mf) hipLaunchKernelGGL((mlp_block2_kernel<2, 2, true, true, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);
-    else hipLaunchKernelGGL((mlp_block2_kernel<2, 2, true, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);
+    if (mf) b2_launch<2, 2, true, true, true>(grid, bytes, st, sh, a);
+    else b2_launch<2, 2, true, true>(grid, bytes, st, sh, a);
   } else if (mf) {
-    if (tr) hipLaunchKernelGGL((mlp_block2_kernel<2, 2, true, false, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);
-    else hipLaunchKernelGGL((mlp_block2_kernel<2, 2, false, false, true>), dim3(1), dim3(blk2::NT), bytes, st, sh, a);
-  } else if (d0 <= 8) {
-    if (C <= 2) B2K(2, 2); else B2K(2, 4);
+    if (tr) b2_launch<2, 2, true, false, true>(grid, bytes, st, sh, a);
+    else b2_launch<2, 2, false, false, true>(grid, bytes, st, sh, a);
   } else {
-    if (C <= 2) B2K(8, 2); else B2K(8, 4);
-  }
+#define B2K(ND, CM)                                                   \
+  do {                                                                \
+    if (tr) b2_launch<ND, CM, true>(grid, bytes, st, sh, a);          \
+    else b2_launch<ND, CM, false>(grid, bytes, st, sh, a);            \
+  } while (0)
+    if (d0 <= 8) {
+      if (C <= 2) B2K(2, 2); else B2K(2, 4);
+    } else {
+      if (C <= 2) B2K(8, 2); else B2K(8, 4);
+    }
 #undef B2K
+  }
   return hipGetLastError();
 }
 
