@@ -452,6 +452,9 @@ def _physical_devices(ctx):
 
 def main():
     a = parse()
+    # the DDP bucket reducer's device-side all-reduce timing (allreduce_ms in the trainer's logs) adds
+    # two stamp kernels and two cross-stream edges per step: off for the timed step unless asked
+    os.environ.setdefault("DCT_REDUCER_TIMING", "0")
     import copy
 
     import torch

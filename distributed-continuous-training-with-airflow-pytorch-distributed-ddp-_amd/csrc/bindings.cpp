@@ -506,6 +506,7 @@ PYBIND11_MODULE(_dct_native, m) {
       .def_property_readonly("launched", &dct::BucketReducer::launched)
       .def_property_readonly("launched_before_finalize", &dct::BucketReducer::launched_before_finalize)
       .def_property_readonly("comm_stream", &dct::BucketReducer::comm_stream)
+      .def_property_readonly("inline_mode", &dct::BucketReducer::inline_mode)
       .def("enable_timing", &dct::BucketReducer::enable_timing, py::arg("check") = false)
       .def("read_timing", &dct::BucketReducer::read_timing)
       .def("reset_timing", &dct::BucketReducer::reset_timing);

@@ -103,6 +103,8 @@ struct MlpArgs {
   // optional (row-parallel kernel): wave 0 adds the s_memrealtime ticks (100 MHz) its exchange
   // took over the launch - the allreduce_ms metric of the fused DDP step
   unsigned long long* xg_ticks;
+  // kernel-specific A/B knob (mlp_block3.hip: wave priority split), 0 = the kernel's default
+  int tune;
 };
 
 constexpr int XG_MAXW = 8;  // ranks of the in-kernel exchange (one node)
@@ -116,6 +118,9 @@ hipError_t mlp_launch_block(const MlpShape& sh, const MlpArgs& a, hipStream_t st
 // one-barrier successor of mlp_block (mlp_block2.hip); DCT_MLP_BLOCK=v1 selects the old one
 bool mlp_block2_ok(const MlpShape& sh, const MlpArgs& a);
 hipError_t mlp_launch_block2(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
+// two-barrier successor (mlp_block3.hip, the default); DCT_MLP_BLOCK=2 selects mlp_block2
+bool mlp_block3_ok(const MlpShape& sh, const MlpArgs& a);
+hipError_t mlp_launch_block3(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
 hipError_t mlp_launch_eval_L2(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
 hipError_t mlp_launch_eval_L3(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
 hipError_t mlp_launch_eval_L4(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);

@@ -123,6 +123,11 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
   pending_.assign(nb, 0);
   launched_.assign(nb, 0);
   hip_check(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking), "hipStreamCreate");
+  // DCT_REDUCER_INLINE=1: collectives on the compute stream itself - no overlap with backward,
+  // but no cross-stream edges either (each costs ~5-15 us inside a replayed HIP graph, measured
+  // with the one-rank communicator: profiles/ddp_reducer_w1_r3.log)
+  const char* inl = getenv("DCT_REDUCER_INLINE");
+  inline_ = inl && inl[0] == '1';
   ready_events_.resize(nb);
   for (auto& e : ready_events_) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
   hip_check(hipEventCreateWithFlags(&done_event_, hipEventDisableTiming), "hipEventCreate");
@@ -177,13 +182,16 @@ void BucketReducer::reset_timing() {
 
 void BucketReducer::launch_bucket(int b, uintptr_t compute_stream) {
   hipStream_t cs = reinterpret_cast<hipStream_t>(compute_stream);
-  hip_check(hipEventRecord(ready_events_[b], cs), "hipEventRecord");
-  hip_check(hipStreamWaitEvent(comm_stream_, ready_events_[b], 0), "hipStreamWaitEvent");
+  hipStream_t rs = inline_ ? cs : comm_stream_;
+  if (!inline_) {
+    hip_check(hipEventRecord(ready_events_[b], cs), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(comm_stream_, ready_events_[b], 0), "hipStreamWaitEvent");
+  }
   if (timing_ && b == 0)
-    hip_check((hipError_t)dct_reducer_stamp(stamps_, reinterpret_cast<void*>(comm_stream_)), "reducer stamp");
+    hip_check((hipError_t)dct_reducer_stamp(stamps_, reinterpret_cast<void*>(rs)), "reducer stamp");
   if (comm_) {
     comm_->allreduce(flat_ + (uintptr_t)(offsets_[b] * dsize_), counts_[b], dtype_, op_,
-                     reinterpret_cast<uintptr_t>(comm_stream_));
+                     reinterpret_cast<uintptr_t>(rs));
   }
   launched_[b] = 1;
   n_launched_++;
@@ -208,11 +216,14 @@ int BucketReducer::mark_ready(int param_idx, uintptr_t compute_stream) {
 
 void BucketReducer::finalize(uintptr_t compute_stream) {
   hipStream_t cs = reinterpret_cast<hipStream_t>(compute_stream);
+  hipStream_t rs = inline_ ? cs : comm_stream_;
   n_before_finalize_ = n_launched_;
   if (timing_) {  // end of backward on the compute stream, ordered before the comm stream's close
     hip_check((hipError_t)dct_reducer_stamp(stamps_ + 1, reinterpret_cast<void*>(cs)), "reducer stamp");
-    hip_check(hipEventRecord(tail_event_, cs), "hipEventRecord");
-    hip_check(hipStreamWaitEvent(comm_stream_, tail_event_, 0), "hipStreamWaitEvent");
+    if (!inline_) {
+      hip_check(hipEventRecord(tail_event_, cs), "hipEventRecord");
+      hip_check(hipStreamWaitEvent(comm_stream_, tail_event_, 0), "hipStreamWaitEvent");
+    }
   }
   // buckets whose params did not all receive a gradient (unused params): reduce anyway so
   // the collective sequence matches across ranks (find_unused_parameters=False semantics
@@ -221,9 +232,11 @@ void BucketReducer::finalize(uintptr_t compute_stream) {
     launch_bucket(next_to_launch_, compute_stream);
     next_to_launch_++;
   }
-  if (timing_) hip_check((hipError_t)dct_reducer_close(stamps_, reinterpret_cast<void*>(comm_stream_)), "reducer close");
-  hip_check(hipEventRecord(done_event_, comm_stream_), "hipEventRecord");
-  hip_check(hipStreamWaitEvent(cs, done_event_, 0), "hipStreamWaitEvent");
+  if (timing_) hip_check((hipError_t)dct_reducer_close(stamps_, reinterpret_cast<void*>(rs)), "reducer close");
+  if (!inline_) {
+    hip_check(hipEventRecord(done_event_, comm_stream_), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(cs, done_event_, 0), "hipStreamWaitEvent");
+  }
   if (timing_ && check_) hip_check((hipError_t)dct_reducer_check(stamps_, reinterpret_cast<void*>(cs)), "reducer check");
 }
 

@@ -44,6 +44,7 @@ class BucketReducer {
   // all-reduce really overlapped (part of) the backward
   int launched_before_finalize() const { return n_before_finalize_; }
   uintptr_t comm_stream() const { return reinterpret_cast<uintptr_t>(comm_stream_); }
+  bool inline_mode() const { return inline_; }
   // device-side instrumentation (also inside captured graphs): span / exposed all-reduce time per
   // step; with `check` a compute-stream kernel after the join verifies the stream ordering
   void enable_timing(bool check);
@@ -66,6 +67,7 @@ class BucketReducer {
   hipEvent_t tail_event_ = nullptr;
   unsigned long long* stamps_ = nullptr;  // [8], see step_kernels.hip reducer_close_kernel
   bool timing_ = false, check_ = false;
+  bool inline_ = false;  // DCT_REDUCER_INLINE=1: collectives on the compute stream
 };
 
 // Receive buffers of the in-kernel (xGMI) gradient exchange.  Each rank allocates an

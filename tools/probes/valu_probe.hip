@@ -9,10 +9,11 @@
 #include <cstdlib>
 
 typedef float f2 __attribute__((ext_vector_type(2)));
+constexpr int REP = 16;
 
 template <int KIND, int NCH>
 __global__ void probe(const float* in, float* out, unsigned long long* cyc, int iters) {
-  // cyc[w] = s_memtime cycles, cyc[8 + w] = s_memrealtime ticks (100 MHz) of the timed loop
+  // cyc[w] = s_memtime cycles, cyc[16 + w] = s_memrealtime ticks (100 MHz) of the timed loop
   const int l = threadIdx.x & 63;
   float a = in[l], b = in[(l + 3) & 63];
   float x[NCH];
@@ -24,6 +25,8 @@ __global__ void probe(const float* in, float* out, unsigned long long* cyc, int 
   const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int rep = 0; rep < REP; ++rep)  // REP copies per loop trip: the loop's SALU + branch amortised
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       if constexpr (KIND == 0) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[i]) : "v"(a), "v"(b));
@@ -41,7 +44,7 @@ __global__ void probe(const float* in, float* out, unsigned long long* cyc, int 
   out[threadIdx.x] = s;
   if (l == 0) {
     cyc[threadIdx.x >> 6] = t1 - t0;
-    cyc[8 + (threadIdx.x >> 6)] = r1 - r0;
+    cyc[16 + (threadIdx.x >> 6)] = r1 - r0;
   }
 }
 
@@ -58,18 +61,18 @@ static void ck(hipError_t e, const char* w) {
 
 template <int KIND, int NCH>
 static void run(const char* name, const float* in, float* out, unsigned long long* cyc) {
-  const int iters = 2048;
-  for (int waves : {1, 4, 8}) {
-    unsigned long long h[16] = {};
+  const int iters = 256;
+  for (int waves : {1, 4, 8, 16}) {
+    unsigned long long h[32] = {};
     hipLaunchKernelGGL((probe<KIND, NCH>), dim3(1), dim3(64 * waves), 0, 0, in, out, cyc, iters);  // warm
     hipLaunchKernelGGL((probe<KIND, NCH>), dim3(1), dim3(64 * waves), 0, 0, in, out, cyc, iters);
     ck(hipDeviceSynchronize(), "sync");
-    ck(hipMemcpy(h, cyc, 16 * 8, hipMemcpyDeviceToHost), "cpy");
+    ck(hipMemcpy(h, cyc, 32 * 8, hipMemcpyDeviceToHost), "cpy");
     double lo = 1e30, hi = 0, ns = 0;
     for (int w = 0; w < waves; ++w) {
-      const double c = (double)h[w] / (iters * NCH);
+      const double c = (double)h[w] / (iters * NCH * REP);
       lo = c < lo ? c : lo; hi = c > hi ? c : hi;
-      ns = (double)h[8 + w] * 10.0 / (iters * NCH);
+      ns = (double)h[16 + w] * 10.0 / (iters * NCH * REP);
     }
     printf("%-28s %d chain(s), %d wave(s): %.2f .. %.2f cycles per instruction per wave (%.2f ns; clock %.2f GHz)\n",
            name, NCH, waves, lo, hi, ns, lo / ns);
@@ -79,7 +82,7 @@ static void run(const char* name, const float* in, float* out, unsigned long lon
 int main() {
   float *in, *out;
   unsigned long long* cyc;
-  ck(hipMalloc(&in, 64 * 4), "malloc"); ck(hipMalloc(&out, 1 << 20), "malloc"); ck(hipMalloc(&cyc, 16 * 8), "malloc");
+  ck(hipMalloc(&in, 64 * 4), "malloc"); ck(hipMalloc(&out, 1 << 20), "malloc"); ck(hipMalloc(&cyc, 32 * 8), "malloc");
   hipLaunchKernelGGL(spin, dim3(1024), dim3(256), 0, 0, out, 200000);
   ck(hipDeviceSynchronize(), "spin");
   float h[64];
@@ -93,6 +96,8 @@ int main() {
   run<2, 8>("v_rcp_f32 independent", in, out, cyc);
   run<3, 1>("v_add_f32_dpp dependent", in, out, cyc);
   run<3, 8>("v_add_f32_dpp independent", in, out, cyc);
+  run<0, 2>("v_fma_f32 2 chains", in, out, cyc);
+  run<0, 4>("v_fma_f32 4 chains", in, out, cyc);
   printf("done\n");
   return 0;
 }

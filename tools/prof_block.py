@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Per-phase shader cycles of the 3x128 weather step (csrc/mlp_block2.hip, PROF instantiation:
+"""Per-phase shader cycles of the 3x128 weather step (csrc/mlp_block3.hip, or mlp_block2.hip with
+DCT_MLP_BLOCK=2; PROF instantiation:
 launched whenever a prof buffer is passed; no special build).  Prints each wave's cycles per step
 in every phase; the stamps themselves cost cycles, so compare shares, not totals."""
 import os
@@ -13,8 +14,11 @@ import torch  # noqa: E402
 import dct_amd  # noqa: E402,F401
 from dct_amd.ops.fused_mlp import FusedMLPKernel, mlp_num_params  # noqa: E402
 
-PHASES = ["F1 h1 + keep ballots", "F2 partials + prefetch", "barrier", "F2r h2 (8 partials)",
-          "logits + loss", "dZ2, W2/b2/b1 Adam", "dX reduce-scatter", "dW0/db0 Adam", "dW1 + Adam"]
+PHASES_B2 = ["F1 h1 + keep ballots", "F2 partials + prefetch", "barrier", "F2r h2 (8 partials)",
+             "logits + loss", "dZ2, W2/b2/b1 Adam", "dX reduce-scatter", "dW0/db0 Adam", "dW1 + Adam"]
+PHASES_B3 = ["F1 h1 + keep hash", "F2 partials + prefetch", "barrier A", "h2 own 16 + logit share",
+             "barrier B", "logits + loss", "dZ2 + W2/b1/b2 Adam", "dX + dW0/db0 Adam", "dW1 + Adam"]
+PHASES = PHASES_B2 if os.environ.get("DCT_MLP_BLOCK") == "2" else PHASES_B3
 ONCE = ["prologue (per launch)", "epilogue (per launch)"]
 
 
