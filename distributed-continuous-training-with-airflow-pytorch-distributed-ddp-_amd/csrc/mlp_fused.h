@@ -121,6 +121,9 @@ hipError_t mlp_launch_block2(const MlpShape& sh, const MlpArgs& a, hipStream_t s
 // two-barrier successor (mlp_block3.hip, the default); DCT_MLP_BLOCK=2 selects mlp_block2
 bool mlp_block3_ok(const MlpShape& sh, const MlpArgs& a);
 hipError_t mlp_launch_block3(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
+// 16-wave successor (mlp_block4.hip, the default); DCT_MLP_BLOCK=3 selects mlp_block3
+bool mlp_block4_ok(const MlpShape& sh, const MlpArgs& a);
+hipError_t mlp_launch_block4(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
 hipError_t mlp_launch_eval_L2(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
 hipError_t mlp_launch_eval_L3(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
 hipError_t mlp_launch_eval_L4(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);

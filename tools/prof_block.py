@@ -18,7 +18,8 @@ PHASES_B2 = ["F1 h1 + keep ballots", "F2 partials + prefetch", "barrier", "F2r h
              "logits + loss", "dZ2, W2/b2/b1 Adam", "dX reduce-scatter", "dW0/db0 Adam", "dW1 + Adam"]
 PHASES_B3 = ["F1 h1 + keep hash", "F2 partials + prefetch", "barrier A", "h2 own 16 + logit share",
              "barrier B", "logits + loss", "dZ2 + W2/b1/b2 Adam", "dX + dW0/db0 Adam", "dW1 + Adam"]
-PHASES = PHASES_B2 if os.environ.get("DCT_MLP_BLOCK") == "2" else PHASES_B3
+PHASES = PHASES_B2 if os.environ.get("DCT_MLP_BLOCK") == "2" else PHASES_B3  # block4: same phases
+NWAVES = 8 if os.environ.get("DCT_MLP_BLOCK") in ("2", "3") else 16
 ONCE = ["prologue (per launch)", "epilogue (per launch)"]
 
 
@@ -34,7 +35,7 @@ def main():
     p = torch.randn(P, device=dev) * 0.1
     m, v = torch.zeros_like(p), torch.zeros_like(p)
     loss = torch.zeros(steps, device=dev)
-    prof = torch.zeros(128, dtype=torch.int64, device=dev)
+    prof = torch.zeros(16 * 16, dtype=torch.int64, device=dev)
     k = FusedMLPKernel(dims, bmax=4)
     k.train(p, m, v, X, Y, idx, steps * 4, 4, steps, 0, 0.01, dropout=0.2, loss_out=loss, prof=prof)
     torch.cuda.synchronize()
@@ -43,15 +44,15 @@ def main():
     k.train(p, m, v, X, Y, idx, steps * 4, 4, steps, 0, 0.01, dropout=0.2, loss_out=loss, prof=prof)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    raw = prof.cpu().view(8, 16).double()
+    raw = prof.cpu().view(16, 16)[:NWAVES].double()
     pr = raw[:, :len(PHASES)] / steps
     print(f"stamped launch: {dt / steps * 1e6:.3f} us/step (stamps included)")
-    print("cycles per step        " + "".join(f"  wave{w}" for w in range(8)))
+    print("cycles per step        " + "".join(f" wave{w:<2d}" for w in range(NWAVES)))
     for i, name in enumerate(PHASES):
-        print(f"{name:24s}" + "".join(f"{pr[w, i].item():7.0f}" for w in range(8)))
-    print(f"{'total':24s}" + "".join(f"{pr[w].sum().item():7.0f}" for w in range(8)))
+        print(f"{name:24s}" + "".join(f"{pr[w, i].item():7.0f}" for w in range(NWAVES)))
+    print(f"{'total':24s}" + "".join(f"{pr[w].sum().item():7.0f}" for w in range(NWAVES)))
     for i, name in enumerate(ONCE):
-        print(f"{name:24s}" + "".join(f"{raw[w, 9 + i].item():7.0f}" for w in range(8)))
+        print(f"{name:24s}" + "".join(f"{raw[w, 9 + i].item():7.0f}" for w in range(NWAVES)))
 
 
 if __name__ == "__main__":
