@@ -615,8 +615,9 @@ __global__ __launch_bounds__(blk4::NT, 1) void mlp_block4_kernel(MlpShape sh, Ml
 #undef B4STAMP
 
 bool mlp_block4_ok(const MlpShape& sh, const MlpArgs& a) {
-  const char* env = getenv("DCT_MLP_BLOCK");  // "3" / "2": the 8-wave kernels, "0" / "v1": others
-  if (env && (env[0] == '0' || env[0] == '2' || env[0] == '3' || (env[0] == 'v' && env[1] == '1'))) return false;
+  // opt-in (DCT_MLP_BLOCK=4) until validated on the GPU; "3" / "2": the 8-wave kernels, "0" / "v1": others
+  const char* env = getenv("DCT_MLP_BLOCK");
+  if (!(env && env[0] == '4')) return false;
   const bool prof_ok = a.prof == nullptr || (sh.dims[0] <= 8 && sh.dims[3] <= 2 && a.mode == 0);
   const bool aligned = (sh.woff[1] % 4) == 0 && ((uintptr_t)a.p & 15) == 0 &&
                        (a.mode != 0 || (((uintptr_t)a.m | (uintptr_t)a.v) & 15) == 0);

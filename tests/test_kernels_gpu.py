@@ -31,21 +31,39 @@ def _ref_loss(logits, y, kind):
     return F.mse_loss(logits, F.one_hot(y, logits.shape[1]).float())
 
 
+# DCT_MLP_* settings of a kernel variant name: "lds-<variant>" selects one of the 3x128 trainers
+# (b4 = 16-wave mlp_block4, mf / default = 8-wave mlp_block3, b2 = mlp_block2, v1 = round 2's
+# mlp_block.hip, noblock = the generic LDS trainer); "v" = VALU instead of the 4x4x1 MFMA layer,
+# "r" = W1's second moment in VGPRs instead of LDS (mlp_block4 only)
+_VARIANTS = {"": ("1", "0", "1"), "noblock": ("0", "0", "1"), "v1": ("v1", "0", "1"), "mf": ("1", "1", "1"),
+             "b2": ("2", "1", "1"), "b4": ("4", "1", "1"), "b4v": ("4", "0", "1"), "b4r": ("4", "1", "0")}
+
+
+def _set_kernel_env(monkeypatch, kernel):
+    parts = kernel.split("-")
+    monkeypatch.setenv("DCT_MLP_KERNEL", parts[0])
+    blk, mf, vl = _VARIANTS[parts[1] if len(parts) > 1 else ""]
+    monkeypatch.setenv("DCT_MLP_BLOCK", blk)
+    monkeypatch.setenv("DCT_MLP_BLOCK_MF", mf)
+    monkeypatch.setenv("DCT_B4_VL", vl)
+
+
 def test_native_loaded_and_arch():
     nat = native()
     assert nat.device_count() >= 1
     assert "gfx950" in nat.arch_name(0)
 
 
-@pytest.mark.parametrize("kernel", ["auto", "lds", "lds-noblock", "lds-v1", "lds-mf"])
+KERNELS = ["auto", "lds", "lds-noblock", "lds-v1", "lds-mf", "lds-b2", "lds-b4", "lds-b4v", "lds-b4r"]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("loss", ["ce", "mse"])
 @pytest.mark.parametrize("dims,B", [([5, 64, 2], 4), ([5, 128, 128, 2], 4), ([5, 64, 2], 3), ([9, 48, 64, 3], 4),
                                     ([16, 32, 48, 32, 3], 16), ([5, 128, 128, 2], 16), ([7, 20, 2], 9),
                                     ([7, 20, 2], 8), ([12, 40, 4], 6), ([16, 64, 3], 2), ([5, 64, 2], 1)])
 def test_fused_train_matches_torch_adam(dims, B, loss, kernel, cuda, monkeypatch):
-    monkeypatch.setenv("DCT_MLP_KERNEL", kernel.split("-")[0])
-    monkeypatch.setenv("DCT_MLP_BLOCK", "0" if kernel.endswith("noblock") else ("v1" if kernel.endswith("v1") else "1"))
-    monkeypatch.setenv("DCT_MLP_BLOCK_MF", "1" if kernel.endswith("mf") else "0")
+    _set_kernel_env(monkeypatch, kernel)
     torch.manual_seed(1)
     N, n_items = 301, 50
     X = torch.randn(N, dims[0])
@@ -81,13 +99,11 @@ def test_fused_train_matches_torch_adam(dims, B, loss, kernel, cuda, monkeypatch
     assert torch.allclose(m.cpu(), ref_m, atol=1e-4, rtol=1e-2)
 
 
-@pytest.mark.parametrize("kernel", ["auto", "lds", "lds-noblock", "lds-v1", "lds-mf"])
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("dims,B", [([5, 64, 2], 4), ([5, 128, 128, 2], 4), ([12, 40, 40, 5], 13),
                                     ([9, 48, 64, 3], 4), ([20, 128, 128, 4], 3), ([32, 128, 128, 1], 4)])
 def test_fused_grad_mode_matches_autograd(dims, B, kernel, cuda, monkeypatch):
-    monkeypatch.setenv("DCT_MLP_KERNEL", kernel.split("-")[0])
-    monkeypatch.setenv("DCT_MLP_BLOCK", "0" if kernel.endswith("noblock") else ("v1" if kernel.endswith("v1") else "1"))
-    monkeypatch.setenv("DCT_MLP_BLOCK_MF", "1" if kernel.endswith("mf") else "0")
+    _set_kernel_env(monkeypatch, kernel)
     torch.manual_seed(2)
     N = 64
     X = torch.randn(N, dims[0])
@@ -109,10 +125,9 @@ def test_fused_grad_mode_matches_autograd(dims, B, kernel, cuda, monkeypatch):
 
 @pytest.mark.parametrize("dims,B,D0", [([7, 128, 128, 2], 4, 7), ([30, 128, 128, 3], 3, 30)])
 def test_block_kernel_matches_lds_kernel_with_dropout(dims, B, D0, cuda, monkeypatch):
-    """mlp_block2.hip (one-barrier register-resident 3-layer kernel, the default) and mlp_block.hip
-    (its predecessor, DCT_MLP_BLOCK=v1) vs the generic LDS kernel: same dropout hash, loss and
-    Adam -> the same trajectory up to fp32 summation order."""
-    monkeypatch.setenv("DCT_MLP_KERNEL", "lds")
+    """The register-resident 3-layer kernels (mlp_block4 / 3 / 2 and round 2's mlp_block, with and
+    without the 4x4x1 MFMA layer, W1's second moment in LDS or VGPRs) vs the generic LDS kernel:
+    same dropout hash, loss and Adam -> the same trajectory up to fp32 summation order."""
     torch.manual_seed(4)
     N, n_items = 500, 203
     X = torch.randn(N, D0).to(cuda)
@@ -121,9 +136,9 @@ def test_block_kernel_matches_lds_kernel_with_dropout(dims, B, D0, cuda, monkeyp
     p0 = _flat(_ref_net(dims)).to(cuda)
     steps = math.ceil(n_items / B)
     out = {}
-    for blk in ("1", "1mf", "v1", "0"):
-        monkeypatch.setenv("DCT_MLP_BLOCK", blk[:2] if blk != "1mf" else "1")
-        monkeypatch.setenv("DCT_MLP_BLOCK_MF", "1" if blk == "1mf" else "0")
+    variants = ("lds", "lds-mf", "lds-v1", "lds-b2", "lds-b4", "lds-b4v", "lds-b4r", "lds-noblock")
+    for blk in variants:
+        _set_kernel_env(monkeypatch, blk)
         p, m, v = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
         losses = torch.zeros(steps, device=cuda)
         k = FusedMLPKernel(dims, bmax=4)
@@ -131,8 +146,8 @@ def test_block_kernel_matches_lds_kernel_with_dropout(dims, B, D0, cuda, monkeyp
                 step_base=5, loss_out=losses)
         torch.cuda.synchronize()
         out[blk] = (p.cpu(), m.cpu(), v.cpu(), losses.cpu())
-    for blk in ("1", "1mf", "v1"):
-        for a_, b_ in zip(out[blk], out["0"]):
+    for blk in variants[:-1]:
+        for a_, b_ in zip(out[blk], out["lds-noblock"]):
             assert torch.isfinite(a_).all()
             assert (a_ - b_).abs().max() <= 1e-4 * (1 + b_.abs().max()), (blk, float((a_ - b_).abs().max()))
 
