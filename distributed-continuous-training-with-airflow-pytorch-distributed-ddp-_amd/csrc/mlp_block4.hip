@@ -235,6 +235,20 @@ __global__ __launch_bounds__(blk4::NT, 1) void mlp_block4_kernel(MlpShape sh, Ml
   float* h1w = tl + H1W + w * (KS * 4);
   float* h1x = tl + H1X + w * (KS * 4);
   int xb = 0;
+  // wave priority.  Four waves share a SIMD and VALU issue goes to the oldest ready wave, so the
+  // last-dispatched quarter (waves 12-15) ends up the step's critical path: it runs its
+  // latency-bound loss chain ~5x slower than wave 0 while the older waves idle at barrier A
+  // (profiles/block4_r3.log).  tune 1: priority = dispatch quarter (youngest highest); tune 2:
+  // youngest quarter only; 0: none.
+  {
+    const int qw = w >> 2;
+    const int tune = a.tune;
+    if (tune == 1 || (tune == 2 && qw == 3)) {
+      if (qw == 1) __builtin_amdgcn_s_setprio(1);
+      else if (qw == 2 && tune == 1) __builtin_amdgcn_s_setprio(2);
+      else if (qw == 3) __builtin_amdgcn_s_setprio(3);
+    }
+  }
   if constexpr (PROF) {
     t_last = __builtin_amdgcn_s_memtime();
     pacc[9] = t_last - t_kstart;  // prologue: parameters + moments in, LDS init, first batch
@@ -643,23 +657,26 @@ hipError_t mlp_launch_block4(const MlpShape& sh, const MlpArgs& a, hipStream_t s
   const bool wd = a.wd != 0.f;
   const char* vle = getenv("DCT_B4_VL");  // "0": W1's second moment in VGPRs (spills at 128 / lane)
   const bool vl = !(vle && vle[0] == '0');
+  const char* pe = getenv("DCT_B4_PRIO");
+  MlpArgs a2 = a;
+  a2.tune = pe ? atoi(pe) : a.tune;
   if (a.prof) {
-    if (mf) b4_launch<1, 2, true, true, true, true, true>(st, sh, a);
-    else b4_launch<1, 2, true, true, false, true, true>(st, sh, a);
+    if (mf) b4_launch<1, 2, true, true, true, true, true>(st, sh, a2);
+    else b4_launch<1, 2, true, true, false, true, true>(st, sh, a2);
   } else if (mf) {
-    if (!tr) b4_launch<1, 2, false, false, true>(st, sh, a);
+    if (!tr) b4_launch<1, 2, false, false, true>(st, sh, a2);
     else if (wd) {
-      if (vl) b4_launch<1, 2, true, false, true, true, true>(st, sh, a);
-      else b4_launch<1, 2, true, false, true, true, false>(st, sh, a);
+      if (vl) b4_launch<1, 2, true, false, true, true, true>(st, sh, a2);
+      else b4_launch<1, 2, true, false, true, true, false>(st, sh, a2);
     } else {
-      if (vl) b4_launch<1, 2, true, false, true, false, true>(st, sh, a);
-      else b4_launch<1, 2, true, false, true, false, false>(st, sh, a);
+      if (vl) b4_launch<1, 2, true, false, true, false, true>(st, sh, a2);
+      else b4_launch<1, 2, true, false, true, false, false>(st, sh, a2);
     }
   } else {
 #define B4K(NDL, CM)                                                \
   do {                                                              \
-    if (tr) b4_launch<NDL, CM, true, false, false, true, true>(st, sh, a); \
-    else b4_launch<NDL, CM, false>(st, sh, a);                      \
+    if (tr) b4_launch<NDL, CM, true, false, false, true, true>(st, sh, a2); \
+    else b4_launch<NDL, CM, false>(st, sh, a2);                      \
   } while (0)
     if (d0 <= 8) {
       if (C <= 2) B4K(1, 2); else B4K(1, 4);
