@@ -1,0 +1,590 @@
+// Lean two-barrier trainer for BASELINE's weather MLP exactly: D0 -> 128 -> 128 -> 2 (D0 <= 8,
+// batch <= 4, train mode, CE or MSE) - models/mlp.py preset weather-mlp-3x128, the reference's
+// WeatherClassifier with a second 128-wide hidden layer (jobs/train_lightning_ddp.py:57-62,69,88,
+// 122).  Same contract and work split as mlp_block3.hip (which keeps serving every other shape and
+// the grad mode); this one removes latency from the step's serial chain, which the per-phase stamps
+// of block3 showed is where the time goes (profiles/block3_r3.log: the loss alone ~1700 cycles per
+// wave, the layer-0 forward ~870, the W2 owners ~1780 for a handful of updates):
+//   * dropout factors of the NEXT step are hashed during this step's Adam (throughput-bound) instead
+//     of heading the layer-0 forward and the h2 reduction;
+//   * two-class loss in one lane per (row, class): logits all-reduced over the 8 wave shares with
+//     one linear LDS read (lane = wave' * 8 + class * 4 + row) and three cross-lane adds, the other
+//     class by one row rotation, softmax as rcp(1 + exp(z_other - z)) - no max / log / division on
+//     the path to dlogits (the reported loss is a softplus off that path), no IEEE divisions at all;
+//   * every LDS operand of the backward (W2 of the previous publish, b2, labels) is read before
+//     barrier B; the W2 owners take dlogit(row, class) from their own lane and one DPP rotation;
+//   * the input tile of the layer-0 forward stays in registers for dW0;
+//   * W1 Adam pairs its two rows per k (o and o + 64) on one reciprocal: 1/d0 = d1 / (d0 d1).
+// Step layout per wave w (8 waves, 2 per SIMD), lane l, unit u = 16 w + l / 4, row r0 = l % 4:
+//   F1 (h1[u][r0]) -> F2 k-slice partials (4x4x1 MFMA) -> BARRIER A -> h2 of the wave's 16 outputs,
+//   logit shares, h2 > 0 ballot -> BARRIER B -> loss -> dZ2, W2 / b1 / b2 Adam -> dZ1 (reduce-
+//   scatter) -> W0 / b0 Adam -> dW1 (MFMA) + W1 Adam.
+#include "mlp_block_util.h"
+
+namespace dct {
+
+namespace blk5 {
+constexpr int H = 128, NT = 512, NW = 8, KS = 16, DMAX = 8, B = 4, C = 2;
+constexpr int XT = 0;                     // [3][DMAX][4] input tiles, feature-major (4 rows each)
+constexpr int LAB = XT + 3 * DMAX * 4;    // [3][4] labels (int), 16 reserved
+constexpr int MSK = LAB + 16;             // [2][NW] uint64: h2 > 0 of (o = 16w + b/4, row b%4)
+constexpr int LOGP = MSK + 2 * NW * 2;    // [2][NW][C][4] logit shares (wave, class, row)
+constexpr int H1W = LOGP + 2 * NW * 8;    // [NW][KS][4] wave-private h1[k][row]
+constexpr int H1X = H1W + NW * KS * 4;    // [NW][4][KS] the same tile transposed (MFMA A operands)
+constexpr int PSTR = 36;                  // partials: [o][wave][4] with a 36-float o stride
+constexpr int PART = H1X + NW * KS * 4;   // [2][H][PSTR]
+constexpr int W2L = PART + 2 * H * PSTR;  // [2][H][C] W2[c][o] (o-major), published by the owners
+constexpr int B2L = W2L + 2 * H * C;      // [2][4] b2
+constexpr int TOTAL = B2L + 8;
+constexpr int STG = H * H;
+constexpr int LDS_FLOATS = TOTAL > 2 * STG ? TOTAL : 2 * STG;  // two staging tiles (prologue/epilogue)
+static_assert(LDS_FLOATS * 4 <= 160 * 1024, "fits the CU");
+static_assert((H1W % 4) == 0 && (PART % 4) == 0 && (MSK % 4) == 0 && (LAB % 4) == 0 && (W2L % 4) == 0 &&
+                  (B2L % 4) == 0 && (H1X % 4) == 0 && (LOGP % 4) == 0,
+              "16-B aligned tiles");
+using Stg = bku::Stage<H, NT>;
+constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
+}  // namespace blk5
+
+#define B5STAMP(k)                                              \
+  if constexpr (PROF) {                                         \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    pacc[(k)] += t_ - t_last;                                   \
+    t_last = t_;                                                \
+  }
+
+// dropout factor of element (layer li, row r, unit u) at global step gstep: 0 or 1 / (1 - p)
+__device__ __forceinline__ float b5_drop(uint32_t seed, uint32_t gstep, int li, int r, int u, float p, float scale) {
+  const uint32_t h = mix_hash(seed, gstep, (uint32_t)((li * 64 + r) * 65536 + u));
+  return u01(h) < p ? 0.f : scale;
+}
+
+// Adam (scaled moments, bku::adam_scaled) of two parameters sharing one reciprocal
+template <bool WD>
+__device__ __forceinline__ void adam_pair(float& p0, float g0, float& m0, float& v0, float& p1, float g1, float& m1,
+                                          float& v1, float b1, float b2, float wd, float A, float E) {
+  if constexpr (WD) { g0 = fmaf(wd, p0, g0); g1 = fmaf(wd, p1, g1); }
+  m0 = fmaf(b1, m0, g0);
+  m1 = fmaf(b1, m1, g1);
+  v0 = fmaf(b2, v0, g0 * g0);
+  v1 = fmaf(b2, v1, g1 * g1);
+  const float d0 = fmaf(__builtin_amdgcn_sqrtf(v0), A, E), d1 = fmaf(__builtin_amdgcn_sqrtf(v1), A, E);
+  const float R = __builtin_amdgcn_rcpf(d0 * d1);
+  p0 = fmaf(-m0, d1 * R, p0);
+  p1 = fmaf(-m1, d0 * R, p1);
+}
+
+// 4x4 transpose across a quad on the 4x4x1 MFMA: lane m holds v[i'] = A[m][i'] -> lane n gets
+// A[0..3][n].  Call i' multiplies column i' by the one-hot e[i'] = (lane % 4 == i'), so the products
+// land in lane i' only (C[b][m][n] = A[m][i'] delta(n, i')) and 4 accumulating calls assemble the
+// transpose exactly (x * 1 + 0); no VALU work.
+__device__ __forceinline__ bku::f32x4_t quad_transpose_mf(const float (&v)[4], const float (&e)[4]) {
+  bku::f32x4_t t = (bku::f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) t = bku::mfma4(v[i], e[i], t);
+  return t;
+}
+
+// reduce-scatter of 16 per-lane values over lane bits 2..5 (the 16 lanes sharing lane % 4): lane l
+// ends with the sum of value l >> 2.  Levels: bit 5 (permlane32 swap), bit 4 (permlane16 swap),
+// bit 3 (row rotation by 8 = lane ^ 8), bit 2 (lane ^ 4 through the LDS crossbar).
+__device__ __forceinline__ float rs_bits2to5(float (&P)[16], int lane) {
+  using namespace bku;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) P[i] = swap32_sum(P[i], P[i + 8]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) P[i] = swap16_sum(P[i], P[i + 4]);
+  const bool b3 = (lane >> 3) & 1, b2 = (lane >> 2) & 1;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const float keep = b3 ? P[i + 2] : P[i], send = b3 ? P[i] : P[i + 2];
+    P[i] = keep + dpp<ROR8>(send);
+  }
+  const float keep = b2 ? P[1] : P[0], send = b2 ? P[0] : P[1];
+  return keep + __shfl_xor(send, 4);  // lane ^ 4 (no single row rotation pairs both directions)
+}
+
+// LK: 0 = cross-entropy, 1 = MSE against the one-hot label; WD: L2 term in the update
+template <bool WD, int LK, bool PROF = false, bool DXM = true>
+__global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, MlpArgs a) {
+  using namespace blk5;
+  using namespace bku;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int D0 = sh.dims[0];
+  const int r0 = l & 3;                 // layer-0 / layer-1 role: row r0 of unit u
+  const int u = KS * w + (l >> 2);
+  const int wo0 = sh.woff[0], bo0 = sh.boff[0], wo1 = sh.woff[1], bo1 = sh.boff[1];
+  const int wo2 = sh.woff[2], bo2 = sh.boff[2];
+  unsigned long long pacc[PROF ? 11 : 1] = {};
+  unsigned long long t_last = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
+  const unsigned long long t_kstart = t_last;
+
+  // ---- W1 + moments: issued first, coalesced, redistributed through LDS below
+  v4f sp[Stg::LD], sm[Stg::LD], sv[Stg::LD];
+#pragma unroll
+  for (int i = 0; i < Stg::LD; ++i) {
+    const int f = wo1 + 4 * (i * NT + tid);
+    sp[i] = *reinterpret_cast<const v4f*>(a.p + f);
+    sm[i] = *reinterpret_cast<const v4f*>(a.m + f);
+    sv[i] = *reinterpret_cast<const v4f*>(a.v + f);
+  }
+  // W0 slices of unit u (inputs d = r0 and r0 + 4), b0[u]
+  float w0[2], m0[2], v0[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int d = r0 + 4 * i;
+    const bool ok = d < D0;
+    const int f = wo0 + u * D0 + (ok ? d : 0);
+    w0[i] = ok ? a.p[f] : 0.f;
+    m0[i] = ok ? a.m[f] : 0.f;
+    v0[i] = ok ? a.v[f] : 0.f;
+  }
+  float pb0 = a.p[bo0 + u], mb0 = a.m[bo0 + u], vb0 = a.v[bo0 + u];
+  // W2 column u (both classes in every lane of the quad); lane r0 < 2 owns W2[r0][u] (+ moments);
+  // b1[u] in every lane of the quad; b2 owned by wave 0, lanes 0 / 1
+  float pw2[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) pw2[c] = a.p[wo2 + c * H + u];
+  const bool own_w2 = r0 < C;
+  const int fw2 = wo2 + (own_w2 ? r0 : 0) * H + u;
+  float mw2 = own_w2 ? a.m[fw2] : 0.f, vw2 = own_w2 ? a.v[fw2] : 0.f;
+  float pb1 = a.p[bo1 + u], mb1 = a.m[bo1 + u], vb1 = a.v[bo1 + u];
+  const bool own_b2 = w == 0 && l < C;
+  const int fb2 = bo2 + (own_b2 ? l : 0);
+  float pb2 = own_b2 ? a.p[fb2] : 0.f, mb2 = own_b2 ? a.m[fb2] : 0.f, vb2 = own_b2 ? a.v[fb2] : 0.f;
+
+  // step counter and the first batch's row indices through the scalar cache (their round trips
+  // overlap the W1 loads)
+  int t0 = a.t0;
+  uint32_t step_base = a.step_base;
+  if (a.step_counter) {
+    t0 = sload(a.step_counter);
+    step_base = (uint32_t)t0;
+  }
+  const int Bsz = a.B;
+  const int bs0 = min(Bsz, a.n_items);
+  int ridx[B];
+#pragma unroll
+  for (int b = 0; b < B; ++b) ridx[b] = b < bs0 ? sload(a.idx + b) : 0;
+  float x_first = 0.f;
+  int lab_first = 0;
+  {
+    const int b = tid & 3, d = tid >> 2;
+    const int rb = ridx[0] * (b == 0) + ridx[1] * (b == 1) + ridx[2] * (b == 2) + ridx[3] * (b == 3);
+    if (tid < B * DMAX && b < bs0 && d < D0) x_first = a.X[(size_t)rb * a.ldx + d];
+    if (tid < B && tid < bs0) lab_first = a.Y[rb];
+  }
+
+  // ---- W1 k-slice + moments into registers through the swizzled staging tiles
+  float w1[2][KS], m1[2][KS], v1[2][KS];
+  Stg::put(lds, sp, tid);
+  Stg::put(lds + STG, sm, tid);
+  __syncthreads();
+  Stg::get<KS>(lds, w1, l, KS / 4 * w);
+  Stg::get<KS>(lds + STG, m1, l, KS / 4 * w);
+  __syncthreads();
+  Stg::put(lds, sv, tid);
+  __syncthreads();
+  Stg::get<KS>(lds, v1, l, KS / 4 * w);
+  __syncthreads();  // staging reads done before the tiles (same LDS) are zeroed
+
+  // ---- LDS: first batch into input buffer 0, W2 / b2 into publish buffer 0
+  for (int e = 4 * tid; e < TOTAL; e += 4 * NT) *reinterpret_cast<float4*>(lds + e) = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  if (tid < B * DMAX) lds[XT + (tid >> 2) * 4 + (tid & 3)] = x_first;
+  if (tid < B) reinterpret_cast<int*>(lds + LAB)[tid] = lab_first;
+  if (own_w2) lds[W2L + u * C + r0] = r0 ? pw2[1] : pw2[0];
+  if (own_b2) lds[B2L + l] = pb2;
+  // prefetch roles: thread -> (row pb, feature pk) of the next batch, or (row pb, label)
+  const int nel = Bsz * D0;
+  int role = 0, pb = 0, pk = 0;
+  if (tid < nel) { role = 1; pb = tid / D0; pk = tid - pb * D0; }
+  else if (tid < nel + Bsz) { role = 2; pb = tid - nel; }
+  int ridx_next = 0;
+  if (role && Bsz + pb < a.n_items) ridx_next = a.idx[Bsz + pb];
+  const uint32_t* pf_base = role == 1 ? reinterpret_cast<const uint32_t*>(a.X) + pk : reinterpret_cast<const uint32_t*>(a.Y);
+  const int pf_stride = role == 1 ? a.ldx : (role == 2 ? 1 : 0);
+  __syncthreads();
+
+  const float p_drop = a.dropout;
+  const bool drop = p_drop > 0.f;
+  const float scale = drop ? 1.0f / (1.0f - p_drop) : 1.0f;
+  const float l2b1 = log2f(a.b1), l2b2 = log2f(a.b2);
+  const float c1 = 1.f - a.b1, c2 = 1.f - a.b2;
+  const float rc1 = 1.f / c1, rc2 = 1.f / c2, sqc2 = sqrtf(c2);
+  // Adam moments to the scaled form adam_scaled keeps (back on store)
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int k = 0; k < KS; ++k) { m1[j][k] *= rc1; v1[j][k] *= rc2; }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { m0[i] *= rc1; v0[i] *= rc2; }
+  mb0 *= rc1; vb0 *= rc2; mw2 *= rc1; vw2 *= rc2; mb1 *= rc1; vb1 *= rc2; mb2 *= rc1; vb2 *= rc2;
+  // dropout factors of this lane's (row r0, unit u) elements at the first step
+  float f1 = b5_drop(a.seed, step_base, 0, r0, u, p_drop, scale);
+  float f2 = b5_drop(a.seed, step_base, 1, r0, u, p_drop, scale);
+  float* h1w = lds + H1W + w * (KS * 4);
+  float* h1x = lds + H1X + w * (KS * 4);
+  float eye[4];  // one-hot of lane % 4 (B operands of the MFMA quad transposes)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) eye[i] = r0 == i ? 1.f : 0.f;
+  const int cb = (l >> 2) & 1;  // loss role: class cb of row r0 (wave share l / 8)
+  int xb = 0;
+  if (a.tune == 1 && w >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  if (a.tune == 2 && w < NW / 2) __builtin_amdgcn_s_setprio(1);
+  if constexpr (PROF) {
+    t_last = __builtin_amdgcn_s_memtime();
+    pacc[9] = t_last - t_kstart;
+  }
+  for (int s = 0; s < a.steps; ++s) {
+    const int bs = min(Bsz, a.n_items - s * Bsz);
+    const uint32_t gstep = step_base + (uint32_t)s;
+    const int xbn = xb == 2 ? 0 : xb + 1;
+    const int pbuf = s & 1, nbuf = pbuf ^ 1;
+    const float* xT = lds + XT + xb * DMAX * 4;
+    const bool have_next = (s + 1 < a.steps);
+    const int bs_next = have_next ? min(Bsz, a.n_items - (s + 1) * Bsz) : 0;
+    const uint32_t raw_next = pf_base[(size_t)ridx_next * pf_stride];
+    const int nx2 = min((s + 2) * Bsz + pb, a.n_items - 1);
+    const int ridx_next2 = a.idx[nx2 < 0 ? 0 : nx2];
+
+    // ---- F1: h1[u][r0] (quad reduce-scatter over the input slices); the tile stays for dW0
+    const float4 xa = *reinterpret_cast<const float4*>(xT + r0 * 4);
+    const float4 xc = *reinterpret_cast<const float4*>(xT + (r0 + 4) * 4);
+    float h1;
+    {
+      const float acc0 = w0[0] * xa.x + w0[1] * xc.x, acc1 = w0[0] * xa.y + w0[1] * xc.y;
+      const float acc2 = w0[0] * xa.z + w0[1] * xc.z, acc3 = w0[0] * xa.w + w0[1] * xc.w;
+      const bool qb1 = (r0 >> 1) & 1, qb0 = r0 & 1;
+      const float k0 = qb1 ? acc2 : acc0, k1 = qb1 ? acc3 : acc1;
+      const float s0 = qb1 ? acc0 : acc2, s1 = qb1 ? acc1 : acc3;
+      const float e0 = k0 + dpp<QP_X2>(s0), e1 = k1 + dpp<QP_X2>(s1);
+      const float kq = qb0 ? e1 : e0, sq = qb0 ? e0 : e1;
+      h1 = fmaxf(kq + dpp<QP_X1>(sq) + pb0, 0.f) * f1;
+      h1w[l] = h1;                    // [k = l / 4][row = l % 4]
+      h1x[r0 * KS + (l >> 2)] = h1;   // [row][k]
+    }
+    __builtin_amdgcn_wave_barrier();
+    B5STAMP(0)
+    // ---- F2: this wave's k-slice partials of all 128 outputs x 4 rows (4x4x1 MFMA: A = h[k][lane % 4],
+    // B = the lane's own weight; C lands as acc[j][row] of output o = l + 64 j)
+    {
+      f32x4_t cj[2] = {(f32x4_t){0.f, 0.f, 0.f, 0.f}, (f32x4_t){0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int q = 0; q < KS / 4; ++q) {
+        const float4 hq = *reinterpret_cast<const float4*>(h1x + r0 * KS + 4 * q);
+        const float hv[4] = {hq.x, hq.y, hq.z, hq.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) cj[j] = mfma4(hv[e], w1[j][4 * q + e], cj[j]);
+      }
+      float* part = lds + PART + pbuf * (H * PSTR);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        *reinterpret_cast<float4*>(part + (l + 64 * j) * PSTR + w * 4) = make_float4(cj[j][0], cj[j][1], cj[j][2], cj[j][3]);
+    }
+    // next batch into the next input buffer (its last readers finished before the previous barrier B)
+    if (role) {
+      const uint32_t v = (have_next && pb < bs_next) ? raw_next : 0u;
+      uint32_t* dst = (role == 1) ? reinterpret_cast<uint32_t*>(lds + XT + xbn * DMAX * 4) + pk * 4 + pb
+                                  : reinterpret_cast<uint32_t*>(lds + LAB) + xbn * 4 + pb;
+      *dst = v;
+    }
+    ridx_next = role ? ridx_next2 : 0;
+    B5STAMP(1)
+    lds_barrier();  // A: all partials of this step are in (and W2 / b2 of the previous publish)
+    B5STAMP(2)
+
+    // ---- backward operands published before A: W2 columns l, l + 64 (dZ2), b2 of class cb, the
+    // label of row r0 - issued first, consumed after barrier B
+    const float2 wv0 = *reinterpret_cast<const float2*>(lds + W2L + pbuf * (H * C) + l * C);
+    const float2 wv1 = *reinterpret_cast<const float2*>(lds + W2L + pbuf * (H * C) + (l + 64) * C);
+    const float b2c = lds[B2L + pbuf * 4 + cb];
+    const int lab = reinterpret_cast<const int*>(lds + LAB)[xb * 4 + r0];
+    // ---- h2[u][r0] of this wave's 16 outputs, its logit shares, the h2 > 0 mask
+    float h2;
+    {
+      const float* pr = lds + PART + pbuf * (H * PSTR) + u * PSTR + r0;
+      float q[NW];
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) q[ww] = pr[4 * ww];
+      const float z = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+      h2 = fmaxf(z + pb1, 0.f) * f2;
+      const float t0s = sum_bits2to5(pw2[0] * h2), t1s = sum_bits2to5(pw2[1] * h2);  // row r0's shares
+      const unsigned long long msk = __ballot(h2 > 0.f);
+      if (l < 8) lds[LOGP + pbuf * (NW * 8) + w * 8 + l] = cb ? t1s : t0s;  // [wave][class][row]
+      if (l == 0)
+        *reinterpret_cast<uint2*>(lds + MSK + pbuf * (NW * 2) + w * 2) = make_uint2((uint32_t)msk, (uint32_t)(msk >> 32));
+    }
+    B5STAMP(3)
+    lds_barrier();  // B: logit shares and masks of every wave are in
+    B5STAMP(4)
+
+    // ---- loss: lane (share l / 8, class cb, row r0) -> logit (r0, cb) of the batch
+    const uint2 mw0 = *reinterpret_cast<const uint2*>(lds + MSK + pbuf * (NW * 2) + 2 * (l >> 4));
+    const uint2 mw1 = *reinterpret_cast<const uint2*>(lds + MSK + pbuf * (NW * 2) + 2 * ((l >> 4) + 4));
+    float dz, lv;
+    {
+      float lg = lds[LOGP + pbuf * (NW * 8) + l];
+      lg += dpp<ROR8>(lg);          // shares w', w' ^ 1 (lane bit 3)
+      lg = swap16_sum(lg, lg);      // lane bit 4
+      lg = swap32_sum(lg, lg);      // lane bit 5
+      const float z = lg + b2c;
+      const float zo = dpp<ROR4>(z);  // the other class of the same row (lane bit 2 flipped in the
+                                      // row-replicated copies)
+      const bool live = r0 < bs;
+      const float invb = __builtin_amdgcn_rcpf((float)(bs > 0 ? bs : 1));
+      const float inv = live ? invb : 0.f;
+      const float y = (cb == lab) ? 1.f : 0.f;
+      if constexpr (LK == 0) {
+        const float t = zo - z;
+        const float e = __builtin_amdgcn_exp2f(t * LOG2E);
+        const float pc = __builtin_amdgcn_rcpf(1.f + e);  // softmax of class cb
+        dz = (pc - y) * inv;
+        // row loss (lane of the labelled class): softplus(z_other - z_label), off the dz path
+        const float sp = fmaxf(t, 0.f) + LN2 * __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-fabsf(t) * LOG2E));
+        lv = (live && cb == lab) ? sp : 0.f;
+      } else {
+        const float d = z - y;
+        dz = d * inv;               // d (2 / C) / bs
+        lv = live ? 0.5f * d * d : 0.f;  // / C
+      }
+    }
+    // dlogits of the batch, wave-uniform: dz3[r][c] lives in lane 4c + r
+    float dz3[4][C];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < C; ++c) dz3[r][c] = rl(dz, 4 * c + r);
+    if (w == 0) {  // batch loss: lanes 0..7 hold (class, row) terms
+      float t = lv + dpp<QP_X1>(lv);
+      t += dpp<QP_X2>(t);
+      t += dpp<ROR4>(t);
+      if (l == 0 && a.loss_out) a.loss_out[s] = bs > 0 ? t * __builtin_amdgcn_rcpf((float)bs) : 0.f;
+    }
+    B5STAMP(5)
+
+    const int t = t0 + s + 1;
+    const float step_size = a.lr * __builtin_amdgcn_rcpf(1.f - pow_t(l2b1, (float)t));
+    const float rbc2 = __builtin_amdgcn_rsqf(1.f - pow_t(l2b2, (float)t));
+    const float rss = __builtin_amdgcn_rcpf(step_size);
+    const float aA = sqc2 * rbc2 * rss * rc1, aE = a.eps * rss * rc1;
+    // ---- dZ2 of outputs o = l + 64 j, all rows (old W2, mask bits of the owning wave)
+    float dz2[2][4];
+    {
+      const int sh4 = 4 * (l & 15);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float2 wv = j ? wv1 : wv0;
+        const uint2 mw = j ? mw1 : mw0;
+        const uint32_t nib = ((sh4 < 32 ? mw.x : mw.y) >> (sh4 & 31)) & 15u;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float g = wv.x * dz3[r][0] + wv.y * dz3[r][1];
+          dz2[j][r] = ((nib >> r) & 1u) ? g * scale : 0.f;
+        }
+      }
+    }
+    // ---- owners: dW2[:, u], db1[u] (quad sums), W2 / b1 / b2 Adam, W2 / b2 published
+    {
+      const float d_own = dz, d_oth = dpp<ROR4>(dz);  // dlogit (r0, cb), (r0, 1 - cb)
+      const float dr0 = cb ? d_oth : d_own, dr1 = cb ? d_own : d_oth;
+      const float gw0 = quad_sum(dr0 * h2), gw1 = quad_sum(dr1 * h2);
+      float gdz = pw2[0] * dr0 + pw2[1] * dr1;
+      gdz = h2 > 0.f ? gdz * scale : 0.f;
+      const float gb1 = quad_sum(gdz);
+      // updates run in every lane (no control flow around loop-carried registers: a conditional update
+      // costs a register copy per value at the loop back edge); only the owners' results are kept
+      // (W2[r0][u] is broadcast from quad lanes 0 / 1, b2 published by wave 0's lanes 0 / 1)
+      float pown = (r0 & 1) ? pw2[1] : pw2[0];
+      const float gown = (r0 & 1) ? gw1 : gw0;
+      adam_pair<WD>(pown, gown, mw2, vw2, pb1, gb1, mb1, vb1, a.b1, a.b2, a.wd, aA, aE);
+      pw2[0] = dpp<QB0>(pown);
+      pw2[1] = dpp<QB1>(pown);
+      if (own_w2) lds[W2L + nbuf * (H * C) + u * C + r0] = pown;
+      const float gb = (l & 1) ? (dz3[0][1] + dz3[1][1]) + (dz3[2][1] + dz3[3][1])
+                               : (dz3[0][0] + dz3[1][0]) + (dz3[2][0] + dz3[3][0]);
+      adam_scaled<WD>(pb2, gb, mb2, vb2, a.b1, a.b2, a.wd, aA, aE);
+      if (own_b2) lds[B2L + nbuf * 4 + l] = pb2;
+    }
+    B5STAMP(6)
+    // ---- dZ1 = W1^T dZ2 over this wave's k-slice, lane l keeps its own (unit u, row r0)
+    float dz1 = 0.f;
+    if constexpr (DXM) {
+      // on the 4x4x1 MFMA: each quad's 4x4 blocks of W1 (rows o = 4b + i + 64 j, columns k = 4q + m)
+      // and of dZ2 are transposed across the quad (MFMA, exact), so the call index runs over the block's 8
+      // outputs and lane (b, n) accumulates sum_o W1[o][4q + m] dZ2[o][n] for m = 0..3; the 16
+      // blocks' partials are then reduce-scattered over lane bits 2..5 to lane (b' = k, n)
+      float dzt[2][4];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const f32x4_t t = quad_transpose_mf(dz2[j], eye);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dzt[j][i] = t[i];
+      }
+      float P[16];
+#pragma unroll
+      for (int q = 0; q < KS / 4; ++q) {
+        f32x4_t acc = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float wq[4] = {w1[j][4 * q], w1[j][4 * q + 1], w1[j][4 * q + 2], w1[j][4 * q + 3]};
+          const f32x4_t wt = quad_transpose_mf(wq, eye);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc = mfma4(wt[i], dzt[j][i], acc);
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) P[4 * q + m] = acc[m];
+      }
+      dz1 = rs_bits2to5(P, l);
+    } else {
+      // one 16-value reduce-scatter per batch row (pass p leaves unit k's sum in lanes 4k..4k+3)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        float P[16];
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) P[kk] = w1[0][kk] * dz2[0][p] + w1[1][kk] * dz2[1][p];
+        const float tot = rs_small<16>(P, l);
+        if (r0 == p) dz1 = tot;
+      }
+    }
+    dz1 = h1 > 0.f ? dz1 * scale : 0.f;
+    // ---- dW0 / db0 (the quad holds unit u's four rows; inputs from the F1 tile in registers)
+    {
+      const float dq0 = dpp<QB0>(dz1), dq1 = dpp<QB1>(dz1), dq2 = dpp<QB2>(dz1), dq3 = dpp<QB3>(dz1);
+      const float g0 = dq0 * xa.x + dq1 * xa.y + dq2 * xa.z + dq3 * xa.w;
+      const float g1 = dq0 * xc.x + dq1 * xc.y + dq2 * xc.z + dq3 * xc.w;
+      adam_pair<WD>(w0[0], g0, m0[0], v0[0], w0[1], g1, m0[1], v0[1], a.b1, a.b2, a.wd, aA, aE);  // d >= D0: stays 0
+      adam_scaled<WD>(pb0, (dq0 + dq1) + (dq2 + dq3), mb0, vb0, a.b1, a.b2, a.wd, aA, aE);
+    }
+    // next step's dropout factors (independent work for the Adam stream below)
+    f1 = b5_drop(a.seed, gstep + 1u, 0, r0, u, p_drop, scale);  // p_drop = 0: always 1
+    f2 = b5_drop(a.seed, gstep + 1u, 1, r0, u, p_drop, scale);
+    B5STAMP(7)
+    // ---- dW1 (MFMA: A = h1[4q + lane % 4][r], B = this lane's dZ2, C register m = the gradient of
+    // its own w1[j][4q + m]) + Adam, the two rows j of one k on one reciprocal
+#pragma unroll
+    for (int q = 0; q < KS / 4; ++q) {
+      const float4 hq = *reinterpret_cast<const float4*>(h1w + (4 * q + r0) * 4);
+      const float hv[4] = {hq.x, hq.y, hq.z, hq.w};
+      f32x4_t g[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        g[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) g[j] = mfma4(hv[r], dz2[j][r], g[j]);
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int kk = 4 * q + m;
+        adam_pair<WD>(w1[0][kk], g[0][m], m1[0][kk], v1[0][kk], w1[1][kk], g[1][m], m1[1][kk], v1[1][kk], a.b1, a.b2,
+                      a.wd, aA, aE);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the next step rewrites this wave's h1 tiles
+    B5STAMP(8)
+    xb = xbn;
+  }
+  if (a.step_counter && tid == 0)
+    __hip_atomic_store(a.step_counter, t0 + a.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+  // ---- write back parameters and moments (flat torch order); opaque bases so the prologue's
+  // addresses are recomputed here instead of being kept live across the loop
+  int lo = l, uo = u, to = tid;
+  asm volatile("" : "+v"(lo), "+v"(uo), "+v"(to));
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int k = 0; k < KS; ++k) { m1[j][k] *= c1; v1[j][k] *= c2; }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { m0[i] *= c1; v0[i] *= c2; }
+  mb0 *= c1; vb0 *= c2; mw2 *= c1; vw2 *= c2; mb1 *= c1; vb1 *= c2; mb2 *= c1; vb2 *= c2;
+  __syncthreads();  // every wave is past its last use of the step tiles (the staging aliases them)
+  Stg::own<KS>(lds, w1, lo, KS / 4 * w);
+  Stg::own<KS>(lds + STG, m1, lo, KS / 4 * w);
+  __syncthreads();
+  Stg::store(a.p + wo1, lds, to);
+  Stg::store(a.m + wo1, lds + STG, to);
+  __syncthreads();
+  Stg::own<KS>(lds, v1, lo, KS / 4 * w);
+  __syncthreads();
+  Stg::store(a.v + wo1, lds, to);
+  const int r0o = lo & 3;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int d = r0o + 4 * i;
+    if (d < D0) {
+      const int f = wo0 + uo * D0 + d;
+      a.p[f] = w0[i];
+      a.m[f] = m0[i];
+      a.v[f] = v0[i];
+    }
+  }
+  if (r0o == 0) {
+    a.p[bo0 + uo] = pb0; a.m[bo0 + uo] = mb0; a.v[bo0 + uo] = vb0;
+    a.p[bo1 + uo] = pb1; a.m[bo1 + uo] = mb1; a.v[bo1 + uo] = vb1;
+  }
+  if (own_w2) {
+    const int f = wo2 + r0o * H + uo;
+    a.p[f] = (r0o & 1) ? pw2[1] : pw2[0]; a.m[f] = mw2; a.v[f] = vw2;
+  }
+  if (own_b2) { a.p[fb2] = pb2; a.m[fb2] = mb2; a.v[fb2] = vb2; }
+  if constexpr (PROF) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pacc[10] = __builtin_amdgcn_s_memtime() - t_last;
+    if (l == 0) {
+#pragma unroll
+      for (int i = 0; i < 11; ++i) atomicAdd(a.prof + w * 16 + i, pacc[i]);
+    }
+  }
+}
+#undef B5STAMP
+
+bool mlp_block5_ok(const MlpShape& sh, const MlpArgs& a) {
+  // DCT_MLP_BLOCK: unset / "1" / "5" select this kernel; "4" / "3" / "2" / "0" / "v1" the others (A/B)
+  const char* env = getenv("DCT_MLP_BLOCK");
+  if (env && (env[0] == '0' || env[0] == '2' || env[0] == '3' || env[0] == '4' || env[0] == 'v')) return false;
+  const bool aligned = (sh.woff[1] % 4) == 0 && ((uintptr_t)a.p & 15) == 0 && (((uintptr_t)a.m | (uintptr_t)a.v) & 15) == 0;
+  return aligned && sh.L == 3 && sh.dims[1] == blk5::H && sh.dims[2] == blk5::H && sh.dims[0] >= 1 &&
+         sh.dims[0] <= blk5::DMAX && sh.dims[3] == blk5::C && a.B >= 1 && a.B <= blk5::B && a.mode == 0 &&
+         (a.loss_kind == 0 || a.loss_kind == 1) && a.cursor == nullptr && a.pending == nullptr && a.stage == nullptr &&
+         a.xg_world <= 1;
+}
+
+template <bool WD, int LK, bool PROF = false, bool DXM = true>
+static void b5_launch(size_t bytes, hipStream_t st, const MlpShape& sh, const MlpArgs& a) {
+  static const hipError_t attr = hipFuncSetAttribute((const void*)mlp_block5_kernel<WD, LK, PROF, DXM>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  (void)attr;
+  hipLaunchKernelGGL((mlp_block5_kernel<WD, LK, PROF, DXM>), dim3(1), dim3(blk5::NT), bytes, st, sh, a);
+}
+
+hipError_t mlp_launch_block5(const MlpShape& sh, const MlpArgs& a, hipStream_t st) {
+  const size_t bytes = (size_t)blk5::LDS_FLOATS * sizeof(float);
+  const bool wd = a.wd != 0.f;
+  const char* pe = getenv("DCT_B3_PRIO");
+  MlpArgs a2 = a;
+  a2.tune = pe ? atoi(pe) : a.tune;
+  // DCT_B5_DXM=0: the dZ1 product on the VALU (4 reduce-scatter passes) instead of the MFMA (A/B)
+  const char* de = getenv("DCT_B5_DXM");
+  const bool dxm = !(de && de[0] == '0');
+  if (a.prof && a.loss_kind == 0) {
+    if (dxm) b5_launch<true, 0, true, true>(bytes, st, sh, a2);
+    else b5_launch<true, 0, true, false>(bytes, st, sh, a2);
+  } else if (a.prof) {
+    b5_launch<true, 1, true>(bytes, st, sh, a2);
+  } else if (!dxm && a.loss_kind == 0 && !wd) {
+    b5_launch<false, 0, false, false>(bytes, st, sh, a2);
+  } else if (a.loss_kind == 0) {
+    if (wd) b5_launch<true, 0>(bytes, st, sh, a2);
+    else b5_launch<false, 0>(bytes, st, sh, a2);
+  } else {
+    if (wd) b5_launch<true, 1>(bytes, st, sh, a2);
+    else b5_launch<false, 1>(bytes, st, sh, a2);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace dct

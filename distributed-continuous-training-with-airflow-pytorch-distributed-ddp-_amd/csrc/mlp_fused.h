@@ -121,9 +121,13 @@ hipError_t mlp_launch_block2(const MlpShape& sh, const MlpArgs& a, hipStream_t s
 // two-barrier successor (mlp_block3.hip, the default); DCT_MLP_BLOCK=2 selects mlp_block2
 bool mlp_block3_ok(const MlpShape& sh, const MlpArgs& a);
 hipError_t mlp_launch_block3(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
-// 16-wave successor (mlp_block4.hip, the default); DCT_MLP_BLOCK=3 selects mlp_block3
+// 16-wave variant (mlp_block4.hip, opt-in DCT_MLP_BLOCK=4)
 bool mlp_block4_ok(const MlpShape& sh, const MlpArgs& a);
 hipError_t mlp_launch_block4(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
+// lean two-barrier trainer for the exact weather shape D0<=8 -> 128 -> 128 -> 2, train mode
+// (mlp_block5.hip, the default there); DCT_MLP_BLOCK=3 selects mlp_block3
+bool mlp_block5_ok(const MlpShape& sh, const MlpArgs& a);
+hipError_t mlp_launch_block5(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
 hipError_t mlp_launch_eval_L2(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
 hipError_t mlp_launch_eval_L3(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
 hipError_t mlp_launch_eval_L4(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);

@@ -142,6 +142,7 @@ int dct_mlp_train(const void* shape, const MlpArgs* a, void* stream) {
   if (a->B < 1 || a->B > sh.bmax) return (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (dct::mlp_block4_ok(sh, *a)) return (int)dct::mlp_launch_block4(sh, *a, st);
+  if (dct::mlp_block5_ok(sh, *a)) return (int)dct::mlp_launch_block5(sh, *a, st);
   if (dct::mlp_block3_ok(sh, *a)) return (int)dct::mlp_launch_block3(sh, *a, st);
   if (dct::mlp_block2_ok(sh, *a)) return (int)dct::mlp_launch_block2(sh, *a, st);
   if (dct::mlp_block_ok(sh, *a)) return (int)dct::mlp_launch_block(sh, *a, st);

@@ -32,11 +32,13 @@ def _ref_loss(logits, y, kind):
 
 
 # DCT_MLP_* settings of a kernel variant name: "lds-<variant>" selects one of the 3x128 trainers
-# (b4 = 16-wave mlp_block4, mf / default = 8-wave mlp_block3, b2 = mlp_block2, v1 = round 2's
+# (default / mf = mlp_block5 for the exact weather shape D0 <= 8 -> 128 -> 128 -> 2 in train mode and
+# 8-wave mlp_block3 for every other 3x128 shape, b3 = mlp_block3 everywhere, b4 = 16-wave mlp_block4,
+# b2 = mlp_block2, v1 = round 2's
 # mlp_block.hip, noblock = the generic LDS trainer); "v" = VALU instead of the 4x4x1 MFMA layer,
 # "r" = W1's second moment in VGPRs instead of LDS (mlp_block4 only)
 _VARIANTS = {"": ("1", "0", "1"), "noblock": ("0", "0", "1"), "v1": ("v1", "0", "1"), "mf": ("1", "1", "1"),
-             "b2": ("2", "1", "1"), "b4": ("4", "1", "1"), "b4v": ("4", "0", "1"), "b4r": ("4", "1", "0")}
+             "b2": ("2", "1", "1"), "b3": ("3", "1", "1"), "b3v": ("3", "0", "1"), "b4": ("4", "1", "1"), "b4v": ("4", "0", "1"), "b4r": ("4", "1", "0")}
 
 
 def _set_kernel_env(monkeypatch, kernel):
@@ -54,7 +56,7 @@ def test_native_loaded_and_arch():
     assert "gfx950" in nat.arch_name(0)
 
 
-KERNELS = ["auto", "lds", "lds-noblock", "lds-v1", "lds-mf", "lds-b2", "lds-b4", "lds-b4v", "lds-b4r"]
+KERNELS = ["auto", "lds", "lds-noblock", "lds-v1", "lds-mf", "lds-b3", "lds-b3v", "lds-b2", "lds-b4", "lds-b4v", "lds-b4r"]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -136,7 +138,7 @@ def test_block_kernel_matches_lds_kernel_with_dropout(dims, B, D0, cuda, monkeyp
     p0 = _flat(_ref_net(dims)).to(cuda)
     steps = math.ceil(n_items / B)
     out = {}
-    variants = ("lds", "lds-mf", "lds-v1", "lds-b2", "lds-b4", "lds-b4v", "lds-b4r", "lds-noblock")
+    variants = ("lds", "lds-mf", "lds-b3", "lds-b3v", "lds-v1", "lds-b2", "lds-b4", "lds-b4v", "lds-b4r", "lds-noblock")
     for blk in variants:
         _set_kernel_env(monkeypatch, blk)
         p, m, v = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)

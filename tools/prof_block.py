@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Per-phase shader cycles of the 3x128 weather step (csrc/mlp_block3.hip, or mlp_block2.hip with
-DCT_MLP_BLOCK=2; PROF instantiation:
+"""Per-phase shader cycles of the 3x128 weather step (csrc/mlp_block5.hip by default, mlp_block3.hip
+with DCT_MLP_BLOCK=3, mlp_block2.hip with DCT_MLP_BLOCK=2, the 16-wave mlp_block4 with 4; PROF instantiation:
 launched whenever a prof buffer is passed; no special build).  Prints each wave's cycles per step
 in every phase; the stamps themselves cost cycles, so compare shares, not totals."""
 import os
@@ -19,7 +19,7 @@ PHASES_B2 = ["F1 h1 + keep ballots", "F2 partials + prefetch", "barrier", "F2r h
 PHASES_B3 = ["F1 h1 + keep hash", "F2 partials + prefetch", "barrier A", "h2 own 16 + logit share",
              "barrier B", "logits + loss", "dZ2 + W2/b1/b2 Adam", "dX + dW0/db0 Adam", "dW1 + Adam"]
 PHASES = PHASES_B2 if os.environ.get("DCT_MLP_BLOCK") == "2" else PHASES_B3  # block4: same phases
-NWAVES = 8 if os.environ.get("DCT_MLP_BLOCK") in ("2", "3") else 16
+NWAVES = 16 if os.environ.get("DCT_MLP_BLOCK") == "4" else 8
 ONCE = ["prologue (per launch)", "epilogue (per launch)"]
 
 
