@@ -87,7 +87,7 @@ __device__ __forceinline__ bku::f32x4_t quad_transpose_mf(const float (&v)[4], c
 
 // reduce-scatter of 16 per-lane values over lane bits 2..5 (the 16 lanes sharing lane % 4): lane l
 // ends with the sum of value l >> 2.  Levels: bit 5 (permlane32 swap), bit 4 (permlane16 swap),
-// bit 3 (row rotation by 8 = lane ^ 8), bit 2 (lane ^ 4 through the LDS crossbar).
+// bit 3 (row rotation by 8 = lane ^ 8), bit 2 (row rotations by 4 / 12 = lane ^ 4 inside the row).
 __device__ __forceinline__ float rs_bits2to5(float (&P)[16], int lane) {
   using namespace bku;
 #pragma unroll
@@ -101,7 +101,25 @@ __device__ __forceinline__ float rs_bits2to5(float (&P)[16], int lane) {
     P[i] = keep + dpp<ROR8>(send);
   }
   const float keep = b2 ? P[1] : P[0], send = b2 ? P[0] : P[1];
-  return keep + __shfl_xor(send, 4);  // lane ^ 4 (no single row rotation pairs both directions)
+  // lane ^ 4 inside the row: row_ror:N makes lane i read lane (i - N) % 16 (tools/probes/dpp_dir_probe),
+  // so lanes with bit 2 clear read i + 4 through row_ror:12, the others i - 4 through row_ror:4
+  const float t4 = dpp<ROR4>(send), t12 = dpp<0x12C>(send);
+  return keep + (b2 ? t4 : t12);
+}
+
+// Adam (scaled moments) of two parameters held as one 64-bit register pair: the moment / parameter
+// updates are packed fp32 (v_pk_fma / v_pk_mul: one issue for both lanes of the pair), the two
+// square roots scalar, one reciprocal for the pair as in adam_pair
+typedef float v2f __attribute__((ext_vector_type(2)));
+template <bool WD>
+__device__ __forceinline__ void adam_v2(v2f& p, v2f g, v2f& m, v2f& v, float b1, float b2, float wd, float A, float E) {
+  if constexpr (WD) g = (v2f)(wd) * p + g;
+  m = (v2f)(b1) * m + g;
+  v = (v2f)(b2) * v + g * g;
+  const v2f sq = (v2f){__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)};
+  const v2f d = sq * (v2f)(A) + (v2f)(E);
+  const float R = __builtin_amdgcn_rcpf(d.x * d.y);
+  p = p - m * ((v2f){d.y, d.x} * R);
 }
 
 // LK: 0 = cross-entropy, 1 = MSE against the one-hot label; WD: L2 term in the update
@@ -221,6 +239,17 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
 #pragma unroll
   for (int i = 0; i < 2; ++i) { m0[i] *= rc1; v0[i] *= rc2; }
   mb0 *= rc1; vb0 *= rc2; mw2 *= rc1; vw2 *= rc2; mb1 *= rc1; vb1 *= rc2; mb2 *= rc1; vb2 *= rc2;
+  // the step loop keeps W1 and its moments as 64-bit pairs of consecutive k (packed Adam; the dW1 MFMA
+  // accumulators come out in the same pairs)
+  v2f W[2][KS / 2], Mo[2][KS / 2], Vo[2][KS / 2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int h = 0; h < KS / 2; ++h) {
+      W[j][h] = (v2f){w1[j][2 * h], w1[j][2 * h + 1]};
+      Mo[j][h] = (v2f){m1[j][2 * h], m1[j][2 * h + 1]};
+      Vo[j][h] = (v2f){v1[j][2 * h], v1[j][2 * h + 1]};
+    }
   // dropout factors of this lane's (row r0, unit u) elements at the first step
   float f1 = b5_drop(a.seed, step_base, 0, r0, u, p_drop, scale);
   float f2 = b5_drop(a.seed, step_base, 1, r0, u, p_drop, scale);
@@ -270,16 +299,22 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     // ---- F2: this wave's k-slice partials of all 128 outputs x 4 rows (4x4x1 MFMA: A = h[k][lane % 4],
     // B = the lane's own weight; C lands as acc[j][row] of output o = l + 64 j)
     {
-      f32x4_t cj[2] = {(f32x4_t){0.f, 0.f, 0.f, 0.f}, (f32x4_t){0.f, 0.f, 0.f, 0.f}};
+      // one accumulator per (j, q): chains of 4 dependent MFMAs (40 cycles each) instead of 16
+      f32x4_t cq[2][KS / 4];
 #pragma unroll
       for (int q = 0; q < KS / 4; ++q) {
         const float4 hq = *reinterpret_cast<const float4*>(h1x + r0 * KS + 4 * q);
         const float hv[4] = {hq.x, hq.y, hq.z, hq.w};
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int j = 0; j < 2; ++j) {
+          cq[j][q] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int j = 0; j < 2; ++j) cj[j] = mfma4(hv[e], w1[j][4 * q + e], cj[j]);
+          for (int e = 0; e < 4; ++e) cq[j][q] = mfma4(hv[e], W[j][2 * q + (e >> 1)][e & 1], cq[j][q]);
+        }
       }
+      f32x4_t cj[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) cj[j] = (cq[j][0] + cq[j][1]) + (cq[j][2] + cq[j][3]);
       float* part = lds + PART + pbuf * (H * PSTR);
 #pragma unroll
       for (int j = 0; j < 2; ++j)
@@ -427,16 +462,18 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
       float P[16];
 #pragma unroll
       for (int q = 0; q < KS / 4; ++q) {
-        f32x4_t acc = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        f32x4_t acc[2];  // one chain per j (4 dependent MFMAs each)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const float wq[4] = {w1[j][4 * q], w1[j][4 * q + 1], w1[j][4 * q + 2], w1[j][4 * q + 3]};
+          const float wq[4] = {W[j][2 * q].x, W[j][2 * q].y, W[j][2 * q + 1].x, W[j][2 * q + 1].y};
           const f32x4_t wt = quad_transpose_mf(wq, eye);
+          acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int i = 0; i < 4; ++i) acc = mfma4(wt[i], dzt[j][i], acc);
+          for (int i = 0; i < 4; ++i) acc[j] = mfma4(wt[i], dzt[j][i], acc[j]);
         }
+        const f32x4_t at = acc[0] + acc[1];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) P[4 * q + m] = acc[m];
+        for (int m = 0; m < 4; ++m) P[4 * q + m] = at[m];
       }
       dz1 = rs_bits2to5(P, l);
     } else {
@@ -445,7 +482,7 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
       for (int p = 0; p < 4; ++p) {
         float P[16];
 #pragma unroll
-        for (int kk = 0; kk < KS; ++kk) P[kk] = w1[0][kk] * dz2[0][p] + w1[1][kk] * dz2[1][p];
+        for (int kk = 0; kk < KS; ++kk) P[kk] = W[0][kk >> 1][kk & 1] * dz2[0][p] + W[1][kk >> 1][kk & 1] * dz2[1][p];
         const float tot = rs_small<16>(P, l);
         if (r0 == p) dz1 = tot;
       }
@@ -464,7 +501,7 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     f2 = b5_drop(a.seed, gstep + 1u, 1, r0, u, p_drop, scale);
     B5STAMP(7)
     // ---- dW1 (MFMA: A = h1[4q + lane % 4][r], B = this lane's dZ2, C register m = the gradient of
-    // its own w1[j][4q + m]) + Adam, the two rows j of one k on one reciprocal
+    // its own w1[j][4q + m]) + packed Adam on pairs of consecutive k
 #pragma unroll
     for (int q = 0; q < KS / 4; ++q) {
       const float4 hq = *reinterpret_cast<const float4*>(h1w + (4 * q + r0) * 4);
@@ -477,11 +514,11 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
         for (int r = 0; r < 4; ++r) g[j] = mfma4(hv[r], dz2[j][r], g[j]);
       }
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int kk = 4 * q + m;
-        adam_pair<WD>(w1[0][kk], g[0][m], m1[0][kk], v1[0][kk], w1[1][kk], g[1][m], m1[1][kk], v1[1][kk], a.b1, a.b2,
-                      a.wd, aA, aE);
-      }
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          adam_v2<WD>(W[j][2 * q + h], (v2f){g[j][2 * h], g[j][2 * h + 1]}, Mo[j][2 * q + h], Vo[j][2 * q + h], a.b1,
+                      a.b2, a.wd, aA, aE);
     }
     __builtin_amdgcn_wave_barrier();  // the next step rewrites this wave's h1 tiles
     B5STAMP(8)
@@ -494,6 +531,14 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   // addresses are recomputed here instead of being kept live across the loop
   int lo = l, uo = u, to = tid;
   asm volatile("" : "+v"(lo), "+v"(uo), "+v"(to));
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int h = 0; h < KS / 2; ++h) {
+      w1[j][2 * h] = W[j][h].x; w1[j][2 * h + 1] = W[j][h].y;
+      m1[j][2 * h] = Mo[j][h].x; m1[j][2 * h + 1] = Mo[j][h].y;
+      v1[j][2 * h] = Vo[j][h].x; v1[j][2 * h + 1] = Vo[j][h].y;
+    }
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll

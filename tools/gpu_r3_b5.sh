@@ -1,32 +1,27 @@
 #!/bin/bash
-# Round 3: lean weather kernel (mlp_block5.hip) - numerics tests, long-run A/B against block3 and the
-# VALU dZ1 variant, per-phase stamps, the driver's bench window.
+# Round 3: lean weather kernel (mlp_block5.hip) - numerics tests, long-run A/B (block, dZ1 on the MFMA,
+# wave priority), per-phase stamps, the driver's bench window.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 O=gpurun_out
-timeout -k 10 60 ./tools/probes/dpp_dir_probe > $O/dpp_dir_probe.log 2>&1; cat $O/dpp_dir_probe.log
-DCT_B5_DXM=0 timeout -k 10 300 python -u -m pytest -q -rf --timeout 120 --timeout-method thread tests/test_kernels_gpu.py \
-  -k "fused_train and dims1 and lds-mf" > $O/pytest_b5_dxm0.log 2>&1
-tail -3 $O/pytest_b5_dxm0.log
 timeout -k 10 400 python -u -m pytest -q -rf -x --timeout 120 --timeout-method thread tests/test_kernels_gpu.py \
   -k "fused_train or block_kernel or grad_mode or dropout or eval" > $O/pytest_b5.log 2>&1
-rc=$?; tail -5 $O/pytest_b5.log; [ $rc -eq 0 ] || exit 1
+rc=$?; tail -3 $O/pytest_b5.log; [ $rc -eq 0 ] || exit 1
 : > $O/b5_ab.log
-for cfg in "5 1" "5 0" "3 1" "5 1" "5 0" "3 1"; do
-  set -- $cfg
-  DCT_MLP_BLOCK=$1 DCT_B5_DXM=$2 timeout -k 10 200 python bench.py --steps 20000 --warmup 2000 --no-reference-model > $O/bench_b5_$1_$2.json 2>&1 || exit $?
-  python -c "import json; d=json.loads([l for l in open('$O/bench_b5_$1_$2.json') if l.startswith('{')][-1]); print('block$1 dxm$2 %.3f us/step %.0f samples/s loss %s -> %s' % (d['extra']['us_per_step'], d['value'], d['extra']['loss_first'], d['extra']['loss_last']))" >> $O/b5_ab.log
+for cfg in ${B5_CFGS:-"5,1,0" "5,0,0" "5,1,1" "5,1,0" "5,0,0" "5,1,1"}; do
+  IFS=, read blk dxm prio <<< "$cfg"
+  DCT_MLP_BLOCK=$blk DCT_B5_DXM=$dxm DCT_B3_PRIO=$prio timeout -k 10 200 python bench.py --steps 20000 --warmup 2000 --no-reference-model > $O/bench_b5.json 2>&1 || exit $?
+  python -c "import json; d=json.loads([l for l in open('$O/bench_b5.json') if l.startswith('{')][-1]); print('block$blk dxm$dxm prio$prio %.3f us/step %.0f samples/s loss %s -> %s' % (d['extra']['us_per_step'], d['value'], d['extra']['loss_first'], d['extra']['loss_last']))" >> $O/b5_ab.log
 done
 cat $O/b5_ab.log
-for cfg in "5 1" "5 0"; do
-  set -- $cfg
-  DCT_MLP_BLOCK=$1 DCT_B5_DXM=$2 timeout -k 10 120 python tools/prof_block.py 4000 > $O/prof_b5_$2.log 2>&1 || exit $?
-  cat $O/prof_b5_$2.log
+for dxm in 1 0; do
+  DCT_B5_DXM=$dxm timeout -k 10 120 python tools/prof_block.py 4000 > $O/prof_b5_$dxm.log 2>&1 || exit $?
+  cat $O/prof_b5_$dxm.log
 done
 for i in 1 2; do
   timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_b5_s20_$i.log 2>&1 || exit $?
-  grep '^{' $O/bench_b5_s20_$i.log | cut -c1-300
+  grep '^{' $O/bench_b5_s20_$i.log | cut -c1-200
 done
 echo done
