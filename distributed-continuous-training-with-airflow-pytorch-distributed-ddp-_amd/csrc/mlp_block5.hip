@@ -53,9 +53,21 @@ constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
     t_last = t_;                                                \
   }
 
-// dropout factor of element (layer li, row r, unit u) at global step gstep: 0 or 1 / (1 - p)
-__device__ __forceinline__ float b5_drop(uint32_t seed, uint32_t gstep, int li, int r, int u, float p, float scale) {
-  const uint32_t h = mix_hash(seed, gstep, (uint32_t)((li * 64 + r) * 65536 + u));
+// dropout factor of element (layer li, row r, unit u) at global step gstep: 0 or 1 / (1 - p).  Same
+// bits as mix_hash(seed, gstep, (li * 64 + r) * 65536 + u) (mlp_fused_impl.h), split into the
+// wave-uniform step part (scalar ALU), the lane's constant element part (b5_elem, once per launch)
+// and the per-element finalizer: two vector multiplies per mask instead of five
+__device__ __forceinline__ uint32_t b5_elem(int li, int r, int u) {
+  return ((uint32_t)((li * 64 + r) * 65536 + u) + 0x165667B1u) * 0xC2B2AE3Du;
+}
+__device__ __forceinline__ float b5_drop(uint32_t seed, uint32_t gstep, uint32_t elem, float p, float scale) {
+  uint32_t h = (seed * 0x9E3779B1u) ^ ((gstep + 0x7F4A7C15u) * 0x85EBCA77u);
+  h ^= elem;
+  h ^= h >> 16;
+  h *= 0x7feb352du;
+  h ^= h >> 15;
+  h *= 0x846ca68bu;
+  h ^= h >> 16;
   return u01(h) < p ? 0.f : scale;
 }
 
@@ -251,8 +263,9 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
       Vo[j][h] = (v2f){v1[j][2 * h], v1[j][2 * h + 1]};
     }
   // dropout factors of this lane's (row r0, unit u) elements at the first step
-  float f1 = b5_drop(a.seed, step_base, 0, r0, u, p_drop, scale);
-  float f2 = b5_drop(a.seed, step_base, 1, r0, u, p_drop, scale);
+  const uint32_t el0 = b5_elem(0, r0, u), el1 = b5_elem(1, r0, u);
+  float f1 = b5_drop(a.seed, step_base, el0, p_drop, scale);
+  float f2 = b5_drop(a.seed, step_base, el1, p_drop, scale);
   float* h1w = lds + H1W + w * (KS * 4);
   float* h1x = lds + H1X + w * (KS * 4);
   float eye[4];  // one-hot of lane % 4 (B operands of the MFMA quad transposes)
@@ -497,8 +510,8 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
       adam_scaled<WD>(pb0, (dq0 + dq1) + (dq2 + dq3), mb0, vb0, a.b1, a.b2, a.wd, aA, aE);
     }
     // next step's dropout factors (independent work for the Adam stream below)
-    f1 = b5_drop(a.seed, gstep + 1u, 0, r0, u, p_drop, scale);  // p_drop = 0: always 1
-    f2 = b5_drop(a.seed, gstep + 1u, 1, r0, u, p_drop, scale);
+    f1 = b5_drop(a.seed, gstep + 1u, el0, p_drop, scale);  // p_drop = 0: always 1
+    f2 = b5_drop(a.seed, gstep + 1u, el1, p_drop, scale);
     B5STAMP(7)
     // ---- dW1 (MFMA: A = h1[4q + lane % 4][r], B = this lane's dZ2, C register m = the gradient of
     // its own w1[j][4q + m]) + packed Adam on pairs of consecutive k

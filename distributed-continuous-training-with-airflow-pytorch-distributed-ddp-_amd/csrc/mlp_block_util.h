@@ -9,7 +9,7 @@ namespace bku {
 
 constexpr int QP_X1 = 0xB1;     // quad_perm [1,0,3,2]: lane ^ 1
 constexpr int QP_X2 = 0x4E;     // quad_perm [2,3,0,1]: lane ^ 2
-constexpr int ROR4 = 0x124;     // row_ror:4 (lane i of a 16-lane row reads lane (i + 4) % 16)
+constexpr int ROR4 = 0x124;     // row_ror:4 (lane i of a 16-lane row reads lane (i - 4) % 16: tools/probes/dpp_dir_probe)
 constexpr int ROR8 = 0x128;     // row_ror:8 == lane ^ 8 inside a 16-lane row
 constexpr int HMIRROR = 0x141;  // row_half_mirror: lane i <-> 7 - i inside each 8 lanes (lane ^ 7)
 constexpr int QB0 = 0x00, QB1 = 0x55, QB2 = 0xAA, QB3 = 0xFF;  // quad broadcast of lane 0..3

@@ -10,7 +10,7 @@ timeout -k 10 400 python -u -m pytest -q -rf -x --timeout 120 --timeout-method t
   -k "fused_train or block_kernel or grad_mode or dropout or eval" > $O/pytest_b5.log 2>&1
 rc=$?; tail -3 $O/pytest_b5.log; [ $rc -eq 0 ] || exit 1
 : > $O/b5_ab.log
-for cfg in ${B5_CFGS:-"5,1,0" "5,0,0" "5,1,1" "5,1,0" "5,0,0" "5,1,1"}; do
+for cfg in ${B5_CFGS:-5,1,0 5,0,0 5,1,1 5,1,0 5,0,0 5,1,1}; do
   IFS=, read blk dxm prio <<< "$cfg"
   DCT_MLP_BLOCK=$blk DCT_B5_DXM=$dxm DCT_B3_PRIO=$prio timeout -k 10 200 python bench.py --steps 20000 --warmup 2000 --no-reference-model > $O/bench_b5.json 2>&1 || exit $?
   python -c "import json; d=json.loads([l for l in open('$O/bench_b5.json') if l.startswith('{')][-1]); print('block$blk dxm$dxm prio$prio %.3f us/step %.0f samples/s loss %s -> %s' % (d['extra']['us_per_step'], d['value'], d['extra']['loss_first'], d['extra']['loss_last']))" >> $O/b5_ab.log
