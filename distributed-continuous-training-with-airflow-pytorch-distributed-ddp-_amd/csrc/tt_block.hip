@@ -369,7 +369,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
           zp[r] = f32_to_bf16(z);
           fp[r] = f32_to_bf16(gelu_f(z));
         }
-        if (a.save)
+        if (a.save && a.pre)  // null: the fused backward recomputes pre from a2 (BwdArgs::a2)
           *reinterpret_cast<uint2*>(a.pre + (size_t)(row0 + row) * FF + col0) =
               make_uint2(zp[0] | ((uint32_t)zp[1] << 16), zp[2] | ((uint32_t)zp[3] << 16));
         *reinterpret_cast<uint2*>(RS + row * F_LD + col0) =
@@ -425,8 +425,9 @@ struct BwdArgs {
   const float* h; const float* mean1; const float* rstd1; const float* ln1_w;
   const uint16_t* qkv; const uint16_t* o; const float* lse;
   const float* h1; const float* mean2; const float* rstd2; const float* ln2_w;
-  const uint16_t* pre;
+  const uint16_t* pre;  // null: recompute pre = a2 W1^T + b1 (same MFMAs and roundings as the forward)
   const uint16_t* wT;
+  const uint16_t* a2; const uint16_t* w1; const float* b1;  // the recompute's operands
   uint16_t* dpre; uint16_t* dh1_16; uint16_t* dqkv; float* dh; uint16_t* dh16;
   float *dln1_w, *dln1_b, *dln2_w, *dln2_b;
   uint64_t* prof;
@@ -552,6 +553,9 @@ __device__ __forceinline__ void rows_to_bf16(const float* G, uint16_t* X, int wv
   *reinterpret_cast<bf16x8*>(X + rl * XB_LD + 16 * g + 8) = o[1];
 }
 
+// RECOMP: the forward did not store the FFN pre-activation (32 KB per sample written, then read back
+// here); P1 recomputes it from the saved a2 (8 KB) and W1 in the dF tile's own lane layout instead
+template <bool RECOMP>
 __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* G = reinterpret_cast<float*>(smem);
@@ -581,7 +585,8 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
     float4 dv[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) dv[q] = dp[q];
-    load_tile<FF * 2, F_LD * 2>(R, a.pre + (size_t)row0 * FF);
+    if constexpr (RECOMP) load_tile<DM * 2, XB_LD * 2>(Os, a.a2 + (size_t)row0 * DM);  // Os is free until P4
+    else load_tile<FF * 2, F_LD * 2>(R, a.pre + (size_t)row0 * FF);
     red[threadIdx.x] = 0.f;
     float4* gp = reinterpret_cast<float4*>(G + rl * HS_LD + 16 * g);
     bf16x8 o[2];
@@ -621,20 +626,57 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) acc[i][t] = mfma32(bw[t], af[i], acc[i][t]);  // C = [column][token]
     }
-    // each lane: 4 consecutive columns of one token -> one 8-byte LDS read-modify-write per tile
+    if constexpr (RECOMP) {
+      // pre = a2 W1^T + b1 for the same (column, token) lanes: the forward's P5 MFMAs (A = W1 rows,
+      // B = a2 rows, k-steps in the same order) and its bf16 rounding -> bit-identical pre
+      f32x4 pz[4][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) pz[i][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < DM / 32; ++ks) {
+        bf16x8 af[4], bw[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          bw[t] = *reinterpret_cast<const bf16x8*>(a.w1 + (size_t)(64 * wv + 16 * t + c) * DM + 32 * ks + 8 * g);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Os + (16 * i + c) * XB_LD + 32 * ks + 8 * g);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) pz[i][t] = mfma32(bw[t], af[i], pz[i][t]);
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        uint2* pp = reinterpret_cast<uint2*>(R + (16 * i + c) * F_LD + 64 * wv + 16 * t + 4 * g);
-        const uint2 pv = *pp;
-        const uint16_t pr[4] = {(uint16_t)(pv.x & 0xFFFF), (uint16_t)(pv.x >> 16), (uint16_t)(pv.y & 0xFFFF),
-                                (uint16_t)(pv.y >> 16)};
-        uint16_t dp[4];
+        const float4 bv = *reinterpret_cast<const float4*>(a.b1 + 64 * wv + 16 * t + 4 * g);
+        const float bvs[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dp[r] = f32_to_bf16(acc[i][t][r] * gelu_grad_f(bf16_to_f32(pr[r])));
-        *pp = make_uint2(dp[0] | ((uint32_t)dp[1] << 16), dp[2] | ((uint32_t)dp[3] << 16));
+        for (int i = 0; i < 4; ++i) {
+          uint16_t dp[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            dp[r] = f32_to_bf16(acc[i][t][r] * gelu_grad_f(bf16_to_f32(f32_to_bf16(pz[i][t][r] + bvs[r]))));
+          *reinterpret_cast<uint2*>(R + (16 * i + c) * F_LD + 64 * wv + 16 * t + 4 * g) =
+              make_uint2(dp[0] | ((uint32_t)dp[1] << 16), dp[2] | ((uint32_t)dp[3] << 16));
+        }
       }
+    } else {
+      // each lane: 4 consecutive columns of one token -> one 8-byte LDS read-modify-write per tile
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          uint2* pp = reinterpret_cast<uint2*>(R + (16 * i + c) * F_LD + 64 * wv + 16 * t + 4 * g);
+          const uint2 pv = *pp;
+          const uint16_t pr[4] = {(uint16_t)(pv.x & 0xFFFF), (uint16_t)(pv.x >> 16), (uint16_t)(pv.y & 0xFFFF),
+                                  (uint16_t)(pv.y >> 16)};
+          uint16_t dp[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dp[r] = f32_to_bf16(acc[i][t][r] * gelu_grad_f(bf16_to_f32(pr[r])));
+          *pp = make_uint2(dp[0] | ((uint32_t)dp[1] << 16), dp[2] | ((uint32_t)dp[3] << 16));
+        }
+    }
     // dpre out: this wave's 64-column block of all 64 rows (128 B per row, 16-byte chunks)
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -868,7 +910,7 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
   const bool save = p[13] != 0;
   uintptr_t any = 0;
   for (int i = 0; i < 27; ++i) {
-    const bool needed = i < 13 || i == 25 || save;
+    const bool needed = (i < 13 || i == 25 || save) && i != 24;  // pre (24) optional: see BwdArgs::pre
     if (needed && !p[i]) return (int)hipErrorInvalidValue;
     any |= p[i];
   }
@@ -903,12 +945,17 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
 int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
                      void* stream) {
   using namespace dct::ttb;
-  if ((n_ptrs != 23 && n_ptrs != 24) || T != dct::ttb::T || DM != dct::ttb::DM || H != NH || FF != dct::ttb::FF || Bsz <= 0)
+  // 23 (+1 prof) pointers; 26 (+1 prof): + a2, w1 (bf16 [FF][DM]), b1 - with pre (p[12]) null the
+  // kernel recomputes the pre-activation from them
+  const bool ext = n_ptrs == 26 || n_ptrs == 27;
+  if ((n_ptrs != 23 && n_ptrs != 24 && !ext) || T != dct::ttb::T || DM != dct::ttb::DM || H != NH ||
+      FF != dct::ttb::FF || Bsz <= 0)
     return (int)hipErrorInvalidValue;
+  const bool recomp = ext && p[12] == 0;
   uintptr_t any = 0;
-  for (int i = 0; i < 23; ++i) {
-    if (!p[i]) return (int)hipErrorInvalidValue;
-    if (i < 19) any |= p[i];
+  for (int i = 0; i < (ext ? 26 : 23); ++i) {
+    if (!p[i] && !(i == 12 && recomp) && !(i >= 23 && !recomp)) return (int)hipErrorInvalidValue;
+    if (i < 19 || i >= 23) any |= p[i];
   }
   if (any & 15) return (int)hipErrorInvalidValue;
   BwdArgs a;
@@ -919,16 +966,23 @@ int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
   a.dpre = (uint16_t*)p[14]; a.dh1_16 = (uint16_t*)p[15]; a.dqkv = (uint16_t*)p[16]; a.dh = (float*)p[17];
   a.dh16 = (uint16_t*)p[18];
   a.dln1_w = (float*)p[19]; a.dln1_b = (float*)p[20]; a.dln2_w = (float*)p[21]; a.dln2_b = (float*)p[22];
-  a.prof = n_ptrs == 24 ? (uint64_t*)p[23] : nullptr;
+  a.a2 = ext ? (const uint16_t*)p[23] : nullptr;
+  a.w1 = ext ? (const uint16_t*)p[24] : nullptr;
+  a.b1 = ext ? (const float*)p[25] : nullptr;
+  a.prof = n_ptrs == 24 ? (uint64_t*)p[23] : (n_ptrs == 27 ? (uint64_t*)p[26] : nullptr);
   a.scale = scale;
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)tt_block_bwd_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, BWD_LDS);
-    if (e != hipSuccess) return (int)e;
+    for (const void* k : {(const void*)tt_block_bwd_kernel<false>, (const void*)tt_block_bwd_kernel<true>}) {
+      const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, BWD_LDS);
+      if (e != hipSuccess) return (int)e;
+    }
     attr = true;
   }
-  hipLaunchKernelGGL(tt_block_bwd_kernel, dim3(Bsz), dim3(256), BWD_LDS, reinterpret_cast<hipStream_t>(stream), a);
+  if (recomp)
+    hipLaunchKernelGGL(tt_block_bwd_kernel<true>, dim3(Bsz), dim3(256), BWD_LDS, reinterpret_cast<hipStream_t>(stream), a);
+  else
+    hipLaunchKernelGGL(tt_block_bwd_kernel<false>, dim3(Bsz), dim3(256), BWD_LDS, reinterpret_cast<hipStream_t>(stream), a);
   return (int)hipGetLastError();
 }
 

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 from typing import Dict, Iterable, List, Optional
 
 import torch
@@ -555,7 +556,11 @@ class _TTBlockFn(torch.autograd.Function):
         o = torch.empty(M, dm, dtype=bf, device=dev)
         lse = torch.empty(B * H * T, dtype=f32, device=dev)
         h1, out = torch.empty(M, dm, dtype=f32, device=dev), torch.empty(M, dm, dtype=f32, device=dev)
-        f, pre = torch.empty(M, FF, dtype=bf, device=dev), torch.empty(M, FF, dtype=bf, device=dev)
+        f = torch.empty(M, FF, dtype=bf, device=dev)
+        # with the fused backward the FFN pre-activation is not stored (32 KB per sample written and read
+        # back): tt_block_bwd_kernel recomputes it from a2 and W1 (DCT_TT_RECOMPUTE_PRE=0: store it)
+        recomp = _TT_FUSED_BWD and os.environ.get("DCT_TT_RECOMPUTE_PRE", "1") != "0"
+        pre = torch.empty(0 if recomp else M, FF, dtype=bf, device=dev)
         wT = torch.empty(2 * FF * dm + 4 * dm * dm, dtype=bf, device=dev)  # W2^T | W1^T | Wo^T | Wqkv^T
         vecs = [t.contiguous() for t in (ln1_w, ln1_b, bqkv, bo, ln2_w, ln2_b, b1, b2)]
         ptrs = [h, vecs[0], vecs[1], wqkvb, vecs[2], wob, vecs[3], vecs[4], vecs[5], w1b, vecs[6], w2b, vecs[7],
@@ -563,7 +568,8 @@ class _TTBlockFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(dm // H)
         if _TT_PROF is not None:  # tools/debug/tt_phase_prof.py
             ptrs.append(_tt_prof_buf("fwd", B, dev))
-        nat.tt_block_fwd([t.data_ptr() for t in ptrs], B, T, dm, H, FF, float(eps), scale, st)
+        nat.tt_block_fwd([0 if t is pre and recomp else t.data_ptr() for t in ptrs], B, T, dm, H, FF, float(eps),
+                         scale, st)
         ctx.save_for_backward(h, st4, a1, wqkvb, qkv, o, lse, wob, h1, a2, w1b, w2b, f, pre, wT, vecs[0], vecs[4])
         ctx.params = (ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2)
         ctx.dims = (B, H, T, dm // H, scale)
@@ -574,9 +580,9 @@ class _TTBlockFn(torch.autograd.Function):
         h, st4, a1, wqkvb, qkv, o, lse, wob, h1, a2, w1b, w2b, f, pre, wT, ln1w, ln2w = ctx.saved_tensors
         p = ctx.params
         B, H, T, D, scale = ctx.dims
-        if _TT_FUSED_BWD:
+        if _TT_FUSED_BWD or pre.numel() == 0:  # no stored pre-activation: only the fused backward recomputes it
             return (*_tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, p, B, H, T,
-                                         scale), None, None, None, None)
+                                         scale, w1b), None, None, None, None)
         dh1, dl2w, dl2b, dw1, db1, dw2, db2 = _prenorm_ffn_bwd(dout, (h1, st4[2], st4[3], a2, w1b, w2b, f, pre),
                                                                p[6:])
         dh, dl1w, dl1b, dwqkv, dbqkv, dwo, dbo = _prenorm_attn_bwd(
@@ -594,7 +600,8 @@ def _tt_prof_buf(kind: str, B: int, dev) -> torch.Tensor:
     return buf
 
 
-def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, params, B, H, T, scale):
+def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, params, B, H, T, scale,
+                        w1b=None):
     """Backward of the fused block: ONE kernel for the whole dX chain (csrc/tt_block.hip
     tt_block_bwd_kernel: dF/gelu', W1, LN2, Wo, attention, Wqkv, LN1 per sample) writing the dZ
     operands of the four dW GEMMs, which then run split-K over all rows with the bias gradients
@@ -604,7 +611,8 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
     ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2 = params
     dout = dout.contiguous().float()
     M, dm = h.shape
-    FF = pre.shape[1]
+    FF = w1.shape[0]
+    recomp = pre.numel() == 0
     dev, bf = h.device, torch.bfloat16
     dpre = torch.empty(M, FF, dtype=bf, device=dev)
     dh1_16 = torch.empty(M, dm, dtype=bf, device=dev)
@@ -614,9 +622,14 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
     lg = [_grad_dst(t, zero=True) for t in (ln1_w, ln1_b, ln2_w, ln2_b)]
     ptrs = [dout, h, st4[0], st4[1], ln1w, qkv, o, lse, h1, st4[2], st4[3], ln2w, pre, wT,
             dpre, dh1_16, dqkv, dh, dh16] + [g for g, _ in lg]
+    addrs = [t.data_ptr() for t in ptrs]
+    if recomp:  # pre-activation recomputed from a2 / W1 / b1 inside the kernel
+        addrs[12] = 0
+        b1c = b1.detach().contiguous()
+        addrs += [a2.data_ptr(), w1b.data_ptr(), b1c.data_ptr()]
     if _TT_PROF is not None:
-        ptrs.append(_tt_prof_buf("bwd", B, dev))
-    nat.tt_block_bwd([t.data_ptr() for t in ptrs], B, T, dm, H, FF, scale, st)
+        addrs.append(_tt_prof_buf("bwd", B, dev).data_ptr())
+    nat.tt_block_bwd(addrs, B, T, dm, H, FF, scale, st)
     dout16 = _bf16_of(dout)
     items = [(dout16, f, w2, b2), (dpre, a2, w1, b1), (dh1_16, o, wo, bo), (dqkv, a1, wqkv, bqkv)]
     b = _BOUND
