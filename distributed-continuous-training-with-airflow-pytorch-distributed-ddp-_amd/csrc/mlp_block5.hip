@@ -134,8 +134,10 @@ __device__ __forceinline__ void adam_v2(v2f& p, v2f g, v2f& m, v2f& v, float b1,
   p = p - m * ((v2f){d.y, d.x} * R);
 }
 
-// LK: 0 = cross-entropy, 1 = MSE against the one-hot label; WD: L2 term in the update
-template <bool WD, int LK, bool PROF = false, bool DXM = true>
+// LK: 0 = cross-entropy, 1 = MSE against the one-hot label; WD: L2 term in the update; ADAM = false:
+// grad mode (the DDP step: ONE step at the device batch cursor, gradients + batch loss to grad_out,
+// the previous step's all-reduced loss to loss_out[cursor - 1]; no moments read or written)
+template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true>
 __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, MlpArgs a) {
   using namespace blk5;
   using namespace bku;
@@ -156,8 +158,10 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   for (int i = 0; i < Stg::LD; ++i) {
     const int f = wo1 + 4 * (i * NT + tid);
     sp[i] = *reinterpret_cast<const v4f*>(a.p + f);
-    sm[i] = *reinterpret_cast<const v4f*>(a.m + f);
-    sv[i] = *reinterpret_cast<const v4f*>(a.v + f);
+    if constexpr (ADAM) {
+      sm[i] = *reinterpret_cast<const v4f*>(a.m + f);
+      sv[i] = *reinterpret_cast<const v4f*>(a.v + f);
+    }
   }
   // W0 slices of unit u (inputs d = r0 and r0 + 4), b0[u]
   float w0[2], m0[2], v0[2];
@@ -167,10 +171,10 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     const bool ok = d < D0;
     const int f = wo0 + u * D0 + (ok ? d : 0);
     w0[i] = ok ? a.p[f] : 0.f;
-    m0[i] = ok ? a.m[f] : 0.f;
-    v0[i] = ok ? a.v[f] : 0.f;
+    m0[i] = (ok && ADAM) ? a.m[f] : 0.f;
+    v0[i] = (ok && ADAM) ? a.v[f] : 0.f;
   }
-  float pb0 = a.p[bo0 + u], mb0 = a.m[bo0 + u], vb0 = a.v[bo0 + u];
+  float pb0 = a.p[bo0 + u], mb0 = ADAM ? a.m[bo0 + u] : 0.f, vb0 = ADAM ? a.v[bo0 + u] : 0.f;
   // W2 column u (both classes in every lane of the quad); lane r0 < 2 owns W2[r0][u] (+ moments);
   // b1[u] in every lane of the quad; b2 owned by wave 0, lanes 0 / 1
   float pw2[C];
@@ -178,11 +182,11 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   for (int c = 0; c < C; ++c) pw2[c] = a.p[wo2 + c * H + u];
   const bool own_w2 = r0 < C;
   const int fw2 = wo2 + (own_w2 ? r0 : 0) * H + u;
-  float mw2 = own_w2 ? a.m[fw2] : 0.f, vw2 = own_w2 ? a.v[fw2] : 0.f;
-  float pb1 = a.p[bo1 + u], mb1 = a.m[bo1 + u], vb1 = a.v[bo1 + u];
+  float mw2 = (own_w2 && ADAM) ? a.m[fw2] : 0.f, vw2 = (own_w2 && ADAM) ? a.v[fw2] : 0.f;
+  float pb1 = a.p[bo1 + u], mb1 = ADAM ? a.m[bo1 + u] : 0.f, vb1 = ADAM ? a.v[bo1 + u] : 0.f;
   const bool own_b2 = w == 0 && l < C;
   const int fb2 = bo2 + (own_b2 ? l : 0);
-  float pb2 = own_b2 ? a.p[fb2] : 0.f, mb2 = own_b2 ? a.m[fb2] : 0.f, vb2 = own_b2 ? a.v[fb2] : 0.f;
+  float pb2 = own_b2 ? a.p[fb2] : 0.f, mb2 = (own_b2 && ADAM) ? a.m[fb2] : 0.f, vb2 = (own_b2 && ADAM) ? a.v[fb2] : 0.f;
 
   // step counter and the first batch's row indices through the scalar cache (their round trips
   // overlap the W1 loads)
@@ -193,10 +197,11 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     step_base = (uint32_t)t0;
   }
   const int Bsz = a.B;
-  const int bs0 = min(Bsz, a.n_items);
+  const int cur0 = (!ADAM && a.cursor) ? sload(a.cursor) : 0;  // grad mode: batch index from the device cursor
+  const int bs0 = min(Bsz, a.n_items - cur0 * Bsz);
   int ridx[B];
 #pragma unroll
-  for (int b = 0; b < B; ++b) ridx[b] = b < bs0 ? sload(a.idx + b) : 0;
+  for (int b = 0; b < B; ++b) ridx[b] = b < bs0 ? sload(a.idx + cur0 * Bsz + b) : 0;
   float x_first = 0.f;
   int lab_first = 0;
   {
@@ -209,15 +214,24 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   // ---- W1 k-slice + moments into registers through the swizzled staging tiles
   float w1[2][KS], m1[2][KS], v1[2][KS];
   Stg::put(lds, sp, tid);
-  Stg::put(lds + STG, sm, tid);
+  if constexpr (ADAM) Stg::put(lds + STG, sm, tid);
   __syncthreads();
   Stg::get<KS>(lds, w1, l, KS / 4 * w);
-  Stg::get<KS>(lds + STG, m1, l, KS / 4 * w);
-  __syncthreads();
-  Stg::put(lds, sv, tid);
-  __syncthreads();
-  Stg::get<KS>(lds, v1, l, KS / 4 * w);
+  if constexpr (ADAM) {
+    Stg::get<KS>(lds + STG, m1, l, KS / 4 * w);
+    __syncthreads();
+    Stg::put(lds, sv, tid);
+    __syncthreads();
+    Stg::get<KS>(lds, v1, l, KS / 4 * w);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int k = 0; k < KS; ++k) m1[j][k] = v1[j][k] = 0.f;
+  }
   __syncthreads();  // staging reads done before the tiles (same LDS) are zeroed
+  // grad mode: the previous DDP step's all-reduced loss (still in grad_out[P]) to its slot
+  if (!ADAM && tid == 0 && cur0 > 0 && a.loss_out) a.loss_out[cur0 - 1] = a.grad_out[sh.P];
 
   // ---- LDS: first batch into input buffer 0, W2 / b2 into publish buffer 0
   for (int e = 4 * tid; e < TOTAL; e += 4 * NT) *reinterpret_cast<float4*>(lds + e) = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -232,7 +246,7 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   if (tid < nel) { role = 1; pb = tid / D0; pk = tid - pb * D0; }
   else if (tid < nel + Bsz) { role = 2; pb = tid - nel; }
   int ridx_next = 0;
-  if (role && Bsz + pb < a.n_items) ridx_next = a.idx[Bsz + pb];
+  if (role && (cur0 + 1) * Bsz + pb < a.n_items) ridx_next = a.idx[(cur0 + 1) * Bsz + pb];
   const uint32_t* pf_base = role == 1 ? reinterpret_cast<const uint32_t*>(a.X) + pk : reinterpret_cast<const uint32_t*>(a.Y);
   const int pf_stride = role == 1 ? a.ldx : (role == 2 ? 1 : 0);
   __syncthreads();
@@ -280,15 +294,16 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     pacc[9] = t_last - t_kstart;
   }
   for (int s = 0; s < a.steps; ++s) {
-    const int bs = min(Bsz, a.n_items - s * Bsz);
+    const int sb = s + cur0;  // batch index (grad mode: at the device cursor)
+    const int bs = min(Bsz, a.n_items - sb * Bsz);
     const uint32_t gstep = step_base + (uint32_t)s;
     const int xbn = xb == 2 ? 0 : xb + 1;
     const int pbuf = s & 1, nbuf = pbuf ^ 1;
     const float* xT = lds + XT + xb * DMAX * 4;
     const bool have_next = (s + 1 < a.steps);
-    const int bs_next = have_next ? min(Bsz, a.n_items - (s + 1) * Bsz) : 0;
+    const int bs_next = have_next ? min(Bsz, a.n_items - (sb + 1) * Bsz) : 0;
     const uint32_t raw_next = pf_base[(size_t)ridx_next * pf_stride];
-    const int nx2 = min((s + 2) * Bsz + pb, a.n_items - 1);
+    const int nx2 = min((sb + 2) * Bsz + pb, a.n_items - 1);
     const int ridx_next2 = a.idx[nx2 < 0 ? 0 : nx2];
 
     // ---- F1: h1[u][r0] (quad reduce-scatter over the input slices); the tile stays for dW0
@@ -410,7 +425,12 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
       float t = lv + dpp<QP_X1>(lv);
       t += dpp<QP_X2>(t);
       t += dpp<ROR4>(t);
-      if (l == 0 && a.loss_out) a.loss_out[s] = bs > 0 ? t * __builtin_amdgcn_rcpf((float)bs) : 0.f;
+      const float bl = bs > 0 ? t * __builtin_amdgcn_rcpf((float)bs) : 0.f;
+      if constexpr (ADAM) {
+        if (l == 0 && a.loss_out) a.loss_out[s] = bl;
+      } else {
+        if (l == 0) a.grad_out[sh.P] = bl;
+      }
     }
     B5STAMP(5)
 
@@ -448,14 +468,20 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
       // (W2[r0][u] is broadcast from quad lanes 0 / 1, b2 published by wave 0's lanes 0 / 1)
       float pown = (r0 & 1) ? pw2[1] : pw2[0];
       const float gown = (r0 & 1) ? gw1 : gw0;
-      adam_pair<WD>(pown, gown, mw2, vw2, pb1, gb1, mb1, vb1, a.b1, a.b2, a.wd, aA, aE);
-      pw2[0] = dpp<QB0>(pown);
-      pw2[1] = dpp<QB1>(pown);
-      if (own_w2) lds[W2L + nbuf * (H * C) + u * C + r0] = pown;
       const float gb = (l & 1) ? (dz3[0][1] + dz3[1][1]) + (dz3[2][1] + dz3[3][1])
                                : (dz3[0][0] + dz3[1][0]) + (dz3[2][0] + dz3[3][0]);
-      adam_scaled<WD>(pb2, gb, mb2, vb2, a.b1, a.b2, a.wd, aA, aE);
-      if (own_b2) lds[B2L + nbuf * 4 + l] = pb2;
+      if constexpr (ADAM) {
+        adam_pair<WD>(pown, gown, mw2, vw2, pb1, gb1, mb1, vb1, a.b1, a.b2, a.wd, aA, aE);
+        pw2[0] = dpp<QB0>(pown);
+        pw2[1] = dpp<QB1>(pown);
+        if (own_w2) lds[W2L + nbuf * (H * C) + u * C + r0] = pown;
+        adam_scaled<WD>(pb2, gb, mb2, vb2, a.b1, a.b2, a.wd, aA, aE);
+        if (own_b2) lds[B2L + nbuf * 4 + l] = pb2;
+      } else {  // grad mode (one step): dW2[r0][u], db1[u], db2 to the flat gradient
+        if (own_w2) a.grad_out[fw2] = gown;
+        if (r0 == 0) a.grad_out[bo1 + u] = gb1;
+        if (own_b2) a.grad_out[fb2] = gb;
+      }
     }
     B5STAMP(6)
     // ---- dZ1 = W1^T dZ2 over this wave's k-slice, lane l keeps its own (unit u, row r0)
@@ -506,8 +532,14 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
       const float dq0 = dpp<QB0>(dz1), dq1 = dpp<QB1>(dz1), dq2 = dpp<QB2>(dz1), dq3 = dpp<QB3>(dz1);
       const float g0 = dq0 * xa.x + dq1 * xa.y + dq2 * xa.z + dq3 * xa.w;
       const float g1 = dq0 * xc.x + dq1 * xc.y + dq2 * xc.z + dq3 * xc.w;
-      adam_pair<WD>(w0[0], g0, m0[0], v0[0], w0[1], g1, m0[1], v0[1], a.b1, a.b2, a.wd, aA, aE);  // d >= D0: stays 0
-      adam_scaled<WD>(pb0, (dq0 + dq1) + (dq2 + dq3), mb0, vb0, a.b1, a.b2, a.wd, aA, aE);
+      if constexpr (ADAM) {
+        adam_pair<WD>(w0[0], g0, m0[0], v0[0], w0[1], g1, m0[1], v0[1], a.b1, a.b2, a.wd, aA, aE);  // d >= D0: stays 0
+        adam_scaled<WD>(pb0, (dq0 + dq1) + (dq2 + dq3), mb0, vb0, a.b1, a.b2, a.wd, aA, aE);
+      } else {
+        if (r0 < D0) a.grad_out[wo0 + u * D0 + r0] = g0;
+        if (r0 + 4 < D0) a.grad_out[wo0 + u * D0 + r0 + 4] = g1;
+        if (r0 == 0) a.grad_out[bo0 + u] = (dq0 + dq1) + (dq2 + dq3);
+      }
     }
     // next step's dropout factors (independent work for the Adam stream below)
     f1 = b5_drop(a.seed, gstep + 1u, el0, p_drop, scale);  // p_drop = 0: always 1
@@ -526,12 +558,19 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
 #pragma unroll
         for (int r = 0; r < 4; ++r) g[j] = mfma4(hv[r], dz2[j][r], g[j]);
       }
+      if constexpr (ADAM) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-          adam_v2<WD>(W[j][2 * q + h], (v2f){g[j][2 * h], g[j][2 * h + 1]}, Mo[j][2 * q + h], Vo[j][2 * q + h], a.b1,
-                      a.b2, a.wd, aA, aE);
+          for (int h = 0; h < 2; ++h)
+            adam_v2<WD>(W[j][2 * q + h], (v2f){g[j][2 * h], g[j][2 * h + 1]}, Mo[j][2 * q + h], Vo[j][2 * q + h], a.b1,
+                        a.b2, a.wd, aA, aE);
+      } else {  // dW1[o = l + 64 j][16 w + 4 q .. + 3]: one 16-byte store per (j, q)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          *reinterpret_cast<float4*>(a.grad_out + wo1 + (l + 64 * j) * H + KS * w + 4 * q) =
+              make_float4(g[j][0], g[j][1], g[j][2], g[j][3]);
+      }
     }
     __builtin_amdgcn_wave_barrier();  // the next step rewrites this wave's h1 tiles
     B5STAMP(8)
@@ -539,6 +578,10 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   }
   if (a.step_counter && tid == 0)
     __hip_atomic_store(a.step_counter, t0 + a.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if constexpr (!ADAM) {
+    if (a.cursor && tid == 0) __hip_atomic_store(a.cursor, cur0 + a.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;  // parameters unchanged
+  }
 
   // ---- write back parameters and moments (flat torch order); opaque bases so the prologue's
   // addresses are recomputed here instead of being kept live across the loop
@@ -606,17 +649,18 @@ bool mlp_block5_ok(const MlpShape& sh, const MlpArgs& a) {
   if (env && (env[0] == '0' || env[0] == '2' || env[0] == '3' || env[0] == '4' || env[0] == 'v')) return false;
   const bool aligned = (sh.woff[1] % 4) == 0 && ((uintptr_t)a.p & 15) == 0 && (((uintptr_t)a.m | (uintptr_t)a.v) & 15) == 0;
   return aligned && sh.L == 3 && sh.dims[1] == blk5::H && sh.dims[2] == blk5::H && sh.dims[0] >= 1 &&
-         sh.dims[0] <= blk5::DMAX && sh.dims[3] == blk5::C && a.B >= 1 && a.B <= blk5::B && a.mode == 0 &&
-         (a.loss_kind == 0 || a.loss_kind == 1) && a.cursor == nullptr && a.pending == nullptr && a.stage == nullptr &&
-         a.xg_world <= 1;
+         sh.dims[0] <= blk5::DMAX && sh.dims[3] == blk5::C && a.B >= 1 && a.B <= blk5::B &&
+         // train mode, or grad mode for ONE step (the DDP step path: grads + loss to grad_out, device cursor)
+         ((a.mode == 0 && a.cursor == nullptr) || (a.mode == 1 && a.steps == 1 && a.grad_out != nullptr)) &&
+         (a.loss_kind == 0 || a.loss_kind == 1) && a.pending == nullptr && a.stage == nullptr && a.xg_world <= 1;
 }
 
-template <bool WD, int LK, bool PROF = false, bool DXM = true>
+template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true>
 static void b5_launch(size_t bytes, hipStream_t st, const MlpShape& sh, const MlpArgs& a) {
-  static const hipError_t attr = hipFuncSetAttribute((const void*)mlp_block5_kernel<WD, LK, PROF, DXM>,
+  static const hipError_t attr = hipFuncSetAttribute((const void*)mlp_block5_kernel<WD, LK, PROF, DXM, ADAM>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   (void)attr;
-  hipLaunchKernelGGL((mlp_block5_kernel<WD, LK, PROF, DXM>), dim3(1), dim3(blk5::NT), bytes, st, sh, a);
+  hipLaunchKernelGGL((mlp_block5_kernel<WD, LK, PROF, DXM, ADAM>), dim3(1), dim3(blk5::NT), bytes, st, sh, a);
 }
 
 hipError_t mlp_launch_block5(const MlpShape& sh, const MlpArgs& a, hipStream_t st) {
@@ -628,7 +672,10 @@ hipError_t mlp_launch_block5(const MlpShape& sh, const MlpArgs& a, hipStream_t s
   // DCT_B5_DXM=0: the dZ1 product on the VALU (4 reduce-scatter passes) instead of the MFMA (A/B)
   const char* de = getenv("DCT_B5_DXM");
   const bool dxm = !(de && de[0] == '0');
-  if (a.prof && a.loss_kind == 0) {
+  if (a.mode == 1) {  // grad mode: no Adam, no moments
+    if (a.loss_kind == 0) b5_launch<false, 0, false, true, false>(bytes, st, sh, a2);
+    else b5_launch<false, 1, false, true, false>(bytes, st, sh, a2);
+  } else if (a.prof && a.loss_kind == 0) {
     if (dxm) b5_launch<true, 0, true, true>(bytes, st, sh, a2);
     else b5_launch<true, 0, true, false>(bytes, st, sh, a2);
   } else if (a.prof) {
