@@ -63,7 +63,9 @@ KERNELS = ["auto", "lds", "lds-noblock", "lds-v1", "lds-mf", "lds-b3", "lds-b3v"
 @pytest.mark.parametrize("loss", ["ce", "mse"])
 @pytest.mark.parametrize("dims,B", [([5, 64, 2], 4), ([5, 128, 128, 2], 4), ([5, 64, 2], 3), ([9, 48, 64, 3], 4),
                                     ([16, 32, 48, 32, 3], 16), ([5, 128, 128, 2], 16), ([7, 20, 2], 9),
-                                    ([7, 20, 2], 8), ([12, 40, 4], 6), ([16, 64, 3], 2), ([5, 64, 2], 1)])
+                                    ([7, 20, 2], 8), ([12, 40, 4], 6), ([16, 64, 3], 2), ([5, 64, 2], 1),
+                                    # mlp_block5 below its full batch and at its input-width bounds
+                                    ([3, 128, 128, 2], 3), ([8, 128, 128, 2], 1), ([1, 128, 128, 2], 2)])
 def test_fused_train_matches_torch_adam(dims, B, loss, kernel, cuda, monkeypatch):
     _set_kernel_env(monkeypatch, kernel)
     torch.manual_seed(1)
@@ -101,9 +103,40 @@ def test_fused_train_matches_torch_adam(dims, B, loss, kernel, cuda, monkeypatch
     assert torch.allclose(m.cpu(), ref_m, atol=1e-4, rtol=1e-2)
 
 
+@pytest.mark.parametrize("kernel", ["auto", "lds-b3"])
+@pytest.mark.parametrize("loss", ["ce", "mse"])
+def test_weather_3x128_weight_decay_matches_torch_adam(kernel, loss, cuda, monkeypatch):
+    """The 3x128 trainers' L2 term (torch Adam weight_decay: g += wd * p) - mlp_block5's WD
+    instantiation by default, mlp_block3's with lds-b3 - against torch.optim.Adam."""
+    _set_kernel_env(monkeypatch, kernel)
+    torch.manual_seed(6)
+    dims, B, N, n_items = [5, 128, 128, 2], 4, 200, 60
+    X = torch.randn(N, 5)
+    Y = torch.randint(0, 2, (N,))
+    idx = torch.randperm(N)[:n_items]
+    net = _ref_net(dims)
+    p = _flat(net).to(cuda)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    steps = n_items // B
+    losses = torch.zeros(steps, device=cuda)
+    k = FusedMLPKernel(dims, bmax=4)
+    k.train(p, m, v, X.to(cuda), Y.to(cuda, torch.int32), idx.to(cuda, torch.int32), n_items=n_items, batch=B,
+            steps=steps, t0=0, lr=0.01, weight_decay=0.05, loss=loss, loss_out=losses)
+    opt = torch.optim.Adam(net.parameters(), lr=0.01, weight_decay=0.05)
+    for s in range(steps):
+        rows = idx[s * B:(s + 1) * B]
+        opt.zero_grad()
+        _ref_loss(net(X[rows]), Y[rows], loss).backward()
+        opt.step()
+    err = (p.cpu() - _flat(net)).abs()
+    assert err.median() < 1e-5, err.median()
+    assert err.max() < 2e-3, err.max()
+
+
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("dims,B", [([5, 64, 2], 4), ([5, 128, 128, 2], 4), ([12, 40, 40, 5], 13),
-                                    ([9, 48, 64, 3], 4), ([20, 128, 128, 4], 3), ([32, 128, 128, 1], 4)])
+                                    ([9, 48, 64, 3], 4), ([20, 128, 128, 4], 3), ([32, 128, 128, 1], 4),
+                                    ([8, 128, 128, 2], 3), ([2, 128, 128, 2], 1)])
 def test_fused_grad_mode_matches_autograd(dims, B, kernel, cuda, monkeypatch):
     _set_kernel_env(monkeypatch, kernel)
     torch.manual_seed(2)
