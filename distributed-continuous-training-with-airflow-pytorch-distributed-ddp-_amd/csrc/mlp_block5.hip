@@ -148,11 +148,28 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   const int u = KS * w + (l >> 2);
   const int wo0 = sh.woff[0], bo0 = sh.boff[0], wo1 = sh.woff[1], bo1 = sh.boff[1];
   const int wo2 = sh.woff[2], bo2 = sh.boff[2];
-  unsigned long long pacc[PROF ? 11 : 1] = {};
+  unsigned long long pacc[PROF ? 16 : 1] = {};
   unsigned long long t_last = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
   const unsigned long long t_kstart = t_last;
 
-  // ---- W1 + moments: issued first, coalesced, redistributed through LDS below
+  // ---- batch indices first: the first batch's row of lane tid < 32 (row fb, feature fd) and the next
+  // batch's prefetch element, as VECTOR loads (a scalar load's wait would stall the whole prologue
+  // behind it, lgkmcnt is shared with the LDS staging); the dependent X / Y gathers follow the W1 loads
+  const int Bsz = a.B;
+  const int cur0 = (!ADAM && a.cursor) ? sload(a.cursor) : 0;  // grad mode: batch index from the device cursor
+  const int bs0 = min(Bsz, a.n_items - cur0 * Bsz);
+  const int fb = tid & 3, fd = tid >> 2;
+  const bool first_ok = tid < B * DMAX && fb < bs0;
+  const int rb_first = first_ok ? a.idx[cur0 * Bsz + fb] : 0;
+  // prefetch roles: thread -> (row pb, feature pk) of the next batch, or (row pb, label)
+  const int nel = Bsz * D0;
+  int role = 0, pb = 0, pk = 0;
+  if (tid < nel) { role = 1; pb = tid / D0; pk = tid - pb * D0; }
+  else if (tid < nel + Bsz) { role = 2; pb = tid - nel; }
+  int ridx_next = 0;
+  if (role && (cur0 + 1) * Bsz + pb < a.n_items) ridx_next = a.idx[(cur0 + 1) * Bsz + pb];
+
+  // ---- W1 + moments: coalesced, redistributed through LDS below
   v4f sp[Stg::LD], sm[Stg::LD], sv[Stg::LD];
 #pragma unroll
   for (int i = 0; i < Stg::LD; ++i) {
@@ -196,32 +213,24 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     t0 = sload(a.step_counter);
     step_base = (uint32_t)t0;
   }
-  const int Bsz = a.B;
-  const int cur0 = (!ADAM && a.cursor) ? sload(a.cursor) : 0;  // grad mode: batch index from the device cursor
-  const int bs0 = min(Bsz, a.n_items - cur0 * Bsz);
-  int ridx[B];
-#pragma unroll
-  for (int b = 0; b < B; ++b) ridx[b] = b < bs0 ? sload(a.idx + cur0 * Bsz + b) : 0;
   float x_first = 0.f;
   int lab_first = 0;
-  {
-    const int b = tid & 3, d = tid >> 2;
-    const int rb = ridx[0] * (b == 0) + ridx[1] * (b == 1) + ridx[2] * (b == 2) + ridx[3] * (b == 3);
-    if (tid < B * DMAX && b < bs0 && d < D0) x_first = a.X[(size_t)rb * a.ldx + d];
-    if (tid < B && tid < bs0) lab_first = a.Y[rb];
-  }
+  if (first_ok && fd < D0) x_first = a.X[(size_t)rb_first * a.ldx + fd];
+  if (tid < B && tid < bs0) lab_first = a.Y[rb_first];  // tid < 4: fb = tid
 
   // ---- W1 k-slice + moments into registers through the swizzled staging tiles
   float w1[2][KS], m1[2][KS], v1[2][KS];
+  if constexpr (PROF) pacc[11] = __builtin_amdgcn_s_memtime() - t_kstart;  // loads issued
   Stg::put(lds, sp, tid);
   if constexpr (ADAM) Stg::put(lds + STG, sm, tid);
-  __syncthreads();
+  lds_barrier();
+  if constexpr (PROF) pacc[12] = __builtin_amdgcn_s_memtime() - t_kstart;  // W1 + m staged
   Stg::get<KS>(lds, w1, l, KS / 4 * w);
   if constexpr (ADAM) {
     Stg::get<KS>(lds + STG, m1, l, KS / 4 * w);
-    __syncthreads();
+    lds_barrier();
     Stg::put(lds, sv, tid);
-    __syncthreads();
+    lds_barrier();
     Stg::get<KS>(lds, v1, l, KS / 4 * w);
   } else {
 #pragma unroll
@@ -229,28 +238,23 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
 #pragma unroll
       for (int k = 0; k < KS; ++k) m1[j][k] = v1[j][k] = 0.f;
   }
-  __syncthreads();  // staging reads done before the tiles (same LDS) are zeroed
+  lds_barrier();  // staging reads done before the tiles (same LDS) are zeroed
+  if constexpr (PROF) pacc[13] = __builtin_amdgcn_s_memtime() - t_kstart;  // all three in registers
   // grad mode: the previous DDP step's all-reduced loss (still in grad_out[P]) to its slot
   if (!ADAM && tid == 0 && cur0 > 0 && a.loss_out) a.loss_out[cur0 - 1] = a.grad_out[sh.P];
 
   // ---- LDS: first batch into input buffer 0, W2 / b2 into publish buffer 0
   for (int e = 4 * tid; e < TOTAL; e += 4 * NT) *reinterpret_cast<float4*>(lds + e) = make_float4(0.f, 0.f, 0.f, 0.f);
-  __syncthreads();
+  lds_barrier();
   if (tid < B * DMAX) lds[XT + (tid >> 2) * 4 + (tid & 3)] = x_first;
   if (tid < B) reinterpret_cast<int*>(lds + LAB)[tid] = lab_first;
   if (own_w2) lds[W2L + u * C + r0] = r0 ? pw2[1] : pw2[0];
   if (own_b2) lds[B2L + l] = pb2;
-  // prefetch roles: thread -> (row pb, feature pk) of the next batch, or (row pb, label)
-  const int nel = Bsz * D0;
-  int role = 0, pb = 0, pk = 0;
-  if (tid < nel) { role = 1; pb = tid / D0; pk = tid - pb * D0; }
-  else if (tid < nel + Bsz) { role = 2; pb = tid - nel; }
-  int ridx_next = 0;
-  if (role && (cur0 + 1) * Bsz + pb < a.n_items) ridx_next = a.idx[(cur0 + 1) * Bsz + pb];
   const uint32_t* pf_base = role == 1 ? reinterpret_cast<const uint32_t*>(a.X) + pk : reinterpret_cast<const uint32_t*>(a.Y);
   const int pf_stride = role == 1 ? a.ldx : (role == 2 ? 1 : 0);
-  __syncthreads();
+  lds_barrier();
 
+  if constexpr (PROF) pacc[14] = __builtin_amdgcn_s_memtime() - t_kstart;  // LDS init + first batch
   const float p_drop = a.dropout;
   const bool drop = p_drop > 0.f;
   const float scale = drop ? 1.0f / (1.0f - p_drop) : 1.0f;
@@ -602,15 +606,15 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
 #pragma unroll
   for (int i = 0; i < 2; ++i) { m0[i] *= c1; v0[i] *= c2; }
   mb0 *= c1; vb0 *= c2; mw2 *= c1; vw2 *= c2; mb1 *= c1; vb1 *= c2; mb2 *= c1; vb2 *= c2;
-  __syncthreads();  // every wave is past its last use of the step tiles (the staging aliases them)
+  lds_barrier();  // every wave is past its last use of the step tiles (the staging aliases them)
   Stg::own<KS>(lds, w1, lo, KS / 4 * w);
   Stg::own<KS>(lds + STG, m1, lo, KS / 4 * w);
-  __syncthreads();
+  lds_barrier();
   Stg::store(a.p + wo1, lds, to);
   Stg::store(a.m + wo1, lds + STG, to);
-  __syncthreads();
+  lds_barrier();
   Stg::own<KS>(lds, v1, lo, KS / 4 * w);
-  __syncthreads();
+  lds_barrier();
   Stg::store(a.v + wo1, lds, to);
   const int r0o = lo & 3;
 #pragma unroll
@@ -637,7 +641,7 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     pacc[10] = __builtin_amdgcn_s_memtime() - t_last;
     if (l == 0) {
 #pragma unroll
-      for (int i = 0; i < 11; ++i) atomicAdd(a.prof + w * 16 + i, pacc[i]);
+      for (int i = 0; i < 15; ++i) atomicAdd(a.prof + w * 16 + i, pacc[i]);
     }
   }
 }

@@ -20,6 +20,7 @@ PHASES_B3 = ["F1 h1 + keep hash", "F2 partials + prefetch", "barrier A", "h2 own
              "barrier B", "logits + loss", "dZ2 + W2/b1/b2 Adam", "dX + dW0/db0 Adam", "dW1 + Adam"]
 PHASES = PHASES_B2 if os.environ.get("DCT_MLP_BLOCK") == "2" else PHASES_B3  # block4: same phases
 NWAVES = 16 if os.environ.get("DCT_MLP_BLOCK") == "4" else 8
+_blk = os.environ.get("DCT_MLP_BLOCK", "")
 ONCE = ["prologue (per launch)", "epilogue (per launch)"]
 
 
@@ -53,6 +54,10 @@ def main():
     print(f"{'total':24s}" + "".join(f"{pr[w].sum().item():7.0f}" for w in range(NWAVES)))
     for i, name in enumerate(ONCE):
         print(f"{name:24s}" + "".join(f"{raw[w, 9 + i].item():7.0f}" for w in range(NWAVES)))
+    if _blk not in ("2", "3", "4"):  # mlp_block5: cumulative prologue marks (cycles since kernel start)
+        for i, name in enumerate(["prologue: loads issued", "prologue: W1+m staged", "prologue: in registers",
+                                  "prologue: LDS init done"]):
+            print(f"{name:24s}" + "".join(f"{raw[w, 11 + i].item():7.0f}" for w in range(NWAVES)))
 
 
 if __name__ == "__main__":
