@@ -151,7 +151,7 @@ def _warmup(loop, n_items, warmup, loss):
         if k:
             loop.run_steps(n_items, k, loss, first_step=first)
             first += k
-            if i == 0 and getattr(loop, "xg", None) is not None:
+            if i == 0 and (getattr(loop, "xg", None) is not None or getattr(loop, "gx", None) is not None):
                 # the in-kernel exchange is checked after its FIRST launch: if peers cannot see
                 # each other's writes, only that launch pays the spin timeout before the RCCL
                 # fallback, not every warmup launch
@@ -335,7 +335,7 @@ def measure(a, ctx):
 
     # warmup (also builds / captures the step graphs outside the timed region)
     _warmup(loop, n_items, a.warmup, loss)
-    if getattr(eng, "xg", None) is not None:
+    if getattr(eng, "xg", None) is not None or getattr(eng, "gx", None) is not None:
         ok = eng.xg_verify(fallback=True)
         if ok and not _params_in_sync(ctx, eng.p):
             # the exchange completed but the replicas differ (should never happen): resync and
@@ -353,7 +353,8 @@ def measure(a, ctx):
         torch.cuda.synchronize()
     dt = _timed(ctx, lambda: loop.run_steps(n_items, a.steps, loss, first_step=a.warmup), device_barrier=dbar)
 
-    xg_ok = eng.xg_verify(fallback=True) if getattr(eng, "xg", None) is not None else None
+    xg_ok = (eng.xg_verify(fallback=True) if (getattr(eng, "xg", None) is not None
+                                               or getattr(eng, "gx", None) is not None) else None)
     if cpu:
         engine_desc = "autograd(cpu)" + ("+gloo-bucket-allreduce" if ctx.is_distributed else "")
     elif tt:
@@ -363,7 +364,7 @@ def measure(a, ctx):
         engine_desc = ("graph-mlp-executor(bf16 mfma gemm)" + ("+rccl-bucket-allreduce" if ctx.is_distributed else "")
                        + ("+hipgraph" if eng.graph_used else ""))
     elif eng.xg is not None or eng.ddp:
-        engine_desc = eng.step_mode if eng.xg is not None else (
+        engine_desc = eng.step_mode if (eng.xg is not None or eng.gx is not None) else (
             "fused+rccl-allreduce" + ("+update-then-grad" if eng.fused_update else "+adam")
             + ("+hipgraph" if eng.graph_used else ""))
     else:

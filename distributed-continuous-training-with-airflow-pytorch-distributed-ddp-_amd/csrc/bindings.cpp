@@ -264,6 +264,23 @@ PYBIND11_MODULE(_dct_native, m) {
       py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("p_bf16"), py::arg("n"), py::arg("lr"),
       py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("t"), py::arg("grad_scale"),
       py::arg("decoupled"), py::arg("step_counter"), py::arg("stream"));
+  m.def("xg_adam_buffer_bytes", &dct_xg_adam_buffer_bytes, py::arg("n"), py::arg("world"));
+  m.def(
+      "xg_allreduce_adam",
+      [](uintptr_t g, uintptr_t p, uintptr_t mo, uintptr_t vo, int64_t n, int64_t np, uintptr_t step_counter,
+         float lr, float b1, float b2, float eps, float wd, const dct::PeerExchange& xg, double timeout_s,
+         uintptr_t stream) {
+        if (xg.bytes() < dct_xg_adam_buffer_bytes(n, xg.world()))
+          throw std::invalid_argument("xg_allreduce_adam: exchange buffer too small for n");
+        check(dct_xg_allreduce_adam(P<float>(g), P<float>(p), P<float>(mo), P<float>(vo), n, np,
+                                    P<const int>(step_counter), lr, b1, b2, eps, wd, P<void>(xg.recv()),
+                                    P<void* const>(xg.peers()), P<unsigned>(xg.status()), xg.world(), xg.rank(),
+                                    (long long)(timeout_s * 1e8), reinterpret_cast<void*>(stream)),
+              "xg_allreduce_adam");
+      },
+      py::arg("g"), py::arg("p"), py::arg("m"), py::arg("v"), py::arg("n"), py::arg("P"), py::arg("step_counter"),
+      py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("xg"),
+      py::arg("timeout_s"), py::arg("stream"));
   m.def("adam_flat_step",
         [](uintptr_t p, uintptr_t g, uintptr_t mo, uintptr_t vo, uintptr_t p_bf16, int64_t n, float lr, float b1,
            float b2, float eps, float wd, int64_t t, float grad_scale, int decoupled, uintptr_t step_counter,

@@ -103,4 +103,9 @@ int dct_gather_rows(const void* src, const int* idx, void* dst, int64_t n_rows, 
 // device-side barrier of the xGMI peer exchange (step_kernels.hip; barrier slots at byte offset off)
 int dct_xg_barrier(void* recv, void* const* peers, int64_t off, unsigned* status, int world, int rank, unsigned tag,
                    long long timeout_ticks, void* stream);
+// peer-to-peer gradient all-reduce + flat Adam over a PeerExchange (xg_adam.hip)
+int64_t dct_xg_adam_buffer_bytes(int64_t n, int world);
+int dct_xg_allreduce_adam(float* g, float* p, float* m, float* v, int64_t n, int64_t P, const int* step_counter,
+                          float lr, float b1, float b2, float eps, float wd, void* recv, void* const* peers,
+                          unsigned* status, int world, int rank, long long timeout_ticks, void* stream);
 }

@@ -76,27 +76,48 @@ def setup_peer_exchange(kernel, ctx: DistContext, batch: int):
 
     Before any buffer is exported every rank checks ``hipDeviceCanAccessPeer`` towards every
     other rank's device (:func:`peer_report`); one failing pair sends all ranks to RCCL."""
+    return _open_exchange(ctx, kernel.xg_supported(batch), lambda: kernel.xg_buffer_bytes(ctx.world_size),
+                          f"dims {kernel.dims}, batch {batch}", strict=True)
+
+
+def setup_grad_exchange(ctx: DistContext, n: int):
+    """Collective: a PeerExchange sized for the fused peer all-reduce + Adam kernel
+    (csrc/xg_adam.hip) over ``n`` floats, or None on every rank.
+
+    The DDP step path of the models the single-wave kernel does not train (the register-resident
+    3x128 weather trainer in grad mode) uses it instead of RCCL all-reduce + flat Adam.  Selection
+    follows ``DCT_ALLREDUCE`` (``rccl`` never; ``DCT_XG_GRAD=0`` turns this exchange off alone);
+    under ``DCT_ALLREDUCE=xgmi`` an unavailable exchange is not an error here - the RCCL step path
+    remains."""
+    from ..ops._native import native
+
+    on = os.environ.get("DCT_XG_GRAD", "1") != "0"
+    return _open_exchange(ctx, on, lambda: native().xg_adam_buffer_bytes(n, ctx.world_size),
+                          f"grad exchange of {n} floats", strict=False)
+
+
+def _open_exchange(ctx: DistContext, supported: bool, nbytes, what: str, strict: bool):
     m = mode()
     W = ctx.world_size
     single_node = ctx.local_world_size == W
     peers_ok = True
-    if m != "rccl" and ctx.device.type == "cuda" and 2 <= W <= 8 and single_node:
+    if m != "rccl" and ctx.device.type == "cuda" and 2 <= W <= 8 and single_node and supported:
         peers_ok = peer_report(ctx)[2]
         if not peers_ok and ctx.rank == 0:
             print("[dct] some rank pair is not peer-accessible (hipDeviceCanAccessPeer)", flush=True)
     eligible = (m != "rccl" and ctx.device.type == "cuda" and 2 <= W <= 8 and single_node and peers_ok
-                and kernel.xg_supported(batch))
+                and supported)
     # every rank must take the same decision before any collective below diverges
     if not ctx.all_reduce_bool_and(eligible):
-        if m == "xgmi":
+        if m == "xgmi" and strict:
             raise RuntimeError("DCT_ALLREDUCE=xgmi but the in-kernel all-reduce is not applicable "
-                               f"(world {W}, single node {single_node}, dims {kernel.dims}, batch {batch})")
+                               f"(world {W}, single node {single_node}, {what})")
         return None
     from ..ops._native import native
 
     xg, handle, err = None, b"", None
     try:
-        xg = native().PeerExchange(W, ctx.rank, kernel.xg_buffer_bytes(W))
+        xg = native().PeerExchange(W, ctx.rank, int(nbytes()))
         handle = xg.ipc_handle()
     except Exception as e:  # noqa: BLE001
         err = e
@@ -108,12 +129,37 @@ def setup_peer_exchange(kernel, ctx: DistContext, batch: int):
             err = e
     ok = ctx.all_reduce_bool_and(err is None)
     if not ok:
-        if m == "xgmi":
+        if m == "xgmi" and strict:
             raise RuntimeError(f"in-kernel all-reduce setup failed on some rank (this rank: {err!r})")
         if ctx.rank == 0:
             print(f"[dct] xGMI peer exchange unavailable ({err!r}); using RCCL per step", flush=True)
         return None
     return xg
+
+
+def allreduce_adam_(xg, g, p, m, v, n_params: int, step_counter, lr: float, betas, eps: float,
+                    weight_decay: float, timeout: Optional[float] = None):
+    """Enqueue the fused peer all-reduce + Adam step (csrc/xg_adam.hip) on the current stream.
+
+    ``g`` (fp32, the gradients then optionally the local loss) is replaced by the rank average -
+    summed in rank order, so bit-identical on every rank - and Adam (L2 weight decay, step
+    t = ``*step_counter``) updates ``p/m/v[:n_params]``.  Collective: every rank enqueues it once
+    per step, after the kernel that advanced the step counter."""
+    import torch
+
+    from ..ops._native import native
+
+    for t in (g, p, m, v):
+        if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+            raise ValueError("allreduce_adam_: g/p/m/v must be contiguous fp32 cuda tensors")
+    if not (p.numel() == m.numel() == v.numel() == n_params <= g.numel()):
+        raise ValueError("allreduce_adam_: p/m/v must hold n_params elements and g at least as many")
+    if not (step_counter.is_cuda and step_counter.dtype == torch.int32):
+        raise ValueError("allreduce_adam_: step_counter must be a cuda int32 tensor")
+    native().xg_allreduce_adam(g.data_ptr(), p.data_ptr(), m.data_ptr(), v.data_ptr(), g.numel(), n_params,
+                               step_counter.data_ptr(), float(lr), float(betas[0]), float(betas[1]), float(eps),
+                               float(weight_decay), xg, timeout_s() if timeout is None else float(timeout),
+                               torch.cuda.current_stream(p.device).cuda_stream)
 
 
 def device_barrier(xg, stream: int, timeout: Optional[float] = None):

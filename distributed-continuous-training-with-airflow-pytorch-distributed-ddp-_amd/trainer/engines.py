@@ -125,14 +125,17 @@ class FusedMLPEngine(_EngineBase):
             self.gbuf = torch.zeros(self.P + 1, dtype=torch.float32, device=dev)
             self._broadcast_params()
         self.xg = None  # in-kernel xGMI all-reduce (parallel/xgmi.py)
+        self.gx = None  # DDP step path: fused peer all-reduce + Adam kernel over xGMI (csrc/xg_adam.hip)
         if ctx.is_distributed:
-            from ..parallel.xgmi import setup_peer_exchange, timeout_s
+            from ..parallel.xgmi import setup_grad_exchange, setup_peer_exchange, timeout_s
 
             self.xg = setup_peer_exchange(self.kernel, ctx, self.B)
             self.xg_timeout_s = timeout_s()
             # exchange time of the launches (s_memrealtime ticks, 100 MHz) -> allreduce_ms per epoch
             self.xg_ticks = torch.zeros(1, dtype=torch.int64, device=dev) if self.xg is not None else None
-            if self.xg is None and self.comm is None:
+            if self.xg is None and not self.fused_update:
+                self.gx = setup_grad_exchange(ctx, self.P + 1)
+            if self.xg is None and self.gx is None and self.comm is None:
                 raise RuntimeError("distributed fused engine needs RCCL (backend nccl) or the in-kernel "
                                    "xGMI exchange; neither is available")
         self.last_allreduce_ms = None
@@ -187,12 +190,19 @@ class FusedMLPEngine(_EngineBase):
         fa.load_state_dict(sd)
         self.global_step = global_step
         self.step_counter.fill_(int(fa.step_count))
-        if self.xg is not None:  # exchange tags derive from the step counter: drop stale granules
-            torch.cuda.synchronize(self.device)
-            self.ctx.barrier()
-            self.xg.reset(torch.cuda.current_stream().cuda_stream)
-            torch.cuda.synchronize(self.device)
-            self.ctx.barrier()
+        self._reset_exchanges()  # exchange tags derive from the step counter: drop stale granules
+
+    def _reset_exchanges(self):
+        """Collective: zero the exchanges' receive buffers (and status) once every rank is idle."""
+        xs = [x for x in (self.xg, self.gx) if x is not None]
+        if not xs:
+            return
+        torch.cuda.synchronize(self.device)
+        self.ctx.barrier()
+        for x in xs:
+            x.reset(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize(self.device)
+        self.ctx.barrier()
 
     # ------------------------------------------------------------------ data
     def attach_data(self, X: torch.Tensor, Y: torch.Tensor, train_rows: torch.Tensor, val_rows: torch.Tensor):
@@ -248,6 +258,8 @@ class FusedMLPEngine(_EngineBase):
             return "fused-persistent+xgmi-inkernel-allreduce"
         if not self.ddp:
             return "fused-persistent"
+        if self.gx is not None:
+            return "fused-step+xgmi-allreduce-adam" + ("+graph" if self.use_graph else "")
         return "fused-step+rccl" + ("+graph" if self.use_graph else "")
 
     def run_steps(self, n_items: int, steps: int, loss_out: torch.Tensor, first_step: int = 0):
@@ -301,7 +313,8 @@ class FusedMLPEngine(_EngineBase):
 
     def _ddp_step(self, n_items: int, loss_out: torch.Tensor):
         """One DDP step at the device cursor: fused fwd/bwd (grads + local loss -> gbuf) ->
-        RCCL ncclAvg all-reduce of gbuf (X5 + X6 in one collective) -> fused flat Adam."""
+        RCCL ncclAvg all-reduce of gbuf (X5 + X6 in one collective) -> fused flat Adam; with the
+        peer exchange (self.gx) the last two are one kernel over the xGMI mappings."""
         from ..ops._native import native
 
         a = self.adam
@@ -320,6 +333,12 @@ class FusedMLPEngine(_EngineBase):
                           t0=0, lr=a["lr"], dropout=self.dropout, seed=self.rank_seed, loss=self.loss,
                           grad_out=self.gbuf, step_counter=self.step_counter, cursor=self.cursor,
                           loss_out=loss_out)
+        if self.gx is not None:
+            from ..parallel.xgmi import allreduce_adam_
+
+            allreduce_adam_(self.gx, self.gbuf, self.p, self.m, self.v, self.P, self.step_counter, a["lr"],
+                            a["betas"], a["eps"], a["weight_decay"], timeout=self.xg_timeout_s)
+            return
         self.comm.allreduce(self.gbuf.data_ptr(), self.P + 1, nat.DT_F32, nat.OP_AVG, stream)
         adam_flat_(self.p, self.gbuf[: self.P], self.m, self.v, 1, a["lr"], a["betas"], a["eps"],
                    a["weight_decay"], step_counter=self.step_counter)
@@ -332,8 +351,10 @@ class FusedMLPEngine(_EngineBase):
 
         nat = native()
         # RCCL lazy init and kernel attribute setup must happen outside the capture
-        scratch = torch.zeros(64, dtype=torch.float32, device=self.device)
-        self.comm.allreduce(scratch.data_ptr(), 64, nat.DT_F32, nat.OP_SUM, torch.cuda.current_stream().cuda_stream)
+        if self.gx is None:
+            scratch = torch.zeros(64, dtype=torch.float32, device=self.device)
+            self.comm.allreduce(scratch.data_ptr(), 64, nat.DT_F32, nat.OP_SUM,
+                                torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize(self.device)
         state = (self.p, self.m, self.v, self.step_counter, self.cursor, self.gbuf, loss_out, self.pending,
                  self.stage)
@@ -343,6 +364,7 @@ class FusedMLPEngine(_EngineBase):
         torch.cuda.synchronize(self.device)
         for t, sv in zip(state, saved):
             t.copy_(sv)
+        self._reset_exchanges()  # the rolled-back step counter re-issues the eager step's tags
         g = torch.cuda.CUDAGraph()
         try:
             s = torch.cuda.Stream(self.device)
@@ -367,12 +389,14 @@ class FusedMLPEngine(_EngineBase):
         loss_out = getattr(self, "_loss_buf", None)
         if loss_out is None or loss_out.numel() < steps:
             self._loss_buf = loss_out = torch.zeros(max(1, steps), dtype=torch.float32, device=self.device)
-        if self.xg is not None:
+        if self.xg is not None or self.gx is not None:
             torch.cuda.synchronize(self.device)
             self.ctx.barrier()  # start the epoch's kernels together (the exchange spins are bounded)
         self.run_steps(n_items, steps, loss_out[:steps])
         check_device("fused epoch")
-        if self.xg is not None:
+        if self.gx is not None:
+            self.xg_verify(fallback=False)
+        elif self.xg is not None:
             self.xg_verify(fallback=False)
             # wave 0's exchange time over the epoch (the in-kernel all-reduce: X5 + X6 of SURVEY 2.6)
             self.last_allreduce_ms = float(self.xg_ticks.item()) / 1e5
@@ -384,14 +408,15 @@ class FusedMLPEngine(_EngineBase):
         """Collective check of the in-kernel exchange.  On a timeout either raise (training: the
         steps of that launch are incomplete) or, with ``fallback``, re-sync every rank from rank 0
         and continue on the RCCL step path (benchmarks)."""
-        if self.xg is None:
+        x = self.xg if self.xg is not None else self.gx
+        if x is None:
             return True
         from ..parallel.xgmi import check
 
-        st = check(self.xg, self.ctx)
+        st = check(x, self.ctx)
         if st == 0:
             return True
-        msg = f"in-kernel xGMI all-reduce timed out (step tag {st})"
+        msg = f"in-kernel xGMI all-reduce timed out (step tag {st & 0x7FFFFFFF})"
         if not fallback:
             raise RuntimeError(msg)
         if self.ctx.rank == 0:
@@ -402,17 +427,20 @@ class FusedMLPEngine(_EngineBase):
     def device_barrier(self) -> bool:
         """Enqueue the in-kernel exchange's device-side barrier on the current stream (collective).
         False when the exchange is not active (the caller then uses the process-group barrier)."""
-        if self.xg is None:
+        x = self.xg if self.xg is not None else self.gx
+        if x is None:
             return False
         from ..parallel.xgmi import device_barrier
 
-        device_barrier(self.xg, torch.cuda.current_stream(self.device).cuda_stream, self.xg_timeout_s)
+        device_barrier(x, torch.cuda.current_stream(self.device).cuda_stream, self.xg_timeout_s)
         return True
 
     def xg_disable(self):
         """Leave the in-kernel exchange: replicas re-synced from rank 0, RCCL step path from now on."""
         self.xg = None
+        self.gx = None
         self._bound = None
+        self._graphs = {}  # captured with the exchange's kernels
         if self.comm is None:
             raise RuntimeError("in-kernel exchange disabled and no RCCL communicator is available to fall back to")
         torch.cuda.synchronize(self.device)

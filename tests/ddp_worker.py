@@ -50,7 +50,8 @@ def main():
         json.dump({"params": flat, "global_step": trainer.global_step,
                    "restart": int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")), "val_loss": trainer.callback_metrics.get("val_loss"),
                    "best": ck.best_model_path, "engine": trainer.engine.name,
-                   "xg": getattr(trainer.engine, "xg", None) is not None}, f)
+                   "xg": getattr(trainer.engine, "xg", None) is not None,
+                   "gx": getattr(trainer.engine, "gx", None) is not None}, f)
 
 
 if __name__ == "__main__":

@@ -6,7 +6,8 @@ Self-skips below 2 visible devices (the 1-GPU boxes of the per-round GPU tier); 
 runs W = 2 and W = min(8, devices).  Same worker as the CPU tier (tests/ddp_worker.py), so the
 CPU gloo tests, the shared-GPU IPC rehearsals and this tier check one contract:
   * the fused engine 5-64-2 (in-kernel xGMI all-reduce; RCCL per step when disabled),
-  * the fused engine 3x128 (grad-mode kernel + RCCL ncclAvg + fused Adam, graph-replayed),
+  * the fused engine 3x128 (grad-mode kernel + fused peer all-reduce/Adam kernel, or RCCL ncclAvg
+    + flat Adam; graph-replayed),
   * the autograd engine (native BucketReducer on its comm stream) on the 5-64-2 MLP,
 replicas bit-identical, parameters equal the emulation, only rank 0 writes checkpoints/MLflow.
 """
@@ -99,11 +100,16 @@ def test_fused_5_64_2_ddp_across_gpus(tmp_path, W, mode):
 
 @needs2
 @pytest.mark.parametrize("W", _worlds())
-def test_fused_3x128_rccl_ddp_across_gpus(tmp_path, W):
+@pytest.mark.parametrize("gx", ["1", "0"])
+def test_fused_3x128_ddp_across_gpus(tmp_path, W, gx):
+    """gx=1: grad-mode kernel + fused peer all-reduce + Adam over xGMI (csrc/xg_adam.hip);
+    gx=0: grad-mode kernel + RCCL ncclAvg + flat Adam."""
     rows, epochs = 600, 2
-    r = _torchrun(W, 29731 + W, [tmp_path, epochs, rows, "gpu", "hidden=128,128"])
+    r = _torchrun(W, 29731 + W + (10 if gx == "1" else 0), [tmp_path, epochs, rows, "gpu", "hidden=128,128"],
+                  env={"DCT_XG_GRAD": gx})
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    _check(tmp_path, W, rows, epochs, (128, 128), 3e-3)
+    info = _check(tmp_path, W, rows, epochs, (128, 128), 3e-3)
+    assert info["gx"] == (gx == "1")
 
 
 @needs2
