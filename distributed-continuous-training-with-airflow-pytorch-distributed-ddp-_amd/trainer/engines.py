@@ -138,6 +138,16 @@ class FusedMLPEngine(_EngineBase):
             if self.xg is None and self.gx is None and self.comm is None:
                 raise RuntimeError("distributed fused engine needs RCCL (backend nccl) or the in-kernel "
                                    "xGMI exchange; neither is available")
+        elif self.ddp and not self.fused_update and os.environ.get("DCT_XG_GRAD") == "1":
+            # single-GPU rehearsal (DCT_FORCE_DDP=1 DCT_XG_GRAD=1): the exchange kernel of one rank
+            # (no pushes, no polls) in place of the one-rank RCCL all-reduce + flat Adam
+            from ..ops._native import native
+            from ..parallel.xgmi import timeout_s
+
+            nat = native()
+            self.gx = nat.PeerExchange(1, 0, nat.xg_adam_buffer_bytes(self.P + 1, 1))
+            self.gx.set_peers([self.gx.recv])
+            self.xg_timeout_s = timeout_s()
         self.last_allreduce_ms = None
         self._bound = None
         self._fast_run = None  # (loss_out, n_items, step limit, bound launch, loss ptr) of the last run

@@ -83,8 +83,10 @@ def _spawn(fn, *args, timeout=300):
     return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout)
 
 
-@pytest.mark.parametrize("W,n,wd", [(2, 17539, 0.0), (4, 1001, 0.01)])
+@pytest.mark.parametrize("W,n,wd", [(2, 17539, 0.0), (2, 1001, 0.01)])
 def test_in_process_allreduce_adam_matches_torch(W, n, wd, tmp_path, cuda):
+    """W = 2 only: a process's streams share GPU_MAX_HW_QUEUES (4) hardware queues round-robin,
+    and two ranks on one queue would serialise (W = 4 runs as processes in the engine test)."""
     steps = 6
     out = tmp_path / "xa.json"
     r = _spawn("_in_process_run", W, steps, n, wd, str(out))
