@@ -59,16 +59,22 @@ template <int XW>
 __global__ __launch_bounds__(256) void xg_allreduce_adam_kernel(XgAdamArgs a) {
   const int npair = (a.n + 1) >> 1;
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (__hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;  // failed earlier
-  const int W = a.world, rank = a.rank;
+  // every independent load first (status, step counter, gradients, Adam state): one memory
+  // latency instead of a chain of five; out-of-range lanes read a clamped, valid element
+  const unsigned st = __hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const uint32_t t = (uint32_t)__hip_atomic_load(a.step_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t tag = t;
-  const int par = (int)(t & 1u) * W;
-  const int nbytes = 2 * W * npair * 16;
   const int i_c = i < npair ? i : npair - 1;  // every lane polls a valid slot; only i < npair writes
   const int e0 = 2 * i_c, e1 = 2 * i_c + 1;
   const float g0 = a.g[e0];
-  const float g1 = e1 < a.n ? a.g[e1] : 0.f;
+  const float g1 = a.g[e1 < a.n ? e1 : e0];
+  const int q0 = e0 < a.P ? e0 : a.P - 1, q1 = e1 < a.P ? e1 : a.P - 1;
+  float p0 = a.p[q0], m0 = a.m[q0], w0 = a.v[q0];
+  float p1 = a.p[q1], m1 = a.m[q1], w1 = a.v[q1];
+  if (st != 0u) return;  // an earlier exchange timed out: leave everything as it is
+  const int W = a.world, rank = a.rank;
+  const uint32_t tag = t;
+  const int par = (int)(t & 1u) * W;
+  const int nbytes = 2 * W * npair * 16;
   if (i < npair) {
     xa_v4u d;
     d.x = __float_as_uint(g0);
@@ -84,26 +90,31 @@ __global__ __launch_bounds__(256) void xg_allreduce_adam_kernel(XgAdamArgs a) {
       }
     }
   }
-  const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(a.recv, 0, nbytes, 0x00020000);
   float v0[XW], v1[XW];
-  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-  for (int spin = 0;; ++spin) {
-    bool ok = true;
 #pragma unroll
-    for (int q = 0; q < XW; ++q) {
-      const int qq = q < W ? q : 0;
-      const xa_v4u d = __builtin_amdgcn_raw_buffer_load_b128(rr, ((par + qq) * npair + i_c) * 16, 0, XA_SYS);
-      v0[q] = __uint_as_float(d.x);
-      v1[q] = __uint_as_float(d.z);
-      ok &= ((d.y == tag) & (d.w == tag)) | (q >= W) | (q == rank);
+  for (int q = 0; q < XW; ++q) v0[q] = v1[q] = 0.f;
+  if (W > 1) {
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(a.recv, 0, nbytes, 0x00020000);
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    for (int spin = 0;; ++spin) {
+      bool ok = true;
+#pragma unroll
+      for (int q = 0; q < XW; ++q) {
+        if (q < W && q != rank) {  // wave-uniform
+          const xa_v4u d = __builtin_amdgcn_raw_buffer_load_b128(rr, ((par + q) * npair + i_c) * 16, 0, XA_SYS);
+          v0[q] = __uint_as_float(d.x);
+          v1[q] = __uint_as_float(d.z);
+          ok &= (d.y == tag) & (d.w == tag);
+        }
+      }
+      if (__all(ok)) break;
+      if ((spin & 15) == 15 && (long long)(__builtin_amdgcn_s_memrealtime() - t_start) > a.timeout_ticks) {
+        if (threadIdx.x == 0)
+          __hip_atomic_store(a.status, 0x80000000u | tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
     }
-    if (__all(ok)) break;
-    if ((spin & 15) == 15 && (long long)(__builtin_amdgcn_s_memrealtime() - t_start) > a.timeout_ticks) {
-      if (threadIdx.x == 0)
-        __hip_atomic_store(a.status, 0x80000000u | tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;
-    }
-    __builtin_amdgcn_s_sleep(1);
   }
   if (i >= npair) return;
   float s0 = 0.f, s1 = 0.f;
@@ -122,18 +133,16 @@ __global__ __launch_bounds__(256) void xg_allreduce_adam_kernel(XgAdamArgs a) {
   const float step_size = a.lr / (1.f - pow_t(log2f(a.b1), tf));
   const float rbc2 = rsqrtf(1.f - pow_t(log2f(a.b2), tf));
   if (e0 < a.P) {
-    float p = a.p[e0], m = a.m[e0], v = a.v[e0];
-    xa_adam(p, r0, m, v, a, step_size, rbc2);
-    a.p[e0] = p;
-    a.m[e0] = m;
-    a.v[e0] = v;
+    xa_adam(p0, r0, m0, w0, a, step_size, rbc2);
+    a.p[e0] = p0;
+    a.m[e0] = m0;
+    a.v[e0] = w0;
   }
   if (e1 < a.P) {
-    float p = a.p[e1], m = a.m[e1], v = a.v[e1];
-    xa_adam(p, r1, m, v, a, step_size, rbc2);
-    a.p[e1] = p;
-    a.m[e1] = m;
-    a.v[e1] = v;
+    xa_adam(p1, r1, m1, w1, a, step_size, rbc2);
+    a.p[e1] = p1;
+    a.m[e1] = m1;
+    a.v[e1] = w1;
   }
 }
 
@@ -148,7 +157,7 @@ int dct_xg_allreduce_adam(float* g, float* p, float* m, float* v, int64_t n, int
                           float lr, float b1, float b2, float eps, float wd, void* recv, void* const* peers,
                           unsigned* status, int world, int rank, long long timeout_ticks, void* stream) {
   if (world < 1 || world > dct::XA_MAXW || rank < 0 || rank >= world || !g || !p || !m || !v || !step_counter ||
-      !recv || !peers || !status || n < 1 || P < 0 || P > n || dct_xg_adam_buffer_bytes(n, world) > INT32_MAX)
+      !recv || !peers || !status || n < 1 || P < 1 || P > n || dct_xg_adam_buffer_bytes(n, world) > INT32_MAX)
     return (int)hipErrorInvalidValue;
   dct::XgAdamArgs a;
   a.g = g;
