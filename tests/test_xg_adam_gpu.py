@@ -166,7 +166,7 @@ def _ddp_reference(res, steps, B):
     return torch.cat([p.detach().reshape(-1) for p in params]), torch.tensor(losses)
 
 
-@pytest.mark.parametrize("W", [2, 4])
+@pytest.mark.parametrize("W", [2, 4, 8])
 def test_engine_ddp_step_with_peer_allreduce_adam(W, tmp_path, cuda):
     """FusedMLPEngine at world size W (processes sharing the GPU, IPC-mapped buffers): the 3x128
     DDP step path runs grad kernel -> fused peer all-reduce + Adam, graph-captured in chunks with
