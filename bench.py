@@ -29,6 +29,7 @@ sides, max over ranks.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import math
 import os
@@ -103,12 +104,23 @@ def _timed(ctx, fn, device_barrier=None):
         if ctx.is_distributed:
             dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
         return float(dt_t.item())
+    # no cyclic-GC pass inside the window: the collector is paused for the K steps (the window
+    # allocates almost nothing).  Measured on MI355X (profiles/bench_window_gc_r3.log): with it on,
+    # the first window's completion wait was 0.34 ms instead of 0.10 ms in some processes; a
+    # gc.collect() right before the window instead costs ~50 us of cold-cache enqueue.
+    gc_mode = os.environ.get("DCT_BENCH_GC", "pause")  # pause | on | collect
+    gc_paused = gc_mode != "on" and gc.isenabled()
+    if gc_paused:
+        if gc_mode == "collect":
+            gc.collect()
+        gc.disable()
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()
     _release_together(ctx)
     t0 = time.perf_counter()
     fn()
+    t_enq = time.perf_counter()
     if device_barrier is not None and device_barrier():
         torch.cuda.synchronize()  # the xGMI barrier queued behind the steps on every rank
     elif ctx.backend == "nccl":
@@ -118,6 +130,11 @@ def _timed(ctx, fn, device_barrier=None):
         torch.cuda.synchronize()
         ctx.barrier()  # host-side (gloo) or a no-op at world size 1
     dt = time.perf_counter() - t0
+    if gc_paused:
+        gc.enable()
+    if os.environ.get("DCT_BENCH_DEBUG", "0") == "1":
+        print(f"[bench debug] window {dt * 1e6:.1f} us: enqueue {(t_enq - t0) * 1e6:.1f} us, "
+              f"wait {(t0 + dt - t_enq) * 1e6:.1f} us", flush=True)
     dt_t = torch.tensor([dt], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
     if ctx.is_distributed:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
@@ -352,6 +369,8 @@ def measure(a, ctx):
     if dbar is not None and dbar():  # first launch of the barrier kernel (code-object load) untimed
         torch.cuda.synchronize()
     dt = _timed(ctx, lambda: loop.run_steps(n_items, a.steps, loss, first_step=a.warmup), device_barrier=dbar)
+    for _ in range(int(os.environ.get("DCT_BENCH_DEBUG_REPEAT", "0"))):  # debug: the same window again
+        _timed(ctx, lambda: loop.run_steps(n_items, a.steps, loss, first_step=a.warmup), device_barrier=dbar)
 
     xg_ok = (eng.xg_verify(fallback=True) if (getattr(eng, "xg", None) is not None
                                                or getattr(eng, "gx", None) is not None) else None)
@@ -451,8 +470,36 @@ def _physical_devices(ctx):
     return ctx.all_gather_object(mine) if ctx.is_distributed else [mine]
 
 
+def _host_spin_wait():
+    """Host threads spin on GPU completion signals instead of sleeping on an interrupt
+    (hipDeviceScheduleSpin), set before torch initialises the device.  The default wait spins
+    briefly and then blocks; a window that outlasts the spin (the 3x128 20-step window, ~100 us of
+    kernel) then pays the interrupt wake-up - measured 0.1-0.4 ms, bimodal across processes
+    (profiles/host_wait_ab_r3.log).  DCT_HOST_SPIN=0 keeps the runtime default."""
+    if os.environ.get("DCT_HOST_SPIN", "1") == "0" or "torch" in sys.modules:
+        return
+    import ctypes
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    lib = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so") if spec and spec.origin else ""
+    try:
+        hip = ctypes.CDLL(lib if os.path.exists(lib) else "libamdhip64.so")
+        n = ctypes.c_int(0)
+        if hip.hipGetDeviceCount(ctypes.byref(n)) != 0 or n.value < 1:
+            return
+        # the flag is per device: the one this rank will drive (init_distributed: LOCAL_RANK,
+        # ranks beyond the device count share devices round-robin)
+        if hip.hipSetDevice(int(os.environ.get("LOCAL_RANK", "0")) % n.value) == 0:
+            hip.hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
+    except OSError:
+        pass
+
+
 def main():
     a = parse()
+    if a.device != "cpu":
+        _host_spin_wait()
     # the DDP bucket reducer's device-side all-reduce timing (allreduce_ms in the trainer's logs) adds
     # two stamp kernels and two cross-stream edges per step: off for the timed step unless asked
     os.environ.setdefault("DCT_REDUCER_TIMING", "0")

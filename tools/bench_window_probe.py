@@ -26,7 +26,7 @@ def main():
     total = warmup + steps * reps
     rows = int(math.ceil((total + 8) * 4 / 0.8)) + 1024
     X, Y = weather_tensors(rows, seed=0, dim=5)
-    model = build_mlp("weather", 5)
+    model = build_mlp(os.environ.get("PROBE_MODEL", "weather"), 5)  # e.g. weather-mlp-3x128
     eng = FusedMLPEngine(model, ctx, 4, seed=42, adam=adam_hparams_from(model.configure_optimizers()))
     n_train = int(0.8 * rows)
     perm = torch.randperm(rows, generator=torch.Generator().manual_seed(42))
