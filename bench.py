@@ -470,36 +470,8 @@ def _physical_devices(ctx):
     return ctx.all_gather_object(mine) if ctx.is_distributed else [mine]
 
 
-def _host_spin_wait():
-    """Host threads spin on GPU completion signals instead of sleeping on an interrupt
-    (hipDeviceScheduleSpin), set before torch initialises the device.  The default wait spins
-    briefly and then blocks; a window that outlasts the spin (the 3x128 20-step window, ~100 us of
-    kernel) then pays the interrupt wake-up - measured 0.1-0.4 ms, bimodal across processes
-    (profiles/host_wait_ab_r3.log).  DCT_HOST_SPIN=0 keeps the runtime default."""
-    if os.environ.get("DCT_HOST_SPIN", "1") == "0" or "torch" in sys.modules:
-        return
-    import ctypes
-    import importlib.util
-
-    spec = importlib.util.find_spec("torch")
-    lib = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so") if spec and spec.origin else ""
-    try:
-        hip = ctypes.CDLL(lib if os.path.exists(lib) else "libamdhip64.so")
-        n = ctypes.c_int(0)
-        if hip.hipGetDeviceCount(ctypes.byref(n)) != 0 or n.value < 1:
-            return
-        # the flag is per device: the one this rank will drive (init_distributed: LOCAL_RANK,
-        # ranks beyond the device count share devices round-robin)
-        if hip.hipSetDevice(int(os.environ.get("LOCAL_RANK", "0")) % n.value) == 0:
-            hip.hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
-    except OSError:
-        pass
-
-
 def main():
     a = parse()
-    if a.device != "cpu":
-        _host_spin_wait()
     # the DDP bucket reducer's device-side all-reduce timing (allreduce_ms in the trainer's logs) adds
     # two stamp kernels and two cross-stream edges per step: off for the timed step unless asked
     os.environ.setdefault("DCT_REDUCER_TIMING", "0")
