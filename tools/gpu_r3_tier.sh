@@ -37,13 +37,8 @@ for t in blk_A blk_V; do
   echo "== $t"; python3 tools/pmc_summary.py $O/pmc_$t 20 6 2>&1 | head -10
 done > $O/pmc_tier_summary.txt
 cat $O/pmc_tier_summary.txt
-# tabular: split-K two-pass partials for every slice count (default: <= 4 slices, else fp32 atomics)
-: > $O/tab_twopass_ab.log
-for tp in auto 1 auto 1; do
-  if [ $tp = auto ]; then unset DCT_GEMM_SPLIT_TWO_PASS; else export DCT_GEMM_SPLIT_TWO_PASS=$tp; fi
-  timeout -k 10 300 python bench.py --model tabular-mlp-4x1024 > $O/bench_tab_tp.json 2>&1 || exit $?
-  python -c "import json; d=json.loads([l for l in open('$O/bench_tab_tp.json') if l.startswith('{')][-1]); print('tabular two_pass=$tp %.4f ms/step %.0f samples/s' % (d['ms_per_step'], d['value']))" >> $O/tab_twopass_ab.log
+for m in tabular-mlp-4x1024 tabtransformer; do
+  timeout -k 10 300 python bench.py --model $m > $O/bench_tier_$m.log 2>&1 || exit $?
+  grep '^{' $O/bench_tier_$m.log | cut -c1-200
 done
-unset DCT_GEMM_SPLIT_TWO_PASS
-cat $O/tab_twopass_ab.log
 echo done
