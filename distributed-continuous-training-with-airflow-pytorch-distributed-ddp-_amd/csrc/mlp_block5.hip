@@ -156,18 +156,29 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   // batch's prefetch element, as VECTOR loads (a scalar load's wait would stall the whole prologue
   // behind it, lgkmcnt is shared with the LDS staging); the dependent X / Y gathers follow the W1 loads
   const int Bsz = a.B;
-  const int cur0 = (!ADAM && a.cursor) ? sload(a.cursor) : 0;  // grad mode: batch index from the device cursor
-  const int bs0 = min(Bsz, a.n_items - cur0 * Bsz);
   const int fb = tid & 3, fd = tid >> 2;
-  const bool first_ok = tid < B * DMAX && fb < bs0;
-  const int rb_first = first_ok ? a.idx[cur0 * Bsz + fb] : 0;
   // prefetch roles: thread -> (row pb, feature pk) of the next batch, or (row pb, label)
   const int nel = Bsz * D0;
   int role = 0, pb = 0, pk = 0;
   if (tid < nel) { role = 1; pb = tid / D0; pk = tid - pb * D0; }
   else if (tid < nel + Bsz) { role = 2; pb = tid - nel; }
+  // grad mode with a staging buffer (the DDP step path, one launch per step): the previous launch
+  // left this launch's batch in a.stage ([0] = batch index + 1, [64 + role slot] = x / label
+  // words), so the first batch is one load issued with nothing in front of it instead of the
+  // cursor -> idx -> x chain of three dependent round trips
+  const bool stp = !ADAM && a.stage != nullptr;
+  uint32_t st_tag = 0u, st_x = 0u, st_lab = 0u;
+  if (stp) {
+    st_tag = a.stage[0];
+    if (tid < B * DMAX && fd < D0 && fb < Bsz) st_x = a.stage[64 + fb * D0 + fd];
+    if (tid < Bsz) st_lab = a.stage[64 + nel + tid];
+  }
+  const int cur0 = (!ADAM && a.cursor) ? sload(a.cursor) : 0;  // grad mode: batch index from the device cursor
+  const int bs0 = min(Bsz, a.n_items - cur0 * Bsz);
+  const bool first_ok = tid < B * DMAX && fb < bs0;
+  const int rb_first = (first_ok && !stp) ? a.idx[cur0 * Bsz + fb] : 0;
   int ridx_next = 0;
-  if (role && (cur0 + 1) * Bsz + pb < a.n_items) ridx_next = a.idx[(cur0 + 1) * Bsz + pb];
+  if (!stp && role && (cur0 + 1) * Bsz + pb < a.n_items) ridx_next = a.idx[(cur0 + 1) * Bsz + pb];
 
   // ---- W1 + moments: coalesced, redistributed through LDS below
   v4f sp[Stg::LD], sm[Stg::LD], sv[Stg::LD];
@@ -215,8 +226,22 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   }
   float x_first = 0.f;
   int lab_first = 0;
-  if (first_ok && fd < D0) x_first = a.X[(size_t)rb_first * a.ldx + fd];
-  if (tid < B && tid < bs0) lab_first = a.Y[rb_first];  // tid < 4: fb = tid
+  if (stp) {
+    // the next batch's indices (its x / label words are fetched in the step and staged for the
+    // next launch); issued behind the parameter loads
+    if (role && (cur0 + 1) * Bsz + pb < a.n_items) ridx_next = a.idx[(cur0 + 1) * Bsz + pb];
+    if ((int)st_tag == cur0 + 1) {  // wave-uniform: staged by the launch before, for this batch
+      if (first_ok && fd < D0) x_first = __uint_as_float(st_x);
+      if (tid < B && tid < bs0) lab_first = (int)st_lab;
+    } else {  // first launch of a run / after a reset: the gather
+      const int rb = first_ok ? a.idx[cur0 * Bsz + fb] : 0;
+      if (first_ok && fd < D0) x_first = a.X[(size_t)rb * a.ldx + fd];
+      if (tid < B && tid < bs0) lab_first = a.Y[rb];
+    }
+  } else {
+    if (first_ok && fd < D0) x_first = a.X[(size_t)rb_first * a.ldx + fd];
+    if (tid < B && tid < bs0) lab_first = a.Y[rb_first];  // tid < 4: fb = tid
+  }
 
   // ---- W1 k-slice + moments into registers through the swizzled staging tiles
   float w1[2][KS], m1[2][KS], v1[2][KS];
@@ -351,6 +376,11 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         *reinterpret_cast<float4*>(part + (l + 64 * j) * PSTR + w * 4) = make_float4(cj[j][0], cj[j][1], cj[j][2], cj[j][3]);
+    }
+    if (stp) {  // grad mode: hand the next batch to the next launch (tag last, 0 = nothing staged)
+      const int bs_st = min(Bsz, a.n_items - (sb + 1) * Bsz);
+      if (role) a.stage[64 + tid] = pb < bs_st ? raw_next : 0u;
+      if (tid == 0) a.stage[0] = bs_st > 0 ? (uint32_t)(sb + 2) : 0u;
     }
     // next batch into the next input buffer (its last readers finished before the previous barrier B)
     if (role) {
@@ -656,7 +686,8 @@ bool mlp_block5_ok(const MlpShape& sh, const MlpArgs& a) {
          sh.dims[0] <= blk5::DMAX && sh.dims[3] == blk5::C && a.B >= 1 && a.B <= blk5::B &&
          // train mode, or grad mode for ONE step (the DDP step path: grads + loss to grad_out, device cursor)
          ((a.mode == 0 && a.cursor == nullptr) || (a.mode == 1 && a.steps == 1 && a.grad_out != nullptr)) &&
-         (a.loss_kind == 0 || a.loss_kind == 1) && a.pending == nullptr && a.stage == nullptr && a.xg_world <= 1;
+         (a.loss_kind == 0 || a.loss_kind == 1) && a.pending == nullptr && (a.stage == nullptr || a.mode == 1) &&
+         a.xg_world <= 1;
 }
 
 template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true>

@@ -141,6 +141,11 @@ int dct_mlp_train(const void* shape, const MlpArgs* a, void* stream) {
   if (!sh.supported) return (int)hipErrorInvalidValue;
   if (a->B < 1 || a->B > sh.bmax) return (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (a->stage && !dct::mlp_block5_ok(sh, *a)) {  // only mlp_block5's grad mode stages batches here
+    MlpArgs b = *a;
+    b.stage = nullptr;
+    return dct_mlp_train(shape, &b, stream);
+  }
   if (dct::mlp_block4_ok(sh, *a)) return (int)dct::mlp_launch_block4(sh, *a, st);
   if (dct::mlp_block5_ok(sh, *a)) return (int)dct::mlp_launch_block5(sh, *a, st);
   if (dct::mlp_block3_ok(sh, *a)) return (int)dct::mlp_launch_block3(sh, *a, st);

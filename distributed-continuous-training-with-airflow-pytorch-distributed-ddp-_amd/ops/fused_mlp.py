@@ -144,7 +144,7 @@ class FusedMLPKernel:
             float(lr), float(betas[0]), float(betas[1]), float(eps), float(weight_decay), float(dropout),
             int(seed) & 0xFFFFFFFF, int(step_base) & 0xFFFFFFFF, ptr(loss_out), mode, LOSS_KINDS[loss],
             ptr(step_counter), ptr(cursor), ptr(prof), ptr(pending),
-            ptr(stage) if (stage is not None and self.plan.use_wave) else 0,
+            ptr(stage) if (stage is not None and (self.plan.use_wave or mode == 1)) else 0,
             stream if stream is not None else stream_handle(),
             **xg_args,
         )

@@ -339,10 +339,12 @@ class FusedMLPEngine(_EngineBase):
                               cursor=self.cursor, loss_out=loss_out, pending=self.pending, stage=self.stage)
             self.comm.allreduce(self.gbuf.data_ptr(), self.P + 1, nat.DT_F32, nat.OP_AVG, stream)
             return
+        # the 3x128 grad kernel (mlp_block5) hands the next batch to the next launch through
+        # self.stage (tagged with its batch index: a mismatch after a cursor jump falls back to the gather)
         self.kernel.train(self.p, None, None, self.X, self.Y, self.idx, n_items=n_items, batch=self.B, steps=1,
                           t0=0, lr=a["lr"], dropout=self.dropout, seed=self.rank_seed, loss=self.loss,
                           grad_out=self.gbuf, step_counter=self.step_counter, cursor=self.cursor,
-                          loss_out=loss_out)
+                          loss_out=loss_out, stage=None if self.kernel.plan.use_wave else self.stage)
         if self.gx is not None:
             from ..parallel.xgmi import allreduce_adam_
 

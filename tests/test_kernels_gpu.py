@@ -158,6 +158,43 @@ def test_fused_grad_mode_matches_autograd(dims, B, kernel, cuda, monkeypatch):
     assert abs(g[P].item() - l.item()) < 1e-5
 
 
+@pytest.mark.parametrize("dims,B,n_items", [([5, 128, 128, 2], 4, 30), ([8, 128, 128, 2], 3, 13),
+                                            ([1, 128, 128, 2], 2, 9)])
+def test_block5_grad_mode_staged_batches(dims, B, n_items, cuda):
+    """mlp_block5's grad mode at the device cursor (the DDP step path, one launch per step): each
+    launch stages the next batch's x / label words in ``stage`` (tagged batch + 1) and the next
+    launch reads them instead of gathering.  Every launch's gradients and loss must equal the
+    unstaged launch of the same batch bit for bit - staged hits, the partial last batch, and a
+    cursor jump (tag mismatch -> gather) included."""
+    torch.manual_seed(6)
+    N = 200
+    X = torch.randn(N, dims[0]).to(cuda)
+    Y = torch.randint(0, dims[-1], (N,)).to(cuda, torch.int32)
+    idx = torch.randperm(N)[:n_items].to(cuda, torch.int32)
+    p = _flat(_ref_net(dims)).to(cuda)
+    P = mlp_num_params(dims)
+    k = FusedMLPKernel(dims, bmax=4)
+    nb = math.ceil(n_items / B)
+    order = list(range(nb)) + [1, 2, 0]  # contiguous run, then a jump back
+    stage = torch.zeros(256, dtype=torch.int32, device=cuda)
+    cur_s = torch.zeros(1, dtype=torch.int32, device=cuda)
+    cur_r = torch.zeros(1, dtype=torch.int32, device=cuda)
+    for b in order:
+        gs, gr = torch.zeros(P + 1, device=cuda), torch.zeros(P + 1, device=cuda)
+        if int(cur_s.item()) != b:
+            cur_s.fill_(b)
+        cur_r.fill_(b)
+        k.train(p, None, None, X, Y, idx, n_items=n_items, batch=B, steps=1, t0=0, lr=0.01, grad_out=gs,
+                cursor=cur_s, stage=stage)
+        k.train(p, None, None, X, Y, idx, n_items=n_items, batch=B, steps=1, t0=0, lr=0.01, grad_out=gr,
+                cursor=cur_r)
+        torch.cuda.synchronize()
+        assert torch.equal(gs, gr), (b, (gs - gr).abs().max())
+        assert int(cur_s.item()) == b + 1
+        tag = int(stage[0].item())
+        assert tag == (b + 2 if (b + 1) * B < n_items else 0), (b, tag)
+
+
 @pytest.mark.parametrize("dims,B,D0", [([7, 128, 128, 2], 4, 7), ([30, 128, 128, 3], 3, 30)])
 def test_block_kernel_matches_lds_kernel_with_dropout(dims, B, D0, cuda, monkeypatch):
     """The register-resident 3-layer kernels (mlp_block4 / 3 / 2 and round 2's mlp_block, with and
