@@ -110,6 +110,9 @@ class FusedMLPEngine(_EngineBase):
         self.fused_update = self.kernel.fused_update_supported(self.B) and os.environ.get("DCT_FUSED_UPDATE", "1") != "0"
         self.pending = torch.zeros(1, dtype=torch.int32, device=dev)
         self.stage = torch.zeros(64 * 4, dtype=torch.int32, device=dev)  # next-batch hand-off
+        # mlp_block5 grad-mode batch hand-off between DDP step launches (opt-in: DCT_B5_STAGE=1; the
+        # first measurement put the grad kernel 0.5 us slower with it, profiles/block5_stage_ab_r3.log)
+        self._b5_stage = os.environ.get("DCT_B5_STAGE", "0") == "1"
         self._graphs = {}
         self.graph_chunk = int(os.environ.get("DCT_GRAPH_CHUNK", "256"))
         self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -339,12 +342,12 @@ class FusedMLPEngine(_EngineBase):
                               cursor=self.cursor, loss_out=loss_out, pending=self.pending, stage=self.stage)
             self.comm.allreduce(self.gbuf.data_ptr(), self.P + 1, nat.DT_F32, nat.OP_AVG, stream)
             return
-        # the 3x128 grad kernel (mlp_block5) hands the next batch to the next launch through
-        # self.stage (tagged with its batch index: a mismatch after a cursor jump falls back to the gather)
+        # DCT_B5_STAGE=1: the 3x128 grad kernel (mlp_block5) hands the next batch to the next launch
+        # through self.stage (tagged with its batch index: a mismatch after a cursor jump gathers)
         self.kernel.train(self.p, None, None, self.X, self.Y, self.idx, n_items=n_items, batch=self.B, steps=1,
                           t0=0, lr=a["lr"], dropout=self.dropout, seed=self.rank_seed, loss=self.loss,
                           grad_out=self.gbuf, step_counter=self.step_counter, cursor=self.cursor,
-                          loss_out=loss_out, stage=None if self.kernel.plan.use_wave else self.stage)
+                          loss_out=loss_out, stage=None if (self.kernel.plan.use_wave or not self._b5_stage) else self.stage)
         if self.gx is not None:
             from ..parallel.xgmi import allreduce_adam_
 
