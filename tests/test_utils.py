@@ -70,3 +70,52 @@ def test_native_build_relinks_when_the_object_set_changes(tmp_path, monkeypatch)
     _build.build()
     assert len(links) == 3 and links[2] == links[0]  # ... but the .so is relinked from it
     assert not _build.is_stale()
+
+
+class _StubCtx:
+    """Just what parallel/xgmi.py's exchange setup asks of a DistContext (one process stands for
+    every rank: the collective AND of a decision is the local value)."""
+
+    def __init__(self, world, device="cpu", local_world=None):
+        import torch
+
+        self.world_size, self.rank = world, 0
+        self.local_world_size = world if local_world is None else local_world
+        self.device = torch.device(device)
+        self.calls = []
+
+    def all_reduce_bool_and(self, v):
+        self.calls.append(bool(v))
+        return bool(v)
+
+
+@pytest.mark.parametrize("env,world,local,dev", [({}, 2, None, "cpu"), ({}, 1, None, "cpu"),
+                                                 ({"DCT_XG_GRAD": "0"}, 2, None, "cpu"),
+                                                 ({"DCT_ALLREDUCE": "rccl"}, 8, None, "cpu"),
+                                                 ({}, 16, 8, "cpu")])
+def test_grad_exchange_setup_declines_collectively(env, world, local, dev, monkeypatch):
+    """setup_grad_exchange (the 3x128 DDP step's peer all-reduce + Adam kernel) is only taken with
+    every rank on one node, on GPUs, 2..8 ranks and not turned off; otherwise every rank gets None
+    after one collective decision (so no rank goes on to export IPC handles alone), and
+    DCT_ALLREDUCE=xgmi does not make its absence an error (RCCL remains the step path)."""
+    from dct_amd.parallel.xgmi import setup_grad_exchange
+
+    for k in ("DCT_XG_GRAD", "DCT_ALLREDUCE"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    ctx = _StubCtx(world, dev, local)
+    assert setup_grad_exchange(ctx, 17539) is None
+    assert ctx.calls == [False]
+    monkeypatch.setenv("DCT_ALLREDUCE", "xgmi")
+    ctx = _StubCtx(world, dev, local)
+    assert setup_grad_exchange(ctx, 17539) is None
+
+
+def test_xg_adam_buffer_size_matches_the_kernel_layout():
+    """[2 parities][W ranks][ceil(n / 2) element pairs] x 16-B granules (csrc/xg_adam.hip)."""
+    from dct_amd.ops._native import native
+
+    nat = native()
+    assert nat.xg_adam_buffer_bytes(17539, 8) == 2 * 8 * 8770 * 16
+    assert nat.xg_adam_buffer_bytes(4, 2) == 2 * 2 * 2 * 16
