@@ -95,8 +95,17 @@ static dct::MlpArgs make_train_args(const MlpPlan& plan, uintptr_t p, uintptr_t 
   a.xg_status = P<unsigned int>(xg_status);
   a.xg_timeout = xg_timeout;
   a.xg_poll = xg_poll;
-  if (xg_world > 1 && !(plan.use_wave && dct_mlp_wave_supported(plan.sh()->dims, plan.sh()->L, B)))
-    throw std::invalid_argument("in-kernel all-reduce needs the single-wave kernel");
+  if (xg_world > 1) {
+    const dct::MlpShape* sh = plan.sh();
+    const bool wave = plan.use_wave && dct_mlp_wave_supported(sh->dims, sh->L, B);
+    const bool blk5 = !plan.use_wave && mode == 0 && dct::mlp_block5_shape_ok(sh->dims, sh->L, B) &&
+                      dct::mlp_block5_xg_bytes(xg_world) > 0;
+    if (!wave && !blk5)
+      throw std::invalid_argument("in-kernel all-reduce needs the single-wave kernel or the 3x128 block kernel "
+                                  "(train mode, 2 / 4 / 8 ranks)");
+    if (!xg_recv || !xg_peers || !xg_status || xg_rank < 0 || xg_rank >= xg_world)
+      throw std::invalid_argument("in-kernel all-reduce: exchange buffers / rank missing");
+  }
   if (pending && (mode != 1 || !plan.use_wave || !mo || !vo))
     throw std::invalid_argument("update-then-grad needs grad mode, m/v and the single-wave kernel");
   if (cursor && mode != 1) throw std::invalid_argument("cursor is only valid in grad mode");
@@ -546,6 +555,12 @@ PYBIND11_MODULE(_dct_native, m) {
       .def_property_readonly("bytes", &dct::PeerExchange::bytes)
       .def_property_readonly("world", &dct::PeerExchange::world)
       .def_property_readonly("rank", &dct::PeerExchange::rank);
+  // exchange buffer bytes of the 3x128 block kernel's in-kernel data-parallel launches (0: no such
+  // launch for this shape / batch / world size)
+  m.def("mlp_block5_xg_bytes", [](const std::vector<int>& dims, int B, int world) -> int64_t {
+    if (dims.size() != 4 || !dct::mlp_block5_shape_ok(dims.data(), 3, B)) return 0;
+    return (int64_t)dct::mlp_block5_xg_bytes(world);
+  }, py::arg("dims"), py::arg("batch"), py::arg("world"));
   m.def("mlp_xg_slab_granules", [](const std::vector<int>& dims) {
     return (int64_t)dct_mlp_xg_slab_granules(dims.data(), (int)dims.size() - 1);
   });

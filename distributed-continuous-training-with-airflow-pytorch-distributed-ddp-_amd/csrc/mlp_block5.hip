@@ -35,7 +35,8 @@ constexpr int PSTR = 36;                  // partials: [o][wave][4] with a 36-fl
 constexpr int PART = H1X + NW * KS * 4;   // [2][H][PSTR]
 constexpr int W2L = PART + 2 * H * PSTR;  // [2][H][C] W2[c][o] (o-major), published by the owners
 constexpr int B2L = W2L + 2 * H * C;      // [2][4] b2
-constexpr int TOTAL = B2L + 8;
+constexpr int ABT = B2L + 8;              // [4] data-parallel launches: a wave's exchange timed out
+constexpr int TOTAL = ABT + 4;
 constexpr int STG = H * H;
 constexpr int LDS_FLOATS = TOTAL > 2 * STG ? TOTAL : 2 * STG;  // two staging tiles (prologue/epilogue)
 static_assert(LDS_FLOATS * 4 <= 160 * 1024, "fits the CU");
@@ -45,6 +46,74 @@ static_assert((H1W % 4) == 0 && (PART % 4) == 0 && (MSK % 4) == 0 && (LAB % 4) =
 using Stg = bku::Stage<H, NT>;
 constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
 }  // namespace blk5
+
+// ---- data parallelism inside the persistent launch (XW = 2 / 4 / 8 ranks, one per GPU) ---------
+// The reference averages every rank's gradients each step (DDP, jobs/train_lightning_ddp.py:136)
+// and logs the cross-rank mean loss (sync_dist, :70).  Here that happens in the trainer's own
+// launch, over receive buffers every rank maps from its peers (IPC over xGMI, parallel/xgmi.py),
+// as a reduce-scatter + all-gather with the optimizer state SHARDED by it (ZeRO-1 style):
+//   * every lane holds 16 W1 pairs (rows l, l + 64 x 8 k-pairs of its wave's k-slice, pair
+//     i = 8 j + h) and 2 small pairs ({W0[u][r0], W0[u][r0 + 4]}, {W2[r0 & 1][u], its bias: b0[u],
+//     b1[u] or b2[l & 1] by r0}); rank i % XW owns W1 pair i of every lane, rank w % XW the small
+//     pairs of wave w - so one CU pushes 2 x 16 (XW-1)/XW granules per lane per step instead of
+//     16 (XW - 1) for a full all-reduce, and runs 1/XW of the W1 Adam;
+//   * RS: each gradient pair is pushed, as it leaves the MFMA, to its owner's slot [src][slot];
+//     the owner polls its slots, sums the XW contributions IN RANK ORDER, applies Adam;
+//   * AG: the owner pushes the new parameter pair into every peer's slot [pair]; everyone polls
+//     the pairs it does not own.  Replicas are bit-identical by construction (one writer each);
+//   * the batch loss rides in one granule per rank (rank-ordered mean = sync_dist's);
+//   * at launch end the owned Adam moments are all-gathered the same way, so p / m / v in HBM
+//     are complete and identical on every rank (checkpoints, resume and fallbacks see one state).
+// Granules are 16-B {value, tag, value, tag} write-through stores (the data IS the flag, each
+// 8-B half tag-checked); tag = global step + 1, two parity slabs: a rank rewrites a slab of
+// step s + 2 only after every peer's step s + 1 granules reached it, i.e. after they finished
+// reading step s.  Spins are bounded (xg_timeout): a timeout records the tag in xg_status, the
+// workgroup leaves at the next barrier and the launch writes NOTHING back (HBM keeps the state
+// the launch started from; the engine re-syncs or raises).
+namespace b5x {
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+constexpr int SYS = 17;              // sc0 | sc1: write-through stores, L2-bypassing loads
+constexpr int NP = 16, NS = 2;       // W1 pairs / small pairs per lane
+constexpr int G = blk5::NT * 16;     // bytes of one slot: one 16-B granule per thread
+template <int XW>
+struct Lay {
+  static constexpr int NO = NP / XW;                       // W1 pairs a rank owns per lane
+  static constexpr int RSS = NO + NS;                      // RS slots per (parity, source)
+  // RS slots are indexed by the source's distance from the owner, (src - owner) mod XW (1..XW-1),
+  // so a rank polls its sources without knowing their absolute index
+  static constexpr int AG = 2 * XW * RSS * G;              // [2][NP + NS] all-gather slots
+  static constexpr int LS = AG + 2 * (NP + NS) * G;        // [2][XW] loss granules
+  static constexpr int EP = LS + ((2 * XW * 16 + 255) & ~255);  // [NP + NS][m, v] launch-end moments
+  static constexpr int BYTES = EP + (NP + NS) * 2 * G;
+  static __device__ __forceinline__ int rs(int par, int src, int slot) { return ((par * XW + src) * RSS + slot) * G; }
+  static __device__ __forceinline__ int ag(int par, int slot) { return AG + (par * (NP + NS) + slot) * G; }
+  static __device__ __forceinline__ int ls(int par, int src) { return LS + (par * XW + src) * 16; }
+  static __device__ __forceinline__ int ep(int slot, int mv) { return EP + (slot * 2 + mv) * G; }
+};
+__device__ __forceinline__ void put(__amdgpu_buffer_rsrc_t rs, int off, float x, float y, uint32_t tag) {
+  v4u d;
+  d.x = __float_as_uint(x);
+  d.y = tag;
+  d.z = __float_as_uint(y);
+  d.w = tag;
+  __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, 0, SYS);
+}
+__device__ __forceinline__ bool get(__amdgpu_buffer_rsrc_t rs, int off, uint32_t tag, float& x, float& y) {
+  const v4u d = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, SYS);
+  x = __uint_as_float(d.x);
+  y = __uint_as_float(d.z);
+  return (d.y == tag) & (d.w == tag);
+}
+// v[XW t + rank] out of v[XW t .. XW t + XW - 1] for a wave-uniform rank: XW - 1 selects on an
+// SGPR condition, no branch and no dynamically indexed register
+template <int XW, class T>
+__device__ __forceinline__ T pick(const T* v, int rank) {
+  T r = v[0];
+#pragma unroll
+  for (int k = 1; k < XW; ++k) r = rank == k ? v[k] : r;
+  return r;
+}
+}  // namespace b5x
 
 #define B5STAMP(k)                                              \
   if constexpr (PROF) {                                         \
@@ -136,11 +205,15 @@ __device__ __forceinline__ void adam_v2(v2f& p, v2f g, v2f& m, v2f& v, float b1,
 
 // LK: 0 = cross-entropy, 1 = MSE against the one-hot label; WD: L2 term in the update; ADAM = false:
 // grad mode (the DDP step: ONE step at the device batch cursor, gradients + batch loss to grad_out,
-// the previous step's all-reduced loss to loss_out[cursor - 1]; no moments read or written)
-template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true>
+// the previous step's all-reduced loss to loss_out[cursor - 1]; no moments read or written);
+// XW > 1: train mode of one rank of XW data-parallel ranks (b5x above)
+template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true, int XW = 1>
 __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, MlpArgs a) {
   using namespace blk5;
   using namespace bku;
+  static_assert(XW == 1 || (ADAM && !PROF && (XW == 2 || XW == 4 || XW == 8)), "exchange: train mode, 2/4/8 ranks");
+  using XL = b5x::Lay<XW>;
+  constexpr int NO = XL::NO;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const int D0 = sh.dims[0];
@@ -209,12 +282,21 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
 #pragma unroll
   for (int c = 0; c < C; ++c) pw2[c] = a.p[wo2 + c * H + u];
   const bool own_w2 = r0 < C;
-  const int fw2 = wo2 + (own_w2 ? r0 : 0) * H + u;
-  float mw2 = (own_w2 && ADAM) ? a.m[fw2] : 0.f, vw2 = (own_w2 && ADAM) ? a.v[fw2] : 0.f;
+  // (XW > 1: every lane updates W2[r0 & 1][u] - quad lanes 2 / 3 duplicate lanes 0 / 1)
+  const int fw2 = wo2 + (XW > 1 ? (r0 & 1) : (own_w2 ? r0 : 0)) * H + u;
+  float mw2 = ((own_w2 || XW > 1) && ADAM) ? a.m[fw2] : 0.f, vw2 = ((own_w2 || XW > 1) && ADAM) ? a.v[fw2] : 0.f;
   float pb1 = a.p[bo1 + u], mb1 = ADAM ? a.m[bo1 + u] : 0.f, vb1 = ADAM ? a.v[bo1 + u] : 0.f;
   const bool own_b2 = w == 0 && l < C;
   const int fb2 = bo2 + (own_b2 ? l : 0);
   float pb2 = own_b2 ? a.p[fb2] : 0.f, mb2 = (own_b2 && ADAM) ? a.m[fb2] : 0.f, vb2 = (own_b2 && ADAM) ? a.v[fb2] : 0.f;
+  // XW > 1: the bias this lane updates in its second small pair: b0[u] (r0 0), b1[u] (r0 1), b2[l & 1]
+  const int fbx = r0 == 0 ? bo0 + u : (r0 == 1 ? bo1 + u : bo2 + (l & 1));
+  float pbx = 0.f, mbx = 0.f, vbx = 0.f;
+  if constexpr (XW > 1) {
+    pbx = a.p[fbx];
+    mbx = a.m[fbx];
+    vbx = a.v[fbx];
+  }
 
   // step counter and the first batch's row indices through the scalar cache (their round trips
   // overlap the W1 loads)
@@ -294,6 +376,7 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
 #pragma unroll
   for (int i = 0; i < 2; ++i) { m0[i] *= rc1; v0[i] *= rc2; }
   mb0 *= rc1; vb0 *= rc2; mw2 *= rc1; vw2 *= rc2; mb1 *= rc1; vb1 *= rc2; mb2 *= rc1; vb2 *= rc2;
+  mbx *= rc1; vbx *= rc2;
   // the step loop keeps W1 and its moments as 64-bit pairs of consecutive k (packed Adam; the dW1 MFMA
   // accumulators come out in the same pairs)
   v2f W[2][KS / 2], Mo[2][KS / 2], Vo[2][KS / 2];
@@ -305,6 +388,46 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
       Mo[j][h] = (v2f){m1[j][2 * h], m1[j][2 * h + 1]};
       Vo[j][h] = (v2f){v1[j][2 * h], v1[j][2 * h + 1]};
     }
+  // ---- XW > 1: the moments of the owned W1 pairs only (slot t = pair rank + XW t), the exchange's
+  // buffer descriptors, this rank's small-pair ownership
+  const int xrank = XW > 1 ? a.xg_rank : 0;
+  v2f MoO[NO], VoO[NO];
+  __amdgpu_buffer_rsrc_t xrr = __builtin_amdgcn_make_buffer_rsrc((void*)a.xg_recv, 0, 0, 0x00020000), xpr[XW];
+  // (the wave index through readfirstlane: a scalar condition, uniform branches)
+  const bool sown = XW == 1 || (__builtin_amdgcn_readfirstlane(w) % XW) == xrank;
+  bool xbad = false;  // this wave's exchange timed out
+  unsigned long long xticks = 0;
+  if constexpr (XW > 1) {
+#pragma unroll
+    for (int t = 0; t < NO; ++t) {
+      v2f cm[XW], cv[XW];
+#pragma unroll
+      for (int k = 0; k < XW; ++k) {
+        cm[k] = Mo[(XW * t + k) >> 3][(XW * t + k) & 7];
+        cv[k] = Vo[(XW * t + k) >> 3][(XW * t + k) & 7];
+      }
+      MoO[t] = b5x::pick<XW>(cm, xrank);
+      VoO[t] = b5x::pick<XW>(cv, xrank);
+    }
+    xrr = __builtin_amdgcn_make_buffer_rsrc((void*)a.xg_recv, 0, XL::BYTES, 0x00020000);
+#pragma unroll
+    for (int q = 0; q < XW; ++q) xpr[q] = __builtin_amdgcn_make_buffer_rsrc((void*)a.xg_peers[q], 0, XL::BYTES, 0x00020000);
+  }
+  // bounded spin of one wave until sweep() (this lane's loads of one pass, true when all tags
+  // match) holds in every lane; false after xg_timeout (the tag is recorded in xg_status)
+  auto xwait = [&](uint32_t tag, auto&& sweep) -> bool {
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    for (int spin = 0;; ++spin) {
+      asm volatile("" ::: "memory");  // every pass re-issues its loads
+      if (__all(sweep())) return true;
+      if ((spin & 15) == 15 && (long long)(__builtin_amdgcn_s_memrealtime() - t_start) > a.xg_timeout) {
+        if (l == 0) __hip_atomic_store(a.xg_status, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  const int tb = tid * 16;  // this thread's granule inside a slot
   // dropout factors of this lane's (row r0, unit u) elements at the first step
   const uint32_t el0 = b5_elem(0, r0, u), el1 = b5_elem(1, r0, u);
   float f1 = b5_drop(a.seed, step_base, el0, p_drop, scale);
@@ -393,6 +516,11 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     B5STAMP(1)
     lds_barrier();  // A: all partials of this step are in (and W2 / b2 of the previous publish)
     B5STAMP(2)
+    if constexpr (XW > 1) {
+      // a wave's exchange of the previous step timed out (flag written before this barrier):
+      // the whole workgroup leaves together, the epilogue writes nothing back
+      if (lds[ABT] != 0.f) break;
+    }
 
     // ---- backward operands published before A: W2 columns l, l + 64 (dZ2), b2 of class cb, the
     // label of row r0 - issued first, consumed after barrier B
@@ -455,12 +583,23 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int c = 0; c < C; ++c) dz3[r][c] = rl(dz, 4 * c + r);
+    const uint32_t xtag = gstep + 1u;  // XW > 1: this step's exchange tag and parity slab
+    const int xpar = (int)(gstep & 1u);
+    float xbl = 0.f;                   // XW > 1: this rank's batch loss (wave 0)
     if (w == 0) {  // batch loss: lanes 0..7 hold (class, row) terms
       float t = lv + dpp<QP_X1>(lv);
       t += dpp<QP_X2>(t);
       t += dpp<ROR4>(t);
       const float bl = bs > 0 ? t * __builtin_amdgcn_rcpf((float)bs) : 0.f;
-      if constexpr (ADAM) {
+      if constexpr (ADAM && XW > 1) {
+        // sync_dist: one granule to every peer now, the rank-ordered mean after the all-gather
+        xbl = rl(bl, 0);
+        if (l == 0) {
+#pragma unroll
+          for (int q = 0; q < XW; ++q)
+            if (q != xrank) b5x::put(xpr[q], XL::ls(xpar, xrank), xbl, 0.f, xtag);
+        }
+      } else if constexpr (ADAM) {
         if (l == 0 && a.loss_out) a.loss_out[s] = bl;
       } else {
         if (l == 0) a.grad_out[sh.P] = bl;
@@ -490,6 +629,7 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
       }
     }
     // ---- owners: dW2[:, u], db1[u] (quad sums), W2 / b1 / b2 Adam, W2 / b2 published
+    float xg_own = 0.f, xg_bx = 0.f;  // XW > 1: this lane's second small gradient pair
     {
       const float d_own = dz, d_oth = dpp<ROR4>(dz);  // dlogit (r0, cb), (r0, 1 - cb)
       const float dr0 = cb ? d_oth : d_own, dr1 = cb ? d_own : d_oth;
@@ -504,7 +644,10 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
       const float gown = (r0 & 1) ? gw1 : gw0;
       const float gb = (l & 1) ? (dz3[0][1] + dz3[1][1]) + (dz3[2][1] + dz3[3][1])
                                : (dz3[0][0] + dz3[1][0]) + (dz3[2][0] + dz3[3][0]);
-      if constexpr (ADAM) {
+      if constexpr (ADAM && XW > 1) {  // exchanged with the W0 gradients below
+        xg_own = gown;
+        xg_bx = r0 == 1 ? gb1 : gb;  // (r0 0: db0, known after dZ1)
+      } else if constexpr (ADAM) {
         adam_pair<WD>(pown, gown, mw2, vw2, pb1, gb1, mb1, vb1, a.b1, a.b2, a.wd, aA, aE);
         pw2[0] = dpp<QB0>(pown);
         pw2[1] = dpp<QB1>(pown);
@@ -562,11 +705,26 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     }
     dz1 = h1 > 0.f ? dz1 * scale : 0.f;
     // ---- dW0 / db0 (the quad holds unit u's four rows; inputs from the F1 tile in registers)
+    v2f xs_g0 = (v2f){0.f, 0.f}, xs_g1 = (v2f){0.f, 0.f};  // XW > 1: the small gradient pairs
     {
       const float dq0 = dpp<QB0>(dz1), dq1 = dpp<QB1>(dz1), dq2 = dpp<QB2>(dz1), dq3 = dpp<QB3>(dz1);
       const float g0 = dq0 * xa.x + dq1 * xa.y + dq2 * xa.z + dq3 * xa.w;
       const float g1 = dq0 * xc.x + dq1 * xc.y + dq2 * xc.z + dq3 * xc.w;
-      if constexpr (ADAM) {
+      if constexpr (ADAM && XW > 1) {
+        // the two small pairs go to the wave's owner rank now (its Adam runs after the dW1 loop)
+        if (r0 == 0) xg_bx = (dq0 + dq1) + (dq2 + dq3);
+        xs_g0 = (v2f){g0, g1};
+        xs_g1 = (v2f){xg_own, xg_bx};
+        if (!sown) {
+#pragma unroll
+          for (int q = 0; q < XW; ++q)
+            if (q == w % XW) {
+              const int rel = (xrank - q + XW) % XW;
+              b5x::put(xpr[q], XL::rs(xpar, rel, NO) + tb, g0, g1, xtag);
+              b5x::put(xpr[q], XL::rs(xpar, rel, NO + 1) + tb, xg_own, xg_bx, xtag);
+            }
+        }
+      } else if constexpr (ADAM) {
         adam_pair<WD>(w0[0], g0, m0[0], v0[0], w0[1], g1, m0[1], v0[1], a.b1, a.b2, a.wd, aA, aE);  // d >= D0: stays 0
         adam_scaled<WD>(pb0, (dq0 + dq1) + (dq2 + dq3), mb0, vb0, a.b1, a.b2, a.wd, aA, aE);
       } else {
@@ -581,6 +739,9 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     B5STAMP(7)
     // ---- dW1 (MFMA: A = h1[4q + lane % 4][r], B = this lane's dZ2, C register m = the gradient of
     // its own w1[j][4q + m]) + packed Adam on pairs of consecutive k
+    v2f GO[NO];  // XW > 1: gradients of the W1 pairs this rank owns
+#pragma unroll
+    for (int t = 0; t < NO; ++t) GO[t] = (v2f){0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < KS / 4; ++q) {
       const float4 hq = *reinterpret_cast<const float4*>(h1w + (4 * q + r0) * 4);
@@ -592,7 +753,18 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
 #pragma unroll
         for (int r = 0; r < 4; ++r) g[j] = mfma4(hv[r], dz2[j][r], g[j]);
       }
-      if constexpr (ADAM) {
+      if constexpr (ADAM && XW > 1) {
+        // pair i = 8 j + 2 q + h to its owner i % XW (slot i / XW there), or kept if owned here
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int i = 8 * j + 2 * q + h;
+            const float gx = g[j][2 * h], gy = g[j][2 * h + 1];
+            if ((i % XW) == xrank) GO[i / XW] = (v2f){gx, gy};
+            else b5x::put(xpr[i % XW], XL::rs(xpar, (xrank - i % XW + XW) % XW, i / XW) + tb, gx, gy, xtag);
+          }
+      } else if constexpr (ADAM) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -606,9 +778,206 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
               make_float4(g[j][0], g[j][1], g[j][2], g[j][3]);
       }
     }
+    if constexpr (ADAM && XW > 1) {
+      // ---- the owner's part: reduce-scatter poll, rank-ordered sums, Adam, all-gather pushes;
+      // then the all-gather poll of every pair owned elsewhere (specialised per rank: all
+      // register indices are constants)
+      const unsigned long long xt0 = __builtin_amdgcn_s_memrealtime();
+      const float invw = 1.f / (float)XW;
+      do {
+        // reduce-scatter poll: slots of sources at distance 1..XW-1 (the sum starts at the owner's
+        // own gradient and follows the ranks after it: a fixed order, so runs are reproducible)
+        float rv[XW][NO][2], sv[XW][2][2];
+        if (!xwait(xtag, [&]() -> bool {
+              bool k = true;
+#pragma unroll
+              for (int q = 1; q < XW; ++q)
+#pragma unroll
+                for (int t = 0; t < NO; ++t) k &= b5x::get(xrr, XL::rs(xpar, q, t) + tb, xtag, rv[q][t][0], rv[q][t][1]);
+              return k;
+            })) {
+          xbad = true;
+          break;
+        }
+        // the small pairs' slots (owner waves only; pushed before the W1 pairs, so normally in):
+        // first pass issued here, checked after the W1 Adam - their registers are not in flight
+        // together with the W1 slots'
+        auto small_sweep = [&]() -> bool {
+          bool k = true;
+#pragma unroll
+          for (int q = 1; q < XW; ++q) {
+            k &= b5x::get(xrr, XL::rs(xpar, q, NO) + tb, xtag, sv[q][0][0], sv[q][0][1]);
+            k &= b5x::get(xrr, XL::rs(xpar, q, NO + 1) + tb, xtag, sv[q][1][0], sv[q][1][1]);
+          }
+          return k;
+        };
+        bool sok = true;
+        if (sown) sok = small_sweep();
+        // Adam on the owned W1 pairs (slot t = pair XW t + rank), pushed to every peer
+        v2f WO[NO];
+#pragma unroll
+        for (int t = 0; t < NO; ++t) {
+          v2f cw[XW];
+#pragma unroll
+          for (int k = 0; k < XW; ++k) cw[k] = W[(XW * t + k) >> 3][(XW * t + k) & 7];
+          WO[t] = b5x::pick<XW>(cw, xrank);
+          v2f gs = GO[t];
+#pragma unroll
+          for (int q = 1; q < XW; ++q) gs += (v2f){rv[q][t][0], rv[q][t][1]};
+          adam_v2<WD>(WO[t], gs * (v2f)(invw), MoO[t], VoO[t], a.b1, a.b2, a.wd, aA, aE);
+          const int agoff = XL::ag(xpar, XW * t + xrank) + tb;
+#pragma unroll
+          for (int q = 0; q < XW; ++q)
+            if (q != xrank) b5x::put(xpr[q], agoff, WO[t].x, WO[t].y, xtag);
+        }
+        if (sown && !__all(sok) && !xwait(xtag, small_sweep)) {
+          xbad = true;
+          break;
+        }
+        if (sown) {
+          v2f s0 = xs_g0, s1 = xs_g1;
+#pragma unroll
+          for (int q = 1; q < XW; ++q) {
+            s0 += (v2f){sv[q][0][0], sv[q][0][1]};
+            s1 += (v2f){sv[q][1][0], sv[q][1][1]};
+          }
+          s0 *= (v2f)(invw);
+          s1 *= (v2f)(invw);
+          adam_pair<WD>(w0[0], s0.x, m0[0], v0[0], w0[1], s0.y, m0[1], v0[1], a.b1, a.b2, a.wd, aA, aE);
+          float pown = (r0 & 1) ? pw2[1] : pw2[0];
+          adam_pair<WD>(pown, s1.x, mw2, vw2, pbx, s1.y, mbx, vbx, a.b1, a.b2, a.wd, aA, aE);
+          xs_g1.x = pown;  // the new W2 element (broadcast below)
+#pragma unroll
+          for (int q = 0; q < XW; ++q)
+            if (q != xrank) {
+              b5x::put(xpr[q], XL::ag(xpar, b5x::NP) + tb, w0[0], w0[1], xtag);
+              b5x::put(xpr[q], XL::ag(xpar, b5x::NP + 1) + tb, pown, pbx, xtag);
+            }
+        }
+        // all-gather poll: every pair slot (the owned ones are not checked), the small pairs of a
+        // wave owned elsewhere, and in wave 0 the losses (lane q: rank q's)
+        float av[b5x::NP][2], sa[2][2], lq = 0.f, lq1;
+        const int lsrc = l < XW ? l : 0;
+        const bool lskip = w != 0 || l >= XW || l == xrank;
+        if (!xwait(xtag, [&]() -> bool {
+              bool k = true;
+#pragma unroll
+              for (int i = 0; i < b5x::NP; ++i)
+                k &= b5x::get(xrr, XL::ag(xpar, i) + tb, xtag, av[i][0], av[i][1]) | ((i % XW) == xrank);
+              if (!sown) {
+                k &= b5x::get(xrr, XL::ag(xpar, b5x::NP) + tb, xtag, sa[0][0], sa[0][1]);
+                k &= b5x::get(xrr, XL::ag(xpar, b5x::NP + 1) + tb, xtag, sa[1][0], sa[1][1]);
+              }
+              if (w == 0) k &= b5x::get(xrr, XL::ls(xpar, lsrc), xtag, lq, lq1) | lskip;
+              return k;
+            })) {
+          xbad = true;
+          break;
+        }
+#pragma unroll
+        for (int i = 0; i < b5x::NP; ++i)
+          W[i >> 3][i & 7] = (i % XW) == xrank ? WO[i / XW] : (v2f){av[i][0], av[i][1]};
+        if (!sown) {
+          w0[0] = sa[0][0];
+          w0[1] = sa[0][1];
+          xs_g1.x = sa[1][0];
+          pbx = sa[1][1];
+        }
+        if (w == 0) {  // sync_dist: the rank-ordered mean of the XW batch losses
+          float tot = 0.f;
+#pragma unroll
+          for (int q = 0; q < XW; ++q) tot += (q == xrank) ? xbl : rl(lq, q);
+          if (l == 0 && a.loss_out) a.loss_out[s] = tot * invw;
+        }
+      } while (false);
+      if (xbad) {
+        if (l == 0) lds[ABT] = 1.f;  // read by every wave behind the next barrier A
+      } else {
+        // W2[r0 & 1][u], b0[u], b1[u] to the quad; W2 / b2 published for the next step
+        const float pown = xs_g1.x;
+        pw2[0] = dpp<QB0>(pown);
+        pw2[1] = dpp<QB1>(pown);
+        pb0 = dpp<QB0>(pbx);
+        pb1 = dpp<QB1>(pbx);
+        if (own_w2) lds[W2L + nbuf * (H * C) + u * C + r0] = pown;
+        if (w == 0 && (l == 2 || l == 3)) lds[B2L + nbuf * 4 + (l & 1)] = pbx;
+      }
+      xticks += __builtin_amdgcn_s_memrealtime() - xt0;
+    }
     __builtin_amdgcn_wave_barrier();  // the next step rewrites this wave's h1 tiles
     B5STAMP(8)
     xb = xbn;
+  }
+  if constexpr (XW > 1) {
+    if (a.xg_ticks && tid == 0) atomicAdd(a.xg_ticks, xticks);
+    lds_barrier();
+    if (lds[ABT] != 0.f) return;  // an exchange timed out: HBM keeps the launch's starting state
+    // ---- all-gather of the owned Adam moments (scaled form on every rank alike), so m / v in HBM
+    // are complete on every rank; launch-unique tag (high bit: never a step tag)
+    const uint32_t etag = 0x80000000u | (step_base + (uint32_t)a.steps);
+    do {
+#pragma unroll
+      for (int t = 0; t < NO; ++t) {
+        const int o0 = XL::ep(XW * t + xrank, 0) + tb, o1 = XL::ep(XW * t + xrank, 1) + tb;
+#pragma unroll
+        for (int q = 0; q < XW; ++q)
+          if (q != xrank) {
+            b5x::put(xpr[q], o0, MoO[t].x, MoO[t].y, etag);
+            b5x::put(xpr[q], o1, VoO[t].x, VoO[t].y, etag);
+          }
+      }
+      if (sown) {
+#pragma unroll
+        for (int q = 0; q < XW; ++q)
+          if (q != xrank) {
+            b5x::put(xpr[q], XL::ep(b5x::NP, 0) + tb, m0[0], m0[1], etag);
+            b5x::put(xpr[q], XL::ep(b5x::NP, 1) + tb, v0[0], v0[1], etag);
+            b5x::put(xpr[q], XL::ep(b5x::NP + 1, 0) + tb, mw2, mbx, etag);
+            b5x::put(xpr[q], XL::ep(b5x::NP + 1, 1) + tb, vw2, vbx, etag);
+          }
+      }
+      // every moment register is (re)defined on every path, so none of the prologue's full-width
+      // moments stays live across the step loop
+      float em[b5x::NP][2][2], es[2][2][2];
+      const bool ok = xwait(etag, [&]() -> bool {
+        bool k = true;
+#pragma unroll
+        for (int i = 0; i < b5x::NP; ++i) {
+          const bool own = (i % XW) == xrank;
+          k &= b5x::get(xrr, XL::ep(i, 0) + tb, etag, em[i][0][0], em[i][0][1]) | own;
+          k &= b5x::get(xrr, XL::ep(i, 1) + tb, etag, em[i][1][0], em[i][1][1]) | own;
+        }
+        if (!sown) {
+#pragma unroll
+          for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+            for (int mv = 0; mv < 2; ++mv)
+              k &= b5x::get(xrr, XL::ep(b5x::NP + k2, mv) + tb, etag, es[k2][mv][0], es[k2][mv][1]);
+        }
+        return k;
+      });
+#pragma unroll
+      for (int i = 0; i < b5x::NP; ++i) {
+        const bool own = (i % XW) == xrank;
+        Mo[i >> 3][i & 7] = own ? MoO[i / XW] : (v2f){em[i][0][0], em[i][0][1]};
+        Vo[i >> 3][i & 7] = own ? VoO[i / XW] : (v2f){em[i][1][0], em[i][1][1]};
+      }
+      if (!ok) {
+        xbad = true;
+        break;
+      }
+      if (!sown) {
+        m0[0] = es[0][0][0]; m0[1] = es[0][0][1];
+        v0[0] = es[0][1][0]; v0[1] = es[0][1][1];
+        mw2 = es[1][0][0]; mbx = es[1][0][1];
+        vw2 = es[1][1][0]; vbx = es[1][1][1];
+      }
+    } while (false);
+    if (xbad) lds[ABT] = 1.f;
+    lds_barrier();
+    if (lds[ABT] != 0.f) return;
+    mbx *= c1;
+    vbx *= c2;
   }
   if (a.step_counter && tid == 0)
     __hip_atomic_store(a.step_counter, t0 + a.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -657,15 +1026,25 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
       a.v[f] = v0[i];
     }
   }
-  if (r0o == 0) {
-    a.p[bo0 + uo] = pb0; a.m[bo0 + uo] = mb0; a.v[bo0 + uo] = vb0;
-    a.p[bo1 + uo] = pb1; a.m[bo1 + uo] = mb1; a.v[bo1 + uo] = vb1;
+  if constexpr (XW > 1) {  // the second small pair: W2[r0 & 1][u] (lanes 0 / 1) and its bias
+    if (r0o < 2 || (w == 0 && (lo == 2 || lo == 3))) {
+      a.p[fbx] = pbx; a.m[fbx] = mbx; a.v[fbx] = vbx;
+    }
+    if (own_w2) {
+      const int f = wo2 + r0o * H + uo;
+      a.p[f] = (r0o & 1) ? pw2[1] : pw2[0]; a.m[f] = mw2; a.v[f] = vw2;
+    }
+  } else {
+    if (r0o == 0) {
+      a.p[bo0 + uo] = pb0; a.m[bo0 + uo] = mb0; a.v[bo0 + uo] = vb0;
+      a.p[bo1 + uo] = pb1; a.m[bo1 + uo] = mb1; a.v[bo1 + uo] = vb1;
+    }
+    if (own_w2) {
+      const int f = wo2 + r0o * H + uo;
+      a.p[f] = (r0o & 1) ? pw2[1] : pw2[0]; a.m[f] = mw2; a.v[f] = vw2;
+    }
+    if (own_b2) { a.p[fb2] = pb2; a.m[fb2] = mb2; a.v[fb2] = vb2; }
   }
-  if (own_w2) {
-    const int f = wo2 + r0o * H + uo;
-    a.p[f] = (r0o & 1) ? pw2[1] : pw2[0]; a.m[f] = mw2; a.v[f] = vw2;
-  }
-  if (own_b2) { a.p[fb2] = pb2; a.m[fb2] = mb2; a.v[fb2] = vb2; }
   if constexpr (PROF) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pacc[10] = __builtin_amdgcn_s_memtime() - t_last;
@@ -677,52 +1056,73 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
 }
 #undef B5STAMP
 
+// in-kernel data-parallel launches of this kernel: 2, 4 or 8 ranks (one node), train mode
+static bool b5_xg_world_ok(int w) { return w == 2 || w == 4 || w == 8; }
+
 bool mlp_block5_ok(const MlpShape& sh, const MlpArgs& a) {
-  // DCT_MLP_BLOCK: unset / "1" / "5" select this kernel; "4" / "3" / "2" / "0" / "v1" the others (A/B)
-  const char* env = getenv("DCT_MLP_BLOCK");
-  if (env && (env[0] == '0' || env[0] == '2' || env[0] == '3' || env[0] == '4' || env[0] == 'v')) return false;
   const bool aligned = (sh.woff[1] % 4) == 0 && ((uintptr_t)a.p & 15) == 0 && (((uintptr_t)a.m | (uintptr_t)a.v) & 15) == 0;
-  return aligned && sh.L == 3 && sh.dims[1] == blk5::H && sh.dims[2] == blk5::H && sh.dims[0] >= 1 &&
-         sh.dims[0] <= blk5::DMAX && sh.dims[3] == blk5::C && a.B >= 1 && a.B <= blk5::B &&
+  const bool xg_ok = a.xg_world <= 1 ||
+                     (a.mode == 0 && b5_xg_world_ok(a.xg_world) && a.xg_rank >= 0 && a.xg_rank < a.xg_world &&
+                      a.xg_recv != nullptr && a.xg_peers != nullptr && a.xg_status != nullptr && a.prof == nullptr);
+  return aligned && mlp_block5_shape_ok(sh.dims, sh.L, a.B) &&
          // train mode, or grad mode for ONE step (the DDP step path: grads + loss to grad_out, device cursor)
          ((a.mode == 0 && a.cursor == nullptr) || (a.mode == 1 && a.steps == 1 && a.grad_out != nullptr)) &&
-         (a.loss_kind == 0 || a.loss_kind == 1) && a.pending == nullptr && (a.stage == nullptr || a.mode == 1) &&
-         a.xg_world <= 1;
+         (a.loss_kind == 0 || a.loss_kind == 1) && a.pending == nullptr && (a.stage == nullptr || a.mode == 1) && xg_ok;
 }
 
-template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true>
+bool mlp_block5_shape_ok(const int* dims, int L, int B) {
+  return L == 3 && dims[1] == blk5::H && dims[2] == blk5::H && dims[0] >= 1 && dims[0] <= blk5::DMAX &&
+         dims[3] == blk5::C && B >= 1 && B <= blk5::B;
+}
+
+size_t mlp_block5_xg_bytes(int world) {
+  switch (world) {
+    case 2: return (size_t)b5x::Lay<2>::BYTES;
+    case 4: return (size_t)b5x::Lay<4>::BYTES;
+    case 8: return (size_t)b5x::Lay<8>::BYTES;
+    default: return 0;
+  }
+}
+
+template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true, int XW = 1>
 static void b5_launch(size_t bytes, hipStream_t st, const MlpShape& sh, const MlpArgs& a) {
-  static const hipError_t attr = hipFuncSetAttribute((const void*)mlp_block5_kernel<WD, LK, PROF, DXM, ADAM>,
+  static const hipError_t attr = hipFuncSetAttribute((const void*)mlp_block5_kernel<WD, LK, PROF, DXM, ADAM, XW>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   (void)attr;
-  hipLaunchKernelGGL((mlp_block5_kernel<WD, LK, PROF, DXM, ADAM>), dim3(1), dim3(blk5::NT), bytes, st, sh, a);
+  hipLaunchKernelGGL((mlp_block5_kernel<WD, LK, PROF, DXM, ADAM, XW>), dim3(1), dim3(blk5::NT), bytes, st, sh, a);
+}
+
+template <int XW>
+static void b5_launch_xg(size_t bytes, hipStream_t st, const MlpShape& sh, const MlpArgs& a) {
+  const bool wd = a.wd != 0.f;
+  if (a.loss_kind == 0) {
+    if (wd) b5_launch<true, 0, false, true, true, XW>(bytes, st, sh, a);
+    else b5_launch<false, 0, false, true, true, XW>(bytes, st, sh, a);
+  } else {
+    if (wd) b5_launch<true, 1, false, true, true, XW>(bytes, st, sh, a);
+    else b5_launch<false, 1, false, true, true, XW>(bytes, st, sh, a);
+  }
 }
 
 hipError_t mlp_launch_block5(const MlpShape& sh, const MlpArgs& a, hipStream_t st) {
   const size_t bytes = (size_t)blk5::LDS_FLOATS * sizeof(float);
   const bool wd = a.wd != 0.f;
-  const char* pe = getenv("DCT_B3_PRIO");
-  MlpArgs a2 = a;
-  a2.tune = pe ? atoi(pe) : a.tune;
-  // DCT_B5_DXM=0: the dZ1 product on the VALU (4 reduce-scatter passes) instead of the MFMA (A/B)
-  const char* de = getenv("DCT_B5_DXM");
-  const bool dxm = !(de && de[0] == '0');
-  if (a.mode == 1) {  // grad mode: no Adam, no moments
-    if (a.loss_kind == 0) b5_launch<false, 0, false, true, false>(bytes, st, sh, a2);
-    else b5_launch<false, 1, false, true, false>(bytes, st, sh, a2);
-  } else if (a.prof && a.loss_kind == 0) {
-    if (dxm) b5_launch<true, 0, true, true>(bytes, st, sh, a2);
-    else b5_launch<true, 0, true, false>(bytes, st, sh, a2);
-  } else if (a.prof) {
-    b5_launch<true, 1, true>(bytes, st, sh, a2);
-  } else if (!dxm && a.loss_kind == 0 && !wd) {
-    b5_launch<false, 0, false, false>(bytes, st, sh, a2);
+  if (a.xg_world > 1) {
+    if (a.xg_world == 2) b5_launch_xg<2>(bytes, st, sh, a);
+    else if (a.xg_world == 4) b5_launch_xg<4>(bytes, st, sh, a);
+    else b5_launch_xg<8>(bytes, st, sh, a);
+  } else if (a.mode == 1) {  // grad mode: no Adam, no moments
+    if (a.loss_kind == 0) b5_launch<false, 0, false, true, false>(bytes, st, sh, a);
+    else b5_launch<false, 1, false, true, false>(bytes, st, sh, a);
+  } else if (a.prof) {  // per-phase cycle stamps (tools/prof_block.py)
+    if (a.loss_kind == 0) b5_launch<true, 0, true>(bytes, st, sh, a);
+    else b5_launch<true, 1, true>(bytes, st, sh, a);
   } else if (a.loss_kind == 0) {
-    if (wd) b5_launch<true, 0>(bytes, st, sh, a2);
-    else b5_launch<false, 0>(bytes, st, sh, a2);
+    if (wd) b5_launch<true, 0>(bytes, st, sh, a);
+    else b5_launch<false, 0>(bytes, st, sh, a);
   } else {
-    if (wd) b5_launch<true, 1>(bytes, st, sh, a2);
-    else b5_launch<false, 1>(bytes, st, sh, a2);
+    if (wd) b5_launch<true, 1>(bytes, st, sh, a);
+    else b5_launch<false, 1>(bytes, st, sh, a);
   }
   return hipGetLastError();
 }

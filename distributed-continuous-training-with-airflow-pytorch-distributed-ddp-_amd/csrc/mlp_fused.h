@@ -128,6 +128,10 @@ hipError_t mlp_launch_block4(const MlpShape& sh, const MlpArgs& a, hipStream_t s
 // (mlp_block5.hip, the default there); DCT_MLP_BLOCK=3 selects mlp_block3
 bool mlp_block5_ok(const MlpShape& sh, const MlpArgs& a);
 hipError_t mlp_launch_block5(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
+// its shape (D0 <= 8 -> 128 -> 128 -> 2, batch <= 4) and the exchange buffer of its in-kernel
+// data-parallel launches at `world` = 2 / 4 / 8 ranks (0: not supported)
+bool mlp_block5_shape_ok(const int* dims, int L, int B);
+size_t mlp_block5_xg_bytes(int world);
 hipError_t mlp_launch_eval_L2(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
 hipError_t mlp_launch_eval_L3(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);
 hipError_t mlp_launch_eval_L4(const MlpShape& sh, const MlpArgs& a, int grid, hipStream_t st);

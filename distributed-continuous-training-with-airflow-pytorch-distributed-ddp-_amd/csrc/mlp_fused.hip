@@ -146,6 +146,10 @@ int dct_mlp_train(const void* shape, const MlpArgs* a, void* stream) {
     b.stage = nullptr;
     return dct_mlp_train(shape, &b, stream);
   }
+  if (a->xg_world > 1) {  // in-kernel data parallelism: only the 3x128 block kernel has it here
+    if (!dct::mlp_block5_ok(sh, *a)) return (int)hipErrorInvalidValue;
+    return (int)dct::mlp_launch_block5(sh, *a, st);
+  }
   if (dct::mlp_block4_ok(sh, *a)) return (int)dct::mlp_launch_block4(sh, *a, st);
   if (dct::mlp_block5_ok(sh, *a)) return (int)dct::mlp_launch_block5(sh, *a, st);
   if (dct::mlp_block3_ok(sh, *a)) return (int)dct::mlp_launch_block3(sh, *a, st);

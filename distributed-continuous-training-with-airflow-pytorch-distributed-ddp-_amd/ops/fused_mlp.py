@@ -130,9 +130,10 @@ class FusedMLPKernel:
             raise ValueError("loss_out must be cuda fp32 [steps]")
         xg_args = {}
         if xg is not None and xg.world > 1:
-            if mode != 0 or cursor is not None or pending is not None or not self.xg_supported(batch):
-                raise ValueError("in-kernel all-reduce needs train mode on the single-wave 2-layer kernel")
-            need = 2 * xg.world * self.xg_slab_granules() * 8
+            if mode != 0 or cursor is not None or pending is not None or not self.xg_supported(batch, xg.world):
+                raise ValueError("in-kernel all-reduce needs train mode on the single-wave 2-layer kernel or the "
+                                 "3x128 block kernel (2 / 4 / 8 ranks)")
+            need = self.xg_buffer_bytes(xg.world, batch)
             if xg.bytes < need:
                 raise ValueError(f"exchange buffer too small ({xg.bytes} < {need} bytes)")
             xg_args = dict(xg_recv=xg.recv, xg_peers=xg.peers, xg_world=xg.world, xg_rank=xg.rank,
@@ -171,9 +172,10 @@ class FusedMLPKernel:
             raise ValueError("loss_out must be contiguous cuda fp32")
         xg_args = {}
         if xg is not None and xg.world > 1:
-            if not self.xg_supported(batch):
-                raise ValueError("in-kernel all-reduce needs the single-wave 2-layer kernel")
-            need = 2 * xg.world * self.xg_slab_granules() * 8
+            if not self.xg_supported(batch, xg.world):
+                raise ValueError("in-kernel all-reduce needs the single-wave 2-layer kernel or the 3x128 block "
+                                 "kernel (2 / 4 / 8 ranks)")
+            need = self.xg_buffer_bytes(xg.world, batch)
             if xg.bytes < need:
                 raise ValueError(f"exchange buffer too small ({xg.bytes} < {need} bytes)")
             xg_args = dict(xg_recv=xg.recv, xg_peers=xg.peers, xg_world=xg.world, xg_rank=xg.rank,
@@ -195,12 +197,24 @@ class FusedMLPKernel:
         """8-byte granules per (parity, source rank) slab of the exchange buffer (0 = unsupported)."""
         return int(native().mlp_xg_slab_granules(list(self.dims)))
 
-    def xg_supported(self, batch: int) -> bool:
-        return (len(self.dims) == 3 and self.plan.use_wave and self.xg_slab_granules() > 0
-                and 1 <= batch <= min(self.bmax, 8))
+    def xg_supported(self, batch: int, world: Optional[int] = None) -> bool:
+        """True when training launches can average gradients INSIDE the kernel: the single-wave
+        kernel's 2-layer nets (any 2..8 ranks), or the 3x128 block kernel (csrc/mlp_block5.hip:
+        reduce-scatter + all-gather with sharded Adam, 2 / 4 / 8 ranks; ``world=None`` asks whether
+        some world size qualifies)."""
+        if len(self.dims) == 3 and self.plan.use_wave and self.xg_slab_granules() > 0:
+            return 1 <= batch <= min(self.bmax, 8)
+        return self._block5_bytes(batch, world if world is not None else 2) > 0
 
-    def xg_buffer_bytes(self, world: int) -> int:
-        return 2 * world * self.xg_slab_granules() * 8
+    def _block5_bytes(self, batch: int, world: int) -> int:
+        if self.plan.use_wave or len(self.dims) != 4 or batch > self.bmax:
+            return 0
+        return int(native().mlp_block5_xg_bytes(list(self.dims), int(batch), int(world)))
+
+    def xg_buffer_bytes(self, world: int, batch: int = 4) -> int:
+        if self.plan.use_wave:
+            return 2 * world * self.xg_slab_granules() * 8
+        return self._block5_bytes(batch, world)
 
     def evaluate(self, p, X, Y, idx, n_items: int, acc_out: torch.Tensor, loss: str = "ce",
                  logits_out: Optional[torch.Tensor] = None, grid: Optional[int] = None,

@@ -41,6 +41,17 @@ def timeout_s() -> float:
     return float(os.environ.get("DCT_XG_TIMEOUT_S", "20"))
 
 
+def inkernel_enabled() -> bool:
+    """DCT_XG_INKERNEL=0 keeps the persistent launches out of the exchange (the per-step paths -
+    peer all-reduce + Adam kernel or RCCL - take over); default on."""
+    return os.environ.get("DCT_XG_INKERNEL", "1") != "0"
+
+
+def probe_timeout_s() -> float:
+    """Spin limit of the first exchange launch of a run (trainer/engines.py _probe_exchange)."""
+    return float(os.environ.get("DCT_XG_PROBE_TIMEOUT_S", "3"))
+
+
 def peer_report(ctx: DistContext):
     """Collective: which physical GPU every rank drives and whether they can map each other.
 
@@ -76,8 +87,9 @@ def setup_peer_exchange(kernel, ctx: DistContext, batch: int):
 
     Before any buffer is exported every rank checks ``hipDeviceCanAccessPeer`` towards every
     other rank's device (:func:`peer_report`); one failing pair sends all ranks to RCCL."""
-    return _open_exchange(ctx, kernel.xg_supported(batch), lambda: kernel.xg_buffer_bytes(ctx.world_size),
-                          f"dims {kernel.dims}, batch {batch}", strict=True)
+    return _open_exchange(ctx, kernel.xg_supported(batch, ctx.world_size),
+                          lambda: kernel.xg_buffer_bytes(ctx.world_size, batch), f"dims {kernel.dims}, batch {batch}",
+                          strict=True)
 
 
 def setup_grad_exchange(ctx: DistContext, n: int):

@@ -129,15 +129,26 @@ class FusedMLPEngine(_EngineBase):
             self._broadcast_params()
         self.xg = None  # in-kernel xGMI all-reduce (parallel/xgmi.py)
         self.gx = None  # DDP step path: fused peer all-reduce + Adam kernel over xGMI (csrc/xg_adam.hip)
+        self._xg_probed = False
         if ctx.is_distributed:
+            from ..parallel.xgmi import inkernel_enabled
+            from ..parallel.xgmi import mode as xg_mode
             from ..parallel.xgmi import setup_grad_exchange, setup_peer_exchange, timeout_s
 
-            self.xg = setup_peer_exchange(self.kernel, ctx, self.B)
+            # the persistent launch averages gradients itself when its kernel can (5-64-2 single-wave
+            # kernel; the 3x128 block kernel at 2 / 4 / 8 ranks) - the same answer on every rank, so
+            # the collective setup below is entered by all or none
+            if (self.kernel.xg_supported(self.B, ctx.world_size) and ctx.device.type == "cuda"
+                    and inkernel_enabled()):
+                self.xg = setup_peer_exchange(self.kernel, ctx, self.B)
             self.xg_timeout_s = timeout_s()
             # exchange time of the launches (s_memrealtime ticks, 100 MHz) -> allreduce_ms per epoch
             self.xg_ticks = torch.zeros(1, dtype=torch.int64, device=dev) if self.xg is not None else None
             if self.xg is None and not self.fused_update:
                 self.gx = setup_grad_exchange(ctx, self.P + 1)
+            if xg_mode() == "xgmi" and self.xg is None and self.gx is None:
+                raise RuntimeError("DCT_ALLREDUCE=xgmi but neither the in-kernel exchange nor the peer "
+                                   "all-reduce + Adam kernel is available for this model / world size")
             if self.xg is None and self.gx is None and self.comm is None:
                 raise RuntimeError("distributed fused engine needs RCCL (backend nccl) or the in-kernel "
                                    "xGMI exchange; neither is available")
@@ -404,10 +415,14 @@ class FusedMLPEngine(_EngineBase):
         loss_out = getattr(self, "_loss_buf", None)
         if loss_out is None or loss_out.numel() < steps:
             self._loss_buf = loss_out = torch.zeros(max(1, steps), dtype=torch.float32, device=self.device)
+        first = 0
         if self.xg is not None or self.gx is not None:
             torch.cuda.synchronize(self.device)
             self.ctx.barrier()  # start the epoch's kernels together (the exchange spins are bounded)
-        self.run_steps(n_items, steps, loss_out[:steps])
+            if not self._xg_probed:
+                first = self._probe_exchange(n_items, steps, loss_out[:steps])
+        if first < steps:
+            self.run_steps(n_items, steps - first, loss_out[:steps], first_step=first)
         check_device("fused epoch")
         if self.gx is not None:
             self.xg_verify(fallback=False)
@@ -419,7 +434,36 @@ class FusedMLPEngine(_EngineBase):
         self.global_step += steps
         return loss_out[:steps]
 
-    def xg_verify(self, fallback: bool) -> bool:
+    def _probe_exchange(self, n_items: int, steps: int, loss_out: torch.Tensor) -> int:
+        """First steps of a run through the peer exchange with a SHORT spin limit, then a
+        collective check: if some rank cannot see its peers' writes (xGMI mapping, IPC mode), the
+        job pays seconds, not the full timeout per launch, and continues on RCCL with every rank
+        re-synced from rank 0.  Returns the steps of this epoch already applied."""
+        from ..parallel.xgmi import probe_timeout_s
+
+        self._xg_probed = True
+        k = min(steps, int(os.environ.get("DCT_XG_PROBE_STEPS", "4")))
+        # a timed-out exchange may leave a step half applied (xg_adam: per block): every rank keeps
+        # its pre-probe state to return to - replicas were identical before the probe
+        snap = [t.clone() for t in (self.p, self.m, self.v, self.step_counter)]
+        a = self.adam
+        if self.xg is not None:
+            self.kernel.train(self.p, self.m, self.v, self.X, self.Y, self.idx, n_items=n_items, batch=self.B,
+                              steps=k, t0=0, lr=a["lr"], betas=a["betas"], eps=a["eps"],
+                              weight_decay=a["weight_decay"], dropout=self.dropout, seed=self.rank_seed,
+                              loss_out=loss_out, loss=self.loss, step_counter=self.step_counter, xg=self.xg,
+                              xg_timeout_s=probe_timeout_s())
+        else:
+            full, self.xg_timeout_s = self.xg_timeout_s, probe_timeout_s()
+            try:
+                self.run_steps(n_items, k, loss_out, first_step=0)
+            finally:
+                self.xg_timeout_s = full
+        if self.xg_verify(fallback=True, snapshot=snap):
+            return k
+        return 0  # every rank is back at its pre-probe state: the epoch runs whole on RCCL
+
+    def xg_verify(self, fallback: bool, snapshot=None) -> bool:
         """Collective check of the in-kernel exchange.  On a timeout either raise (training: the
         steps of that launch are incomplete) or, with ``fallback``, re-sync every rank from rank 0
         and continue on the RCCL step path (benchmarks)."""
@@ -436,7 +480,7 @@ class FusedMLPEngine(_EngineBase):
             raise RuntimeError(msg)
         if self.ctx.rank == 0:
             print(f"[dct] {msg}; re-syncing from rank 0 and falling back to RCCL", flush=True)
-        self.xg_disable()
+        self.xg_disable(snapshot)
         return False
 
     def device_barrier(self) -> bool:
@@ -450,8 +494,10 @@ class FusedMLPEngine(_EngineBase):
         device_barrier(x, torch.cuda.current_stream(self.device).cuda_stream, self.xg_timeout_s)
         return True
 
-    def xg_disable(self):
-        """Leave the in-kernel exchange: replicas re-synced from rank 0, RCCL step path from now on."""
+    def xg_disable(self, snapshot=None):
+        """Leave the in-kernel exchange: replicas re-synced from rank 0, RCCL step path from now on.
+        ``snapshot`` (p, m, v, step_counter taken while the replicas were in sync) is restored on
+        every rank first, so no half-applied step of a timed-out exchange survives."""
         self.xg = None
         self.gx = None
         self._bound = None
@@ -459,6 +505,9 @@ class FusedMLPEngine(_EngineBase):
         if self.comm is None:
             raise RuntimeError("in-kernel exchange disabled and no RCCL communicator is available to fall back to")
         torch.cuda.synchronize(self.device)
+        if snapshot is not None:
+            for t, sv in zip((self.p, self.m, self.v, self.step_counter), snapshot):
+                t.copy_(sv)
         for t in (self.p, self.m, self.v, self.step_counter):
             self.ctx.broadcast_(t, src=0)
         torch.cuda.synchronize(self.device)

@@ -19,6 +19,11 @@ from dct_amd.trainer.engines import FusedMLPEngine, adam_hparams_from  # noqa: E
 
 def main():
     out_path, steps, B = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    # "step": the DDP step path (grad kernel + peer all-reduce/Adam kernel); "inkernel": the
+    # persistent 3x128 launch with its own reduce-scatter / all-gather (csrc/mlp_block5.hip)
+    path = sys.argv[4] if len(sys.argv) > 4 else "step"
+    if path == "step":
+        os.environ["DCT_XG_INKERNEL"] = "0"
     os.environ.setdefault("DCT_GRAPH_CHUNK", "16")
     ctx = init_distributed("gpu", backend="gloo")
     X, Y = weather_tensors(3000, seed=1)
@@ -36,9 +41,10 @@ def main():
     eng.run_steps(n, steps - first, loss, first_step=first)
     torch.cuda.synchronize()
     st = eng.xg_verify(fallback=False)
-    res = {"mode": eng.step_mode, "gx": eng.gx is not None, "graph_used": eng.graph_used, "ok": st,
-           "step_counter": int(eng.step_counter.item()), "params": eng.p.cpu().tolist(),
-           "m": eng.m.cpu().tolist(), "losses": loss.cpu().tolist(), "rows": local.tolist()}
+    res = {"mode": eng.step_mode, "gx": eng.gx is not None, "xg": eng.xg is not None, "graph_used": eng.graph_used,
+           "ok": st, "step_counter": int(eng.step_counter.item()), "params": eng.p.cpu().tolist(),
+           "m": eng.m.cpu().tolist(), "v": eng.v.cpu().tolist(), "losses": loss.cpu().tolist(),
+           "rows": local.tolist()}
     allres = ctx.all_gather_object(res)
     if ctx.rank == 0:
         with open(out_path, "w") as f:

@@ -271,3 +271,50 @@ def test_end_to_end_etl_train_rollout_local(tmp_path, monkeypatch):
     client = dags_mod._FAKE_CLIENT
     assert client.online_endpoints.get("weather-ep").traffic == {"blue": 100}
     assert {"model.ckpt", "score.py", "conda.yaml", "norm_stats.json"} <= set(os.listdir(tmp_path / "deploy"))
+
+
+def test_train_3x128_package_and_serve(tmp_path, monkeypatch):
+    """serve what you train.  jobs/train_ddp.py trains BASELINE's weather-mlp-3x128
+    (5-128-128-2) for one epoch on CPU into an MLflow file store; prepare_package derives the
+    architecture from the best checkpoint (not the reference's one hidden layer), and score.py's
+    init()/run() serve it: probabilities [n, 2] equal to the trained model's softmax.  The
+    reference 5-64-2 package keeps working (test above)."""
+    import subprocess
+    import sys
+
+    from dct_amd.ckpt.lightning_io import load_checkpoint
+    from dct_amd.models.mlp import build_mlp
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    uri = "file://" + str(tmp_path / "mlruns")
+    r = subprocess.run([sys.executable, os.path.join(root, "jobs", "train_ddp.py"), "--model", "weather-mlp-3x128",
+                        "--epochs", "1", "--synthetic-rows", "400", "--accelerator", "cpu",
+                        "--model-dir", str(tmp_path / "models"), "--tracking-uri", uri],
+                       capture_output=True, text=True, timeout=600, env=dict(os.environ, WORLD_SIZE="1"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    d = tmp_path / "deploy"
+    info = prepare_package(str(d), tracking_uri=uri)
+    ck = load_checkpoint(info["checkpoint"])
+    assert ck["state_dict"]["net.3.weight"].shape == (128, 128) and ck["state_dict"]["net.6.weight"].shape == (2, 128)
+    model = build_mlp("weather-mlp-3x128", 5)
+    model.load_state_dict(ck["state_dict"])
+    model.eval()
+    score = _load_score(d, monkeypatch)
+    score.init()
+    x = torch.randn(7, 5).tolist()
+    out = score.run(json.dumps({"data": x}))
+    probs = torch.tensor(out["probabilities"])
+    assert probs.shape == (7, 2)
+    assert torch.allclose(probs, torch.softmax(model(torch.tensor(x)), dim=1), atol=1e-6)
+    assert "error" in score.run(json.dumps({"data": [[1.0, 2.0]]}))
+
+
+def test_mlp_architecture_from_state_dict():
+    from dct_amd.deploy.package import mlp_architecture
+    from dct_amd.models.mlp import WeatherClassifier, build_mlp
+
+    assert mlp_architecture(WeatherClassifier(5).state_dict()) == {"input_dim": 5, "hidden": [64], "classes": 2}
+    assert mlp_architecture(build_mlp("tabular-mlp-4x1024", 256).state_dict()) == {
+        "input_dim": 256, "hidden": [1024, 1024, 1024], "classes": 2}
+    with pytest.raises(ValueError):
+        mlp_architecture({"blocks.0.weight": torch.zeros(2, 2)})

@@ -1,0 +1,202 @@
+"""In-kernel data parallelism of the BASELINE 3x128 weather trainer (csrc/mlp_block5.hip, b5x):
+each step's gradients are reduce-scattered to their owner rank, which applies Adam to its shard
+and all-gathers the new parameters, inside the persistent launch (one launch per rank per epoch).
+
+Reference semantics: DDP averages every rank's gradients before an identical Adam step on each
+rank (jobs/train_lightning_ddp.py:136) and ``sync_dist`` logs the mean loss (:70).
+Checked against a plain-torch fp32 emulation of W ranks (sum of per-rank grads / W, torch Adam):
+parameters, the Adam moments (all-gathered at every launch end, so every rank holds the full
+optimizer state) and the synced losses; replicas must be bit-identical."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import dct_amd  # noqa: F401
+from dct_amd.data.sampler import distributed_indices
+from dct_amd.data.synthetic import weather_tensors
+from dct_amd.ops._native import native
+from dct_amd.ops.fused_mlp import FusedMLPKernel
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DIMS = [5, 128, 128, 2]
+
+
+def _net(seed=0):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Linear(5, 128), torch.nn.ReLU(), torch.nn.Linear(128, 128), torch.nn.ReLU(),
+                               torch.nn.Linear(128, 2))
+
+
+def _flat(ts):
+    return torch.cat([t.detach().reshape(-1) for t in ts])
+
+
+def ddp_reference(net, X, Y, shards, B, steps, lr=0.01):
+    """W-rank DDP emulation: per-rank CE grads summed / W, one torch Adam step; returns the flat
+    parameters, exp_avg, exp_avg_sq and the per-step mean losses."""
+    params = list(net.parameters())
+    opt = torch.optim.Adam(params, lr=lr)
+    losses = []
+    for s in range(steps):
+        gsum = [torch.zeros_like(p) for p in params]
+        lsum = 0.0
+        for sh in shards:
+            rows = sh[s * B:(s + 1) * B]
+            loss = F.cross_entropy(net(X[rows]), Y[rows])
+            for a, g in zip(gsum, torch.autograd.grad(loss, params)):
+                a += g
+            lsum += loss.item()
+        for p, g in zip(params, gsum):
+            p.grad = g / len(shards)
+        opt.step()
+        losses.append(lsum / len(shards))
+    st = [opt.state[p] for p in params]
+    return (_flat(params), _flat([s["exp_avg"] for s in st]), _flat([s["exp_avg_sq"] for s in st]),
+            torch.tensor(losses))
+
+
+def _in_process_run(W, steps, split, B, out_path):
+    """W 'ranks' as concurrent persistent launches on W streams of one GPU (peers = raw pointers);
+    the steps run as two launches per rank, so the launch-end moment all-gather feeds the second
+    launch's prologue."""
+    nat = native()
+    cuda = torch.device("cuda", 0)
+    kern = FusedMLPKernel(DIMS, bmax=4)
+    assert not kern.plan.use_wave and kern.xg_supported(B, W)
+    xs = [nat.PeerExchange(W, r, kern.xg_buffer_bytes(W, B)) for r in range(W)]
+    for x in xs:
+        x.set_peers([y.recv for y in xs])
+    X, Y = weather_tensors(3000, seed=5)
+    shards = [distributed_indices(3000, W, r, shuffle=True, seed=42, epoch=0) for r in range(W)]
+    p0 = _flat(_net(1).state_dict().values())
+    ps = [p0.clone().to(cuda) for _ in range(W)]
+    ms = [torch.zeros_like(ps[0]) for _ in range(W)]
+    vs = [torch.zeros_like(ps[0]) for _ in range(W)]
+    losses = [torch.zeros(steps, device=cuda) for _ in range(W)]
+    scs = [torch.zeros(1, dtype=torch.int32, device=cuda) for _ in range(W)]
+    Xd, Yd = X.to(cuda), Y.to(cuda, torch.int32)
+    idx = [s.to(cuda, torch.int32) for s in shards]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(cuda) for _ in range(W)]
+    for first, k in ((0, split), (split, steps - split)):
+        for r in range(W):
+            kern.train(ps[r], ms[r], vs[r], Xd, Yd, idx[r][first * B:], n_items=idx[r].numel() - first * B, batch=B,
+                       steps=k, t0=0, lr=0.01, loss_out=losses[r][first:], step_counter=scs[r], xg=xs[r],
+                       xg_timeout_s=5.0, stream=streams[r].cuda_stream)
+    torch.cuda.synchronize()
+    json.dump({"status": [x.read_status() for x in xs], "steps": [int(sc.item()) for sc in scs],
+               "params": [p.cpu().tolist() for p in ps], "m": [m.cpu().tolist() for m in ms],
+               "v": [v.cpu().tolist() for v in vs], "losses": [l.cpu().tolist() for l in losses]},
+              open(out_path, "w"))
+
+
+def _check_vs_reference(res, W, steps, B, seed_net, X, Y, shards):
+    ps = [torch.tensor(p) for p in res["params"]]
+    for r in range(1, W):  # one writer per parameter: replicas bit-identical, optimizer state too
+        assert torch.equal(ps[r], ps[0])
+        assert res["m"][r] == res["m"][0] and res["v"][r] == res["v"][0]
+        assert res["losses"][r] == res["losses"][0]
+    want, want_m, want_v, want_l = ddp_reference(_net(seed_net), X, Y, shards, B, steps)
+    err = (ps[0] - want).abs()
+    assert err.median() < 2e-5 and err.max() < 3e-3, (err.median(), err.max())
+    em = (torch.tensor(res["m"][0]) - want_m).abs()
+    ev = (torch.tensor(res["v"][0]) - want_v).abs()
+    # (trajectories of 60 fp32 steps part by ~1e-3 at most: relative to the moments' scale)
+    assert em.max() < 1e-2 * want_m.abs().max() and ev.max() < 1e-2 * want_v.abs().max(), (em.max(), ev.max())
+    got_v = torch.tensor(res["v"][0])
+    assert (got_v[want_v > 1e-12] > 0).all()  # no shard's moments missing after the all-gather
+    assert torch.allclose(torch.tensor(res["losses"][0]), want_l, atol=2e-4, rtol=1e-3)
+
+
+@pytest.mark.parametrize("W", [2])
+def test_in_process_block5_exchange_matches_ddp_reference(tmp_path, W, cuda):
+    """Fresh process: streams of one process share GPU_MAX_HW_QUEUES (4) hardware queues round-
+    robin, so more 'ranks' than that could land on one queue and serialise; W > 2 runs as separate
+    processes below."""
+    B, steps, split = 4, 60, 23
+    out = tmp_path / "b5x.json"
+    code = (f"import sys; sys.path.insert(0, {ROOT!r}); sys.path.insert(0, {os.path.join(ROOT, 'tests')!r}); "
+            f"import test_xg_block5_gpu as t; t._in_process_run({W}, {steps}, {split}, {B}, {str(out)!r})")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    res = json.loads(out.read_text())
+    assert res["status"] == [0] * W and res["steps"] == [steps] * W
+    X, Y = weather_tensors(3000, seed=5)
+    shards = [distributed_indices(3000, W, r_, shuffle=True, seed=42, epoch=0) for r_ in range(W)]
+    _check_vs_reference(res, W, steps, B, 1, X, Y, shards)
+
+
+def test_block5_exchange_timeout_leaves_state_untouched(cuda):
+    """A rank whose peer never runs gives up after the spin limit, records the tag of its first
+    step, leaves the step counter alone and writes NOTHING back: HBM keeps the launch's starting
+    parameters and moments (the engine then re-syncs or raises)."""
+    nat = native()
+    kern = FusedMLPKernel(DIMS, bmax=4)
+    xs = [nat.PeerExchange(2, r, kern.xg_buffer_bytes(2, 4)) for r in range(2)]
+    for x in xs:
+        x.set_peers([y.recv for y in xs])
+    X, Y = weather_tensors(500, seed=0)
+    p = _flat(_net().state_dict().values()).to(cuda)
+    m = torch.full_like(p, 1e-3)
+    v = torch.full_like(p, 1e-6)
+    p0, m0, v0 = p.clone(), m.clone(), v.clone()
+    sc = torch.full((1,), 7, dtype=torch.int32, device=cuda)
+    idx = torch.arange(400, dtype=torch.int32, device=cuda)
+    kern.train(p, m, v, X.to(cuda), Y.to(cuda, torch.int32), idx, n_items=400, batch=4, steps=20, t0=0, lr=0.01,
+               step_counter=sc, xg=xs[0], xg_timeout_s=0.2)
+    torch.cuda.synchronize()
+    assert xs[0].read_status() == 8  # tag = global step + 1 of the first step (counter 7)
+    assert int(sc.item()) == 7
+    assert torch.equal(p, p0) and torch.equal(m, m0) and torch.equal(v, v0)
+
+
+@pytest.mark.parametrize("W", [2, 4, 8])
+def test_engine_inkernel_exchange_3x128(W, tmp_path, cuda):
+    """FusedMLPEngine at world size W (processes sharing the GPU, IPC-mapped buffers, gloo control
+    plane): the 3x128 model trains in its persistent launch with the in-kernel reduce-scatter /
+    all-gather (no per-step launch), over two launches; replicas and optimizer states are
+    bit-identical and follow torch DDP + Adam."""
+    out = tmp_path / "b5.json"
+    steps, B = 45, 4
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={W}",
+                        "--master-addr=127.0.0.1", f"--master-port={29611 + W}",
+                        os.path.join(ROOT, "tests", "gx_worker.py"), str(out), str(steps), str(B), "inkernel"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    for q in range(W):
+        assert res[q]["xg"] and not res[q]["gx"] and res[q]["ok"], res[q]["mode"]
+        assert res[q]["mode"] == "fused-persistent+xgmi-inkernel-allreduce"
+        assert res[q]["step_counter"] == steps
+        assert res[q]["params"] == res[0]["params"] and res[q]["m"] == res[0]["m"] and res[q]["v"] == res[0]["v"]
+        assert res[q]["losses"] == res[0]["losses"]
+    from test_xg_adam_gpu import _ddp_reference
+
+    want, want_l = _ddp_reference(res, steps, B)
+    got = torch.tensor(res[0]["params"])
+    err = (got - want).abs()
+    assert err.median() < 2e-5 and err.max() < 3e-3, (err.median(), err.max())
+    assert torch.allclose(torch.tensor(res[0]["losses"]), want_l, atol=2e-4, rtol=1e-3)
+
+
+def test_trainer_3x128_two_ranks_one_gpu(tmp_path):
+    """The Trainer at W = 2 on one GPU picks the fused engine with the in-kernel exchange for the
+    3x128 model (first launch probed with a short spin limit), checkpoints on rank 0 only, and
+    trains the emulated DDP trajectory."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29691", os.path.join(ROOT, "tests", "ddp_worker.py"),
+           str(tmp_path), "2", "600", "gpu", "hidden=128,128"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    from test_multigpu import _check
+
+    info = _check(tmp_path, 2, 600, 2, (128, 128), 3e-3)
+    assert info["engine"] == "fused" and info["xg"] and not info["gx"]
