@@ -27,11 +27,11 @@ def target_path() -> str:
     return os.path.join(PKG_DIR, MODULE + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
-# per-source extra flags.  mlp_block2.hip: the SLP vectorizer packs the trainer's independent fp32
+# per-source extra flags.  The 3x128 trainers: the SLP vectorizer packs their independent fp32
 # FMAs into v_pk_fma_f32 plus the v_mov_b32 pairs that marshal their operands - on gfx950 a packed op
-# issues no faster than two plain ones, so the moves are pure overhead in an issue-bound kernel.
-FILE_FLAGS = {"mlp_block2.hip": ["-fno-slp-vectorize"], "mlp_block3.hip": ["-fno-slp-vectorize"], "mlp_block4.hip": ["-fno-slp-vectorize"],
-              "mlp_block5.hip": ["-fno-slp-vectorize"]}
+# issues no faster than two plain ones, so the moves are pure overhead in an issue-bound kernel
+# (mlp_block5 packs its Adam pairs by hand where packing pays).
+FILE_FLAGS = {"mlp_block3.hip": ["-fno-slp-vectorize"], "mlp_block5.hip": ["-fno-slp-vectorize"]}
 
 
 def _sources():

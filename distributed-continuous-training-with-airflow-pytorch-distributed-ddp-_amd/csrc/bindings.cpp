@@ -43,8 +43,8 @@ struct MlpPlan {
     if (dct_mlp_make_shape(shape.data(), dims.data(), (int)dims.size() - 1, bmax) != 0)
       throw std::invalid_argument("bad MLP shape");
     supported = dct_mlp_select(sh(), &nt, &maxblk);
-    const char* env = std::getenv("DCT_MLP_KERNEL");
-    const bool force_lds = env && std::string(env) == "lds";
+    dct::knobs_reload();  // plan time: the DCT_* knobs of this process's launches
+    const bool force_lds = dct::knobs().mlp_force_lds != 0;
     use_wave = (!force_lds && dct_mlp_wave_supported(dims.data(), (int)dims.size() - 1, 1)) ? 1 : 0;
     if (use_wave) supported = 1;
   }
@@ -160,6 +160,8 @@ PYBIND11_MODULE(_dct_native, m) {
     return std::string(p.gcnArchName);
   });
   m.def("synchronize", []() { check((int)hipDeviceSynchronize(), "hipDeviceSynchronize"); });
+  // re-read the DCT_* knobs (csrc/knobs.h) - plan / bind time only, never per launch
+  m.def("reload_knobs", []() { dct::knobs_reload(); });
   // PCI bus id of a device: identifies the physical GPU behind a rank (ranks sharing one GPU in a
   // rehearsal report the same id)
   m.def("pci_bus_id", [](int dev) {

@@ -1,6 +1,7 @@
 // Shared helpers for the dct HIP kernels (gfx950 only).
 #pragma once
 #include <hip/hip_runtime.h>
+#include "knobs.h"
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 

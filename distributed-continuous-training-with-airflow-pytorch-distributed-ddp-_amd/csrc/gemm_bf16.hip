@@ -26,6 +26,7 @@
 
 #include "dct_common.h"
 #include "kernels.h"
+#include "knobs.h"
 
 namespace dct {
 
@@ -520,8 +521,7 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
           const int row = m0 + wr * (BM / WM) + i * 16 + row_l + r;
           if (row < g.M) {
             float* dst = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
-            if (g.split_probe) *dst = acc[i][j][r] * g.alpha;
-            else atomicAdd(dst, acc[i][j][r] * g.alpha);
+            atomicAdd(dst, acc[i][j][r] * g.alpha);
           }
         }
       }
@@ -749,7 +749,7 @@ static hipError_t launch_gemm(const dct::GemmArgs& g, hipStream_t st) {
 }
 
 static bool gemm_v2_ok(const dct::GemmArgs& g, int ta, int tb) {
-  if (getenv("DCT_GEMM_V1")) return false;
+  if (dct::knobs().gemm_v1) return false;
   if (g.K % dct::GBK) return false;
   auto aligned = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   if (!aligned(g.A) || !aligned(g.B) || g.lda % 8 || g.ldb % 8) return false;
@@ -768,7 +768,7 @@ static size_t g_split_ws_bytes = 0;
 static int g_split_dev = -1;
 constexpr int SPLIT_CNT_N = 4096;
 static bool split_workspace(size_t bytes, int tiles, hipStream_t st, float** ws, int** cnt) {
-  if (!getenv("DCT_GEMM_SPLIT_WS") || tiles > SPLIT_CNT_N) return false;
+  if (!dct::knobs().gemm_split_ws || tiles > SPLIT_CNT_N) return false;
   int dev = -1;
   if (hipGetDevice(&dev) != hipSuccess) return false;
   if (g_split_ws && g_split_dev == dev && g_split_ws_bytes >= bytes) {
@@ -807,9 +807,9 @@ static float* g_part = nullptr;
 static size_t g_part_bytes = 0;
 static int g_part_dev = -1;
 static float* split_partials(size_t bytes, int max_splits, hipStream_t st) {
-  const char* f = getenv("DCT_GEMM_SPLIT_TWO_PASS");  // unset: auto; "1": always; "0": never
-  if (f && f[0] == '0') return nullptr;
-  if (!(f && f[0] == '1') && max_splits > 4) return nullptr;
+  const int tp = dct::knobs().gemm_two_pass;  // -1: auto; 1: always; 0: never
+  if (tp == 0) return nullptr;
+  if (tp != 1 && max_splits > 4) return nullptr;
   int dev = -1;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   if (g_part && g_part_dev == dev && g_part_bytes >= bytes) return g_part;
@@ -841,14 +841,14 @@ static int device_cus() {
 // CU's load path (~70 GB/s from L2), not the round-trip latency, bounds these one-tile-per-CU
 // grids - so 2 is the default and 4 stays selectable (DCT_GEMM_STAGES=4) for other shapes.
 static int gemm_stages(int grid, int nk_slice) {
-  if (const char* f = getenv("DCT_GEMM_STAGES")) return (atoi(f) >= 4 && nk_slice >= 3) ? 4 : 2;
+  if (dct::knobs().gemm_stages) return (dct::knobs().gemm_stages >= 4 && nk_slice >= 3) ? 4 : 2;
   (void)grid;
   return 2;
 }
 
 template <bool TA, bool TB>
 static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
-  g.split_probe = getenv("DCT_GEMM_SPLIT_PROBE") != nullptr;
+  const dct::Knobs& kn = dct::knobs();
   hipError_t e;
   const int tiles_n = (g.N + dct::GBN - 1) / dct::GBN;
   const int tiles = ((g.M + dct::GBM - 1) / dct::GBM) * tiles_n;
@@ -860,12 +860,12 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
     // workgroups to aim for: one per CU.  512 (two slices per CU) doubled the fp32 atomic traffic
     // for no extra bandwidth: 1024x1024x4096 dW 38 -> 28 us at 256 (profiles/gemm_pipeline_ab_r1.log)
     int target = device_cus();
-    if (const char* f = getenv("DCT_GEMM_SPLIT_WG")) target = std::max(1, atoi(f));
+    if (kn.gemm_split_wg) target = std::max(1, kn.gemm_split_wg);
     splits = std::min(nk / 8, (target + tiles - 1) / tiles);
-    if (const char* f = getenv("DCT_GEMM_SPLITS")) splits = std::min(nk, atoi(f));  // tuning override
+    if (kn.gemm_splits) splits = std::min(nk, kn.gemm_splits);  // tuning override
     if (splits < 1) splits = 1;
   }
-  if (splits > 1 && !g.split_probe) {
+  if (splits > 1) {
     const size_t bytes = (size_t)tiles * splits * dct::GBM * dct::GBN * sizeof(float);
     if (!split_workspace(bytes, tiles, st, &g.split_ws, &g.split_cnt)) g.split_ws = nullptr, g.split_cnt = nullptr;
     if (!g.split_ws) g.split_part = split_partials((size_t)splits * g.M * g.N * sizeof(float), splits, st);
@@ -889,17 +889,16 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
   };
   // DCT_GEMM_8W=1: one 128 x 128 tile per CU worked by 8 waves (two per SIMD) with three k-tiles in
   // flight (4 LDS stages, 128 KB) for grids of at most one tile per CU
-  const char* w8e = getenv("DCT_GEMM_8W");
-  if (w8e && w8e[0] == '1' && splits == 1 && tiles <= device_cus() && nk >= 4)
+  if (kn.gemm_8w && splits == 1 && tiles <= device_cus() && nk >= 4)
     return launch(dct::gemm2_kernel<TA, TB, false, 128, 4, 4>, tiles, 4, 512);
   if constexpr (!TA) {
     // small K and too few 128-row tiles to fill 256 CUs several times over: half-height tiles
-    const bool force128 = getenv("DCT_GEMM_BM128") != nullptr;
+    const bool force128 = kn.gemm_bm128 != 0;
     // ... and whenever 128-row tiles would give at most one workgroup per CU (the 4096 x 1024 MLP
     // layers: 256 tiles): two half-height tiles per CU overlap one's loads with the other's MFMAs,
     // 16.7 -> 14.5 us fwd / 17.4 -> 15.5 us dX at 4096x1024x1024, ahead of hipBLASLt (17.8 / 17.2;
     // profiles/gemm_bm64_ab_r1.log)
-    const int bm64_nk = getenv("DCT_GEMM_BM64_NK") ? atoi(getenv("DCT_GEMM_BM64_NK")) : 4;  // A/B knob
+    const int bm64_nk = kn.gemm_bm64_nk;  // A/B knob
     if (splits == 1 && (nk <= bm64_nk || tiles <= device_cus()) && tiles < 1024 && !force128)
       return launch(dct::gemm2_kernel<TA, TB, false, 64, 2>, ((g.M + 63) / 64) * tiles_n, 2);
   }
@@ -950,9 +949,9 @@ extern "C" int dct_gemm_dw_auto_splits(int M, int N, int K) {
   const int nk = K / dct::GBK;
   if (tiles >= 256 || nk < 8 || K % dct::GBK) return 1;
   int target = device_cus();
-  if (const char* f = getenv("DCT_GEMM_SPLIT_WG")) target = std::max(1, atoi(f));
+  if (dct::knobs().gemm_split_wg) target = std::max(1, dct::knobs().gemm_split_wg);
   int splits = std::min(nk / 8, (target + tiles - 1) / tiles);
-  if (const char* f = getenv("DCT_GEMM_SPLITS")) splits = std::min(nk, atoi(f));
+  if (dct::knobs().gemm_splits) splits = std::min(nk, dct::knobs().gemm_splits);
   return splits < 1 ? 1 : splits;
 }
 
@@ -996,7 +995,8 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   dct::GemmGroup gg{};
   gg.n = n;
-  bool grouped = getenv("DCT_GEMM_NO_GROUP") == nullptr;
+  const dct::Knobs& kn = dct::knobs();
+  bool grouped = !kn.gemm_no_group;
   int total = 0, max_slice = 1;
   for (int i = 0; i < n; ++i) {
     dct::GemmArgs& g = gg.g[i];
@@ -1007,7 +1007,6 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
     g.vec_b = ((((uintptr_t)X[i]) & 15) == 0) && (N[i] % 8 == 0);
     g.colsum = colsum ? colsum[i] : nullptr;
     g.residual = nullptr;
-    g.split_probe = getenv("DCT_GEMM_SPLIT_PROBE") != nullptr;  // timing probe only: plain stores, wrong sums
     const int tiles = ((g.M + dct::GBM - 1) / dct::GBM) * ((g.N + dct::GBN - 1) / dct::GBN);
     const int nk = g.K / dct::GBK;
     if (!gemm_v2_ok(g, 1, 0) || tiles >= 256 || nk < 8) { grouped = false; break; }
@@ -1018,9 +1017,9 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
   // of the fp32 atomics, four times the k-loop per slice): TabTransformer step 0.411 -> 0.368 ms
   // (profiles/tt_dw_mink_ab_r2.log).  DCT_GEMM_DW_MINK pins it.
   int target = device_cus();
-  if (const char* f = getenv("DCT_GEMM_SPLIT_WG")) target = std::max(1, atoi(f));
-  const char* mk_env = getenv("DCT_GEMM_DW_MINK");
-  int min_kt = mk_env ? std::max(2, atoi(mk_env)) : 8;
+  if (kn.gemm_split_wg) target = std::max(1, kn.gemm_split_wg);
+  const bool mk_env = kn.gemm_dw_mink > 0;
+  int min_kt = mk_env ? std::max(2, kn.gemm_dw_mink) : 8;
   for (;;) {
     total = 0;
     max_slice = 1;
@@ -1078,7 +1077,7 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
                          st, C[i], N[i], M[i], N[i]);
     }
   }
-  const bool s4 = getenv("DCT_GEMM_STAGES") && atoi(getenv("DCT_GEMM_STAGES")) >= 4 && max_slice >= 3;
+  const bool s4 = kn.gemm_stages >= 4 && max_slice >= 3;
   const size_t lds = (size_t)(max_slice > 1 ? (s4 ? 8 : 4) : 2) * dct::G2_BYTES;
   auto fn = s4 ? dct::gemm2_grouped_kernel<true, false, 4> : dct::gemm2_grouped_kernel<true, false, 2>;
   e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

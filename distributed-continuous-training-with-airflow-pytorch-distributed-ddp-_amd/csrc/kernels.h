@@ -1,6 +1,7 @@
 // C API of the general NN kernels (GEMM, loss, norm, attention, gather).
 #pragma once
 #include <stdint.h>
+#include "knobs.h"
 
 namespace dct {
 
@@ -22,7 +23,6 @@ struct GemmArgs {
   float alpha;
   float* colsum;  // optional: colsum[m] += sum_k op(A)[m][k] (the bias gradient of a dW GEMM)
   const float* residual;  // optional (fp32 out): C = residual + op(A) op(B) + bias, ld = ldc
-  int split_probe;        // debug timing probe: split-K slices plain-store (wrong result) instead of atomics
   float* split_ws;        // optional split-K workspace [tiles][splits][BM*GBN]: slices store partials, the
   int* split_cnt;         // last slice of a tile (split_cnt[tile] arrival counter) sums them in slice order
   float* split_part;      // optional two-pass split-K: slice s plain-stores its partial C into

@@ -565,9 +565,7 @@ __global__ __launch_bounds__(blk3::NT, 1) void mlp_block3_kernel(MlpShape sh, Ml
 #undef B3STAMP
 
 bool mlp_block3_ok(const MlpShape& sh, const MlpArgs& a) {
-  // DCT_MLP_BLOCK: "3" selects this kernel over mlp_block4.hip (A/B); "2": mlp_block2.hip, "0" / "v1": others
-  const char* env = getenv("DCT_MLP_BLOCK");
-  if (env && (env[0] == '0' || env[0] == '2' || (env[0] == 'v' && env[1] == '1'))) return false;
+  if (knobs().mlp_block == 0) return false;  // DCT_MLP_BLOCK=0: the generic LDS trainer
   // a profiling launch is served for the weather shape (D0 <= 8, C <= 2, train mode) only
   const bool prof_ok = a.prof == nullptr || (sh.dims[0] <= 8 && sh.dims[3] <= 2 && a.mode == 0);
   // 16-byte W1 row loads / stores
@@ -593,12 +591,10 @@ hipError_t mlp_launch_block3(const MlpShape& sh, const MlpArgs& a, hipStream_t s
   const size_t bytes = (size_t)blk3::LDS_FLOATS * sizeof(float);
   // weather shape (D0 <= 8, C <= 2): layer-1 forward and dW1 on the 4x4x1 fp32 MFMA (DCT_MLP_BLOCK_MF=0:
   // VALU); train mode without weight decay drops the L2 term from every Adam update
-  const char* mfe = getenv("DCT_MLP_BLOCK_MF");
-  const bool mf = !(mfe && mfe[0] == '0') && d0 <= 8 && C <= 2;
+  const bool mf = knobs().mlp_block_mf && d0 <= 8 && C <= 2;
   const bool wd = a.wd != 0.f;
-  const char* pe = getenv("DCT_B3_PRIO");
   MlpArgs a2 = a;
-  a2.tune = pe ? atoi(pe) : a.tune;
+  a2.tune = knobs().b3_prio >= 0 ? knobs().b3_prio : a.tune;
   if (a.prof) {
     if (mf) b3_launch<2, 2, true, true, true>(bytes, st, sh, a2);
     else b3_launch<2, 2, true, true>(bytes, st, sh, a2);

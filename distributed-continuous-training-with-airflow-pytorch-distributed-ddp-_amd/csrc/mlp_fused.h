@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "knobs.h"
+
 namespace dct {
 
 constexpr int MLP_MAXL = 4;
@@ -112,20 +114,13 @@ constexpr int XG_MAXW = 8;  // ranks of the in-kernel exchange (one node)
 hipError_t mlp_launch_train_L2(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
 hipError_t mlp_launch_train_L3(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
 hipError_t mlp_launch_train_L4(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
-// register-resident multi-wave kernel for D0 -> 128 -> 128 -> C (mlp_block.hip)
-bool mlp_block_ok(const MlpShape& sh, const MlpArgs& a);
-hipError_t mlp_launch_block(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
-// one-barrier successor of mlp_block (mlp_block2.hip); DCT_MLP_BLOCK=v1 selects the old one
-bool mlp_block2_ok(const MlpShape& sh, const MlpArgs& a);
-hipError_t mlp_launch_block2(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
-// two-barrier successor (mlp_block3.hip, the default); DCT_MLP_BLOCK=2 selects mlp_block2
+// register-resident 8-wave two-barrier trainer for D0 <= 32 -> 128 -> 128 -> C <= 4, train and
+// grad mode (mlp_block3.hip): every 3x128 shape mlp_block5 does not take
 bool mlp_block3_ok(const MlpShape& sh, const MlpArgs& a);
 hipError_t mlp_launch_block3(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
-// 16-wave variant (mlp_block4.hip, opt-in DCT_MLP_BLOCK=4)
-bool mlp_block4_ok(const MlpShape& sh, const MlpArgs& a);
-hipError_t mlp_launch_block4(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
-// lean two-barrier trainer for the exact weather shape D0<=8 -> 128 -> 128 -> 2, train mode
-// (mlp_block5.hip, the default there); DCT_MLP_BLOCK=3 selects mlp_block3
+// lean two-barrier trainer for the exact weather shape D0<=8 -> 128 -> 128 -> 2, train mode, the
+// one-step grad mode and the in-kernel data-parallel launches (mlp_block5.hip, the default there);
+// DCT_MLP_BLOCK=3 selects mlp_block3, DCT_MLP_BLOCK=0 the generic LDS trainer
 bool mlp_block5_ok(const MlpShape& sh, const MlpArgs& a);
 hipError_t mlp_launch_block5(const MlpShape& sh, const MlpArgs& a, hipStream_t st);
 // its shape (D0 <= 8 -> 128 -> 128 -> 2, batch <= 4) and the exchange buffer of its in-kernel

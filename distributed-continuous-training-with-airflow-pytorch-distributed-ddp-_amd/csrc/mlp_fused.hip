@@ -150,11 +150,9 @@ int dct_mlp_train(const void* shape, const MlpArgs* a, void* stream) {
     if (!dct::mlp_block5_ok(sh, *a)) return (int)hipErrorInvalidValue;
     return (int)dct::mlp_launch_block5(sh, *a, st);
   }
-  if (dct::mlp_block4_ok(sh, *a)) return (int)dct::mlp_launch_block4(sh, *a, st);
-  if (dct::mlp_block5_ok(sh, *a)) return (int)dct::mlp_launch_block5(sh, *a, st);
-  if (dct::mlp_block3_ok(sh, *a)) return (int)dct::mlp_launch_block3(sh, *a, st);
-  if (dct::mlp_block2_ok(sh, *a)) return (int)dct::mlp_launch_block2(sh, *a, st);
-  if (dct::mlp_block_ok(sh, *a)) return (int)dct::mlp_launch_block(sh, *a, st);
+  const int blk = dct::knobs().mlp_block;  // -1 auto, 3 mlp_block3, 0 the generic LDS trainer
+  if (blk < 0 && dct::mlp_block5_ok(sh, *a)) return (int)dct::mlp_launch_block5(sh, *a, st);
+  if (blk != 0 && dct::mlp_block3_ok(sh, *a)) return (int)dct::mlp_launch_block3(sh, *a, st);
   switch (sh.L) {
     case 2: return (int)dct::mlp_launch_train_L2(sh, *a, st);
     case 3: return (int)dct::mlp_launch_train_L3(sh, *a, st);

@@ -1353,10 +1353,7 @@ hipError_t launch_rows_d0(const WaveShape& sh, const MlpArgs& a, hipStream_t st)
 
 // the row-parallel kernel takes plain train-mode launches of 2-layer nets (DCT_MLP_ROWS=0: off)
 bool rows_eligible(int L, const MlpArgs& a) {
-  static const bool enabled = [] {
-    const char* e = std::getenv("DCT_MLP_ROWS");
-    return !(e && e[0] == '0');
-  }();
+  const bool enabled = dct::knobs().mlp_rows != 0;
 #ifdef DCT_WAVE_PROF
   const bool prof_ok = true;  // profiling build: the rows kernel stamps its phases into a.prof
 #else

@@ -113,6 +113,7 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
       param_bucket_(std::move(param_bucket)),
       dtype_(dtype),
       op_(op) {
+  dct::knobs_reload();  // bind time: DCT_REDUCER_INLINE
   const size_t nb = offsets_.size();
   if (counts_.size() != nb) throw std::runtime_error("bucket offsets/counts mismatch");
   expected_.assign(nb, 0);
@@ -126,8 +127,7 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
   // DCT_REDUCER_INLINE=1: collectives on the compute stream itself - no overlap with backward,
   // but no cross-stream edges either (each costs ~5-15 us inside a replayed HIP graph, measured
   // with the one-rank communicator: profiles/ddp_reducer_w1_r3.log)
-  const char* inl = getenv("DCT_REDUCER_INLINE");
-  inline_ = inl && inl[0] == '1';
+  inline_ = dct::knobs().reducer_inline != 0;
   ready_events_.resize(nb);
   for (auto& e : ready_events_) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
   hip_check(hipEventCreateWithFlags(&done_event_, hipEventDisableTiming), "hipEventCreate");
@@ -163,6 +163,9 @@ std::vector<double> BucketReducer::read_timing() const {
   std::vector<double> out(4, 0.0);
   if (!stamps_) return out;
   unsigned long long h[8];
+  // the close kernel of the last step runs on the non-blocking comm stream: a legacy-stream copy
+  // is not ordered after it
+  hip_check(hipStreamSynchronize(comm_stream_), "hipStreamSynchronize");
   hip_check(hipMemcpy(h, stamps_, sizeof(h), hipMemcpyDeviceToHost), "read reducer stamps");
   out[0] = (double)h[2] / 1e5;  // s_memrealtime ticks at 100 MHz -> ms
   out[1] = (double)h[3] / 1e5;

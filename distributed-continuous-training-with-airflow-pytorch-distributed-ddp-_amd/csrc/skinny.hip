@@ -440,8 +440,8 @@ int dct_skinny_head(const uint16_t* H, const uint16_t* W, const float* bias, con
   // that still gives >= 128 blocks; otherwise 4 waves x 4 rows
   const bool w8 = C <= 2 && K <= 1024;  // 8-wave blocks: LDS partials 8 x C x K fp32 <= 64 KB
   int nwv = (w8 && B >= 128 * 32) ? 8 : 4, rpw = 4;
-  if (const char* f = getenv("DCT_SKINNY_HEAD_RPW")) rpw = (atoi(f) == 8 && C <= 2) ? 8 : (atoi(f) == 2 ? 2 : 4);
-  if (const char* f = getenv("DCT_SKINNY_HEAD_WAVES")) nwv = (atoi(f) == 8 && w8) ? 8 : 4;  // debug / A-B
+  if (const int f = dct::knobs().skinny_head_rpw) rpw = (f == 8 && C <= 2) ? 8 : (f == 2 ? 2 : 4);
+  if (const int f = dct::knobs().skinny_head_waves) nwv = (f == 8 && w8) ? 8 : 4;  // debug / A-B
   if (nwv == 8 && rpw == 8) rpw = 4;  // 8-wave blocks come with 2 or 4 rows per wave (the grid must match)
   const dim3 grid((B + nwv * rpw - 1) / (nwv * rpw));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -481,7 +481,7 @@ int dct_skinny_dw(const uint16_t* dZ, const uint16_t* X, float* dW, float* db, i
   const int max_splits = (B + 63) / 64;
   splits = splits > max_splits ? max_splits : splits;
   splits = splits < 1 ? 1 : splits;
-  if (const char* f = getenv("DCT_SKINNY_DW_SPLITS")) splits = atoi(f) > 0 ? atoi(f) : splits;  // debug / A-B
+  if (dct::knobs().skinny_dw_splits > 0) splits = dct::knobs().skinny_dw_splits;  // debug / A-B
   const int rows_per = (B + splits - 1) / splits;
   const dim3 grid(kb, (B + rows_per - 1) / rows_per);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);

@@ -262,8 +262,7 @@ __global__ __launch_bounds__(64 * NW) void head_bwd_kernel(HeadArgs a) {
 // 0.4184-0.4221 ms, profiles/tt_head_spb_side_dw_ab_r2.log); DCT_TT_HEAD_SPB=16 selects them.
 static inline int head_spb(int B) {
   (void)B;
-  if (const char* f = getenv("DCT_TT_HEAD_SPB")) return atoi(f) == 16 ? 16 : 4;
-  return 4;
+  return knobs().tt_head_spb;
 }
 
 }  // namespace ttio

@@ -51,6 +51,12 @@ def native():
         ) from e
 
 
+def reload_knobs() -> None:
+    """Re-read the native launchers' DCT_* knobs (csrc/knobs.h).  Plan / bind time only: the
+    launch paths read the struct, never the environment."""
+    native().reload_knobs()
+
+
 def available() -> bool:
     try:
         native()

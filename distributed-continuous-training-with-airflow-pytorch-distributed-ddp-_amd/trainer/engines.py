@@ -29,6 +29,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from ..data.sampler import distributed_indices
+from ..ops._native import reload_knobs
 from ..ops.fused_mlp import FusedMLPKernel, mlp_num_params
 from ..ops.nn import bound_params, join_side_work
 from ..ops.optim import FlatAdam, adam_flat_
@@ -36,6 +37,7 @@ from ..parallel.dist import DistContext, init_native_comm
 from ..parallel.reducer import NativeBucketReducer, TorchBucketReducer, plan_buckets
 from ..utils.debug import assert_reducer_complete, check_device
 from ..utils.debug import enabled as debug_enabled
+from ..utils.debug import reducer_timing_enabled
 
 
 def adam_hparams_from(optimizer) -> Optional[Dict]:
@@ -60,6 +62,8 @@ class _EngineBase:
     name = "base"
 
     def __init__(self, model, ctx: DistContext, batch_size: int, seed: int):
+        if ctx.device.type == "cuda":
+            reload_knobs()  # bind time: the native launchers' DCT_* knobs
         self.model = model
         self.ctx = ctx
         self.B = int(batch_size)
@@ -573,9 +577,11 @@ class AutogradEngine(_EngineBase):
                     self._own_comm = comm = nat.Comm(nat.comm_unique_id(), 1, 0, dev.index or 0)
                 else:
                     comm = init_native_comm(ctx)
-                # device-side all-reduce timing (allreduce_ms) unless DCT_REDUCER_TIMING=0 (bench.py);
-                # DCT_DEBUG=1 adds the stream-ordering check
-                timing = os.environ.get("DCT_REDUCER_TIMING", "1") != "0"
+                # device-side all-reduce timing (allreduce_ms): opt-in (DCT_REDUCER_TIMING=1, or with
+                # DCT_DEBUG=1) - its stamp kernels and the extra cross-stream edge cost every step,
+                # so default training runs the same step the benchmark times; DCT_DEBUG=1 also adds
+                # the stream-ordering check
+                timing = reducer_timing_enabled()
                 self.reducer = NativeBucketReducer(comm, self.flat_g, self.plan, timing=timing,
                                                    check=debug_enabled())
             else:

@@ -36,6 +36,7 @@ from ..ops.optim import FlatAdam
 from ..parallel.dist import DistContext, init_native_comm
 from ..parallel.reducer import NativeBucketReducer, plan_buckets
 from ..utils.debug import enabled as debug_enabled
+from ..utils.debug import reducer_timing_enabled
 
 ACT_IDS = {"relu": 1, "gelu": 2}
 LOSS_IDS = {"ce": 0, "mse": 1}
@@ -54,6 +55,7 @@ class GraphMLPEngine:
 
     def __init__(self, model, ctx: DistContext, batch_size: int, seed: int, adam: Dict,
                  bucket_cap_bytes: int = 8 << 20, first_bucket_bytes: int = 1 << 20, use_graph: Optional[bool] = None):
+        native().reload_knobs()  # bind time: the native launchers' DCT_* knobs
         self.model = model
         self.ctx = ctx
         self.B = int(batch_size)
@@ -105,7 +107,7 @@ class GraphMLPEngine:
                                 first_bucket_bytes=first_bucket_bytes)
             self.bucket_plan = plan
             self.reducer = NativeBucketReducer(self.comm, self.g, plan,
-                                               timing=os.environ.get("DCT_REDUCER_TIMING", "1") != "0",
+                                               timing=reducer_timing_enabled(),
                                                check=debug_enabled())
         self.exe = nat.MlpStepExecutor(self.dims, B, ACT_IDS["relu"], LOSS_IDS[self.loss], self.p.data_ptr(),
                                        self.p_bf16.data_ptr(), self.g.data_ptr(), self.m.data_ptr(),

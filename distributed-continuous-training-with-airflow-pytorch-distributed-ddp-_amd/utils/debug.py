@@ -23,6 +23,13 @@ def enabled() -> bool:
     return os.environ.get("DCT_DEBUG", "0") == "1"
 
 
+def reducer_timing_enabled() -> bool:
+    """Device-side all-reduce timing of the bucket reducers (allreduce_ms): opt-in with
+    DCT_REDUCER_TIMING=1 or DCT_DEBUG=1 (it costs every step two stamp kernels and a
+    cross-stream edge, so the default training step is the one bench.py times)."""
+    return os.environ.get("DCT_REDUCER_TIMING", "0") == "1" or enabled()
+
+
 def check_device(what: str):
     if not enabled():
         return

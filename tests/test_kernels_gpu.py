@@ -32,22 +32,34 @@ def _ref_loss(logits, y, kind):
 
 
 # DCT_MLP_* settings of a kernel variant name: "lds-<variant>" selects one of the 3x128 trainers
-# (default / mf = mlp_block5 for the exact weather shape D0 <= 8 -> 128 -> 128 -> 2 in train mode and
-# 8-wave mlp_block3 for every other 3x128 shape, b3 = mlp_block3 everywhere, b4 = 16-wave mlp_block4,
-# b2 = mlp_block2, v1 = round 2's
-# mlp_block.hip, noblock = the generic LDS trainer); "v" = VALU instead of the 4x4x1 MFMA layer,
-# "r" = W1's second moment in VGPRs instead of LDS (mlp_block4 only)
-_VARIANTS = {"": ("1", "0", "1"), "noblock": ("0", "0", "1"), "v1": ("v1", "0", "1"), "mf": ("1", "1", "1"),
-             "b2": ("2", "1", "1"), "b3": ("3", "1", "1"), "b3v": ("3", "0", "1"), "b4": ("4", "1", "1"), "b4v": ("4", "0", "1"), "b4r": ("4", "1", "0")}
+# (default / mf = mlp_block5 for the exact weather shape D0 <= 8 -> 128 -> 128 -> 2 and 8-wave
+# mlp_block3 for every other 3x128 shape, b3 = mlp_block3 everywhere, noblock = the generic LDS
+# trainer); "v" = mlp_block3's VALU layer-1 instead of the 4x4x1 MFMA
+_VARIANTS = {"": ("-1", "1"), "noblock": ("0", "1"), "b3": ("3", "1"), "b3v": ("3", "0")}
 
 
 def _set_kernel_env(monkeypatch, kernel):
     parts = kernel.split("-")
     monkeypatch.setenv("DCT_MLP_KERNEL", parts[0])
-    blk, mf, vl = _VARIANTS[parts[1] if len(parts) > 1 else ""]
+    blk, mf = _VARIANTS[parts[1] if len(parts) > 1 else ""]
     monkeypatch.setenv("DCT_MLP_BLOCK", blk)
     monkeypatch.setenv("DCT_MLP_BLOCK_MF", mf)
-    monkeypatch.setenv("DCT_B4_VL", vl)
+
+
+@pytest.fixture(autouse=True)
+def _fresh_knobs():
+    """The native launchers read their DCT_* knobs at plan / bind time (csrc/knobs.h): start every
+    test from the environment as it is now (a previous test's monkeypatch is undone by then)."""
+    native().reload_knobs()
+
+
+def setknob(monkeypatch, name, value=None):
+    """Set (or, with value None, clear) one DCT_* knob and re-read the native knob struct."""
+    if value is None:
+        monkeypatch.delenv(name, raising=False)
+    else:
+        monkeypatch.setenv(name, value)
+    native().reload_knobs()
 
 
 def test_native_loaded_and_arch():
@@ -56,7 +68,7 @@ def test_native_loaded_and_arch():
     assert "gfx950" in nat.arch_name(0)
 
 
-KERNELS = ["auto", "lds", "lds-noblock", "lds-v1", "lds-mf", "lds-b3", "lds-b3v", "lds-b2", "lds-b4", "lds-b4v", "lds-b4r"]
+KERNELS = ["auto", "lds", "lds-noblock", "lds-b3", "lds-b3v"]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -197,9 +209,9 @@ def test_block5_grad_mode_staged_batches(dims, B, n_items, cuda):
 
 @pytest.mark.parametrize("dims,B,D0", [([7, 128, 128, 2], 4, 7), ([30, 128, 128, 3], 3, 30)])
 def test_block_kernel_matches_lds_kernel_with_dropout(dims, B, D0, cuda, monkeypatch):
-    """The register-resident 3-layer kernels (mlp_block4 / 3 / 2 and round 2's mlp_block, with and
-    without the 4x4x1 MFMA layer, W1's second moment in LDS or VGPRs) vs the generic LDS kernel:
-    same dropout hash, loss and Adam -> the same trajectory up to fp32 summation order."""
+    """The register-resident 3-layer kernels (mlp_block5 where the shape fits, mlp_block3 with and
+    without the 4x4x1 MFMA layer) vs the generic LDS kernel: same dropout hash, loss and Adam -> the
+    same trajectory up to fp32 summation order."""
     torch.manual_seed(4)
     N, n_items = 500, 203
     X = torch.randn(N, D0).to(cuda)
@@ -208,7 +220,7 @@ def test_block_kernel_matches_lds_kernel_with_dropout(dims, B, D0, cuda, monkeyp
     p0 = _flat(_ref_net(dims)).to(cuda)
     steps = math.ceil(n_items / B)
     out = {}
-    variants = ("lds", "lds-mf", "lds-b3", "lds-b3v", "lds-v1", "lds-b2", "lds-b4", "lds-b4v", "lds-b4r", "lds-noblock")
+    variants = ("lds", "lds-b3", "lds-b3v", "lds-noblock")
     for blk in variants:
         _set_kernel_env(monkeypatch, blk)
         p, m, v = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
@@ -348,7 +360,7 @@ def test_gemm_bf16(M, N, K, ta, tb, cuda):
 def test_gemm_pipeline_depths(M, N, K, ta, tb, out_f32, stages, cuda, monkeypatch):
     """The LDS pipeline depth (2 or 4 stages, counted vmcnt across a raw barrier) must not change
     the product: each depth against the fp32 torch reference of the same bf16 operands."""
-    monkeypatch.setenv("DCT_GEMM_STAGES", stages)
+    setknob(monkeypatch, "DCT_GEMM_STAGES", stages)
     torch.manual_seed(12)
     A = _bf(torch.randn(K, M, device=cuda) if ta else torch.randn(M, K, device=cuda))
     B = _bf(torch.randn(N, K, device=cuda) if tb else torch.randn(K, N, device=cuda))
@@ -370,7 +382,7 @@ def test_gemm_pipeline_depths(M, N, K, ta, tb, out_f32, stages, cuda, monkeypatc
 def test_gemm_8wave_tiles(M, N, K, ta, tb, cuda, monkeypatch):
     """DCT_GEMM_8W=1: 128 x 128 tiles worked by 8 waves (4 x 2, two per SIMD) with 4 LDS stages, with
     the bias + ReLU epilogue, bf16 out, against the fp32 torch reference of the same bf16 operands."""
-    monkeypatch.setenv("DCT_GEMM_8W", "1")
+    setknob(monkeypatch, "DCT_GEMM_8W", "1")
     torch.manual_seed(13)
     A = _bf(torch.randn(K, M, device=cuda) if ta else torch.randn(M, K, device=cuda))
     B = _bf(torch.randn(N, K, device=cuda) if tb else torch.randn(K, N, device=cuda))
@@ -396,9 +408,9 @@ def test_gemm_split_k_two_pass_and_atomic(M, N, K, accumulate, colsum, two_pass,
     kernel sums them in slice order) and the fp32-atomic mode against the fp32 torch reference,
     accumulating into an existing C and with the fused bias column sums."""
     if two_pass != "auto":  # auto: two-pass for <= 4 slices per tile, atomics above
-        monkeypatch.setenv("DCT_GEMM_SPLIT_TWO_PASS", two_pass)
+        setknob(monkeypatch, "DCT_GEMM_SPLIT_TWO_PASS", two_pass)
     else:
-        monkeypatch.delenv("DCT_GEMM_SPLIT_TWO_PASS", raising=False)
+        setknob(monkeypatch, "DCT_GEMM_SPLIT_TWO_PASS")
     torch.manual_seed(M + N)
     A = _bf(torch.randn(K, M, device=cuda))  # dZ [rows][M]
     B = _bf(torch.randn(K, N, device=cuda))  # X  [rows][N]
@@ -433,7 +445,7 @@ def test_gemm_bf16_out_and_fast_path_match_generic(ta, tb, cuda, monkeypatch):
     outs = []
     for v1 in ("0", "1"):
         if v1 == "1":
-            monkeypatch.setenv("DCT_GEMM_V1", "1")
+            setknob(monkeypatch, "DCT_GEMM_V1", "1")
         C = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
         nat.gemm_bf16(A.data_ptr(), B.data_ptr(), C.data_ptr(), 0, M, N, K, A.stride(0), B.stride(0), N, ta, tb, 0, 0,
                       0, 0, torch.cuda.current_stream().cuda_stream)
@@ -551,7 +563,7 @@ def test_layernorm_fwd_bwd(cuda):
 def test_attention_fwd_bwd(Bsz, H, T, D, scalar, cuda, monkeypatch):
     """MFMA path (T, D multiples of 16, T <= 64) and the scalar LDS path against torch SDPA."""
     if scalar:
-        monkeypatch.setenv("DCT_ATTN_SCALAR", "1")
+        setknob(monkeypatch, "DCT_ATTN_SCALAR", "1")
     torch.manual_seed(11)
     dm = H * D
     qkv = _bf(torch.randn(Bsz * T, 3 * dm, device=cuda))
@@ -593,7 +605,7 @@ def test_gather_rows(cuda):
     assert torch.equal(dst, src[idx.long()])
 
 
-def test_gemm_fused_bias_grad_and_mask_epilogues(cuda):
+def test_gemm_fused_bias_grad_and_mask_epilogues(cuda, monkeypatch):
     """dW GEMM with the bias gradient fused (colsum) and the dX GEMM's ReLU-mask / GELU' epilogues."""
     torch.manual_seed(10)
     nat = native()
@@ -604,15 +616,10 @@ def test_gemm_fused_bias_grad_and_mask_epilogues(cuda):
     for v1 in (False, True):
         dW = torch.zeros(Dout, Din, device=cuda)
         db = torch.zeros(Dout, device=cuda)
-        if v1:
-            import os
-            os.environ["DCT_GEMM_V1"] = "1"
-        try:
-            nat.gemm_bf16_ex(dZ.data_ptr(), A.data_ptr(), dW.data_ptr(), 0, Dout, Din, Bt, Dout, Din, Din, 1, 0, 0, 1,
-                             1, 0, db.data_ptr(), st)
-        finally:
-            import os
-            os.environ.pop("DCT_GEMM_V1", None)
+        setknob(monkeypatch, "DCT_GEMM_V1", "1" if v1 else None)
+        nat.gemm_bf16_ex(dZ.data_ptr(), A.data_ptr(), dW.data_ptr(), 0, Dout, Din, Bt, Dout, Din, Din, 1, 0, 0, 1,
+                         1, 0, db.data_ptr(), st)
+        setknob(monkeypatch, "DCT_GEMM_V1")
         torch.cuda.synchronize()
         assert torch.allclose(dW, dZ.float().t() @ A.float(), atol=0.1, rtol=1e-2)
         assert torch.allclose(db, dZ.float().sum(0), atol=0.05, rtol=1e-3)
@@ -665,7 +672,7 @@ def test_fused_skinny_head_matches_fp32_reference_and_chain(B, K, C, kind, rpw, 
     """csrc/skinny.hip skinny_head_kernel (head fwd + CE/MSE + dlogits + dW/db + masked dH in one
     launch) against (a) a plain torch fp32 reference of the same op and (b) the unfused chain
     skinny_fwd -> loss -> skinny_dw -> skinny_dx it replaces in the tabular step executor."""
-    monkeypatch.setenv("DCT_SKINNY_HEAD_RPW", rpw)
+    setknob(monkeypatch, "DCT_SKINNY_HEAD_RPW", rpw)
     torch.manual_seed(B + K + C)
     nat = native()
     st = torch.cuda.current_stream().cuda_stream
@@ -942,7 +949,7 @@ def test_tt_embed_and_head_loss_match_fp32_reference(cuda, B, C, spb, monkeypatc
     from dct_amd.ops.nn import tt_embed, tt_head_loss
 
     if spb != "auto":
-        monkeypatch.setenv("DCT_TT_HEAD_SPB", spb)
+        setknob(monkeypatch, "DCT_TT_HEAD_SPB", spb)
 
     F_, d = 64, 64
     g = torch.Generator(device="cpu").manual_seed(5)
@@ -1006,7 +1013,7 @@ def test_gemm_dw_grouped(cuda, accumulate, grouped, monkeypatch):
     from dct_amd.ops._native import native
 
     if not grouped:
-        monkeypatch.setenv("DCT_GEMM_NO_GROUP", "1")
+        setknob(monkeypatch, "DCT_GEMM_NO_GROUP", "1")
     g = torch.Generator(device="cpu").manual_seed(9)
     rows = 4096
     shapes = [(64, 256), (256, 64), (64, 64), (192, 64)]
@@ -1067,7 +1074,7 @@ def test_gemm_splitk_workspace_fixup_deterministic(M, N, K, accumulate, cuda, mo
     B = _bf(torch.randn(K, N, device=cuda))
     C0 = torch.randn(M, N, device=cuda) if accumulate else torch.zeros(M, N, device=cuda)
     st = torch.cuda.current_stream().cuda_stream
-    monkeypatch.setenv("DCT_GEMM_SPLIT_WS", "1")
+    setknob(monkeypatch, "DCT_GEMM_SPLIT_WS", "1")
 
     def run():
         C = C0.clone()
@@ -1080,7 +1087,7 @@ def test_gemm_splitk_workspace_fixup_deterministic(M, N, K, accumulate, cuda, mo
     ref = C0 + A.float().t() @ B.float()
     assert torch.equal(c1, c2)
     assert torch.allclose(c1, ref, atol=2e-3 * math.sqrt(K), rtol=1e-3)
-    monkeypatch.delenv("DCT_GEMM_SPLIT_WS")
+    setknob(monkeypatch, "DCT_GEMM_SPLIT_WS")
     ca = run()
     assert torch.allclose(c1, ca, atol=1e-3 * math.sqrt(K), rtol=1e-4)
 
