@@ -73,6 +73,9 @@ def parse():
                    help="cpu: BASELINE config 1 (autograd engine, gloo) - the plumbing path")
     p.add_argument("--epoch-rows", type=int, default=None,
                    help="dataset size used for the reported epoch wall-clock (weather 100k, tabular 100M)")
+    p.add_argument("--no-epoch", action="store_true",
+                   help="skip the measured epoch (weather models on GPU: one real epoch of --epoch-rows rows, "
+                        "train + validation, timed after the step window)")
     a = p.parse_args()
     tab = a.model in TABULAR
     tt = a.model in TRANSFORMER
@@ -435,7 +438,7 @@ def measure(a, ctx):
             "ranks": ctx.world_size,
             "ranks_per_device": (round(ctx.world_size / n_dev, 3) if n_dev else None),
             "us_per_step": round(ms_step * 1e3, 3),
-            "epoch_wall_clock_s_train": round(steps_per_epoch * ms_step / 1e3, 6),
+            "epoch_wall_clock_s_train": round(steps_per_epoch * ms_step / 1e3, 6),  # derived
             "epoch_rows": a.epoch_rows,
             "loss_first": round(first_l, 4),
             "loss_last": round(last_l, 4),
@@ -447,6 +450,8 @@ def measure(a, ctx):
             "device": torch.cuda.get_device_name(ctx.device) if not cpu else "cpu",
         },
     }
+    if not (tab or tt or cpu) and not a.no_epoch and a.epoch_rows > 0:
+        out["extra"].update(_measure_epoch(a, ctx, eng))
     if tab:
         flops = 6.0 * sum(eng.dims[i] * eng.dims[i + 1] for i in range(len(eng.dims) - 1)) * a.batch
         out["extra"]["model_tflops_per_gpu"] = round(flops / (ms_step * 1e-3) / 1e12, 1)
@@ -457,6 +462,43 @@ def measure(a, ctx):
         out["extra"]["dtypes"] = {"gemm_operands": "bf16", "accumulation": "fp32",
                                   "master_weights_and_adam": "fp32", "hbm_dataset": "bf16"}
     return out, (finite and in_sync), eng
+
+
+def _measure_epoch(a, ctx, eng):
+    """One REAL epoch of the weather model after the step window (BASELINE metric "epoch
+    wall-clock"; reference jobs/train_lightning_ddp.py:132 trains epochs of the 80 % split and
+    validates after each): a fresh synthetic dataset of --epoch-rows rows (80/20 split) is attached,
+    then the engine's own epoch path runs - host shuffle of this rank's DistributedSampler shard,
+    index upload, every optimizer step of the shard (with the in-kernel exchange at W > 1), the
+    loss read-back, and the full validation pass - bracketed by synchronize + barrier, max over
+    ranks.  Reported next to the value derived from the timed window's step rate."""
+    import torch
+    import torch.distributed as dist
+
+    from dct_amd.data.synthetic import weather_tensors
+
+    X, Y = weather_tensors(a.epoch_rows, seed=1, dim=5)
+    n_train = int(0.8 * a.epoch_rows)
+    perm = torch.randperm(a.epoch_rows, generator=torch.Generator().manual_seed(7))
+    eng.attach_data(X, Y, perm[:n_train], perm[n_train:])
+    torch.cuda.synchronize()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    losses = eng.train_epoch(1, shuffle=True)
+    l_host = losses.cpu()  # the trainer reads the epoch's losses back (epoch-end logging)
+    t1 = time.perf_counter()
+    val_loss, val_acc = eng.validate()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    ts = torch.tensor([t1 - t0, t2 - t0], dtype=torch.float64,
+                      device=ctx.device if ctx.backend == "nccl" else "cpu")
+    if ctx.is_distributed:
+        dist.all_reduce(ts, op=dist.ReduceOp.MAX)
+    tr, tot = (float(x) for x in ts.cpu())
+    return {"epoch_wall_clock_s_measured": round(tot, 6), "epoch_train_s_measured": round(tr, 6),
+            "epoch_steps_per_rank": int(l_host.numel()), "epoch_train_samples_per_s_measured":
+            round(n_train / tr, 1), "epoch_loss_finite": bool(torch.isfinite(l_host).all()),
+            "epoch_val_loss": round(val_loss, 4), "epoch_val_acc": round(val_acc, 4)}
 
 
 def _physical_devices(ctx):
@@ -501,6 +543,7 @@ def main():
         seed_everything(42)
         a_ref = copy.copy(a)
         a_ref.model = "weather"
+        a_ref.no_epoch = True
         ref, ok_ref, _ = measure(a_ref, ctx)
         out["extra"].update({
             "reference_model": ref["config"]["model"],
