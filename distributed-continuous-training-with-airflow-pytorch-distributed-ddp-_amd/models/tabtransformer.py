@@ -87,5 +87,18 @@ class TabTransformer(TrainModule):
         self.log("val_acc", acc, sync_dist=True, prog_bar=True)
         return loss
 
+    def ddp_block_groups(self):
+        """Blocks grouped for data-parallel gradient buckets, in backward order: the upper half of
+        the blocks (with the head / final LayerNorm, whose gradients come first), then the rest
+        (with the token embedding).  The engine aligns its DDP buckets with these groups and
+        issues each group's deferred dW GEMMs as one grouped launch inside the backward of the
+        group's last block, so the first bucket's all-reduce runs under the remaining backward
+        (trainer/engines.py AutogradEngine, ops/nn.py bound_params).  None: one group."""
+        L = len(self.blocks)
+        if L < 2:
+            return None
+        hi = L - L // 2
+        return [list(range(L - 1, L - 1 - hi, -1)), list(range(L - 1 - hi, -1, -1))]
+
     def configure_optimizers(self):
         return torch.optim.Adam(self.parameters(), lr=self.lr)

@@ -18,7 +18,7 @@ from __future__ import annotations
 import contextlib
 import math
 import os
-from typing import Dict, Iterable, List, Optional
+from typing import Dict, Iterable, List, Optional, Sequence
 
 import torch
 import torch.nn.functional as F
@@ -38,11 +38,19 @@ def _stream():
 # ----------------------------------------------------------------------------- engine binding
 class _Binding:
     def __init__(self, params: Iterable[torch.Tensor], shadows: Optional[Dict[int, torch.Tensor]],
-                 side_dw: bool = False, defer_dw: bool = False):
+                 side_dw: bool = False, defer_dw: bool = False, defer_groups: Sequence[int] = ()):
         self.direct = {id(p) for p in params}
         self.shadows = shadows or {}
         self.side_dw = side_dw
         self.defer_dw = defer_dw
+        # deferred dW flush points: block counts (backward order) after which the queued dW GEMMs
+        # are issued right away, e.g. (2, 2) for 4 blocks - see bound_params
+        self.flush_at = set()
+        acc = 0
+        for n in defer_groups:
+            acc += int(n)
+            self.flush_at.add(acc)
+        self.deferred_blocks = 0
 
 
 _BOUND: Optional[_Binding] = None
@@ -50,7 +58,7 @@ _BOUND: Optional[_Binding] = None
 
 @contextlib.contextmanager
 def bound_params(params: Iterable[torch.Tensor], bf16_shadows: Optional[Dict[int, torch.Tensor]] = None,
-                 side_dw: bool = False, defer_dw: bool = False):
+                 side_dw: bool = False, defer_dw: bool = False, defer_groups: Sequence[int] = ()):
     """Engine-scoped fast paths for the ops below (trainer/engines.py AutogradEngine):
 
     * gradient accumulation fusion - the weight-gradient GEMMs / LayerNorm column sums of a
@@ -65,7 +73,12 @@ def bound_params(params: Iterable[torch.Tensor], bf16_shadows: Optional[Dict[int
       :func:`join_side_work` after backward.  Only for callers with no gradient hooks reading the
       buffers during backward (no DDP bucket reducer): the grads land after the hooks fired;
     * ``defer_dw`` - the same GEMMs are queued instead and issued by :func:`join_side_work` as
-      ONE grouped split-K launch for every block (same no-reducer condition).
+      ONE grouped split-K launch for every block (same no-reducer condition);
+    * ``defer_groups`` (with ``defer_dw``) - block counts in backward order after which the queued
+      GEMMs are issued at once, INSIDE the backward of the block closing the group: with a DDP
+      bucket reducer whose buckets follow the same groups (plan_buckets ``split_before``), the
+      group's bucket is complete - and launches from its hooks - when that block's backward
+      returns, so its all-reduce overlaps the earlier blocks' backward.
     """
     global _BOUND
     # leftovers of a backward that never reached join_side_work (an aborted graph capture) belong
@@ -74,7 +87,7 @@ def bound_params(params: Iterable[torch.Tensor], bf16_shadows: Optional[Dict[int
     if _SIDE["pending"]:  # side-stream launches of such a step: order them before this step's work
         torch.cuda.current_stream().wait_event(_SIDE["pending"][-1][0])
         _SIDE["pending"].clear()
-    prev, _BOUND = _BOUND, _Binding(params, bf16_shadows, side_dw, defer_dw)
+    prev, _BOUND = _BOUND, _Binding(params, bf16_shadows, side_dw, defer_dw, defer_groups)
     try:
         yield
     finally:
@@ -102,6 +115,11 @@ def join_side_work():
     if pend:
         torch.cuda.current_stream().wait_event(pend[-1][0])
         pend.clear()
+    _flush_deferred()
+
+
+def _flush_deferred():
+    """Issue the queued dW GEMMs as grouped launches of up to 16 problems (stream order)."""
     dfr = _SIDE["deferred"]
     if dfr:
         nat, st = native(), _stream()
@@ -637,6 +655,9 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
     if direct and b.defer_dw:
         # accumulate straight into the bound grads at the end of backward, every block in one launch
         _SIDE["deferred"].extend(items)
+        b.deferred_blocks += 1
+        if b.deferred_blocks in b.flush_at:  # this block closes a bucket group: issue its dW now
+            _flush_deferred()
         dw2 = db2 = dw1 = db1 = dwo = dbo = dwqkv = dbqkv = None
     elif direct and b.side_dw:
         # the four dW GEMMs accumulate straight into the bound grads: run them on the side stream,

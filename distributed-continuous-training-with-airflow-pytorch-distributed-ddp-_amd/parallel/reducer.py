@@ -40,7 +40,12 @@ class BucketPlan:
 
 
 def plan_buckets(numels: Sequence[int], elem_bytes: int = 4, bucket_cap_bytes: int = 8 << 20,
-                 first_bucket_bytes: int = 1 << 20) -> BucketPlan:
+                 first_bucket_bytes: int = 1 << 20, split_before: Sequence[int] = ()) -> BucketPlan:
+    """Buckets of consecutive parameters filled in REVERSE parameter order (backward order).
+    ``split_before``: parameter indices that close the bucket being filled before they are added
+    (a model whose gradients become ready in groups - the TabTransformer's grouped dW launches -
+    aligns buckets with those groups, so each bucket launches as its group finishes)."""
+    splits = set(int(i) for i in split_before)
     offs, acc = [], 0
     for n in numels:
         offs.append(acc)
@@ -52,7 +57,7 @@ def plan_buckets(numels: Sequence[int], elem_bytes: int = 4, bucket_cap_bytes: i
     cur: List[int] = []
     for i in reversed(range(len(numels))):
         nb = int(numels[i]) * elem_bytes
-        if cur and cur_bytes + nb > cap:
+        if cur and (cur_bytes + nb > cap or i in splits):
             buckets.append((cur[-1], cur[0]))
             cur, cur_bytes = [], 0
             cap = bucket_cap_bytes

@@ -562,7 +562,12 @@ class AutogradEngine(_EngineBase):
                 off += n
         if ctx.is_distributed:
             ctx.broadcast_(self.flat_p, 0) if ctx.backend != "nccl" else self._bcast_nccl()
-        self.plan = plan_buckets(numels, 4, bucket_cap_bytes, first_bucket_bytes)
+        # models whose gradients become ready in block groups (the TabTransformer's grouped deferred
+        # dW, model.ddp_block_groups) get buckets aligned with the groups: each launches as its group's
+        # dW launch is issued, overlapping the earlier blocks' backward (DCT_TT_DDP_GROUPS=0: one
+        # bucket launched at finalize)
+        self._dw_groups, split_before = self._block_groups(model, params)
+        self.plan = plan_buckets(numels, 4, bucket_cap_bytes, first_bucket_bytes, split_before=split_before)
         self.reducer = None
         # DCT_FORCE_DDP=1 at world size 1 on a GPU: the full DDP path (RCCL communicator of one
         # rank, bucket reducer on its comm stream, hooks, graph capture) - how its correctness,
@@ -627,6 +632,21 @@ class AutogradEngine(_EngineBase):
 
     def _bcast_nccl(self):
         self.ctx.broadcast_(self.flat_p, 0)
+
+    def _block_groups(self, model, params):
+        """(deferred-dW group sizes, bucket split indices) of a model with ddp_block_groups(), else
+        ((), ()).  Only for data-parallel runs (a reducer to overlap with)."""
+        groups = model.ddp_block_groups() if hasattr(model, "ddp_block_groups") else None
+        dp = self.ctx.is_distributed or os.environ.get("DCT_FORCE_DDP", "0") == "1"
+        if not groups or len(groups) < 2 or not dp or os.environ.get("DCT_TT_DDP_GROUPS", "1") == "0":
+            return (), ()
+        index = {id(p): i for i, p in enumerate(params)}
+        splits = []
+        for g in groups[:-1]:
+            lo = min(g)  # the group's lowest block: its first parameter opens the bucket
+            first = min(index[id(p)] for p in model.blocks[lo].parameters())
+            splits.append(first - 1)
+        return tuple(len(g) for g in groups), tuple(splits)
 
     def _make_hook(self, i):
         def hook(_p):
@@ -895,9 +915,12 @@ class AutogradEngine(_EngineBase):
         # dW GEMM anyway, so deferring loses no overlap and keeps the grouped-dW win at W > 1
         defer_ok = self.reducer is None or isinstance(self.reducer, NativeBucketReducer)
         defer = defer_ok and os.environ.get("DCT_TT_DW_DEFER", "1") != "0"
+        groups = self._dw_groups if (defer and self.reducer is not None) else ()
         if isinstance(self.reducer, NativeBucketReducer):
-            self.reducer.defer_launch = defer and self._has_deferrable_ops()
-        return bound_params(self.params, self._shadows, side_dw=side, defer_dw=defer)
+            # with block groups every group's dW launch is issued before its bucket's last hook
+            # fires, so the hooks launch the buckets; otherwise they launch at finalize
+            self.reducer.defer_launch = defer and self._has_deferrable_ops() and not groups
+        return bound_params(self.params, self._shadows, side_dw=side, defer_dw=defer, defer_groups=groups)
 
     def _has_deferrable_ops(self) -> bool:
         """True when the model routes weight gradients through the deferred grouped dW path

@@ -68,9 +68,10 @@ def test_tabular_forced_reducer_matches_no_reducer(cuda, monkeypatch):
     assert red.allreduce_ms()[2] == 0
 
 
-def _tt(forced, monkeypatch, defer="1", steps=10, B=128):
+def _tt(forced, monkeypatch, defer="1", steps=10, B=128, groups="1"):
     monkeypatch.setenv("DCT_FORCE_DDP", "1" if forced else "0")
     monkeypatch.setenv("DCT_TT_DW_DEFER", defer)
+    monkeypatch.setenv("DCT_TT_DDP_GROUPS", groups)
     monkeypatch.setenv("DCT_DEBUG", "1")
     ctx = init_distributed("gpu")
     F_ = 64
@@ -91,11 +92,11 @@ def cuda_dev():
     return torch.device("cuda", 0)
 
 
-@pytest.mark.parametrize("defer", ["1", "0"])
-def test_tabtransformer_forced_reducer_matches_no_reducer(cuda, monkeypatch, defer):
+@pytest.mark.parametrize("defer,groups", [("1", "1"), ("1", "0"), ("0", "1")])
+def test_tabtransformer_forced_reducer_matches_no_reducer(cuda, monkeypatch, defer, groups):
     ref, l0, p0 = _tt(False, monkeypatch, defer)
     _, lh, ph = _tt(False, monkeypatch, defer)  # run-to-run spread of the split-K atomics
-    eng, l1, p1 = _tt(True, monkeypatch, defer)
+    eng, l1, p1 = _tt(True, monkeypatch, defer, groups=groups)
     red = eng.reducer
     assert ref.reducer is None and red is not None and eng.graph_used
     assert torch.isfinite(l1).all() and (l1 != 0).all()
@@ -107,9 +108,16 @@ def test_tabtransformer_forced_reducer_matches_no_reducer(cuda, monkeypatch, def
         # (b) the hooks fired during backward although the fused ops return None for the weight
         # gradients they accumulate in place, and they launched the bucket before finalize
         assert red.hook_launches >= 1 and not red.defer_launch
+    elif groups == "1":
+        # grouped deferred dW in two block groups (model.ddp_block_groups): buckets aligned with the
+        # groups, each group's dW issued inside its last block's backward, so the first bucket
+        # launches from the hooks before finalize and its all-reduce overlaps the lower blocks
+        assert not red.defer_launch and red.num_buckets >= 2
+        assert red.hook_launches >= 1 and red.launched_before_finalize >= 1, (red.hook_launches,
+                                                                            red.launched_before_finalize)
     else:
-        # grouped deferred dW: the hooks only count, every bucket launches at finalize after the
-        # grouped launch (one bucket: nothing to overlap anyway)
+        # grouped deferred dW for every block at once (DCT_TT_DDP_GROUPS=0): the hooks only count,
+        # every bucket launches at finalize after the grouped launch (one bucket)
         assert red.defer_launch and red.num_buckets == 1
     span, exposed, steps, bad = red.allreduce_ms()
     assert steps >= 1 and span > 0 and bad == 0, (span, exposed, steps, bad)

@@ -6,12 +6,18 @@ Self-skips below 2 visible devices (the 1-GPU boxes of the per-round GPU tier); 
 runs W = 2 and W = min(8, devices).  Same worker as the CPU tier (tests/ddp_worker.py), so the
 CPU gloo tests, the shared-GPU IPC rehearsals and this tier check one contract:
   * the fused engine 5-64-2 (in-kernel xGMI all-reduce; RCCL per step when disabled),
-  * the fused engine 3x128 (grad-mode kernel + fused peer all-reduce/Adam kernel, or RCCL ncclAvg
-    + flat Adam; graph-replayed),
+  * the fused engine 3x128: the persistent launch with the in-kernel reduce-scatter / all-gather
+    (default), the grad-mode kernel + fused peer all-reduce/Adam kernel, or RCCL ncclAvg + flat
+    Adam (graph-replayed),
   * the autograd engine (native BucketReducer on its comm stream) on the 5-64-2 MLP,
-replicas bit-identical, parameters equal the emulation, only rank 0 writes checkpoints/MLflow.
+replicas bit-identical, parameters equal the emulation, only rank 0 writes checkpoints/MLflow;
+and BASELINE.json configs 4 / 5 (tests/wide_ddp_worker.py): the tabular MLP on the graph engine and
+the TabTransformer on the autograd engine, each with the native bucket reducer over RCCL, against
+the same engine at W = 1 fed the union of the W shards' batches (batch W * B, rank order: the mean
+of the per-rank mean-loss gradients is the gradient of that batch's mean loss).
 """
 import json
+import math
 import os
 import subprocess
 import sys
@@ -100,16 +106,19 @@ def test_fused_5_64_2_ddp_across_gpus(tmp_path, W, mode):
 
 @needs2
 @pytest.mark.parametrize("W", _worlds())
-@pytest.mark.parametrize("gx", ["1", "0"])
-def test_fused_3x128_ddp_across_gpus(tmp_path, W, gx):
-    """gx=1: grad-mode kernel + fused peer all-reduce + Adam over xGMI (csrc/xg_adam.hip);
-    gx=0: grad-mode kernel + RCCL ncclAvg + flat Adam."""
+@pytest.mark.parametrize("mode", ["inkernel", "gx", "rccl"])
+def test_fused_3x128_ddp_across_gpus(tmp_path, W, mode):
+    """inkernel (default at W = 2 / 4 / 8): the persistent mlp_block5 launch with the in-kernel
+    reduce-scatter + all-gather over xGMI (sharded Adam); gx: grad-mode kernel + fused peer
+    all-reduce + Adam kernel (csrc/xg_adam.hip); rccl: grad-mode kernel + RCCL ncclAvg + flat Adam."""
     rows, epochs = 600, 2
-    r = _torchrun(W, 29731 + W + (10 if gx == "1" else 0), [tmp_path, epochs, rows, "gpu", "hidden=128,128"],
-                  env={"DCT_XG_GRAD": gx})
+    env = {"inkernel": {}, "gx": {"DCT_XG_INKERNEL": "0", "DCT_XG_GRAD": "1"},
+           "rccl": {"DCT_XG_INKERNEL": "0", "DCT_XG_GRAD": "0"}}[mode]
+    port = 29731 + W + {"inkernel": 0, "gx": 10, "rccl": 20}[mode]
+    r = _torchrun(W, port, [tmp_path, epochs, rows, "gpu", "hidden=128,128"], env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     info = _check(tmp_path, W, rows, epochs, (128, 128), 3e-3)
-    assert info["gx"] == (gx == "1")
+    assert info["xg"] == (mode == "inkernel") and info["gx"] == (mode == "gx"), info
 
 
 @needs2
@@ -120,3 +129,60 @@ def test_autograd_engine_native_bucket_reducer_across_gpus(tmp_path, W):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     info = _check(tmp_path, W, rows, epochs, (64,), 2e-3)
     assert info["engine"] == "autograd"
+
+
+def _wide_reference(kind, W, steps):
+    """The same engine at W = 1 on this process's GPU, batch W * B, each step's batch the rank-order
+    union of the W shards' batches of that step (distributed_indices, seed 42, epoch 0)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import wide_ddp_worker as ww
+
+    from dct_amd.data.sampler import distributed_indices
+    from dct_amd.parallel.dist import DistContext
+    from dct_amd.trainer.engines import AutogradEngine, adam_hparams_from
+    from dct_amd.trainer.graph_engine import GraphMLPEngine
+
+    model, X, Y, tr, va, B = ww.build(kind)
+    dev = torch.device("cuda", 0)
+    ctx = DistContext(device=dev)
+    shards = [tr[distributed_indices(len(tr), W, r, shuffle=True, seed=42, epoch=0)] for r in range(W)]
+    rows = torch.cat([torch.cat([sh[s * B:(s + 1) * B] for sh in shards]) for s in range(steps)])
+    loss = torch.zeros(steps, device=dev)
+    if kind == "tabular":
+        eng = GraphMLPEngine(model, ctx, W * B, seed=42, adam=adam_hparams_from(model.configure_optimizers()))
+        eng.attach_data(X, Y, tr, va)
+        eng.idx = rows.to(dev, torch.int32)
+        eng.run_steps(rows.numel(), steps, loss)
+        flat = eng.p
+    else:
+        eng = AutogradEngine(model, ctx, W * B, seed=42)
+        eng.attach_data(X.to(dev), Y.to(dev), tr, va)
+        eng.run_device_steps(rows.to(dev), 0, steps, loss)
+        flat = eng.flat_p
+    torch.cuda.synchronize()
+    return flat.detach().cpu(), torch.cat([p.detach().reshape(-1) for p in ww.build(kind)[0].parameters()])
+
+
+@needs2
+@pytest.mark.parametrize("W", _worlds())
+@pytest.mark.parametrize("kind", ["tabular", "tt"])
+def test_wide_models_ddp_across_gpus(tmp_path, W, kind):
+    """BASELINE configs 4 (tabular MLP, graph engine) and 5 (TabTransformer, autograd engine over
+    the fused HIP blocks) at DDP = W: RCCL bucket reducer with >= 2 buckets launched from backward
+    before finalize (the TabTransformer's block-group buckets included), replicas bit-identical,
+    parameters following the W = 1 run of the union batches."""
+    steps = 24
+    r = _torchrun(W, 29771 + W + (10 if kind == "tt" else 0), [tmp_path / "w", kind, steps],
+                  env={"DCT_DEBUG": "1"})
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = [json.loads((tmp_path / f"w_rank{q}.json").read_text()) for q in range(W)]
+    for q in range(W):
+        assert res[q]["backend"] == "nccl" and res[q]["world"] == W
+        assert res[q]["params"] == res[0]["params"], q  # one all-reduce result on every rank
+        assert res[q]["num_buckets"] >= 2 and res[q]["launched_before_finalize"] >= 1, res[q]
+        assert all(map(math.isfinite, res[q]["losses"]))
+    got = torch.tensor(res[0]["params"])
+    want, p0 = _wide_reference(kind, W, steps)
+    # bf16 operands: the W-rank run sums per-rank dW partials, the reference one dW over W * B rows
+    rel = float((got - want).norm() / (want - p0).norm())
+    assert rel < 0.05, rel

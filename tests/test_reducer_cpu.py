@@ -61,3 +61,42 @@ def test_post_accumulate_hooks_fire_for_in_place_grads():
     h.sum().backward()
     for w, r in zip(ws, ref):
         assert torch.allclose(w.grad, r.grad, atol=1e-5)
+
+
+def test_plan_buckets_split_before_aligns_buckets_with_groups():
+    """split_before closes the bucket being filled (reverse parameter order) before a parameter:
+    the TabTransformer's block groups become their own buckets regardless of the byte caps."""
+    plan = plan_buckets([10, 20, 30, 40, 50], 4, bucket_cap_bytes=1 << 20, first_bucket_bytes=1 << 20,
+                        split_before=[2])
+    assert plan.param_bucket == [1, 1, 1, 0, 0]
+    assert plan.offsets == [60, 0] and plan.counts == [90, 60]
+    # without the split: one bucket
+    assert plan_buckets([10, 20, 30, 40, 50], 4, 1 << 20, 1 << 20).param_bucket == [0] * 5
+
+
+def test_tabtransformer_block_groups_split_the_ddp_buckets():
+    """AutogradEngine._block_groups on the TabTransformer: the upper half of the blocks (with the
+    head) and the lower half (with the embedding) as two bucket groups; the split index is the
+    last parameter of the highest block of the lower group."""
+    from dct_amd.models.tabtransformer import TabTransformer
+    from dct_amd.parallel.dist import DistContext
+    from dct_amd.trainer.engines import AutogradEngine
+
+    m = TabTransformer(num_features=8, d_model=16, heads=2, layers=4)
+    assert m.ddp_block_groups() == [[3, 2], [1, 0]]
+    assert TabTransformer(num_features=8, d_model=16, heads=2, layers=3).ddp_block_groups() == [[2, 1], [0]]
+    assert TabTransformer(num_features=8, d_model=16, heads=2, layers=1).ddp_block_groups() is None
+    params = list(m.parameters())
+
+    class _Eng:
+        ctx = DistContext(rank=0, world_size=2)
+
+    groups, splits = AutogradEngine._block_groups(_Eng(), m, params)
+    assert groups == (2, 2)
+    first_b2 = [i for i, p in enumerate(params) if p is next(m.blocks[2].parameters())][0]
+    assert splits == (first_b2 - 1,)
+    plan = plan_buckets([p.numel() for p in params], 4, 8 << 20, 1 << 20, split_before=splits)
+    assert len(plan.counts) == 2
+    upper = {id(p) for b in (2, 3) for p in m.blocks[b].parameters()} | {id(p) for p in m.head.parameters()}
+    for i, p in enumerate(params):
+        assert plan.param_bucket[i] == (0 if id(p) in upper or i > first_b2 else 1)
