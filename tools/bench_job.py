@@ -33,6 +33,7 @@ def main():
     p.add_argument("--epochs", type=int, default=10)
     p.add_argument("--accelerator", default="gpu")
     p.add_argument("--no-mlflow", action="store_true")
+    p.add_argument("--model", default="", help="jobs/train_ddp.py --model (default: the job's own)")
     p.add_argument("--keep", action="store_true", help="keep the work directory (data, checkpoints, mlruns)")
     a = p.parse_args()
 
@@ -59,6 +60,8 @@ def _run(a, work, run_arrow_etl, make_weather_csv):
            "--tracking-uri", "file://" + os.path.join(work, "mlruns")]
     if a.no_mlflow:
         cmd.append("--no-mlflow")
+    if a.model:
+        cmd += ["--model", a.model]
     t0 = time.perf_counter()
     r = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT)
     job_s = time.perf_counter() - t0
@@ -71,6 +74,7 @@ def _run(a, work, run_arrow_etl, make_weather_csv):
     out = {
         "metric": "reference training job wall-clock (ETL'd parquet, 10 epochs, val, ckpt, MLflow)",
         "accelerator": a.accelerator,
+        "model": a.model or "job default",
         "engine": engine.group(1) if engine else None,
         "rows": a.rows,
         "epochs": a.epochs,
