@@ -166,16 +166,22 @@ def _warmup(loop, n_items, warmup, loss):
     (tools/bench_window_probe.py).  Same steps, same data, same order as one launch."""
     calls = max(1, min(warmup, 8))
     first = 0
+    exchange = getattr(loop, "xg", None) is not None or getattr(loop, "gx", None) is not None
+    # replicas are identical before the first exchange launch: keep that state, so a timed-out
+    # launch (the per-step peer all-reduce + Adam kernel can leave some blocks of a step applied)
+    # is rolled back on every rank before the RCCL fallback re-syncs them (ADVICE r3)
+    snap = [t.clone() for t in (loop.p, loop.m, loop.v, loop.step_counter)] if exchange else None
     for i in range(calls):
         k = warmup // calls + (1 if i < warmup % calls else 0)
         if k:
             loop.run_steps(n_items, k, loss, first_step=first)
             first += k
-            if i == 0 and (getattr(loop, "xg", None) is not None or getattr(loop, "gx", None) is not None):
+            if i == 0 and exchange:
                 # the in-kernel exchange is checked after its FIRST launch: if peers cannot see
                 # each other's writes, only that launch pays the spin timeout before the RCCL
                 # fallback, not every warmup launch
-                loop.xg_verify(fallback=True)
+                loop.xg_verify(fallback=True, snapshot=snap)
+                snap = None
 
 
 def _params_in_sync(ctx, p):
