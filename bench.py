@@ -171,6 +171,13 @@ def _warmup(loop, n_items, warmup, loss):
     # launch (the per-step peer all-reduce + Adam kernel can leave some blocks of a step applied)
     # is rolled back on every rank before the RCCL fallback re-syncs them
     snap = [t.clone() for t in (loop.p, loop.m, loop.v, loop.step_counter)] if exchange else None
+    full_timeout = getattr(loop, "xg_timeout_s", None)
+    if exchange:
+        # the first exchange launch spins with the SHORT probe limit (a node whose peers cannot see
+        # each other's writes then costs seconds, not the full training timeout, before the fallback)
+        from dct_amd.parallel.xgmi import probe_timeout_s
+
+        loop.xg_timeout_s, loop._bound, loop._fast_run = probe_timeout_s(), None, None
     for i in range(calls):
         k = warmup // calls + (1 if i < warmup % calls else 0)
         if k:
@@ -182,6 +189,8 @@ def _warmup(loop, n_items, warmup, loss):
                 # fallback, not every warmup launch
                 loop.xg_verify(fallback=True, snapshot=snap)
                 snap = None
+                # back to the full limit (launches rebound with it)
+                loop.xg_timeout_s, loop._bound, loop._fast_run = full_timeout, None, None
 
 
 def _params_in_sync(ctx, p):
