@@ -6,6 +6,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -78,6 +79,13 @@ static dct::MlpArgs make_train_args(const MlpPlan& plan, uintptr_t p, uintptr_t 
   a.t0 = t0;
   a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.wd = wd;
   a.dropout = dropout;
+  // float arithmetic as the kernels' own derivation (same roundings on host and device)
+  a.k_drop_scale = dropout > 0.f ? 1.0f / (1.0f - dropout) : 1.0f;
+  a.k_l2b1 = std::log2(b1);
+  a.k_l2b2 = std::log2(b2);
+  a.k_rc1 = 1.f / (1.f - b1);
+  a.k_rc2 = 1.f / (1.f - b2);
+  a.k_sqc2 = std::sqrt(1.f - b2);
   a.seed = seed;
   a.step_base = step_base;
   a.loss_out = P<float>(loss_out);

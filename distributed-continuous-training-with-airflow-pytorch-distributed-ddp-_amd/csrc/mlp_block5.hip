@@ -19,6 +19,8 @@
 //   F1 (h1[u][r0]) -> F2 k-slice partials (4x4x1 MFMA) -> BARRIER A -> h2 of the wave's 16 outputs,
 //   logit shares, h2 > 0 ballot -> BARRIER B -> loss -> dZ2, W2 / b1 / b2 Adam -> dZ1 (reduce-
 //   scatter) -> W0 / b0 Adam -> dW1 (MFMA) + W1 Adam.
+#include <type_traits>
+
 #include "mlp_block_util.h"
 
 namespace dct {
@@ -113,6 +115,16 @@ __device__ __forceinline__ T pick(const T* v, int rank) {
   for (int k = 1; k < XW; ++k) r = rank == k ? v[k] : r;
   return r;
 }
+template <int V>
+using IC = std::integral_constant<int, V>;
+// f(IC<0>), ..., f(IC<N - 1>)
+template <int N, int I = 0, class F>
+__device__ __host__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(IC<I>{});
+    static_for<N, I + 1>(f);
+  }
+}
 }  // namespace b5x
 
 #define B5STAMP(k)                                              \
@@ -206,8 +218,10 @@ __device__ __forceinline__ void adam_v2(v2f& p, v2f g, v2f& m, v2f& v, float b1,
 // LK: 0 = cross-entropy, 1 = MSE against the one-hot label; WD: L2 term in the update; ADAM = false:
 // grad mode (the DDP step: ONE step at the device batch cursor, gradients + batch loss to grad_out,
 // the previous step's all-reduced loss to loss_out[cursor - 1]; no moments read or written);
-// XW > 1: train mode of one rank of XW data-parallel ranks (b5x above)
-template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true, int XW = 1>
+// XW > 1: train mode of one rank of XW data-parallel ranks (b5x above); RK >= 0: that rank as a
+// compile-time constant (every ownership test folds, the all-gather loads land straight in the W1
+// registers; fewer live registers and spills than the runtime-rank kernel, RK = -1)
+template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true, int XW = 1, int RK = -1>
 __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, MlpArgs a) {
   using namespace blk5;
   using namespace bku;
@@ -362,12 +376,18 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   lds_barrier();
 
   if constexpr (PROF) pacc[14] = __builtin_amdgcn_s_memtime() - t_kstart;  // LDS init + first batch
+  // data-parallel launches take these launch constants from the host (kernarg -> scalar registers):
+  // derived here, the compiler re-materialises their divisions / logarithms inside the step loop.
+  // Measured (profiles/b5_host_constants_ab_r4.log): 8 ranks 17.3 -> 16.4 us/step, but the one-rank
+  // kernel 3.90 -> 3.98 us/step despite 7 % fewer loop instructions (its schedule overlaps the
+  // re-materialised work with the MFMA chains), so XW = 1 keeps deriving them
   const float p_drop = a.dropout;
   const bool drop = p_drop > 0.f;
-  const float scale = drop ? 1.0f / (1.0f - p_drop) : 1.0f;
-  const float l2b1 = log2f(a.b1), l2b2 = log2f(a.b2);
+  const float scale = XW > 1 ? a.k_drop_scale : (drop ? 1.0f / (1.0f - p_drop) : 1.0f);
+  const float l2b1 = XW > 1 ? a.k_l2b1 : log2f(a.b1), l2b2 = XW > 1 ? a.k_l2b2 : log2f(a.b2);
   const float c1 = 1.f - a.b1, c2 = 1.f - a.b2;
-  const float rc1 = 1.f / c1, rc2 = 1.f / c2, sqc2 = sqrtf(c2);
+  const float rc1 = XW > 1 ? a.k_rc1 : 1.f / c1, rc2 = XW > 1 ? a.k_rc2 : 1.f / c2;
+  const float sqc2 = XW > 1 ? a.k_sqc2 : sqrtf(c2);
   // Adam moments to the scaled form adam_scaled keeps (back on store)
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -390,7 +410,7 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     }
   // ---- XW > 1: the moments of the owned W1 pairs only (slot t = pair rank + XW t), the exchange's
   // buffer descriptors, this rank's small-pair ownership
-  const int xrank = XW > 1 ? a.xg_rank : 0;
+  const int xrank = XW > 1 ? (RK >= 0 ? RK : a.xg_rank) : 0;
   v2f MoO[NO], VoO[NO];
   __amdgpu_buffer_rsrc_t xrr = __builtin_amdgcn_make_buffer_rsrc((void*)a.xg_recv, 0, 0, 0x00020000), xpr[XW];
   // (the wave index through readfirstlane: a scalar condition, uniform branches)
@@ -1084,20 +1104,25 @@ size_t mlp_block5_xg_bytes(int world) {
   }
 }
 
-template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true, int XW = 1>
+template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true, int XW = 1, int RK = -1>
 static void b5_launch(size_t bytes, hipStream_t st, const MlpShape& sh, const MlpArgs& a) {
-  static const hipError_t attr = hipFuncSetAttribute((const void*)mlp_block5_kernel<WD, LK, PROF, DXM, ADAM, XW>,
+  static const hipError_t attr = hipFuncSetAttribute((const void*)mlp_block5_kernel<WD, LK, PROF, DXM, ADAM, XW, RK>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   (void)attr;
-  hipLaunchKernelGGL((mlp_block5_kernel<WD, LK, PROF, DXM, ADAM, XW>), dim3(1), dim3(blk5::NT), bytes, st, sh, a);
+  hipLaunchKernelGGL((mlp_block5_kernel<WD, LK, PROF, DXM, ADAM, XW, RK>), dim3(1), dim3(blk5::NT), bytes, st, sh, a);
 }
 
 template <int XW>
 static void b5_launch_xg(size_t bytes, hipStream_t st, const MlpShape& sh, const MlpArgs& a) {
   const bool wd = a.wd != 0.f;
-  if (a.loss_kind == 0) {
-    if (wd) b5_launch<true, 0, false, true, true, XW>(bytes, st, sh, a);
-    else b5_launch<false, 0, false, true, true, XW>(bytes, st, sh, a);
+  if (a.loss_kind == 0 && !wd) {
+    // the reference's configuration (cross-entropy, Adam without weight decay): one kernel per rank
+    b5x::static_for<XW>([&](auto rc) {
+      constexpr int R = decltype(rc)::value;
+      if (a.xg_rank == R) b5_launch<false, 0, false, true, true, XW, R>(bytes, st, sh, a);
+    });
+  } else if (a.loss_kind == 0) {
+    b5_launch<true, 0, false, true, true, XW>(bytes, st, sh, a);
   } else {
     if (wd) b5_launch<true, 1, false, true, true, XW>(bytes, st, sh, a);
     else b5_launch<false, 1, false, true, true, XW>(bytes, st, sh, a);

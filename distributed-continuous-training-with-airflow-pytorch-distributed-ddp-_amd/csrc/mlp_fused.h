@@ -107,6 +107,13 @@ struct MlpArgs {
   unsigned long long* xg_ticks;
   // kernel-specific A/B knob (mlp_block3.hip: wave priority split), 0 = the kernel's default
   int tune;
+  // launch constants derived on the host (bindings.cpp make_train_args): mlp_block5 reads them from
+  // the kernarg segment (scalar registers) instead of deriving them in the kernel, where the compiler
+  // re-materialised the divisions / logarithms inside the step loop to save vector registers
+  float k_drop_scale;  // 1 / (1 - dropout), or 1 without dropout
+  float k_l2b1, k_l2b2;  // log2(b1), log2(b2) (Adam bias corrections as one exp2 each)
+  float k_rc1, k_rc2;  // 1 / (1 - b1), 1 / (1 - b2) (scaled-moment Adam)
+  float k_sqc2;        // sqrt(1 - b2)
 };
 
 constexpr int XG_MAXW = 8;  // ranks of the in-kernel exchange (one node)
