@@ -37,11 +37,11 @@ def _flat(ts):
     return torch.cat([t.detach().reshape(-1) for t in ts])
 
 
-def ddp_reference(net, X, Y, shards, B, steps, lr=0.01):
+def ddp_reference(net, X, Y, shards, B, steps, lr=0.01, wd=0.0):
     """W-rank DDP emulation: per-rank CE grads summed / W, one torch Adam step; returns the flat
     parameters, exp_avg, exp_avg_sq and the per-step mean losses."""
     params = list(net.parameters())
-    opt = torch.optim.Adam(params, lr=lr)
+    opt = torch.optim.Adam(params, lr=lr, weight_decay=wd)
     losses = []
     for s in range(steps):
         gsum = [torch.zeros_like(p) for p in params]
@@ -61,7 +61,7 @@ def ddp_reference(net, X, Y, shards, B, steps, lr=0.01):
             torch.tensor(losses))
 
 
-def _in_process_run(W, steps, split, B, out_path):
+def _in_process_run(W, steps, split, B, out_path, wd=0.0):
     """W 'ranks' as concurrent persistent launches on W streams of one GPU (peers = raw pointers);
     the steps run as two launches per rank, so the launch-end moment all-gather feeds the second
     launch's prologue."""
@@ -87,7 +87,7 @@ def _in_process_run(W, steps, split, B, out_path):
     for first, k in ((0, split), (split, steps - split)):
         for r in range(W):
             kern.train(ps[r], ms[r], vs[r], Xd, Yd, idx[r][first * B:], n_items=idx[r].numel() - first * B, batch=B,
-                       steps=k, t0=0, lr=0.01, loss_out=losses[r][first:], step_counter=scs[r], xg=xs[r],
+                       steps=k, t0=0, lr=0.01, weight_decay=wd, loss_out=losses[r][first:], step_counter=scs[r], xg=xs[r],
                        xg_timeout_s=5.0, stream=streams[r].cuda_stream)
     torch.cuda.synchronize()
     json.dump({"status": [x.read_status() for x in xs], "steps": [int(sc.item()) for sc in scs],
@@ -96,13 +96,13 @@ def _in_process_run(W, steps, split, B, out_path):
               open(out_path, "w"))
 
 
-def _check_vs_reference(res, W, steps, B, seed_net, X, Y, shards):
+def _check_vs_reference(res, W, steps, B, seed_net, X, Y, shards, wd=0.0):
     ps = [torch.tensor(p) for p in res["params"]]
     for r in range(1, W):  # one writer per parameter: replicas bit-identical, optimizer state too
         assert torch.equal(ps[r], ps[0])
         assert res["m"][r] == res["m"][0] and res["v"][r] == res["v"][0]
         assert res["losses"][r] == res["losses"][0]
-    want, want_m, want_v, want_l = ddp_reference(_net(seed_net), X, Y, shards, B, steps)
+    want, want_m, want_v, want_l = ddp_reference(_net(seed_net), X, Y, shards, B, steps, wd=wd)
     err = (ps[0] - want).abs()
     assert err.median() < 2e-5 and err.max() < 3e-3, (err.median(), err.max())
     em = (torch.tensor(res["m"][0]) - want_m).abs()
@@ -114,22 +114,23 @@ def _check_vs_reference(res, W, steps, B, seed_net, X, Y, shards):
     assert torch.allclose(torch.tensor(res["losses"][0]), want_l, atol=2e-4, rtol=1e-3)
 
 
-@pytest.mark.parametrize("W", [2])
-def test_in_process_block5_exchange_matches_ddp_reference(tmp_path, W, cuda):
+@pytest.mark.parametrize("W,wd", [(2, 0.0), (2, 0.01)])
+def test_in_process_block5_exchange_matches_ddp_reference(tmp_path, W, wd, cuda):
     """Fresh process: streams of one process share GPU_MAX_HW_QUEUES (4) hardware queues round-
     robin, so more 'ranks' than that could land on one queue and serialise; W > 2 runs as separate
-    processes below."""
+    processes below.  wd = 0: the per-rank compile-time-rank kernels (the reference's
+    configuration); wd > 0: the runtime-rank kernel (L2 term in every sharded update)."""
     B, steps, split = 4, 60, 23
     out = tmp_path / "b5x.json"
     code = (f"import sys; sys.path.insert(0, {ROOT!r}); sys.path.insert(0, {os.path.join(ROOT, 'tests')!r}); "
-            f"import test_xg_block5_gpu as t; t._in_process_run({W}, {steps}, {split}, {B}, {str(out)!r})")
+            f"import test_xg_block5_gpu as t; t._in_process_run({W}, {steps}, {split}, {B}, {str(out)!r}, wd={wd})")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     res = json.loads(out.read_text())
     assert res["status"] == [0] * W and res["steps"] == [steps] * W
     X, Y = weather_tensors(3000, seed=5)
     shards = [distributed_indices(3000, W, r_, shuffle=True, seed=42, epoch=0) for r_ in range(W)]
-    _check_vs_reference(res, W, steps, B, 1, X, Y, shards)
+    _check_vs_reference(res, W, steps, B, 1, X, Y, shards, wd=wd)
 
 
 def test_block5_exchange_timeout_leaves_state_untouched(cuda):
