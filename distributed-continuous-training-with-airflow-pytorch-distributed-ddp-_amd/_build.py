@@ -31,7 +31,12 @@ def target_path() -> str:
 # FMAs into v_pk_fma_f32 plus the v_mov_b32 pairs that marshal their operands - on gfx950 a packed op
 # issues no faster than two plain ones, so the moves are pure overhead in an issue-bound kernel
 # (mlp_block5 packs its Adam pairs by hand where packing pays).
-FILE_FLAGS = {"mlp_block3.hip": ["-fno-slp-vectorize"], "mlp_block5.hip": ["-fno-slp-vectorize"]}
+# mlp_block5.hip (the one-rank 3x128 launches, the bench headline) also takes the max-ILP machine
+# scheduler: 3.90 -> 3.80 us/step; its data-parallel unit keeps the default scheduler, under which
+# the 8-rank kernels ran faster (12.85 vs 13.12 us/step, profiles/b5_sched_strategy_ab_r4.log).
+FILE_FLAGS = {"mlp_block3.hip": ["-fno-slp-vectorize"],
+              "mlp_block5.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+              "mlp_block5_xg.hip": ["-fno-slp-vectorize"]}
 
 
 def _sources():

@@ -1,0 +1,32 @@
+// Data-parallel launches of the 3x128 weather trainer (mlp_block5_impl.h, XW = 2 / 4 / 8 ranks):
+// the per-rank compile-time-rank kernels of the reference configuration (CE, no weight decay) and
+// the runtime-rank kernels of every other one.  Compiled with the default scheduler: the
+// max-ILP strategy of the one-rank unit measured slower here (profiles/b5_sched_strategy_ab_r4.log).
+#include "mlp_block5_impl.h"
+
+namespace dct {
+
+template <int XW>
+static void b5_launch_xg(size_t bytes, hipStream_t st, const MlpShape& sh, const MlpArgs& a) {
+  const bool wd = a.wd != 0.f;
+  if (a.loss_kind == 0 && !wd) {
+    // the reference's configuration (cross-entropy, Adam without weight decay): one kernel per rank
+    b5x::static_for<XW>([&](auto rc) {
+      constexpr int R = decltype(rc)::value;
+      if (a.xg_rank == R) b5_launch<false, 0, false, true, true, XW, R>(bytes, st, sh, a);
+    });
+  } else if (a.loss_kind == 0) {
+    b5_launch<true, 0, false, true, true, XW>(bytes, st, sh, a);
+  } else {
+    if (wd) b5_launch<true, 1, false, true, true, XW>(bytes, st, sh, a);
+    else b5_launch<false, 1, false, true, true, XW>(bytes, st, sh, a);
+  }
+}
+
+void mlp_launch_block5_xg(int world, size_t bytes, hipStream_t st, const MlpShape& sh, const MlpArgs& a) {
+  if (world == 2) b5_launch_xg<2>(bytes, st, sh, a);
+  else if (world == 4) b5_launch_xg<4>(bytes, st, sh, a);
+  else b5_launch_xg<8>(bytes, st, sh, a);
+}
+
+}  // namespace dct
