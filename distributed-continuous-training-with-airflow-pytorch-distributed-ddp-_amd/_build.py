@@ -34,9 +34,13 @@ def target_path() -> str:
 # mlp_block5.hip (the one-rank 3x128 launches, the bench headline) also takes the max-ILP machine
 # scheduler: 3.90 -> 3.80 us/step; its data-parallel unit keeps the default scheduler, under which
 # the 8-rank kernels ran faster (12.85 vs 13.12 us/step, profiles/b5_sched_strategy_ab_r4.log).
+# The TabTransformer block / io kernels too (VALU-issue bound: TT step 366 -> 356 us with them, the
+# GEMM and skinny units under the same strategy made the tabular step 1 % slower; b5_sched_strategy_ab_r4.log).
 FILE_FLAGS = {"mlp_block3.hip": ["-fno-slp-vectorize"],
               "mlp_block5.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=max-ilp"],
-              "mlp_block5_xg.hip": ["-fno-slp-vectorize"]}
+              "mlp_block5_xg.hip": ["-fno-slp-vectorize"],
+              "tt_block.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+              "tt_io.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
 
 
 def _sources():
