@@ -36,11 +36,17 @@ def target_path() -> str:
 # the 8-rank kernels ran faster (12.85 vs 13.12 us/step, profiles/b5_sched_strategy_ab_r4.log).
 # The TabTransformer block / io kernels too (VALU-issue bound: TT step 366 -> 356 us with them, the
 # GEMM and skinny units under the same strategy made the tabular step 1 % slower; b5_sched_strategy_ab_r4.log).
+# And the one-rank units of the 5-64-2 wave trainer: 0.640 / 0.655 -> 0.632 / 0.647 us/step long run,
+# 20-step window 1.65-1.70 -> 1.60-1.69; its exchange units measured no gain at 2 / 4 ranks sharing a GPU
+# (1.81 / 2.47 vs 1.80 / 2.47 us/step) and keep the default (profiles/wave_sched_strategy_ab_r4.log).
+MAX_ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 FILE_FLAGS = {"mlp_block3.hip": ["-fno-slp-vectorize"],
-              "mlp_block5.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+              "mlp_block5.hip": ["-fno-slp-vectorize"] + MAX_ILP,
               "mlp_block5_xg.hip": ["-fno-slp-vectorize"],
-              "tt_block.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
-              "tt_io.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+              "tt_block.hip": MAX_ILP,
+              "tt_io.hip": MAX_ILP,
+              "mlp_wave_single.hip": MAX_ILP,
+              "mlp_wave_rows_x0.hip": MAX_ILP}
 
 
 def _sources():

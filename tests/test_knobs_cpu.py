@@ -10,7 +10,9 @@ from dct_amd.ops import _native
 def nat():
     if not _native.available():
         pytest.skip("native extension not importable here")
-    return _native.native()
+    n = _native.native()
+    yield n
+    n.reload_knobs()  # torn down after monkeypatch (requested first): back to the real environment
 
 
 def test_knobs_defaults_and_reload(nat, monkeypatch):

@@ -7,7 +7,7 @@ Shapes (batch 4096, 256-1024-1024-1024-2, bench.py --model tabular-mlp-4x1024):
   dX       dZ W           4096x1024x1024 (NN) x2, bf16 out
   dW       dZ^T X         1024x1024x4096 (TN, fp32 split-K) x2, 1024x256x4096
 plus the TabTransformer step's projection / FFN shapes (32768 token rows, d 64, ffn 256).
-Each variant sets DCT_GEMM_STAGES / DCT_GEMM_SPLIT_WG (read by the launcher on every call).
+Each variant sets DCT_GEMM_STAGES / DCT_GEMM_SPLIT_WG and re-reads the knob struct (reload_knobs).
 Prints one JSON line per (shape, variant) with the median over rounds.
 """
 import argparse
@@ -49,8 +49,8 @@ VARIANTS = {
     "s2_splits128": {"DCT_GEMM_STAGES": "2", "DCT_GEMM_SPLITS": "128"},
     "s4_splits128": {"DCT_GEMM_STAGES": "4", "DCT_GEMM_SPLITS": "128"},
 }
-ENV_KEYS = ("DCT_GEMM_STAGES", "DCT_GEMM_SPLIT_WG", "DCT_GEMM_SPLITS", "DCT_GEMM_SPLIT_PROBE", "DCT_GEMM_BM64_NK",
-            "DCT_GEMM_SPLIT_TWO_PASS")
+ENV_KEYS = ("DCT_GEMM_STAGES", "DCT_GEMM_SPLIT_WG", "DCT_GEMM_SPLITS", "DCT_GEMM_BM64_NK", "DCT_GEMM_SPLIT_TWO_PASS",
+            "DCT_GEMM_8W", "DCT_GEMM_BM128")
 if os.environ.get("AB_SET") == "dw":  # split-K sweep on the transformer dW shapes only
     SHAPES = [s for s in SHAPES if s[0].startswith("tt_dw") or s[0] == "dw_l1"]
     VARIANTS = {f"{st}_sp{sp}": {"DCT_GEMM_STAGES": st[1], "DCT_GEMM_SPLITS": str(sp)}
@@ -60,11 +60,10 @@ if os.environ.get("AB_SET") == "bm64":  # half-height tiles (2 workgroups per CU
     SHAPES = [s for s in SHAPES if not s[0].startswith(("tt_dw", "dw_"))]
     VARIANTS = {"bm128": {}, "bm64": {"DCT_GEMM_BM64_NK": "64"}, "bm64_s4": {"DCT_GEMM_BM64_NK": "64",
                                                                               "DCT_GEMM_STAGES": "4"}}
-if os.environ.get("AB_SET") == "probe":  # split-K: atomics vs plain stores (timing probe, wrong results)
-    SHAPES = [s for s in SHAPES if s[0].startswith(("tt_dw", "dw_"))]
-    VARIANTS = {f"{e}_sp{sp}": ({"DCT_GEMM_SPLIT_PROBE": "1"} if e == "plain" else {}) | {"DCT_GEMM_SPLITS": str(sp)}
-                for e in ("atom", "plain") for sp in (4, 16, 64, 128, 256, 512)}
-
+if os.environ.get("AB_SET") == "tab":  # the tabular step's big GEMMs: every 4096 x 1024 x 1024 tiling
+    SHAPES = [s for s in SHAPES if s[0] in ("fwd_l1", "dx_l1")]
+    VARIANTS = {"bm64": {}, "bm128": {"DCT_GEMM_BM128": "1"}, "bm128_s4": {"DCT_GEMM_BM128": "1", "DCT_GEMM_STAGES": "4"},
+                "8w_s4": {"DCT_GEMM_8W": "1"}}
 if os.environ.get("AB_SET") == "layout":  # transformer dW shapes in every operand layout (what would a
     # feature-major copy of the activations buy?): (1,0) = today's dZ^T X on token-major storage
     SHAPES = [(f"{n}_ta{ta}tb{tb}", M, N, K, ta, tb, 1) for n, M, N, K, *_ in SHAPES if n.startswith("tt_dw")
@@ -102,6 +101,7 @@ def main():
             for k in ENV_KEYS:
                 os.environ.pop(k, None)
             os.environ.update(env)
+            nat.reload_knobs()  # the launcher reads the knob struct, not the environment
             for name, M, N, K, ta, tb, of in SHAPES:
                 A, B, C = bufs[name]
 

@@ -55,6 +55,7 @@ def main():
     print(json.dumps({"variant": "chain(4 kernels)", "us": round(timeit(chain), 2)}), flush=True)
     for waves, rpw in ((4, 4), (4, 8), (4, 2), (8, 4), (8, 2)):
         os.environ["DCT_SKINNY_HEAD_WAVES"], os.environ["DCT_SKINNY_HEAD_RPW"] = str(waves), str(rpw)
+        native().reload_knobs()  # the launchers read the knob struct, filled at plan / bind time
         print(json.dumps({"variant": f"fused waves={waves} rows/wave={rpw}", "us": round(timeit(fused), 2)}),
               flush=True)
 
