@@ -426,12 +426,13 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
   // 4 CONSECUTIVE columns 16j + 4g .. +3 -> 8-byte bf16 / 16-byte fp32 row stores instead of
   // 2-byte scattered ones (and 4-wide bias / aux loads).
   if (SPLIT && g.split_ws) {
-    // Workspace split-K (opt-in, DCT_GEMM_SPLIT_WS=1: the deterministic mode): every slice stores
-    // its partial tile (element-major, 1 KB per store instruction across the workgroup), the LAST
-    // slice to arrive at the tile sums all partials in slice order and writes C once, so dW is
-    // bit-reproducible run to run.  Agent-scope stores/loads + fences keep the partials coherent
-    // across the 8 XCDs' L2s - and those fences (L2 writeback per workgroup) make it SLOWER than
-    // the fp32 atomics: tabular 4x1024 step 0.203 -> 0.291 ms (profiles/gemm_splitk_ws_ab_r1.log).
+    // In-launch split-K reduction (DCT_GEMM_SPLIT_WS=1; deterministic): every slice stores its
+    // partial tile with plain stores (element-major, 1 KB per store instruction across the
+    // workgroup) and publishes it with ONE agent-scope release by thread 0 before taking the tile's
+    // ticket; the slice drawing the last ticket acquires once and sums the partials in slice order
+    // (bit-reproducible) into C, so no reduce launch follows.  (A __threadfence() in every thread
+    // plus agent-scope element stores / loads measured SLOWER than fp32 atomics: tabular step 0.203
+    // -> 0.291 ms, profiles/gemm_splitk_ws_ab_r1.log.)
     constexpr int NE = IM * 16;
     float* slot = g.split_ws + ((size_t)tile * splits + split) * (BM * GBN);
 #pragma unroll
@@ -439,20 +440,25 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          __hip_atomic_store(slot + ((i * 4 + j) * 4 + r) * GNT + tid, acc[i][j][r], __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-    __shared__ int is_last;
-    __threadfence();
-    __syncthreads();
+        for (int r = 0; r < 4; ++r) slot[((i * 4 + j) * 4 + r) * GNT + tid] = acc[i][j][r];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's stores have retired; the k-loop's LDS images are free
+    volatile int* is_last = reinterpret_cast<volatile int*>(smem2);  // one __shared__ object: no second array
     if (tid == 0) {
-      const int prev = __hip_atomic_fetch_add(g.split_cnt + tile, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      is_last = (prev == splits - 1);
-      if (is_last) __hip_atomic_store(g.split_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int prev = __hip_atomic_fetch_add(g.split_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == splits - 1;
+      if (last) __hip_atomic_store(g.split_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *is_last = last;
     }
     __syncthreads();
-    if (!is_last) return;
-    __threadfence();
+    if (!*is_last) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
     float sum[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) sum[e] = 0.f;
@@ -468,8 +474,7 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
       } else {
         const float* ps = base + (size_t)sp * (BM * GBN);
 #pragma unroll
-        for (int e = 0; e < NE; ++e)
-          sum[e] += __hip_atomic_load(ps + e * GNT + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int e = 0; e < NE; ++e) sum[e] += ps[e * GNT + tid];
       }
     }
     const int col_l = lane & 15, row_l = (lane >> 4) * 4;

@@ -50,7 +50,7 @@ VARIANTS = {
     "s4_splits128": {"DCT_GEMM_STAGES": "4", "DCT_GEMM_SPLITS": "128"},
 }
 ENV_KEYS = ("DCT_GEMM_STAGES", "DCT_GEMM_SPLIT_WG", "DCT_GEMM_SPLITS", "DCT_GEMM_BM64_NK", "DCT_GEMM_SPLIT_TWO_PASS",
-            "DCT_GEMM_8W", "DCT_GEMM_BM128")
+            "DCT_GEMM_8W", "DCT_GEMM_BM128", "DCT_GEMM_SPLIT_WS")
 if os.environ.get("AB_SET") == "dw":  # split-K sweep on the transformer dW shapes only
     SHAPES = [s for s in SHAPES if s[0].startswith("tt_dw") or s[0] == "dw_l1"]
     VARIANTS = {f"{st}_sp{sp}": {"DCT_GEMM_STAGES": st[1], "DCT_GEMM_SPLITS": str(sp)}
@@ -76,6 +76,7 @@ if os.environ.get("AB_SET") == "dwcmp":  # the tabular dW shapes: default launch
 if os.environ.get("AB_SET") == "twopass":  # split-K dW: two-pass partials + reduce vs fp32 atomics
     SHAPES = [s for s in SHAPES if s[0] in ("dw_l1", "dw_l0") or s[0].startswith("tt_dw")]
     VARIANTS = {"two_pass": {"DCT_GEMM_SPLIT_TWO_PASS": "1"}, "atomics": {"DCT_GEMM_SPLIT_TWO_PASS": "0"},
+                "in_launch": {"DCT_GEMM_SPLIT_WS": "1"},
                 "two_pass_wg512": {"DCT_GEMM_SPLIT_TWO_PASS": "1", "DCT_GEMM_SPLIT_WG": "512"},
                 "two_pass_wg1024": {"DCT_GEMM_SPLIT_TWO_PASS": "1", "DCT_GEMM_SPLIT_WG": "1024"}}
 
