@@ -33,7 +33,7 @@ typedef __attribute__((address_space(3))) void lds_void;
     }                                                                               \
   } while (0)
 
-constexpr int BK = 64;  // k per stage: one image row = 128 B = 8 chunks of 16 B
+// KB: k per stage (64 or 128); an image row is 2 KB bytes = KB / 8 chunks of 16 B
 
 __host__ __device__ inline uint16_t f2bf(float f) {
   uint32_t u = __builtin_bit_cast(uint32_t, f);
@@ -44,17 +44,18 @@ __host__ __device__ inline float bf2f(uint16_t h) {
   return __builtin_bit_cast(float, (uint32_t)h << 16);
 }
 
-// ROWS x 64 bf16 image, row r's 16-B chunk c stored at physical chunk c ^ (r & 7) (conflict-free
+// ROWS x KB bf16 image, row r's 16-B chunk c stored at physical chunk c ^ (r & (CPR - 1)) (conflict-free
 // ds_read_b128 fragments); the DMA writes lane-linear LDS, so the swizzle is on the source address
-template <int ROWS, int NT>
+template <int ROWS, int NT, int KB>
 __device__ __forceinline__ void fill(const uint16_t* __restrict__ G, int ld, int r0, int k0, char* img, int tid) {
-  constexpr int CH = ROWS * 8 / NT;
-  static_assert(CH >= 1 && CH * NT == ROWS * 8, "whole chunks per thread");
+  constexpr int CPR = KB / 8;
+  constexpr int CH = ROWS * CPR / NT;
+  static_assert(CH >= 1 && CH * NT == ROWS * CPR, "whole chunks per thread");
   const int wave = tid >> 6, lane = tid & 63;
 #pragma unroll
   for (int q = 0; q < CH; ++q) {
     const int L = q * NT + wave * 64 + lane;
-    const int r = L >> 3, c = (L & 7) ^ (r & 7);
+    const int r = L / CPR, c = (L % CPR) ^ (r & (CPR - 1));
     const uint16_t* src = G + (size_t)(r0 + r) * ld + k0 + c * 8;
     const uint32_t dst =
         __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void*)(img + (q * NT + wave * 64) * 16));
@@ -66,10 +67,12 @@ __device__ __forceinline__ void fill(const uint16_t* __restrict__ G, int ld, int
   }
 }
 
+template <int KB>
 __device__ __forceinline__ bf16x8 frag(const char* img, int rb, int ks, int lane) {
+  constexpr int CPR = KB / 8;
   const int row = rb + (lane & 15);
   const int c = ks * 4 + (lane >> 4);
-  return *reinterpret_cast<const bf16x8*>(img + row * 128 + ((c ^ (row & 7)) << 4));
+  return *reinterpret_cast<const bf16x8*>(img + row * (2 * KB) + ((c ^ (row & (CPR - 1))) << 4));
 }
 
 template <int F>
@@ -84,22 +87,22 @@ __device__ __forceinline__ unsigned long long stamp() { return __builtin_amdgcn_
 
 // LW > 0: producer / consumer - WM x WN compute waves never issue a load, LW loader waves only
 // fill stages (they wait for their own DMA before the shared barrier)
-template <int BM, int BN, int WM, int WN, int S, int MODE, bool PROF, int LW = 0>
+template <int BM, int BN, int WM, int WN, int S, int MODE, bool PROF, int LW = 0, int KB = 64>
 __global__ __launch_bounds__(64 * (WM * WN + LW)) void probe_gemm(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                          uint16_t* __restrict__ C, int M, int N, int K,
                                                          unsigned long long* __restrict__ prof, int ld) {
   constexpr int NC = 64 * WM * WN;          // compute threads
   constexpr int LNT = LW > 0 ? 64 * LW : NC;  // loading threads
   constexpr int IM = BM / WM / 16, JN = BN / WN / 16;
-  constexpr int IMG_A = BM * 128, STAGE = (BM + BN) * 128;
-  constexpr int F = (BM + BN) * 8 / LNT;  // LDS-DMA instructions per loading thread per stage
+  constexpr int IMG_A = BM * 2 * KB, STAGE = (BM + BN) * 2 * KB;
+  constexpr int F = (BM + BN) * (KB / 8) / LNT;  // LDS-DMA instructions per loading thread per stage
   static_assert(S >= 2 && S <= 4 && 3 * F <= 63, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int tiles_n = N / BN;
   const int m0 = (wg / tiles_n) * BM, n0 = (wg % tiles_n) * BN;
-  const int nk = K / BK;
+  const int nk = K / KB;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool is_loader = LW > 0 && wave >= WM * WN;
   const bool does_load = LW == 0 || is_loader, does_mma = LW == 0 || !is_loader;
@@ -112,8 +115,8 @@ __global__ __launch_bounds__(64 * (WM * WN + LW)) void probe_gemm(const uint16_t
     for (int j = 0; j < JN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   auto fill_stage = [&](int s, int kt) {
     char* base = smem + s * STAGE;
-    fill<BM, LNT>(A, ld, m0, kt * BK, base, ltid);
-    fill<BN, LNT>(B, ld, n0, kt * BK, base + IMG_A, ltid);
+    fill<BM, LNT, KB>(A, ld, m0, kt * KB, base, ltid);
+    fill<BN, LNT, KB>(B, ld, n0, kt * KB, base + IMG_A, ltid);
   };
   unsigned long long t_wait = 0, t_bar = 0, t_comp = 0;
   const unsigned long long t_start = PROF ? stamp() : 0ull;
@@ -136,13 +139,13 @@ __global__ __launch_bounds__(64 * (WM * WN + LW)) void probe_gemm(const uint16_t
     const char* ai = smem + cur * STAGE;
     const char* bi = ai + IMG_A;
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
+    for (int ks = 0; ks < KB / 32; ++ks) {
       if (!does_mma) break;
       bf16x8 af[IM], bfr[JN];
 #pragma unroll
-      for (int i = 0; i < IM; ++i) af[i] = frag(ai, wr * (BM / WM) + i * 16, ks, lane);
+      for (int i = 0; i < IM; ++i) af[i] = frag<KB>(ai, wr * (BM / WM) + i * 16, ks, lane);
 #pragma unroll
-      for (int j = 0; j < JN; ++j) bfr[j] = frag(bi, wc * (BN / WN) + j * 16, ks, lane);
+      for (int j = 0; j < JN; ++j) bfr[j] = frag<KB>(bi, wc * (BN / WN) + j * 16, ks, lane);
 #pragma unroll
       for (int i = 0; i < IM; ++i)
 #pragma unroll
@@ -207,20 +210,20 @@ struct Ctx {
   hipStream_t st;
 };
 
-template <int BM, int BN, int WM, int WN, int S, int MODE, int LW = 0>
+template <int BM, int BN, int WM, int WN, int S, int MODE, int LW = 0, int KB = 64>
 void run(Ctx& c, const char* name, int iters, bool padded = false) {
   const uint16_t* A = padded ? c.Ap : c.A;
   const uint16_t* B = padded ? c.Bp : c.B;
   const int ld = padded ? c.K + 64 : c.K;
-  if (c.M % BM || c.N % BN || c.K % BK) {
+  if (c.M % BM || c.N % BN || c.K % KB) {
     printf("{\"variant\": \"%s\", \"skipped\": \"shape\"}\n", name);
     return;
   }
   constexpr int NT = 64 * (WM * WN + LW);
   const int grid = (c.M / BM) * (c.N / BN);
-  const size_t lds = (size_t)S * (BM + BN) * 128;
-  auto k = probe_gemm<BM, BN, WM, WN, S, MODE, false, LW>;
-  auto kp = probe_gemm<BM, BN, WM, WN, S, MODE, true, LW>;
+  const size_t lds = (size_t)S * (BM + BN) * 2 * KB;
+  auto k = probe_gemm<BM, BN, WM, WN, S, MODE, false, LW, KB>;
+  auto kp = probe_gemm<BM, BN, WM, WN, S, MODE, true, LW, KB>;
   CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   CK(hipFuncSetAttribute((const void*)kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, c.st, A, B, c.C, c.M, c.N, c.K, c.prof, ld);
@@ -269,8 +272,8 @@ void run(Ctx& c, const char* name, int iters, bool padded = false) {
          "{\"total\": %.0f, \"max_total\": %.0f, \"wait\": %.0f, \"barrier\": %.0f, \"issue\": %.0f}, "
          "\"per_kstep\": {\"wait\": %.0f, \"barrier\": %.0f, \"issue\": %.0f}}\n",
          name, c.M, c.N, c.K, grid, NT, lds / 1024, per[per.size() / 2], per[0], flop / per[per.size() / 2] / 1e6, err,
-         s[0] / nw, mx, s[1] / nw, s[2] / nw, s[3] / nw, s[1] / nw / (c.K / BK), s[2] / nw / (c.K / BK),
-         s[3] / nw / (c.K / BK));
+         s[0] / nw, mx, s[1] / nw, s[2] / nw, s[3] / nw, s[1] / nw / (c.K / KB), s[2] / nw / (c.K / KB),
+         s[3] / nw / (c.K / KB));
   fflush(stdout);
   CK(hipEventDestroy(e0));
   CK(hipEventDestroy(e1));
@@ -324,13 +327,14 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(c.href.data(), c.ref, ns * 4, hipMemcpyDeviceToHost));
   const int it = 50;
   run<128, 128, 2, 2, 2, 0>(c, "t128x128_w2x2_s2", it);
-  run<128, 128, 2, 2, 2, 0>(c, "t128x128_w2x2_s2_padded", it, true);
   run<64, 128, 2, 2, 2, 0>(c, "t64x128_w2x2_s2", it);
-  run<64, 128, 2, 2, 2, 0>(c, "t64x128_w2x2_s2_padded", it, true);
-  run<128, 128, 2, 2, 4, 0, 4>(c, "pc_t128x128_w2x2_l4_s4", it);
-  run<128, 128, 2, 2, 4, 0, 4>(c, "pc_t128x128_w2x2_l4_s4_padded", it, true);
-  run<128, 128, 2, 2, 4, 1, 4>(c, "pc_t128x128_w2x2_l4_s4_nomfma_padded", it, true);
   run<128, 128, 2, 2, 4, 0, 8>(c, "pc_t128x128_w2x2_l8_s4", it);
-  run<128, 128, 2, 2, 4, 0, 8>(c, "pc_t128x128_w2x2_l8_s4_padded", it, true);
+  run<128, 128, 2, 2, 2, 0, 0, 128>(c, "t128x128_w2x2_s2_bk128", it);
+  run<64, 128, 2, 2, 2, 0, 0, 128>(c, "t64x128_w2x2_s2_bk128", it);
+  run<128, 128, 2, 2, 2, 0, 8, 128>(c, "pc_t128x128_w2x2_l8_s2_bk128", it);
+  run<128, 128, 2, 2, 2, 1, 8, 128>(c, "pc_t128x128_w2x2_l8_s2_bk128_nomfma", it);
+  run<128, 128, 4, 2, 2, 0, 0, 128>(c, "t128x128_w4x2_s2_bk128", it);
+  run<64, 64, 2, 2, 2, 0, 0, 128>(c, "t64x64_w2x2_s2_bk128", it);
+  run<64, 64, 2, 2, 3, 0, 0, 128>(c, "t64x64_w2x2_s3_bk128", it);
   return 0;
 }
