@@ -228,12 +228,14 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 __device__ __forceinline__ int mc_swz(int k) { return ((k & 3) | ((k >> 1) & 4)) << 1; }
 
-// one ROWS x 64 operand tile -> LDS image (ROWS/32 glds per thread; the MC image is 128 wide)
-template <bool MC, int ROWS = 128, int NT = 256>
+// one ROWS x KT operand tile -> LDS image (the MC image is 128 wide, KT k-rows of 256 B).  KT = 64:
+// row-major (KC) rows of 128 B; KT = 128: rows of 256 B (16 chunks, swizzled by r & 15)
+template <bool MC, int ROWS = 128, int NT = 256, int KT = 64>
 __device__ __forceinline__ void g2_fill(const uint16_t* __restrict__ G, int ld, int R, int r0, int k0, char* img) {
   static_assert(ROWS == 128 || !MC, "k-major (MC) images are 128 columns wide");
-  constexpr int CH = (MC ? 1024 : ROWS * 8) / NT;  // 16-B chunks per thread
-  static_assert(CH >= 1 && CH * NT == (MC ? 1024 : ROWS * 8), "whole chunks per thread");
+  constexpr int CPR = KT / 8;  // 16-B chunks per KC row
+  constexpr int CH = (MC ? KT * 16 : ROWS * CPR) / NT;  // 16-B chunks per thread
+  static_assert(CH >= 1 && CH * NT == (MC ? KT * 16 : ROWS * CPR), "whole chunks per thread");
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
 #pragma unroll
@@ -241,8 +243,8 @@ __device__ __forceinline__ void g2_fill(const uint16_t* __restrict__ G, int ld, 
     const int L = q * NT + wave * 64 + lane;  // linear 16-B chunk of the image
     const uint16_t* src;
     if (!MC) {
-      const int r = L >> 3, pc = L & 7;
-      const int c = pc ^ (r & 7);
+      const int r = L / CPR, pc = L % CPR;
+      const int c = pc ^ (r & (CPR - 1));
       int row = r0 + r;
       row = row < R ? row : R - 1;
       src = G + (size_t)row * ld + k0 + c * 8;
@@ -268,12 +270,12 @@ __device__ __forceinline__ void g2_fill(const uint16_t* __restrict__ G, int ld, 
 }
 
 // 16 x 32 operand fragment (rows rb..rb+15, k-slice ks) in the MFMA A/B layout
-template <bool MC>
+template <bool MC, int KT = 64>
 __device__ __forceinline__ bf16x8 g2_frag(const char* img, int rb, int ks, int lane) {
   if (!MC) {
     const int row = rb + (lane & 15);
     const int c = ks * 4 + (lane >> 4);
-    return *reinterpret_cast<const bf16x8*>(img + row * 128 + ((c ^ (row & 7)) << 4));
+    return *reinterpret_cast<const bf16x8*>(img + row * (2 * KT) + ((c ^ (row & (KT / 8 - 1))) << 4));
   } else {
     const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
     const int k = ks * 32 + 8 * g + q;
@@ -338,10 +340,15 @@ __device__ __forceinline__ int xcd_wgid() {
 
 // WM: waves along M (2: 256 threads, 2 x 2 waves; 4: 512 threads, 4 x 2 waves - two waves per SIMD
 // on a one-tile-per-CU grid, so one wave's LDS reads / waits overlap the other's MFMAs).
-template <bool TA, bool TB, bool SPLIT, int BM, int S, int WM = 2>
+// KT: k per LDS stage.  128 (8-wave tiles only): each KC row contributes 256 contiguous bytes per
+// stage instead of 128 - the one-tile-per-CU grids are bound by the CU's global -> LDS rate, which the
+// longer row segments raise (tools/probes/gemm_probe.hip: 4096 x 1024 x 1024 NT 14.3 -> 12.7 us).
+template <bool TA, bool TB, bool SPLIT, int BM, int S, int WM = 2, int KT = 64>
 __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wgid) {
   static_assert(BM == 128 || (BM == 64 && !TA), "BM = 64 needs a row-major (KC) A image");
   static_assert(WM == 2 || (WM == 4 && !SPLIT && BM == 128), "8-wave tiles: 128 x 128, no split-K");
+  static_assert(KT == 64 || (KT == 128 && WM == 4 && S == 2), "128-deep k stages: 8-wave tiles, 2 stages");
+  constexpr int IMG = 128 * 2 * KT;  // bytes of one 128-row (or MC 128-column) operand image
   constexpr int NT = 128 * WM;
   constexpr int IM = BM / (16 * WM);  // 16-row MFMA tiles per wave (WM x 2 waves)
   extern __shared__ __attribute__((aligned(16))) char smem2[];
@@ -351,7 +358,7 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
   const int tiles_n = (g.N + GBN - 1) / GBN;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int m0 = tm * BM, n0 = tn * GBN;
-  const int nk_all = g.K / GBK;
+  const int nk_all = g.K / KT;
   const int per = (nk_all + splits - 1) / splits;
   const int kt0 = split * per;
   const int kt1 = min(nk_all, kt0 + per);
@@ -367,16 +374,16 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
   // colsum: one wave column (wc == 0) of the first N tile sums its A rows
   const bool do_cs = g.colsum != nullptr && tn == 0 && wc == 0;
   float cs[IM] = {};
-  auto img = [&](int buf, int op) -> char* { return smem2 + (buf * 2 + op) * G2_BYTES; };
+  auto img = [&](int buf, int op) -> char* { return smem2 + (buf * 2 + op) * IMG; };
   auto fill = [&](int buf, int kt) {
-    const int k0 = kt * GBK;
-    if (!TA) g2_fill<false, BM, NT>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
-    else g2_fill<true, 128, NT>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
-    if (TB) g2_fill<false, 128, NT>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
-    else g2_fill<true, 128, NT>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
+    const int k0 = kt * KT;
+    if (!TA) g2_fill<false, BM, NT, KT>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
+    else g2_fill<true, 128, NT, KT>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
+    if (TB) g2_fill<false, 128, NT, KT>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
+    else g2_fill<true, 128, NT, KT>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
   };
   // global_load_lds per thread per fill (A + B)
-  constexpr int FILL_OPS = ((TA ? 1024 : BM * 8) + 1024) / NT;
+  constexpr int FILL_OPS = ((TA ? 16 * KT : BM * KT / 8) + 16 * KT) / NT;
   const int n = kt1 - kt0;
   if (n > 0) {
 #pragma unroll
@@ -390,12 +397,12 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
       const char* ai = img(cur, 0);
       const char* bi = img(cur, 1);
 #pragma unroll
-      for (int ks = 0; ks < GBK / 32; ++ks) {
+      for (int ks = 0; ks < KT / 32; ++ks) {
         bf16x8 af[IM], bfr[4];
 #pragma unroll
-        for (int i = 0; i < IM; ++i) af[i] = g2_frag<AMC>(ai, wr * (BM / WM) + i * 16, ks, lane);
+        for (int i = 0; i < IM; ++i) af[i] = g2_frag<AMC, KT>(ai, wr * (BM / WM) + i * 16, ks, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bfr[j] = g2_frag<BMC>(bi, wc * 64 + j * 16, ks, lane);
+        for (int j = 0; j < 4; ++j) bfr[j] = g2_frag<BMC, KT>(bi, wc * 64 + j * 16, ks, lane);
         if (do_cs) {  // fused bias gradient: row sums of the A fragments (lane: 8 k of row l&15)
 #pragma unroll
           for (int i = 0; i < IM; ++i)
@@ -638,9 +645,9 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
   }
 }
 
-template <bool TA, bool TB, bool SPLIT, int BM = 128, int S = 2, int WM = 2>
+template <bool TA, bool TB, bool SPLIT, int BM = 128, int S = 2, int WM = 2, int KT = 64>
 __global__ __launch_bounds__(128 * WM, WM == 4 ? 2 : (BM == 64 ? 4 : 2)) void gemm2_kernel(GemmArgs g, int splits) {
-  gemm2_body<TA, TB, SPLIT, BM, S, WM>(g, splits, xcd_wgid());
+  gemm2_body<TA, TB, SPLIT, BM, S, WM, KT>(g, splits, xcd_wgid());
 }
 
 // Grouped split-K launch: up to DW_GROUP independent problems (the dW GEMMs of one transformer
@@ -892,10 +899,20 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
     hipLaunchKernelGGL(fn, dim3(grid), dim3(threads), lds, st, g, splits);
     return hipGetLastError();
   };
-  // DCT_GEMM_8W=1: one 128 x 128 tile per CU worked by 8 waves (two per SIMD) with three k-tiles in
-  // flight (4 LDS stages, 128 KB) for grids of at most one tile per CU
-  if (kn.gemm_8w && splits == 1 && tiles <= device_cus() && nk >= 4)
-    return launch(dct::gemm2_kernel<TA, TB, false, 128, 4, 4>, tiles, 4, 512);
+  // between one half and one 128 x 128 tile per CU (the 4096 x 1024 MLP layers: 256 tiles): 8 waves (two per SIMD)
+  // and 128-deep k stages.  Such grids are bound by each CU's global -> LDS rate, and 256-byte row
+  // segments per stage raise it: 4096 x 1024 x 1024 fwd / dX 15.1 / 17.2 -> 13.4 / 14.8 us
+  // (half-height tiles, two per CU, below), tabular step 176.2 -> 175.7 us
+  // (profiles/gemm_k128_ab_r4.log, tools/probes/gemm_probe.hip).  DCT_GEMM_8W=0 turns it off.
+  if (kn.gemm_8w != 0 && splits == 1 && tiles <= device_cus() && 2 * tiles > device_cus() && g.K % 128 == 0 &&
+      g.K >= 512) {
+    auto fn = dct::gemm2_kernel<TA, TB, false, 128, 2, 4, 128>;
+    const size_t lds = (size_t)2 * 2 * (128 * 2 * 128);  // 2 stages x (A + B) images of 128 x 128 bf16
+    e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(fn, dim3(tiles), dim3(512), lds, st, g, 1);
+    return hipGetLastError();
+  }
   if constexpr (!TA) {
     // small K and too few 128-row tiles to fill 256 CUs several times over: half-height tiles
     const bool force128 = kn.gemm_bm128 != 0;

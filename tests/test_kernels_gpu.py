@@ -373,16 +373,20 @@ def test_gemm_pipeline_depths(M, N, K, ta, tb, out_f32, stages, cuda, monkeypatc
     assert (C.float() - ref).abs().max().item() < tol, (C.float() - ref).abs().max().item()
 
 
+@pytest.mark.parametrize("mode", ["-1", "0"])
 @pytest.mark.parametrize("M,N,K,ta,tb", [
     (4096, 1024, 1024, 0, 1),  # tabular forward layer: 256 tiles, one per CU
     (4096, 1024, 1024, 0, 0),  # tabular dX layer (transposed-read B image)
     (1024, 512, 256, 1, 0),    # transposed A image, 4 k-tiles (the prologue fills the whole loop)
+    (2048, 2048, 512, 1, 1),   # transposed A image, KC B image, 256 tiles x 4 128-deep k stages
+    (3000, 1024, 1024, 0, 1),  # 192 tiles, ragged M edge
     (300, 200, 512, 0, 1),     # ragged tile edges
 ])
-def test_gemm_8wave_tiles(M, N, K, ta, tb, cuda, monkeypatch):
-    """DCT_GEMM_8W=1: 128 x 128 tiles worked by 8 waves (4 x 2, two per SIMD) with 4 LDS stages, with
+def test_gemm_8wave_tiles(M, N, K, ta, tb, mode, cuda, monkeypatch):
+    """One-tile-per-CU grids: 128 x 128 tiles worked by 8 waves (4 x 2, two per SIMD) with 2 LDS stages
+    of 128-deep k (default, DCT_GEMM_8W=-1) or the half-height two-per-CU tiles (DCT_GEMM_8W=0), with
     the bias + ReLU epilogue, bf16 out, against the fp32 torch reference of the same bf16 operands."""
-    setknob(monkeypatch, "DCT_GEMM_8W", "1")
+    setknob(monkeypatch, "DCT_GEMM_8W", mode)
     torch.manual_seed(13)
     A = _bf(torch.randn(K, M, device=cuda) if ta else torch.randn(M, K, device=cuda))
     B = _bf(torch.randn(N, K, device=cuda) if tb else torch.randn(K, N, device=cuda))

@@ -62,8 +62,9 @@ if os.environ.get("AB_SET") == "bm64":  # half-height tiles (2 workgroups per CU
                                                                               "DCT_GEMM_STAGES": "4"}}
 if os.environ.get("AB_SET") == "tab":  # the tabular step's big GEMMs: every 4096 x 1024 x 1024 tiling
     SHAPES = [s for s in SHAPES if s[0] in ("fwd_l1", "dx_l1")]
-    VARIANTS = {"bm64": {}, "bm128": {"DCT_GEMM_BM128": "1"}, "bm128_s4": {"DCT_GEMM_BM128": "1", "DCT_GEMM_STAGES": "4"},
-                "8w_s4": {"DCT_GEMM_8W": "1"}}
+    VARIANTS = {"8w_k128": {}, "bm64": {"DCT_GEMM_8W": "0"},
+                "bm128": {"DCT_GEMM_8W": "0", "DCT_GEMM_BM128": "1"},
+                "bm128_s4": {"DCT_GEMM_8W": "0", "DCT_GEMM_BM128": "1", "DCT_GEMM_STAGES": "4"}}
 if os.environ.get("AB_SET") == "layout":  # transformer dW shapes in every operand layout (what would a
     # feature-major copy of the activations buy?): (1,0) = today's dZ^T X on token-major storage
     SHAPES = [(f"{n}_ta{ta}tb{tb}", M, N, K, ta, tb, 1) for n, M, N, K, *_ in SHAPES if n.startswith("tt_dw")
