@@ -124,10 +124,14 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
   pending_.assign(nb, 0);
   launched_.assign(nb, 0);
   hip_check(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking), "hipStreamCreate");
-  // DCT_REDUCER_INLINE=1: collectives on the compute stream itself - no overlap with backward,
-  // but no cross-stream edges either (each costs ~5-15 us inside a replayed HIP graph, measured
-  // with the one-rank communicator: profiles/ddp_reducer_w1_r3.log)
-  inline_ = dct::knobs().reducer_inline != 0;
+  // Collectives on the compute stream itself while the step is being captured into a HIP graph
+  // (DCT_REDUCER_INLINE=-1, default; 1 = always, 0 = never).  In a replayed graph the comm stream
+  // buys no overlap on this ROCm: the replay runs a forked branch's node and the compute node after
+  // the fork one after the other, and every cross-stream edge adds 5-16 us of idle GPU (kernel
+  // trace of the forced-DDP tabular step: profiles/ddp_reducer_graph_edges_r4.log).  Eager steps
+  // keep the comm stream, where the next backward kernels do run beside a bucket's collective.
+  inline_knob_ = dct::knobs().reducer_inline;
+  inline_ = inline_knob_ == 1;
   ready_events_.resize(nb);
   for (auto& e : ready_events_) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
   hip_check(hipEventCreateWithFlags(&done_event_, hipEventDisableTiming), "hipEventCreate");
@@ -183,8 +187,19 @@ void BucketReducer::reset_timing() {
   hip_check(hipMemcpy(stamps_, h, sizeof(h), hipMemcpyHostToDevice), "reset reducer stamps");
 }
 
+bool BucketReducer::step_inline(void* compute_stream) {
+  if (inline_knob_ >= 0) return inline_knob_ == 1;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(reinterpret_cast<hipStream_t>(compute_stream), &st) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return st == hipStreamCaptureStatusActive;
+}
+
 void BucketReducer::launch_bucket(int b, uintptr_t compute_stream) {
   hipStream_t cs = reinterpret_cast<hipStream_t>(compute_stream);
+  inline_ = step_inline(cs);
   hipStream_t rs = inline_ ? cs : comm_stream_;
   if (!inline_) {
     hip_check(hipEventRecord(ready_events_[b], cs), "hipEventRecord");
@@ -219,6 +234,7 @@ int BucketReducer::mark_ready(int param_idx, uintptr_t compute_stream) {
 
 void BucketReducer::finalize(uintptr_t compute_stream) {
   hipStream_t cs = reinterpret_cast<hipStream_t>(compute_stream);
+  inline_ = step_inline(cs);
   hipStream_t rs = inline_ ? cs : comm_stream_;
   n_before_finalize_ = n_launched_;
   if (timing_) {  // end of backward on the compute stream, ordered before the comm stream's close

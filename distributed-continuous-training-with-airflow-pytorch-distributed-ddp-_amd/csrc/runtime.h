@@ -67,7 +67,9 @@ class BucketReducer {
   hipEvent_t tail_event_ = nullptr;
   unsigned long long* stamps_ = nullptr;  // [8], see step_kernels.hip reducer_close_kernel
   bool timing_ = false, check_ = false;
-  bool inline_ = false;  // DCT_REDUCER_INLINE=1: collectives on the compute stream
+  int inline_knob_ = -1;  // DCT_REDUCER_INLINE (1 / 0 / -1 = inline while the compute stream is capturing)
+  bool inline_ = false;   // this step's choice (collectives on the compute stream)
+  bool step_inline(void* compute_stream);
 };
 
 // Receive buffers of the in-kernel (xGMI) gradient exchange.  Each rank allocates an
