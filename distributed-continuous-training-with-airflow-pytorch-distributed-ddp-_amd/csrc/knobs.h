@@ -35,7 +35,7 @@ struct Knobs {
   // wide-MLP step executor (mlp_executor.cpp), bucket reducer (runtime.cpp)
   int fused_head = 1;       // DCT_FUSED_HEAD=0: the four-kernel head chain
   int dw_into_adam = 1;     // DCT_DW_INTO_ADAM=0: dW through g and the reduce pass
-  int reducer_inline = -1;  // DCT_REDUCER_INLINE=1 / 0: collectives on the compute / a comm stream (-1: inline under graph capture)
+  int reducer_inline = 1;   // DCT_REDUCER_INLINE=1 / 0 / -1: collectives on the compute stream / a comm stream / inline under graph capture only
 };
 
 const Knobs& knobs();

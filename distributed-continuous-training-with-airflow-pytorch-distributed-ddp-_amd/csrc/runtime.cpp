@@ -124,12 +124,13 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
   pending_.assign(nb, 0);
   launched_.assign(nb, 0);
   hip_check(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking), "hipStreamCreate");
-  // Collectives on the compute stream itself while the step is being captured into a HIP graph
-  // (DCT_REDUCER_INLINE=-1, default; 1 = always, 0 = never).  In a replayed graph the comm stream
-  // buys no overlap on this ROCm: the replay runs a forked branch's node and the compute node after
-  // the fork one after the other, and every cross-stream edge adds 5-16 us of idle GPU (kernel
-  // trace of the forced-DDP tabular step: profiles/ddp_reducer_graph_edges_r4.log).  Eager steps
-  // keep the comm stream, where the next backward kernels do run beside a bucket's collective.
+  // Collectives on the compute stream itself (DCT_REDUCER_INLINE=1, default; 0 = a comm stream,
+  // -1 = on the compute stream only while the step is captured into a HIP graph).  In a replayed
+  // graph the comm stream buys no overlap on this ROCm: the replay runs a forked branch's node and
+  // the compute node after the fork one after the other, and every cross-stream edge adds 5-16 us
+  // of idle GPU (kernel trace of the forced-DDP tabular step: profiles/ddp_reducer_graph_edges_r4.log);
+  // eagerly the fork / join events cost more than the overlap returns at one rank (tabular step
+  // 227 vs 196 us).  Multi-GPU overlap is unmeasured on these one-GPU boxes: DCT_REDUCER_INLINE=0.
   inline_knob_ = dct::knobs().reducer_inline;
   inline_ = inline_knob_ == 1;
   ready_events_.resize(nb);

@@ -1,14 +1,17 @@
-"""``GraphMLPEngine``: the wide-MLP data-parallel step as ONE replayed hipGraph.
+"""``GraphMLPEngine``: the wide-MLP data-parallel step issued by ONE native step executor.
 
 For MLPs too wide for the single-CU fused kernels (the BASELINE "100M rows x 256 features,
 4-layer MLP-1024h" config) the step is issued by the native ``MlpStepExecutor``
 (csrc/mlp_executor.cpp): HBM-resident bf16 dataset -> device batch gather -> bf16 MFMA GEMMs
 with fused bias/activation epilogues -> fused loss + dlogits -> backward GEMMs writing fp32
-gradients straight into the flat DDP bucket buffer -> RCCL ncclAvg per bucket on a side stream
-as soon as the layer's dW is enqueued (overlap with the earlier layers' backward) -> fused flat
-Adam with bf16 shadow weights.  The batch cursor, Adam step and loss slot live in device memory,
-so the step is captured once and replayed for every full batch of an epoch; the partial last
-batch (reference ``drop_last=False``) runs eagerly with its real row count.
+gradients straight into the flat DDP bucket buffer -> RCCL ncclAvg per bucket as soon as the
+layer's dW is enqueued -> fused flat Adam with bf16 shadow weights.  The batch cursor, Adam step
+and loss slot live in device memory, so the step needs no host round trip: by default the C++
+executor simply enqueues it for every batch (11 launches from C++ stay ahead of the GPU: 171-173
+us/step), and ``DCT_MLP_GRAPH=1`` captures it once into a hipGraph replayed per full batch (175.5-
+176.9 us/step on ROCm 7: every replay starts ~8 us after the previous one ends; 8 steps per graph
+were slower still, profiles/tabular_graph_steps_ab_r2.log, profiles/mlp_graph_vs_eager_ab_r4.log).
+The partial last batch (reference ``drop_last=False``) runs with its real row count.
 
 Gradient buffer ``g`` (flat, parameter order + the loss slot): with a DDP reducer it holds every
 averaged gradient after a step.  WITHOUT one (world size 1), up to two hidden layers hand their
@@ -68,7 +71,9 @@ class GraphMLPEngine:
         self.loss = spec["loss"]
         self.adam = adam
         self.device = dev = ctx.device
-        self.use_graph = (os.environ.get("DCT_GRAPH", "1") != "0") if use_graph is None else use_graph
+        if use_graph is None:
+            use_graph = os.environ.get("DCT_MLP_GRAPH", "0") == "1" and os.environ.get("DCT_GRAPH", "1") != "0"
+        self.use_graph = use_graph
         L = len(self.dims) - 1
         self.L = L
         self.numels = []
