@@ -86,6 +86,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--sets", type=int, default=1,
+                    help="operand sets rotated per launch: > 3 sets of the 4096x1024 shapes exceed the 8 XCDs' L2 "
+                         "(the in-step situation: operands from the Infinity Cache, not a hot L2)")
     a = ap.parse_args()
     nat = native()
     dev = torch.device("cuda", 0)
@@ -94,10 +97,13 @@ def main():
     res = {}
     bufs = {}
     for name, M, N, K, ta, tb, of in SHAPES:
-        A = (torch.rand(K, M, device=dev) * 2 - 1 if ta else torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
-        B = (torch.rand(N, K, device=dev) * 2 - 1 if tb else torch.rand(K, N, device=dev) * 2 - 1).to(torch.bfloat16)
+        sets = []
+        for _ in range(a.sets):
+            A = (torch.rand(K, M, device=dev) * 2 - 1 if ta else torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+            B = (torch.rand(N, K, device=dev) * 2 - 1 if tb else torch.rand(K, N, device=dev) * 2 - 1).to(torch.bfloat16)
+            sets.append((A, B))
         C = torch.empty(M, N, device=dev, dtype=torch.float32 if of else torch.bfloat16)
-        bufs[name] = (A, B, C)
+        bufs[name] = (sets, C)
     for _ in range(a.rounds):
         for vname, env in VARIANTS.items():
             for k in ENV_KEYS:
@@ -105,9 +111,12 @@ def main():
             os.environ.update(env)
             nat.reload_knobs()  # the launcher reads the knob struct, not the environment
             for name, M, N, K, ta, tb, of in SHAPES:
-                A, B, C = bufs[name]
+                sets, C = bufs[name]
+                cyc = [0]
 
                 def run():
+                    A, B = sets[cyc[0] % len(sets)]
+                    cyc[0] += 1
                     nat.gemm_bf16(A.data_ptr(), B.data_ptr(), C.data_ptr(), 0, M, N, K, A.stride(0), B.stride(0), N,
                                   ta, tb, 0, of, 0, 0, st)
                 for _ in range(3):
@@ -122,7 +131,7 @@ def main():
     for k in ENV_KEYS:
         os.environ.pop(k, None)
     for name, M, N, K, ta, tb, of in SHAPES:  # hipBLASLt (torch.matmul) on the same operands
-        A, B, C = bufs[name]
+        (A, B), C = bufs[name][0][0], bufs[name][1]
         At = A.t() if ta else A
         Bt = B.t() if tb else B
         out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
