@@ -168,9 +168,9 @@ std::vector<double> BucketReducer::read_timing() const {
   std::vector<double> out(4, 0.0);
   if (!stamps_) return out;
   unsigned long long h[8];
-  // the close kernel of the last step runs on the non-blocking comm stream: a legacy-stream copy
-  // is not ordered after it
-  hip_check(hipStreamSynchronize(comm_stream_), "hipStreamSynchronize");
+  // the close kernel of the last step runs on the non-blocking comm stream, or inline on the
+  // caller's compute stream: a legacy-stream copy is ordered after neither
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
   hip_check(hipMemcpy(h, stamps_, sizeof(h), hipMemcpyDeviceToHost), "read reducer stamps");
   out[0] = (double)h[2] / 1e5;  // s_memrealtime ticks at 100 MHz -> ms
   out[1] = (double)h[3] / 1e5;
