@@ -346,7 +346,7 @@ __device__ __forceinline__ int xcd_wgid() {
 template <bool TA, bool TB, bool SPLIT, int BM, int S, int WM = 2, int KT = 64>
 __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wgid) {
   static_assert(BM == 128 || (BM == 64 && !TA), "BM = 64 needs a row-major (KC) A image");
-  static_assert(WM == 2 || (WM == 4 && !SPLIT && BM == 128), "8-wave tiles: 128 x 128, no split-K");
+  static_assert(WM == 2 || (WM == 4 && BM == 128), "8-wave tiles: 128 x 128");
   static_assert(KT == 64 || (KT == 128 && WM == 4 && S == 2), "128-deep k stages: 8-wave tiles, 2 stages");
   constexpr int IMG = 128 * 2 * KT;  // bytes of one 128-row (or MC 128-column) operand image
   constexpr int NT = 128 * WM;
@@ -432,7 +432,7 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
   // accumulator is the TRANSPOSED tile: lane (c = lane&15, g = lane>>4) holds row 16i + c and the
   // 4 CONSECUTIVE columns 16j + 4g .. +3 -> 8-byte bf16 / 16-byte fp32 row stores instead of
   // 2-byte scattered ones (and 4-wide bias / aux loads).
-  if (SPLIT && g.split_ws) {
+  if (SPLIT && WM == 2 && g.split_ws) {  // (the 8-wave split kernels never get a workspace)
     // In-launch split-K reduction (DCT_GEMM_SPLIT_WS=1; deterministic): every slice stores its
     // partial tile with plain stores (element-major, 1 KB per store instruction across the
     // workgroup) and publishes it with ONE agent-scope release by thread 0 before taking the tile's
@@ -661,13 +661,13 @@ struct GemmGroup {
   int n;
 };
 
-template <bool TA, bool TB, int S>
-__global__ __launch_bounds__(GNT, 2) void gemm2_grouped_kernel(GemmGroup gg) {
+template <bool TA, bool TB, int S, int WM = 2>
+__global__ __launch_bounds__(128 * WM, 2) void gemm2_grouped_kernel(GemmGroup gg) {
   const int w = xcd_wgid();
   int p = 0;
 #pragma unroll
   for (int i = 1; i < DW_GROUP; ++i) p += (i < gg.n && w >= gg.start[i]) ? 1 : 0;
-  gemm2_body<TA, TB, true, 128, S>(gg.g[p], gg.splits[p], w - gg.start[p]);
+  gemm2_body<TA, TB, true, 128, S, WM>(gg.g[p], gg.splits[p], w - gg.start[p]);
 }
 
 // zero the fp32 C[M, ldc] panel that split-K slices accumulate into (a kernel node, not a
@@ -926,8 +926,14 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
   }
   if (splits > 1) {
     const int grid = tiles * splits;
-    e = gemm_stages(grid, nk_slice) == 4 ? launch(dct::gemm2_kernel<TA, TB, true, 128, 4>, grid, 4)
-                                         : launch(dct::gemm2_kernel<TA, TB, true, 128, 2>, grid, 2);
+    // 8 waves (two per SIMD) on the split-K dW tiles: more loads in flight per CU on these
+    // load-path-bound one-tile-per-CU grids - tabular step 170.9 -> 165.9 us, the TabTransformer's
+    // grouped dW launch unchanged (profiles/gemm_split_8w_ab_r4.log); DCT_GEMM_SPLIT_8W=0 = 4 waves
+    if (kn.gemm_split_8w && !g.split_ws && gemm_stages(grid, nk_slice) != 4)
+      e = launch(dct::gemm2_kernel<TA, TB, true, 128, 2, 4>, grid, 2, 512);
+    else
+      e = gemm_stages(grid, nk_slice) == 4 ? launch(dct::gemm2_kernel<TA, TB, true, 128, 4>, grid, 4)
+                                           : launch(dct::gemm2_kernel<TA, TB, true, 128, 2>, grid, 2);
     if (e != hipSuccess || !g.split_part) return e;
     const int64_t n4 = ((int64_t)g.M * g.N + 3) / 4;
     hipLaunchKernelGGL(dct::splitk_reduce_kernel, dim3((int)std::min<int64_t>(2048, (n4 + 255) / 256)), dim3(256), 0,
@@ -957,11 +963,13 @@ extern "C" int dct_gemm_bf16_dw_partials(const uint16_t* dZ, const uint16_t* X, 
   const int tiles = ((M + dct::GBM - 1) / dct::GBM) * ((N + dct::GBN - 1) / dct::GBN);
   const int nk_slice = (nk + splits - 1) / splits;
   if ((splits - 1) * nk_slice >= nk) return (int)hipErrorInvalidValue;  // an empty slice would store zeros: fine, but keep it tight
-  auto fn = dct::gemm2_kernel<true, false, true, 128, 2>;
+  const bool w8 = dct::knobs().gemm_split_8w != 0;
+  auto fn = w8 ? dct::gemm2_kernel<true, false, true, 128, 2, 4> : dct::gemm2_kernel<true, false, true, 128, 2>;
   const size_t lds = (size_t)(nk_slice > 1 ? 4 : 2) * dct::G2_BYTES;
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(fn, dim3(tiles * splits), dim3(dct::GNT), lds, reinterpret_cast<hipStream_t>(stream), g, splits);
+  hipLaunchKernelGGL(fn, dim3(tiles * splits), dim3(w8 ? 512 : dct::GNT), lds, reinterpret_cast<hipStream_t>(stream),
+                     g, splits);
   return (int)hipGetLastError();
 }
 
@@ -1101,10 +1109,12 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
   }
   const bool s4 = kn.gemm_stages >= 4 && max_slice >= 3;
   const size_t lds = (size_t)(max_slice > 1 ? (s4 ? 8 : 4) : 2) * dct::G2_BYTES;
-  auto fn = s4 ? dct::gemm2_grouped_kernel<true, false, 4> : dct::gemm2_grouped_kernel<true, false, 2>;
+  const bool w8 = kn.gemm_split_8w != 0 && !s4;
+  auto fn = s4 ? dct::gemm2_grouped_kernel<true, false, 4>
+               : (w8 ? dct::gemm2_grouped_kernel<true, false, 2, 4> : dct::gemm2_grouped_kernel<true, false, 2>);
   e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(fn, dim3(total), dim3(dct::GNT), lds, st, gg);
+  hipLaunchKernelGGL(fn, dim3(total), dim3(w8 ? 512 : dct::GNT), lds, st, gg);
   e = hipGetLastError();
   if (e != hipSuccess || !part) return (int)e;
   hipLaunchKernelGGL(dct::splitk_reduce_grouped_kernel,

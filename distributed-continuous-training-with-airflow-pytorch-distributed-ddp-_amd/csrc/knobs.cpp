@@ -32,6 +32,7 @@ void knobs_reload() {
   k.gemm_split_wg = env_int("DCT_GEMM_SPLIT_WG", 0);
   k.gemm_splits = env_int("DCT_GEMM_SPLITS", 0);
   k.gemm_8w = env_int("DCT_GEMM_8W", -1);  // -1 auto, 0 off
+  k.gemm_split_8w = env_int("DCT_GEMM_SPLIT_8W", 1) != 0;
   k.gemm_bm128 = env_set("DCT_GEMM_BM128");
   k.gemm_bm64_nk = env_int("DCT_GEMM_BM64_NK", 4);
   k.gemm_no_group = env_set("DCT_GEMM_NO_GROUP");

@@ -22,6 +22,7 @@ struct Knobs {
   int gemm_split_wg = 0;    // DCT_GEMM_SPLIT_WG: split-K workgroup target (0: one per CU)
   int gemm_splits = 0;      // DCT_GEMM_SPLITS: fixed split-K slice count (0: auto)
   int gemm_8w = -1;         // DCT_GEMM_8W=0: no 8-wave 128-deep-k tiles for <= 1 tile per CU
+  int gemm_split_8w = 1;    // DCT_GEMM_SPLIT_8W=0: 4-wave split-K dW tiles (the 8-wave ones are the default)
   int gemm_bm128 = 0;       // DCT_GEMM_BM128: no half-height tiles
   int gemm_bm64_nk = 4;     // DCT_GEMM_BM64_NK: half-height tiles up to this many k-tiles
   int gemm_no_group = 0;    // DCT_GEMM_NO_GROUP: grouped dW as one launch per problem
