@@ -902,10 +902,11 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
   // between one half and one 128 x 128 tile per CU (the 4096 x 1024 MLP layers: 256 tiles): 8 waves (two per SIMD)
   // and 128-deep k stages.  Such grids are bound by each CU's global -> LDS rate, and 256-byte row
   // segments per stage raise it: 4096 x 1024 x 1024 fwd / dX 15.1 / 17.2 -> 13.4 / 14.8 us
-  // (half-height tiles, two per CU, below), tabular step 176.2 -> 175.7 us
-  // (profiles/gemm_k128_ab_r4.log, tools/probes/gemm_probe.hip).  DCT_GEMM_8W=0 turns it off.
+  // (half-height tiles, two per CU, below), tabular step 176.2 -> 175.7 us; from K = 256 on (the
+  // 256-feature input layer: two k stages) 166.7 -> 163.7 us (profiles/gemm_k128_ab_r4.log,
+  // tools/probes/gemm_probe.hip).  DCT_GEMM_8W=0 turns it off.
   if (kn.gemm_8w != 0 && splits == 1 && tiles <= device_cus() && 2 * tiles > device_cus() && g.K % 128 == 0 &&
-      g.K >= 512) {
+      g.K >= 256) {
     auto fn = dct::gemm2_kernel<TA, TB, false, 128, 2, 4, 128>;
     const size_t lds = (size_t)2 * 2 * (128 * 2 * 128);  // 2 stages x (A + B) images of 128 x 128 bf16
     e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

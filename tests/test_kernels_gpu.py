@@ -377,6 +377,7 @@ def test_gemm_pipeline_depths(M, N, K, ta, tb, out_f32, stages, cuda, monkeypatc
 @pytest.mark.parametrize("M,N,K,ta,tb", [
     (4096, 1024, 1024, 0, 1),  # tabular forward layer: 256 tiles, one per CU
     (4096, 1024, 1024, 0, 0),  # tabular dX layer (transposed-read B image)
+    (4096, 1024, 256, 0, 1),   # tabular input layer: two 128-deep k stages
     (1024, 512, 256, 1, 0),    # transposed A image, 4 k-tiles (the prologue fills the whole loop)
     (2048, 2048, 512, 1, 1),   # transposed A image, KC B image, 256 tiles x 4 128-deep k stages
     (3000, 1024, 1024, 0, 1),  # 192 tiles, ragged M edge
