@@ -45,6 +45,7 @@ void knobs_reload() {
   k.fused_head = env_int("DCT_FUSED_HEAD", 1) != 0;
   k.dw_into_adam = env_int("DCT_DW_INTO_ADAM", 1) != 0;
   k.reducer_inline = env_int("DCT_REDUCER_INLINE", 1);
+  k.rccl_one_rank = env_int("DCT_RCCL_ONE_RANK", 0) == 1;
   if (k.reducer_inline > 1 || k.reducer_inline < -1) k.reducer_inline = -1;
   g_knobs = k;
   g_loaded = true;

@@ -37,6 +37,7 @@ struct Knobs {
   int fused_head = 1;       // DCT_FUSED_HEAD=0: the four-kernel head chain
   int dw_into_adam = 1;     // DCT_DW_INTO_ADAM=0: dW through g and the reduce pass
   int reducer_inline = 1;   // DCT_REDUCER_INLINE=1 / 0 / -1: collectives on the compute stream / a comm stream / inline under graph capture only
+  int rccl_one_rank = 0;    // DCT_RCCL_ONE_RANK=1: call RCCL for one-rank in-place collectives too
 };
 
 const Knobs& knobs();

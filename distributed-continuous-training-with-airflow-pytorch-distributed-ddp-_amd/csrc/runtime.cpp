@@ -66,6 +66,12 @@ Comm::Comm(const std::string& uid, int world, int rank, int device) : world_(wor
   ncclComm_t c;
   nccl_check(ncclCommInitRank(&c, world, id, rank), "ncclCommInitRank");
   comm_ = c;
+  // An in-place all-reduce / broadcast over ONE rank is the identity (x / 1 is exact in fp32), yet
+  // RCCL's one-rank path runs a pre-multiply kernel plus ~4 blit copies / fills per call (~13 us on
+  // MI355X, profiles/rccl_one_rank_r4.log).  One-rank communicators (a DDP job of world size 1, the
+  // DCT_FORCE_DDP=1 rehearsals) skip it; DCT_RCCL_ONE_RANK=1 calls RCCL anyway.
+  dct::knobs_reload();
+  identity_ = world == 1 && !dct::knobs().rccl_one_rank;
 }
 
 Comm::~Comm() {
@@ -73,7 +79,7 @@ Comm::~Comm() {
 }
 
 void Comm::allreduce(uintptr_t buf, int64_t count, int dtype, int op, uintptr_t stream) {
-  if (count <= 0) return;
+  if (count <= 0 || identity_) return;
   nccl_check(ncclAllReduce(reinterpret_cast<void*>(buf), reinterpret_cast<void*>(buf), (size_t)count,
                            to_nccl_dtype(dtype), to_nccl_op(op), reinterpret_cast<ncclComm_t>(comm_),
                            reinterpret_cast<hipStream_t>(stream)),
@@ -81,7 +87,7 @@ void Comm::allreduce(uintptr_t buf, int64_t count, int dtype, int op, uintptr_t 
 }
 
 void Comm::broadcast(uintptr_t buf, int64_t count, int dtype, int root, uintptr_t stream) {
-  if (count <= 0) return;
+  if (count <= 0 || identity_) return;
   nccl_check(ncclBroadcast(reinterpret_cast<void*>(buf), reinterpret_cast<void*>(buf), (size_t)count,
                            to_nccl_dtype(dtype), root, reinterpret_cast<ncclComm_t>(comm_),
                            reinterpret_cast<hipStream_t>(stream)),

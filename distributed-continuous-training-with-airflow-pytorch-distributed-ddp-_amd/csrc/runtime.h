@@ -28,6 +28,7 @@ class Comm {
  private:
   void* comm_ = nullptr;
   int world_ = 1, rank_ = 0, device_ = 0;
+  bool identity_ = false;  // one rank: in-place collectives are the identity, RCCL is not called
 };
 
 class BucketReducer {
