@@ -20,6 +20,7 @@ W (W + 1) / 2) before it is timed.  Times are the max over ranks; ``algbw = byte
 from __future__ import annotations
 
 import json
+import os
 import time
 from typing import Dict, List, Optional, Sequence
 
@@ -50,7 +51,17 @@ def _native_comm(ctx: DistContext):
     if ctx.is_distributed:
         return init_native_comm(ctx)
     nat = native()  # W = 1: a single-rank communicator still exercises the RCCL launch path
-    return nat.Comm(nat.comm_unique_id(), 1, 0, ctx.device.index)
+    # (the benchmark's point, so the Comm must not skip the identity collective - DCT_RCCL_ONE_RANK)
+    prev = os.environ.get("DCT_RCCL_ONE_RANK")
+    os.environ["DCT_RCCL_ONE_RANK"] = "1"
+    try:
+        return nat.Comm(nat.comm_unique_id(), 1, 0, ctx.device.index)
+    finally:
+        if prev is None:
+            os.environ.pop("DCT_RCCL_ONE_RANK", None)
+        else:
+            os.environ["DCT_RCCL_ONE_RANK"] = prev
+        nat.reload_knobs()
 
 
 def _max_over_ranks(ctx: DistContext, x: float) -> float:

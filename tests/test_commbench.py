@@ -59,3 +59,29 @@ def test_native_and_graph_paths_on_device():
     assert all(r["correct"] and r["us"] > 0 for r in recs)
     recs = run(ctx, [4096], "bf16", ("native",), iters=2, warmup=1)
     assert recs[0]["correct"] and recs[0]["bytes"] == 4096
+
+
+@pytest.mark.gpu
+def test_one_rank_collectives_are_the_identity(monkeypatch):
+    """A one-rank communicator skips in-place all-reduce / broadcast (RCCL's one-rank path is a
+    pre-multiply kernel plus blits for the identity); DCT_RCCL_ONE_RANK=1 calls RCCL - both leave
+    the buffer bit-identical."""
+    import torch
+
+    from dct_amd.ops._native import native
+
+    nat = native()
+    x = torch.randn(10_001, device="cuda")
+    for force in ("0", "1"):
+        monkeypatch.setenv("DCT_RCCL_ONE_RANK", force)
+        comm = nat.Comm(nat.comm_unique_id(), 1, 0, 0)
+        y = x.clone()
+        st = torch.cuda.current_stream().cuda_stream
+        comm.allreduce(y.data_ptr(), y.numel(), nat.DT_F32, nat.OP_AVG, st)
+        comm.allreduce(y.data_ptr(), y.numel(), nat.DT_F32, nat.OP_SUM, st)
+        comm.broadcast(y.data_ptr(), y.numel(), nat.DT_F32, 0, st)
+        torch.cuda.synchronize()
+        assert torch.equal(x, y), force
+        del comm
+    monkeypatch.delenv("DCT_RCCL_ONE_RANK")
+    nat.reload_knobs()
