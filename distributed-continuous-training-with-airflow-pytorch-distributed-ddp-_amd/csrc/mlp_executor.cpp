@@ -19,8 +19,9 @@
 //                         the earlier layers' backward GEMMs keep running) ; dA_l = dZ W_l
 //   finalize              compute stream waits for the last bucket
 //   adam_flat             fp32 master update + bf16 shadow weights for the next forward's GEMMs;
-//                         [no reducer: the 2-4-way split-K slices of up to two hidden layers' dW
-//                          are summed here, in slice order, instead of by a reduce pass into g]
+//                         [no reducer: the 2-8-way split-K slices of up to three layers' dW are
+//                          summed here, in slice order, instead of by a reduce pass or fp32
+//                          atomics into g]
 //                         its first thread writes loss_out[cursor] = reduced loss, cursor += 1
 // (the step prologue, gradient zeroing, loss slot and epilogue ride inside the gather, loss and
 // Adam kernels instead of a memset node and three single-thread launches)
@@ -139,7 +140,7 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   int* cur = reinterpret_cast<int*>(cursor);
   int* sc = reinterpret_cast<int*>(step_counter);
-  bool part_used[2] = {false, false};
+  bool part_used[3] = {false, false, false};
   if (reducer_) reducer_->prepare();
   ck(dct_gather_batch_step(reinterpret_cast<const void*>(X), row_bytes, reinterpret_cast<const int*>(Y),
                            reinterpret_cast<const int*>(idx), cur, B_, rows, n_items, acts_[0], y_, sc, g_, P_ + 1, st),
@@ -229,9 +230,9 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
   }
   if (reducer_) reducer_->finalize(stream);
   int np = 0;
-  int64_t poff[2], pn[2];
-  const float* pp[2];
-  int psp[2];
+  int64_t poff[3], pn[3];
+  const float* pp[3];
+  int psp[3];
   for (int q = 0; q < nparts_; ++q) {
     if (!part_used[q]) continue;
     const int l = part_layer_[q];
@@ -256,14 +257,16 @@ int MlpStepExecutor::part_slot(int l) const {
 }
 
 void MlpStepExecutor::plan_partials() {
-  // up to two hidden layers whose dW the launcher would split 2..4 ways (the two-pass regime):
-  // their slices go straight to Adam.  Only without a DDP reducer (it must all-reduce g).
+  // up to three layers whose dW the launcher would split 2..8 ways: their slices go straight to
+  // Adam (no reduce pass for 2-4 slices, no fp32 atomics into g for 5-8 - the tabular input
+  // layer's 1024 x 256 x 4096 dW, 8 slices on 128 workgroups).  Only without a DDP reducer (it
+  // must all-reduce g).
   if (reducer_) return;
-  for (int l = L_ - 1; l >= 0 && nparts_ < 2; --l) {
+  for (int l = L_ - 1; l >= 0 && nparts_ < 3; --l) {
     if (skinny(l)) continue;
     const int M = dims_[l + 1], N = dims_[l];
     const int sp = dct_gemm_dw_auto_splits(M, N, B_);
-    if (sp < 2 || sp > 4 || (woff_[l] & 3) || (((int64_t)M * N) & 3)) continue;
+    if (sp < 2 || sp > 8 || (woff_[l] & 3) || (((int64_t)M * N) & 3)) continue;
     float* buf = nullptr;
     if (hipMalloc(&buf, (size_t)sp * M * N * sizeof(float)) != hipSuccess) {
       (void)hipGetLastError();

@@ -59,8 +59,8 @@ class MlpStepExecutor {
   float lr_ = 1e-3f, b1_ = 0.9f, b2_ = 0.999f, eps_ = 1e-8f, wd_ = 0.f;
   int decoupled_ = 0;
   // split-K dW slices handed to Adam (plan_partials): device buffers [splits][M][N]
-  float* part_[2] = {nullptr, nullptr};
-  int part_layer_[2] = {-1, -1}, part_splits_[2] = {1, 1};
+  float* part_[3] = {nullptr, nullptr, nullptr};
+  int part_layer_[3] = {-1, -1, -1}, part_splits_[3] = {1, 1, 1};
   int nparts_ = 0;
   int part_fallbacks_ = 0;  // steps whose planned split-K slices went through g instead (short batch)
 };

@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "dct_common.h"
 
 namespace dct {
@@ -33,13 +35,13 @@ struct AdamArgs {
   const float* loss_slot;
   float* loss_out;
   int loss_cap;
-  // optional (adam_flat_kernel<true>): split-K partials, <= 4 slices, standing in for g over
-  // whole float4-aligned ranges (the wide-MLP executor's dW GEMMs without a DDP reducer):
-  // g[off + e] = sum_s part[r][s * n + e] in slice order, the values the reduce pass would store
+  // optional (adam_flat_kernel<true, S>): split-K partials, <= S (4 or 8) slices, standing in for g
+  // over up to three whole float4-aligned ranges (the wide-MLP executor's dW GEMMs without a DDP
+  // reducer): g[off + e] = sum_s part[r][s * n + e] in slice order, the values the reduce pass would store
   int nparts;
-  int64_t part_off[2], part_n[2];
-  const float* part[2];
-  int part_splits[2];
+  int64_t part_off[3], part_n[3];
+  const float* part[3];
+  int part_splits[3];
 };
 
 __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, const AdamArgs& a) {
@@ -55,7 +57,7 @@ __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, 
   p -= a.step_size * m / denom;
 }
 
-template <bool PARTS>
+template <bool PARTS, int S = 4>
 __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a) {
   if (a.cursor && blockIdx.x == 0 && threadIdx.x == 0) {
     const int c = a.cursor[0];
@@ -82,24 +84,28 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamArgs a) {
       // every load unconditional (selected addresses, masked values): a load behind a branch
       // drains the load queue (s_waitcnt vmcnt(0)); slices summed in order, as the reduce does
       const int64_t e = 4 * i;
+      // (selects, not a runtime index into the by-value kernel arguments: that would copy them to scratch)
       const bool in0 = a.nparts > 0 && e >= a.part_off[0] && e < a.part_off[0] + a.part_n[0];
       const bool in1 = a.nparts > 1 && e >= a.part_off[1] && e < a.part_off[1] + a.part_n[1];
-      const bool in = in0 || in1;
-      const float4* ps = reinterpret_cast<const float4*>(in1 ? a.part[1] : a.part[0]);
-      const int64_t n4r = (in1 ? a.part_n[1] : a.part_n[0]) >> 2;
-      const int64_t e4 = (e - (in1 ? a.part_off[1] : a.part_off[0])) >> 2;
-      const int sp = in1 ? a.part_splits[1] : a.part_splits[0];
+      const bool in2 = a.nparts > 2 && e >= a.part_off[2] && e < a.part_off[2] + a.part_n[2];
+      const bool in = in0 || in1 || in2;
+      const float4* ps = reinterpret_cast<const float4*>(in2 ? a.part[2] : (in1 ? a.part[1] : a.part[0]));
+      const int64_t n4r = (in2 ? a.part_n[2] : (in1 ? a.part_n[1] : a.part_n[0])) >> 2;
+      const int64_t e4 = (e - (in2 ? a.part_off[2] : (in1 ? a.part_off[1] : a.part_off[0]))) >> 2;
+      const int sp = in ? (in2 ? a.part_splits[2] : (in1 ? a.part_splits[1] : a.part_splits[0])) : 1;
       const float4* q0 = in ? ps + e4 : g4 + i;
-      const float4* q1 = (in && sp > 1) ? ps + n4r + e4 : q0;
-      const float4* q2 = (in && sp > 2) ? ps + 2 * n4r + e4 : q0;
-      const float4* q3 = (in && sp > 3) ? ps + 3 * n4r + e4 : q0;
-      const float4 v0 = *q0, v1 = *q1, v2 = *q2, v3 = *q3;
-      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      const float4 t1 = (in && sp > 1) ? v1 : z4, t2 = (in && sp > 2) ? v2 : z4, t3 = (in && sp > 3) ? v3 : z4;
-      g.x = ((v0.x + t1.x) + t2.x) + t3.x;
-      g.y = ((v0.y + t1.y) + t2.y) + t3.y;
-      g.z = ((v0.z + t1.z) + t2.z) + t3.z;
-      g.w = ((v0.w + t1.w) + t2.w) + t3.w;
+      float4 vs[S];
+#pragma unroll
+      for (int q = 0; q < S; ++q) vs[q] = *((in && q < sp) ? ps + q * n4r + e4 : q0);
+      g = vs[0];
+#pragma unroll
+      for (int q = 1; q < S; ++q) {
+        const bool t = q < sp;
+        g.x += t ? vs[q].x : 0.f;
+        g.y += t ? vs[q].y : 0.f;
+        g.z += t ? vs[q].z : 0.f;
+        g.w += t ? vs[q].w : 0.f;
+      }
     }
     adam_one(p.x, g.x, m.x, v.x, a);
     adam_one(p.y, g.y, m.y, v.y, a);
@@ -175,14 +181,15 @@ int dct_adam_flat_step(float* p, const float* g, float* m, float* v, uint16_t* p
   return (int)hipGetLastError();
 }
 
-// dct_adam_flat_step with up to two gradient ranges read from split-K partials (see AdamArgs)
+// dct_adam_flat_step with up to three gradient ranges read from split-K partials of up to 8 slices
+// (see AdamArgs)
 int dct_adam_flat_step_parts(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, float lr,
                              float b1, float b2, float eps, float wd, float grad_scale, int decoupled,
                              const int* step_counter, int* cursor, const float* loss_slot, float* loss_out,
                              int loss_cap, int nparts, const int64_t* part_off, const int64_t* part_n,
                              const float* const* part, const int* part_splits, void* stream) {
   if (n <= 0) return 0;
-  if (!step_counter || (cursor && !loss_slot) || nparts < 0 || nparts > 2) return (int)hipErrorInvalidValue;
+  if (!step_counter || (cursor && !loss_slot) || nparts < 0 || nparts > 3) return (int)hipErrorInvalidValue;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return (int)hipErrorInvalidValue;
   dct::AdamArgs a{};
   a.p = p; a.g = g; a.m = m; a.v = v; a.p_bf16 = p_bf16; a.n = n;
@@ -195,14 +202,19 @@ int dct_adam_flat_step_parts(float* p, const float* g, float* m, float* v, uint1
   a.loss_out = loss_out;
   a.loss_cap = loss_cap;
   a.nparts = nparts;
+  int max_sp = 1;
   for (int r = 0; r < nparts; ++r) {
     if ((part_off[r] | part_n[r]) & 3 || part_off[r] + part_n[r] > (n & ~3LL) || ((uintptr_t)part[r] & 15) ||
-        part_splits[r] < 1 || part_splits[r] > 4)
+        part_splits[r] < 1 || part_splits[r] > 8)
       return (int)hipErrorInvalidValue;
     a.part_off[r] = part_off[r]; a.part_n[r] = part_n[r]; a.part[r] = part[r]; a.part_splits[r] = part_splits[r];
+    max_sp = std::max(max_sp, part_splits[r]);
   }
-  hipLaunchKernelGGL(dct::adam_flat_kernel<true>, dim3(grid_for((n + 3) / 4, 256)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), a);
+  const dim3 grid(grid_for((n + 3) / 4, 256));
+  if (max_sp > 4)
+    hipLaunchKernelGGL((dct::adam_flat_kernel<true, 8>), grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+  else
+    hipLaunchKernelGGL((dct::adam_flat_kernel<true, 4>), grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
   return (int)hipGetLastError();
 }
 

@@ -14,7 +14,7 @@ were slower still, profiles/tabular_graph_steps_ab_r2.log, profiles/mlp_graph_vs
 The partial last batch (reference ``drop_last=False``) runs with its real row count.
 
 Gradient buffer ``g`` (flat, parameter order + the loss slot): with a DDP reducer it holds every
-averaged gradient after a step.  WITHOUT one (world size 1), up to two hidden layers hand their
+averaged gradient after a step.  WITHOUT one (world size 1), up to three layers hand their
 split-K dW slices straight to the Adam kernel (``exe.partial_layers``), so those layers' weight
 ranges of ``g`` stay ZERO - read gradients through a reducer run (``DCT_FORCE_DDP=1``) or
 ``DCT_DW_INTO_ADAM=0`` for debugging / grad-norm checks.  A batch too short for the planned
