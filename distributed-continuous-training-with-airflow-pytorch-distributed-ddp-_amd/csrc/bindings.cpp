@@ -183,6 +183,7 @@ PYBIND11_MODULE(_dct_native, m) {
     d["skinny_head_waves"] = k.skinny_head_waves; d["skinny_dw_splits"] = k.skinny_dw_splits;
     d["tt_head_spb"] = k.tt_head_spb; d["attn_scalar"] = k.attn_scalar; d["fused_head"] = k.fused_head;
     d["dw_into_adam"] = k.dw_into_adam; d["reducer_inline"] = k.reducer_inline;
+    d["reducer_standin_us"] = k.reducer_standin_us; d["reducer_standin_wgs"] = k.reducer_standin_wgs;
     return d;
   });
   // PCI bus id of a device: identifies the physical GPU behind a rank (ranks sharing one GPU in a

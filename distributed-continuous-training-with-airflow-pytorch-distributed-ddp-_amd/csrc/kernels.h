@@ -34,6 +34,7 @@ struct GemmArgs {
 extern "C" {
 // reducer instrumentation (step_kernels.hip)
 int dct_reducer_stamp(unsigned long long* dst, void* stream);
+int dct_busy_spin(long long ticks, int wgs, void* stream);
 int dct_reducer_close(unsigned long long* s, void* stream);
 int dct_reducer_check(unsigned long long* s, void* stream);
 int dct_phase_accum(unsigned long long* b, int n, void* stream);

@@ -44,9 +44,14 @@ void knobs_reload() {
   k.attn_scalar = env_set("DCT_ATTN_SCALAR");
   k.fused_head = env_int("DCT_FUSED_HEAD", 1) != 0;
   k.dw_into_adam = env_int("DCT_DW_INTO_ADAM", 1) != 0;
-  k.reducer_inline = env_int("DCT_REDUCER_INLINE", 1);
+  k.reducer_inline = env_int("DCT_REDUCER_INLINE", -2);
   k.rccl_one_rank = env_int("DCT_RCCL_ONE_RANK", 0) == 1;
-  if (k.reducer_inline > 1 || k.reducer_inline < -1) k.reducer_inline = -1;
+  if (k.reducer_inline > 1 || k.reducer_inline < -2) k.reducer_inline = -2;
+  k.reducer_standin_us = env_int("DCT_REDUCER_STANDIN_US", 0);
+  k.reducer_standin_wgs = env_int("DCT_REDUCER_STANDIN_WGS", 16);
+  if (k.reducer_standin_us < 0) k.reducer_standin_us = 0;
+  if (k.reducer_standin_wgs < 1) k.reducer_standin_wgs = 1;
+  if (k.reducer_standin_wgs > 1024) k.reducer_standin_wgs = 1024;
   g_knobs = k;
   g_loaded = true;
 }

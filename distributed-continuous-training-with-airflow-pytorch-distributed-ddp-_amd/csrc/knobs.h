@@ -36,7 +36,11 @@ struct Knobs {
   // wide-MLP step executor (mlp_executor.cpp), bucket reducer (runtime.cpp)
   int fused_head = 1;       // DCT_FUSED_HEAD=0: the four-kernel head chain
   int dw_into_adam = 1;     // DCT_DW_INTO_ADAM=0: dW through g and the reduce pass
-  int reducer_inline = 1;   // DCT_REDUCER_INLINE=1 / 0 / -1: collectives on the compute stream / a comm stream / inline under graph capture only
+  int reducer_inline = -2;  // DCT_REDUCER_INLINE: -2 auto (compute stream only for a one-rank communicator without
+                            // a stand-in, else the comm stream), 1 compute stream, 0 comm stream, -1 inline under capture
+  int reducer_standin_us = 0;   // DCT_REDUCER_STANDIN_US: test-only stand-in collective - a busy kernel of this many us
+                                // per step (split over the buckets by size) on the collective's stream
+  int reducer_standin_wgs = 16; // DCT_REDUCER_STANDIN_WGS: its workgroups (one wave each, no LDS)
   int rccl_one_rank = 0;    // DCT_RCCL_ONE_RANK=1: call RCCL for one-rank in-place collectives too
 };
 

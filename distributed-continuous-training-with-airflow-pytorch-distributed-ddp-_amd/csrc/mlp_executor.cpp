@@ -71,7 +71,9 @@ MlpStepExecutor::MlpStepExecutor(const std::vector<int>& dims, int batch, int ac
                                  uintptr_t dz0, uintptr_t dz1, uintptr_t ybuf, uintptr_t stats,
                                  BucketReducer* reducer)
     : dims_(dims), B_(batch), act_(act), loss_kind_(loss_kind), reducer_(reducer) {
-  knobs_reload();  // plan time: the DCT_* knobs this executor's launches read
+  knobs_reload();  // plan time: this executor keeps its own copy of the DCT_* knobs its launches read
+  fused_head_knob_ = knobs().fused_head != 0;
+  dw_into_adam_knob_ = knobs().dw_into_adam != 0;
   L_ = (int)dims.size() - 1;
   if (L_ < 1) throw std::invalid_argument("MlpStepExecutor: need at least one layer");
   if ((int)acts.size() != L_ + 1) throw std::invalid_argument("MlpStepExecutor: need L+1 activation buffers");
@@ -107,7 +109,7 @@ void MlpStepExecutor::set_adam(float lr, float b1, float b2, float eps, float wd
 bool MlpStepExecutor::fused_head() const {
   // ReLU hidden layers only (GELU' needs the pre-activation: the unfused GEMM path); a skinny head
   // whose width fits the kernel's register budget; DCT_FUSED_HEAD=0 keeps the four-kernel chain
-  const bool off = !knobs().fused_head;
+  const bool off = !fused_head_knob_;
   const int l = L_ - 1;
   return !off && act_ == ACT_RELU && skinny(l) && dct_skinny_head_supported(dims_[l], dims_[L_]);
 }
@@ -250,7 +252,7 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
 }
 
 int MlpStepExecutor::part_slot(int l) const {
-  if (!knobs().dw_into_adam) return -1;  // dW through g and the reduce pass
+  if (!dw_into_adam_knob_) return -1;  // dW through g and the reduce pass
   for (int q = 0; q < nparts_; ++q)
     if (part_layer_[q] == l) return q;
   return -1;

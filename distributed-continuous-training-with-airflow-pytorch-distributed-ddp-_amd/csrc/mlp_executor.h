@@ -36,6 +36,7 @@ class MlpStepExecutor {
   MlpStepExecutor& operator=(const MlpStepExecutor&) = delete;
 
  private:
+  bool fused_head_knob_ = true, dw_into_adam_knob_ = true;  // DCT_FUSED_HEAD / DCT_DW_INTO_ADAM at construction
   void forward(int rows, hipStream_t st, int layers = -1);  // layers 0 .. layers-1 (default all)
   bool fused_head() const;
   void plan_partials();

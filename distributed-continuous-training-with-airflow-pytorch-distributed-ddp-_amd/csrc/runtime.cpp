@@ -130,15 +130,24 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
   pending_.assign(nb, 0);
   launched_.assign(nb, 0);
   hip_check(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking), "hipStreamCreate");
-  // Collectives on the compute stream itself (DCT_REDUCER_INLINE=1, default; 0 = a comm stream,
-  // -1 = on the compute stream only while the step is captured into a HIP graph).  In a replayed
-  // graph the comm stream buys no overlap on this ROCm: the replay runs a forked branch's node and
-  // the compute node after the fork one after the other, and every cross-stream edge adds 5-16 us
-  // of idle GPU (kernel trace of the forced-DDP tabular step: profiles/ddp_reducer_graph_edges_r4.log);
-  // eagerly the fork / join events cost more than the overlap returns at one rank (tabular step
-  // 227 vs 196 us).  Multi-GPU overlap is unmeasured on these one-GPU boxes: DCT_REDUCER_INLINE=0.
-  inline_knob_ = dct::knobs().reducer_inline;
+  // Where the collectives run (DCT_REDUCER_INLINE, read once here into this reducer's copy):
+  //   -2 (auto, default): on the compute stream only for a one-rank communicator (the identity: no
+  //      collective runs, and the fork / join events would cost 20-30 us per step for nothing,
+  //      profiles/ddp_reducer_inline_default_ab_r4.log), otherwise on the comm stream, so each
+  //      bucket's all-reduce overlaps the rest of backward (the DDP Reducer's point, reference
+  //      jobs/train_lightning_ddp.py:136);
+  //    1 / 0: always the compute / the comm stream; -1: inline while the step is being captured.
+  // The test-only stand-in collective (DCT_REDUCER_STANDIN_US) counts as a real collective.
+  const Knobs& k = dct::knobs();
+  standin_us_ = k.reducer_standin_us;
+  standin_wgs_ = k.reducer_standin_wgs;
+  inline_knob_ = k.reducer_inline;
+  if (inline_knob_ == -2) {
+    const bool identity = comm_ == nullptr || (comm_->world() == 1 && comm_->is_identity());
+    inline_knob_ = (identity && standin_us_ == 0) ? 1 : 0;
+  }
   inline_ = inline_knob_ == 1;
+  for (int64_t c : counts_) total_count_ += c;
   ready_events_.resize(nb);
   for (auto& e : ready_events_) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
   hip_check(hipEventCreateWithFlags(&done_event_, hipEventDisableTiming), "hipEventCreate");
@@ -217,6 +226,12 @@ void BucketReducer::launch_bucket(int b, uintptr_t compute_stream) {
   if (comm_) {
     comm_->allreduce(flat_ + (uintptr_t)(offsets_[b] * dsize_), counts_[b], dtype_, op_,
                      reinterpret_cast<uintptr_t>(rs));
+  }
+  if (standin_us_ > 0 && total_count_ > 0) {
+    // stand-in collective: busy workgroups for this bucket's share of the per-step time
+    const double us = (double)standin_us_ * (double)counts_[b] / (double)total_count_;
+    hip_check((hipError_t)dct_busy_spin((long long)(us * 100.0), standin_wgs_, reinterpret_cast<void*>(rs)),
+              "stand-in collective");
   }
   launched_[b] = 1;
   n_launched_++;

@@ -24,6 +24,7 @@ class Comm {
   void all_gather(uintptr_t send, uintptr_t recv, int64_t send_count, int dtype, uintptr_t stream);
   int rank() const { return rank_; }
   int world() const { return world_; }
+  bool is_identity() const { return identity_; }
 
  private:
   void* comm_ = nullptr;
@@ -68,7 +69,9 @@ class BucketReducer {
   hipEvent_t tail_event_ = nullptr;
   unsigned long long* stamps_ = nullptr;  // [8], see step_kernels.hip reducer_close_kernel
   bool timing_ = false, check_ = false;
-  int inline_knob_ = -1;  // DCT_REDUCER_INLINE (1 / 0 / -1 = inline while the compute stream is capturing)
+  int inline_knob_ = -1;  // DCT_REDUCER_INLINE resolved (1 / 0 / -1 = inline while the compute stream is capturing)
+  int standin_us_ = 0, standin_wgs_ = 16;  // DCT_REDUCER_STANDIN_US / _WGS (test-only stand-in collective)
+  int64_t total_count_ = 0;
   bool inline_ = false;   // this step's choice (collectives on the compute stream)
   bool step_inline(void* compute_stream);
 };

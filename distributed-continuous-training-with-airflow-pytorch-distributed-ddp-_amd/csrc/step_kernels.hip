@@ -160,6 +160,15 @@ __global__ void reducer_check_kernel(unsigned long long* s) {
   }
 }
 
+// Stand-in collective (test-only, DCT_REDUCER_STANDIN_US, runtime.cpp BucketReducer): each one-wave
+// workgroup stays resident for `ticks` of s_memrealtime (100 MHz) from its own start, sleeping
+// between polls - the CU / queue footprint of an all-reduce of that duration without its traffic,
+// so comm / compute overlap can be measured on a one-GPU box.
+__global__ __launch_bounds__(64) void busy_spin_kernel(long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while ((long long)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
 // Step-phase timing (utils/tracing.py DevicePhaseTimer): b[0..n) stamps of the phase marks of
 // the current step (reducer_stamp_kernel writes them), b[n..2n-1) accumulated ticks per phase,
 // b[2n-1] step count.  One thread; captured into step graphs like any kernel.
@@ -179,6 +188,13 @@ extern "C" {
 
 int dct_phase_accum(unsigned long long* b, int n, void* stream) {
   hipLaunchKernelGGL(dct::phase_accum_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), b, n);
+  return (int)hipGetLastError();
+}
+
+int dct_busy_spin(long long ticks, int wgs, void* stream) {
+  if (ticks <= 0) return 0;
+  if (wgs < 1 || wgs > 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(dct::busy_spin_kernel, dim3(wgs), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), ticks);
   return (int)hipGetLastError();
 }
 

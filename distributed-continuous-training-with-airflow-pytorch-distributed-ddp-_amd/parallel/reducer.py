@@ -44,7 +44,11 @@ def plan_buckets(numels: Sequence[int], elem_bytes: int = 4, bucket_cap_bytes: i
     """Buckets of consecutive parameters filled in REVERSE parameter order (backward order).
     ``split_before``: parameter indices that close the bucket being filled before they are added
     (a model whose gradients become ready in groups - the TabTransformer's grouped dW launches -
-    aligns buckets with those groups, so each bucket launches as its group finishes)."""
+    aligns buckets with those groups, so each bucket launches as its group finishes).  With
+    ``split_before`` the byte caps are ignored: buckets close ONLY at group boundaries.  A group's
+    weight gradients are written by one deferred grouped launch issued inside the backward of the
+    group's lowest block, so a bucket holding only part of a group would complete (its hooks fire)
+    and be all-reduced before those gradients exist."""
     splits = set(int(i) for i in split_before)
     offs, acc = [], 0
     for n in numels:
@@ -57,7 +61,7 @@ def plan_buckets(numels: Sequence[int], elem_bytes: int = 4, bucket_cap_bytes: i
     cur: List[int] = []
     for i in reversed(range(len(numels))):
         nb = int(numels[i]) * elem_bytes
-        if cur and (cur_bytes + nb > cap or i in splits):
+        if cur and (i in splits or (not splits and cur_bytes + nb > cap)):
             buckets.append((cur[-1], cur[0]))
             cur, cur_bytes = [], 0
             cap = bucket_cap_bytes

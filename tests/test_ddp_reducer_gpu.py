@@ -1,13 +1,18 @@
 """The DDP bucket-reducer paths of the wide models on ONE GPU (DCT_FORCE_DDP=1: a one-rank RCCL
-communicator, the native BucketReducer on its comm stream, graph capture - the path BASELINE
-configs 4/5 take at DDP=8, reference jobs/train_lightning_ddp.py:136):
+communicator and the native BucketReducer - the path BASELINE configs 4/5 take at DDP=8,
+reference jobs/train_lightning_ddp.py:136).  The correctness tests set DCT_RCCL_ONE_RANK=1, so
+RCCL's one-rank all-reduce really runs (a one-rank communicator otherwise skips the identity) and
+the auto placement puts it on the reducer's comm stream, as at W > 1:
 
 (a) the trajectories equal the no-reducer path (ncclAvg over one rank is the identity);
-(b) buckets launch from the backward hooks BEFORE finalize() - the all-reduce really overlaps the
-    backward; in the autograd engine the post-accumulate-grad hooks fire although the fused
-    ops write the weight gradients straight into p.grad and return None;
+(b) buckets are ENQUEUED from the backward hooks before finalize() (launch order only - that by
+    itself proves no overlap); in the autograd engine the post-accumulate-grad hooks fire although
+    the fused ops write the weight gradients straight into p.grad and return None;
 (c) allreduce_ms is measured on the device (span and exposed time, also inside replayed graphs)
-    and the debug-mode stream-ordering check stays clean.
+    and the debug-mode stream-ordering check stays clean;
+(d) OVERLAP, with a stand-in collective (DCT_REDUCER_STANDIN_US: a busy kernel of fixed duration
+    on the collective's stream, the footprint of a multi-rank all-reduce): on the comm stream the
+    exposed all-reduce time is a fraction of its span, on the compute stream it is all of it.
 """
 import pytest
 import torch
@@ -32,6 +37,7 @@ def _data(n, d, seed=0):
 
 def _tabular(forced, monkeypatch, B=1024, epochs=2):
     monkeypatch.setenv("DCT_FORCE_DDP", "1" if forced else "0")
+    monkeypatch.setenv("DCT_RCCL_ONE_RANK", "1")
     monkeypatch.setenv("DCT_DEBUG", "1")
     dims = [256, 1024, 1024, 1024, 2]
     torch.manual_seed(0)
@@ -52,6 +58,7 @@ def test_tabular_forced_reducer_matches_no_reducer(cuda, monkeypatch):
     eng, l1 = _tabular(True, monkeypatch)
     red = eng.reducer
     assert red is not None and red.num_buckets >= 2
+    assert not red._r.inline_mode  # a real (one-rank) RCCL collective: auto placement = comm stream
     # (a) same trajectory: the reducer path reduces the split-K dW slices into g before the bucket
     # launch, the no-reducer path sums the same slices in the same order inside Adam
     assert torch.isfinite(l1).all()
@@ -72,6 +79,7 @@ def _tt(forced, monkeypatch, defer="1", steps=10, B=128, groups="1"):
     monkeypatch.setenv("DCT_FORCE_DDP", "1" if forced else "0")
     monkeypatch.setenv("DCT_TT_DW_DEFER", defer)
     monkeypatch.setenv("DCT_TT_DDP_GROUPS", groups)
+    monkeypatch.setenv("DCT_RCCL_ONE_RANK", "1")
     monkeypatch.setenv("DCT_DEBUG", "1")
     ctx = init_distributed("gpu")
     F_ = 64
@@ -133,3 +141,52 @@ def test_phase_timer_reports_step_phases(cuda, monkeypatch):
     for k in ("fwd", "bwd", "allreduce", "opt"):
         assert ph[k] > 0, ph
     assert ph["bwd"] > ph["allreduce"]
+
+
+def _tabular_step_us(monkeypatch, standin_us, inline, steps=64, B=4096):
+    """Forced-DDP tabular 4x1024 step time (us, CUDA events over `steps` eager steps) with a
+    stand-in collective of `standin_us` per step; inline: "1" compute stream, "-2" auto."""
+    monkeypatch.setenv("DCT_REDUCER_STANDIN_US", str(standin_us))
+    monkeypatch.setenv("DCT_REDUCER_INLINE", inline)
+    monkeypatch.setenv("DCT_REDUCER_TIMING", "1")
+    monkeypatch.delenv("DCT_RCCL_ONE_RANK", raising=False)
+    monkeypatch.setenv("DCT_DEBUG", "0")
+    monkeypatch.setenv("DCT_FORCE_DDP", "1")
+    dims = [256, 1024, 1024, 1024, 2]
+    torch.manual_seed(0)
+    model = MLPClassifier(dims[0], hidden=tuple(dims[1:-1]), num_classes=2, dropout=0.0, loss="mse", lr=1e-3)
+    ctx = init_distributed("gpu")
+    eng = GraphMLPEngine(model, ctx, B, seed=42, adam=adam_hparams_from(model.configure_optimizers()))
+    X, Y = _data(steps * B, dims[0], seed=5)
+    rows = torch.arange(X.shape[0])
+    eng.attach_data(X, Y, rows, rows[:B])
+    eng.train_epoch(0)
+    eng.reducer.allreduce_ms(reset=True)
+    n = eng.upload_epoch_indices(1)
+    loss = torch.zeros(steps, device="cuda")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    eng.run_steps(n, steps, loss)
+    e1.record()
+    torch.cuda.synchronize()
+    span, exposed, k, bad = eng.reducer.allreduce_ms()
+    assert k == steps and bad == 0
+    return e0.elapsed_time(e1) * 1e3 / steps, span * 1e3 / k, exposed * 1e3 / k, eng.reducer._r.inline_mode
+
+
+def test_tabular_standin_collective_overlaps_backward(cuda, monkeypatch):
+    """(d) A 60 us stand-in all-reduce per step (split over the buckets by size, 16 one-wave busy
+    workgroups; about an 8-rank all-reduce of the 13.6 MB of fp32 gradients over xGMI).  With the
+    auto placement (comm stream) most of it runs under the remaining backward: the step grows by
+    well under the stand-in's 60 us and the exposed time (end of backward -> last bucket done) is a
+    fraction of the span.  Forced onto the compute stream it serialises: the step grows by ~60 us."""
+    base, _, _, _ = _tabular_step_us(monkeypatch, 0, "-2")
+    comm, span_c, exp_c, inl_c = _tabular_step_us(monkeypatch, 60, "-2")
+    inl, span_i, exp_i, inl_i = _tabular_step_us(monkeypatch, 60, "1")
+    print(f"forced-DDP tabular step: no stand-in {base:.1f} us, 60 us stand-in on the comm stream {comm:.1f} us "
+          f"(span {span_c:.1f}, exposed {exp_c:.1f}), on the compute stream {inl:.1f} us (span {span_i:.1f})")
+    assert not inl_c and inl_i
+    assert span_c >= 55.0, span_c  # the stand-in ran
+    assert inl - base > 45.0, (inl, base)  # serialised on the compute stream
+    assert exp_c < 0.5 * span_c, (span_c, exp_c)
+    assert comm - base < 0.5 * (inl - base), (base, comm, inl)

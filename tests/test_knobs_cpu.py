@@ -21,7 +21,7 @@ def test_knobs_defaults_and_reload(nat, monkeypatch):
     nat.reload_knobs()
     d = nat.knobs()
     assert d["gemm_stages"] == 0 and d["mlp_block"] == -1 and d["tt_head_spb"] == 4
-    assert d["fused_head"] == 1 and d["reducer_inline"] == 1 and d["gemm_bm64_nk"] == 4
+    assert d["fused_head"] == 1 and d["reducer_inline"] == -2 and d["reducer_standin_us"] == 0 and d["gemm_bm64_nk"] == 4
     monkeypatch.setenv("DCT_GEMM_STAGES", "4")
     monkeypatch.setenv("DCT_MLP_BLOCK", "3")
     monkeypatch.setenv("DCT_TT_HEAD_SPB", "16")

@@ -318,3 +318,62 @@ def test_mlp_architecture_from_state_dict():
         "input_dim": 256, "hidden": [1024, 1024, 1024], "classes": 2}
     with pytest.raises(ValueError):
         mlp_architecture({"blocks.0.weight": torch.zeros(2, 2)})
+
+
+def test_train_tabtransformer_package_and_serve(tmp_path, monkeypatch):
+    """BASELINE config 5 is servable.  jobs/train_ddp.py trains a TabTransformer
+    (5 feature tokens, the weather data) for one epoch on CPU into an MLflow file store;
+    prepare_package recognises the checkpoint and writes a score.py that re-declares the model in
+    plain torch from its hyper-parameters; init()/run() give the trained model's softmax."""
+    import subprocess
+    import sys
+
+    from dct_amd.ckpt.lightning_io import load_checkpoint
+    from dct_amd.models import build_model
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    uri = "file://" + str(tmp_path / "mlruns")
+    r = subprocess.run([sys.executable, os.path.join(root, "jobs", "train_ddp.py"), "--model", "tabtransformer",
+                        "--epochs", "1", "--synthetic-rows", "400", "--accelerator", "cpu",
+                        "--model-dir", str(tmp_path / "models"), "--tracking-uri", uri],
+                       capture_output=True, text=True, timeout=600, env=dict(os.environ, WORLD_SIZE="1"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    d = tmp_path / "deploy"
+    info = prepare_package(str(d), tracking_uri=uri)
+    assert "model family: tabtransformer" in (d / "score.py").read_text()
+    ck = load_checkpoint(info["checkpoint"])
+    hp = ck["hyper_parameters"]
+    model = build_model("tabtransformer", hp["num_features"], **{k: hp[k] for k in ("d_model", "heads", "layers")})
+    model.load_state_dict(ck["state_dict"])
+    model.eval()
+    score = _load_score(d, monkeypatch)
+    score.init()
+    x = torch.randn(6, hp["num_features"]).tolist()
+    out = score.run(json.dumps({"data": x}))
+    probs = torch.tensor(out["probabilities"])
+    assert probs.shape == (6, 2)
+    with torch.no_grad():
+        want = torch.softmax(model(torch.tensor(x)), dim=1)
+    assert torch.allclose(probs, want, atol=1e-5), (probs - want).abs().max()
+    assert "error" in score.run(json.dumps({"data": [[1.0, 2.0]]}))
+
+
+def test_prepare_package_refuses_unknown_architecture(tmp_path):
+    """A checkpoint of no servable family fails packaging with an error naming the problem."""
+    uri = "file://" + str(tmp_path / "mlruns")
+    client = MlflowClient(uri)
+    exp = client.get_or_create_experiment("weather_forecasting")
+    run = client.create_run(exp).run_id
+    ck = tmp_path / "odd.ckpt"
+    save_checkpoint(build_checkpoint({"encoder.weight": torch.zeros(4, 4)}, epoch=0, global_step=1,
+                                     hyper_parameters={}), str(ck))
+    client.log_batch(run, metrics=[{"key": "val_loss", "value": 0.5, "step": 1}])
+    client.log_artifact(run, str(ck), "best_checkpoints")
+    with pytest.raises(ValueError, match="unsupported architecture"):
+        prepare_package(str(tmp_path / "d"), tracking_uri=uri)
+    from dct_amd.deploy.package import tabtransformer_architecture
+
+    with pytest.raises(ValueError, match="heads"):
+        from dct_amd.models.tabtransformer import TabTransformer
+
+        tabtransformer_architecture(TabTransformer(num_features=5, d_model=16, heads=2, layers=2).state_dict(), {})

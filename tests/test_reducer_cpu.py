@@ -100,3 +100,34 @@ def test_tabtransformer_block_groups_split_the_ddp_buckets():
     upper = {id(p) for b in (2, 3) for p in m.blocks[b].parameters()} | {id(p) for p in m.head.parameters()}
     for i, p in enumerate(params):
         assert plan.param_bucket[i] == (0 if id(p) in upper or i > first_b2 else 1)
+
+
+def test_block_group_buckets_never_split_inside_a_group():
+    """A TabTransformer whose per-block weights exceed the first-bucket / bucket caps (d_model 192:
+    one block's 12 d^2 fp32 weights are ~1.7 MB > 1 MiB) must still get exactly one bucket per
+    block group: the group's dW GEMMs are issued only inside its lowest block's backward, so a
+    bucket covering part of a group would be all-reduced before its gradients are written."""
+    from dct_amd.models.tabtransformer import TabTransformer
+    from dct_amd.parallel.dist import DistContext
+    from dct_amd.trainer.engines import AutogradEngine
+
+    for d, layers in ((192, 4), (64, 12)):
+        m = TabTransformer(num_features=8, d_model=d, heads=4, layers=layers)
+        params = list(m.parameters())
+
+        class _Eng:
+            ctx = DistContext(rank=0, world_size=2)
+
+        groups, splits = AutogradEngine._block_groups(_Eng(), m, params)
+        plan = plan_buckets([p.numel() for p in params], 4, 1 << 20, 256 << 10, split_before=splits)
+        assert len(plan.counts) == len(groups) == 2
+        group_of = {}
+        for g, blocks in enumerate(m.ddp_block_groups()):
+            for b in blocks:
+                for p in m.blocks[b].parameters():
+                    group_of[id(p)] = g
+        for i, p in enumerate(params):
+            if id(p) in group_of:
+                assert plan.param_bucket[i] == group_of[id(p)], (d, layers, i)
+        # every bucket is a contiguous slice and together they cover the flat buffer once
+        assert sum(plan.counts) == sum(p.numel() for p in params)
