@@ -43,6 +43,7 @@ MAX_ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 FILE_FLAGS = {"mlp_block3.hip": ["-fno-slp-vectorize"],
               "mlp_block5.hip": ["-fno-slp-vectorize"] + MAX_ILP,
               "mlp_block5_xg.hip": ["-fno-slp-vectorize"],
+              "mlp_block5_xgprof.hip": ["-fno-slp-vectorize"],
               "tt_block.hip": MAX_ILP,
               "tt_io.hip": MAX_ILP,
               "mlp_wave_single.hip": MAX_ILP,

@@ -8,14 +8,16 @@ namespace dct {
 
 void mlp_launch_block5_xg(int world, size_t bytes, hipStream_t st, const MlpShape& sh, const MlpArgs& a);
 
-// in-kernel data-parallel launches of this kernel: 2, 4 or 8 ranks (one node), train mode
-static bool b5_xg_world_ok(int w) { return w == 2 || w == 4 || w == 8; }
+// in-kernel data-parallel launches of this kernel: 2 .. 8 ranks (one node), train mode; the profiling
+// instantiations exist for 2 / 4 / 8
+static bool b5_xg_world_ok(int w) { return w >= 2 && w <= 8; }
 
 bool mlp_block5_ok(const MlpShape& sh, const MlpArgs& a) {
   const bool aligned = (sh.woff[1] % 4) == 0 && ((uintptr_t)a.p & 15) == 0 && (((uintptr_t)a.m | (uintptr_t)a.v) & 15) == 0;
   const bool xg_ok = a.xg_world <= 1 ||
                      (a.mode == 0 && b5_xg_world_ok(a.xg_world) && a.xg_rank >= 0 && a.xg_rank < a.xg_world &&
-                      a.xg_recv != nullptr && a.xg_peers != nullptr && a.xg_status != nullptr && a.prof == nullptr);
+                      a.xg_recv != nullptr && a.xg_peers != nullptr && a.xg_status != nullptr &&
+                      (a.prof == nullptr || a.xg_world == 2 || a.xg_world == 4 || a.xg_world == 8));
   return aligned && mlp_block5_shape_ok(sh.dims, sh.L, a.B) &&
          // train mode, or grad mode for ONE step (the DDP step path: grads + loss to grad_out, device cursor)
          ((a.mode == 0 && a.cursor == nullptr) || (a.mode == 1 && a.steps == 1 && a.grad_out != nullptr)) &&
@@ -32,6 +34,10 @@ size_t mlp_block5_xg_bytes(int world) {
     case 2: return (size_t)b5x::Lay<2>::BYTES;
     case 4: return (size_t)b5x::Lay<4>::BYTES;
     case 8: return (size_t)b5x::Lay<8>::BYTES;
+    case 3: return (size_t)b5x::Lay<3>::BYTES;
+    case 5: return (size_t)b5x::Lay<5>::BYTES;
+    case 6: return (size_t)b5x::Lay<6>::BYTES;
+    case 7: return (size_t)b5x::Lay<7>::BYTES;
     default: return 0;
   }
 }

@@ -84,7 +84,8 @@ constexpr int NP = 16, NS = 2;       // W1 pairs / small pairs per lane
 constexpr int G = blk5::NT * 16;     // bytes of one slot: one 16-B granule per thread
 template <int XW>
 struct Lay {
-  static constexpr int NO = NP / XW;                       // W1 pairs a rank owns per lane
+  static constexpr int NO = (NP + XW - 1) / XW;            // W1 pair slots a rank owns per lane (pair
+                                                           // XW t + rank; beyond NP when XW does not divide 16)
   static constexpr int RSS = NO + NS;                      // RS slots per (parity, source)
   // RS slots are indexed by the source's distance from the owner, (src - owner) mod XW (1..XW-1),
   // so a rank polls its sources without knowing their absolute index
@@ -230,7 +231,8 @@ template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true,
 __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, MlpArgs a) {
   using namespace blk5;
   using namespace bku;
-  static_assert(XW == 1 || (ADAM && !PROF && (XW == 2 || XW == 4 || XW == 8)), "exchange: train mode, 2/4/8 ranks");
+  static_assert(XW == 1 || (ADAM && XW >= 2 && XW <= 8), "exchange: train mode, 2..8 ranks");
+  constexpr int PS = XW > 1 ? 32 : 16;  // PROF: stamp slots per wave (XW > 1: the exchange phases 15..20)
   using XL = b5x::Lay<XW>;
   constexpr int NO = XL::NO;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -240,7 +242,7 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   const int u = KS * w + (l >> 2);
   const int wo0 = sh.woff[0], bo0 = sh.boff[0], wo1 = sh.woff[1], bo1 = sh.boff[1];
   const int wo2 = sh.woff[2], bo2 = sh.boff[2];
-  unsigned long long pacc[PROF ? 16 : 1] = {};
+  unsigned long long pacc[PROF ? PS : 1] = {};
   unsigned long long t_last = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
   const unsigned long long t_kstart = t_last;
 
@@ -428,12 +430,15 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
       v2f cm[XW], cv[XW];
 #pragma unroll
       for (int k = 0; k < XW; ++k) {
-        cm[k] = Mo[(XW * t + k) >> 3][(XW * t + k) & 7];
-        cv[k] = Vo[(XW * t + k) >> 3][(XW * t + k) & 7];
+        const int i = XW * t + k < b5x::NP ? XW * t + k : 0;  // (slots past pair 15: never used)
+        cm[k] = Mo[i >> 3][i & 7];
+        cv[k] = Vo[i >> 3][i & 7];
       }
       MoO[t] = b5x::pick<XW>(cm, xrank);
       VoO[t] = b5x::pick<XW>(cv, xrank);
     }
+  }
+  if constexpr (XW > 1) {
     xrr = __builtin_amdgcn_make_buffer_rsrc((void*)a.xg_recv, 0, XL::BYTES, 0x00020000);
 #pragma unroll
     for (int q = 0; q < XW; ++q) xpr[q] = __builtin_amdgcn_make_buffer_rsrc((void*)a.xg_peers[q], 0, XL::BYTES, 0x00020000);
@@ -653,6 +658,55 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
         }
       }
     }
+    // ---- dW1 pass (see its call sites)
+    v2f GO[NO];     // XW > 1 (reduce-scatter): gradients of the W1 pairs this rank owns
+#pragma unroll
+    for (int t = 0; t < NO; ++t) GO[t] = (v2f){0.f, 0.f};
+    auto dw1_pass = [&]() {
+      // ---- dW1 (MFMA: A = h1[4q + lane % 4][r], B = this lane's dZ2, C register m = the gradient of
+      // its own w1[j][4q + m]) + packed Adam on pairs of consecutive k
+#pragma unroll
+      for (int q = 0; q < KS / 4; ++q) {
+        const float4 hq = *reinterpret_cast<const float4*>(h1w + (4 * q + r0) * 4);
+        const float hv[4] = {hq.x, hq.y, hq.z, hq.w};
+        f32x4_t g[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          g[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) g[j] = mfma4(hv[r], dz2[j][r], g[j]);
+        }
+
+        if constexpr (ADAM && XW > 1) {
+          // pair i = 8 j + 2 q + h to its owner i % XW (slot i / XW there), or kept if owned here
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int i = 8 * j + 2 * q + h;
+              const float gx = g[j][2 * h], gy = g[j][2 * h + 1];
+              if ((i % XW) == xrank) GO[i / XW] = (v2f){gx, gy};
+              else b5x::put(xpr[i % XW], XL::rs(xpar, (xrank - i % XW + XW) % XW, i / XW) + tb, gx, gy, xtag);
+            }
+        } else if constexpr (ADAM) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+              adam_v2<WD>(W[j][2 * q + h], (v2f){g[j][2 * h], g[j][2 * h + 1]}, Mo[j][2 * q + h], Vo[j][2 * q + h], a.b1,
+                          a.b2, a.wd, aA, aE);
+        } else {  // dW1[o = l + 64 j][16 w + 4 q .. + 3]: one 16-byte store per (j, q)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            *reinterpret_cast<float4*>(a.grad_out + wo1 + (l + 64 * j) * H + KS * w + 4 * q) =
+                make_float4(g[j][0], g[j][1], g[j][2], g[j][3]);
+        }
+      }
+    };
+    if constexpr (XW > 1) {
+      dw1_pass();
+      B5STAMP(15)  // dW1 MFMA + gradient pushes
+    }
     // ---- owners: dW2[:, u], db1[u] (quad sums), W2 / b1 / b2 Adam, W2 / b2 published
     float xg_own = 0.f, xg_bx = 0.f;  // XW > 1: this lane's second small gradient pair
     {
@@ -762,51 +816,13 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     f1 = b5_drop(a.seed, gstep + 1u, el0, p_drop, scale);  // p_drop = 0: always 1
     f2 = b5_drop(a.seed, gstep + 1u, el1, p_drop, scale);
     B5STAMP(7)
-    // ---- dW1 (MFMA: A = h1[4q + lane % 4][r], B = this lane's dZ2, C register m = the gradient of
-    // its own w1[j][4q + m]) + packed Adam on pairs of consecutive k
-    v2f GO[NO];  // XW > 1: gradients of the W1 pairs this rank owns
-#pragma unroll
-    for (int t = 0; t < NO; ++t) GO[t] = (v2f){0.f, 0.f};
-#pragma unroll
-    for (int q = 0; q < KS / 4; ++q) {
-      const float4 hq = *reinterpret_cast<const float4*>(h1w + (4 * q + r0) * 4);
-      const float hv[4] = {hq.x, hq.y, hq.z, hq.w};
-      f32x4_t g[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        g[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) g[j] = mfma4(hv[r], dz2[j][r], g[j]);
-      }
-      if constexpr (ADAM && XW > 1) {
-        // pair i = 8 j + 2 q + h to its owner i % XW (slot i / XW there), or kept if owned here
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int i = 8 * j + 2 * q + h;
-            const float gx = g[j][2 * h], gy = g[j][2 * h + 1];
-            if ((i % XW) == xrank) GO[i / XW] = (v2f){gx, gy};
-            else b5x::put(xpr[i % XW], XL::rs(xpar, (xrank - i % XW + XW) % XW, i / XW) + tb, gx, gy, xtag);
-          }
-      } else if constexpr (ADAM) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-            adam_v2<WD>(W[j][2 * q + h], (v2f){g[j][2 * h], g[j][2 * h + 1]}, Mo[j][2 * q + h], Vo[j][2 * q + h], a.b1,
-                        a.b2, a.wd, aA, aE);
-      } else {  // dW1[o = l + 64 j][16 w + 4 q .. + 3]: one 16-byte store per (j, q)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          *reinterpret_cast<float4*>(a.grad_out + wo1 + (l + 64 * j) * H + KS * w + 4 * q) =
-              make_float4(g[j][0], g[j][1], g[j][2], g[j][3]);
-      }
-    }
-    if constexpr (ADAM && XW > 1) {
+    // dW1 + packed Adam (one rank) / + reduce-scatter pushes here, after dZ1 and dW0 (XW > 1: issued
+    // earlier, right behind dZ2 - its pushes then travel while dZ1 / dW0 compute)
+    if constexpr (XW == 1) dw1_pass();
       // ---- the owner's part: reduce-scatter poll, rank-ordered sums, Adam, all-gather pushes;
       // then the all-gather poll of every pair owned elsewhere (specialised per rank: all
       // register indices are constants)
+    if constexpr (ADAM && XW > 1) {
       const unsigned long long xt0 = __builtin_amdgcn_s_memrealtime();
       const float invw = 1.f / (float)XW;
       do {
@@ -818,12 +834,14 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
 #pragma unroll
               for (int q = 1; q < XW; ++q)
 #pragma unroll
-                for (int t = 0; t < NO; ++t) k &= b5x::get(xrr, XL::rs(xpar, q, t) + tb, xtag, rv[q][t][0], rv[q][t][1]);
+                for (int t = 0; t < NO; ++t)
+                  k &= b5x::get(xrr, XL::rs(xpar, q, t) + tb, xtag, rv[q][t][0], rv[q][t][1]) | (XW * t + xrank >= b5x::NP);
               return k;
             })) {
           xbad = true;
           break;
         }
+        B5STAMP(16)  // reduce-scatter poll wait
         // the small pairs' slots (owner waves only; pushed before the W1 pairs, so normally in):
         // first pass issued here, checked after the W1 Adam - their registers are not in flight
         // together with the W1 slots'
@@ -844,17 +862,23 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
         for (int t = 0; t < NO; ++t) {
           v2f cw[XW];
 #pragma unroll
-          for (int k = 0; k < XW; ++k) cw[k] = W[(XW * t + k) >> 3][(XW * t + k) & 7];
+          for (int k = 0; k < XW; ++k) {
+            const int i = XW * t + k < b5x::NP ? XW * t + k : 0;
+            cw[k] = W[i >> 3][i & 7];
+          }
           WO[t] = b5x::pick<XW>(cw, xrank);
           v2f gs = GO[t];
 #pragma unroll
           for (int q = 1; q < XW; ++q) gs += (v2f){rv[q][t][0], rv[q][t][1]};
           adam_v2<WD>(WO[t], gs * (v2f)(invw), MoO[t], VoO[t], a.b1, a.b2, a.wd, aA, aE);
           const int agoff = XL::ag(xpar, XW * t + xrank) + tb;
+          if (XW * t + xrank < b5x::NP) {
 #pragma unroll
-          for (int q = 0; q < XW; ++q)
-            if (q != xrank) b5x::put(xpr[q], agoff, WO[t].x, WO[t].y, xtag);
+            for (int q = 0; q < XW; ++q)
+              if (q != xrank) b5x::put(xpr[q], agoff, WO[t].x, WO[t].y, xtag);
+          }
         }
+        B5STAMP(17)  // owned W1 Adam + all-gather pushes
         if (sown && !__all(sok) && !xwait(xtag, small_sweep)) {
           xbad = true;
           break;
@@ -879,6 +903,7 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
               b5x::put(xpr[q], XL::ag(xpar, b5x::NP + 1) + tb, pown, pbx, xtag);
             }
         }
+        B5STAMP(18)  // small pairs: wait, Adam, all-gather pushes
         // all-gather poll: every pair slot (the owned ones are not checked), the small pairs of a
         // wave owned elsewhere, and in wave 0 the losses (lane q: rank q's)
         float av[b5x::NP][2], sa[2][2], lq = 0.f, lq1;
@@ -899,6 +924,7 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
           xbad = true;
           break;
         }
+        B5STAMP(19)  // all-gather poll wait
 #pragma unroll
         for (int i = 0; i < b5x::NP; ++i)
           W[i >> 3][i & 7] = (i % XW) == xrank ? WO[i / XW] : (v2f){av[i][0], av[i][1]};
@@ -928,11 +954,13 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
         if (w == 0 && (l == 2 || l == 3)) lds[B2L + nbuf * 4 + (l & 1)] = pbx;
       }
       xticks += __builtin_amdgcn_s_memrealtime() - xt0;
+      B5STAMP(20)  // all-gather unpack, loss mean, W2 / b2 publish
     }
     __builtin_amdgcn_wave_barrier();  // the next step rewrites this wave's h1 tiles
     B5STAMP(8)
     xb = xbn;
   }
+
   if constexpr (XW > 1) {
     if (a.xg_ticks && tid == 0) atomicAdd(a.xg_ticks, xticks);
     lds_barrier();
@@ -946,7 +974,7 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
         const int o0 = XL::ep(XW * t + xrank, 0) + tb, o1 = XL::ep(XW * t + xrank, 1) + tb;
 #pragma unroll
         for (int q = 0; q < XW; ++q)
-          if (q != xrank) {
+          if (q != xrank && XW * t + xrank < b5x::NP) {
             b5x::put(xpr[q], o0, MoO[t].x, MoO[t].y, etag);
             b5x::put(xpr[q], o1, VoO[t].x, VoO[t].y, etag);
           }
@@ -1075,7 +1103,7 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     pacc[10] = __builtin_amdgcn_s_memtime() - t_last;
     if (l == 0) {
 #pragma unroll
-      for (int i = 0; i < 15; ++i) atomicAdd(a.prof + w * 16 + i, pacc[i]);
+      for (int i = 0; i < PS - 1; ++i) atomicAdd(a.prof + w * PS + i, pacc[i]);
     }
   }
 }

@@ -148,9 +148,13 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
   }
   inline_ = inline_knob_ == 1;
   for (int64_t c : counts_) total_count_ += c;
+  // fork / join events between two streams of ONE device: a device-scope release is all the
+  // collective (and Adam after the join) needs, not the default system-scope fence (its cache
+  // writeback / invalidate is most of an edge's cost)
+  const unsigned ev_flags = hipEventDisableTiming | hipEventReleaseToDevice;
   ready_events_.resize(nb);
-  for (auto& e : ready_events_) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
-  hip_check(hipEventCreateWithFlags(&done_event_, hipEventDisableTiming), "hipEventCreate");
+  for (auto& e : ready_events_) hip_check(hipEventCreateWithFlags(&e, ev_flags), "hipEventCreate");
+  hip_check(hipEventCreateWithFlags(&done_event_, ev_flags), "hipEventCreate");
   dsize_ = (dtype == DT_BF16 || dtype == DT_F16) ? 2 : 4;
 }
 

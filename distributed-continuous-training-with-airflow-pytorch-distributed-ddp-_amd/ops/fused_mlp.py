@@ -132,7 +132,7 @@ class FusedMLPKernel:
         if xg is not None and xg.world > 1:
             if mode != 0 or cursor is not None or pending is not None or not self.xg_supported(batch, xg.world):
                 raise ValueError("in-kernel all-reduce needs train mode on the single-wave 2-layer kernel or the "
-                                 "3x128 block kernel (2 / 4 / 8 ranks)")
+                                 "3x128 block kernel (2 .. 8 ranks)")
             need = self.xg_buffer_bytes(xg.world, batch)
             if xg.bytes < need:
                 raise ValueError(f"exchange buffer too small ({xg.bytes} < {need} bytes)")
@@ -174,7 +174,7 @@ class FusedMLPKernel:
         if xg is not None and xg.world > 1:
             if not self.xg_supported(batch, xg.world):
                 raise ValueError("in-kernel all-reduce needs the single-wave 2-layer kernel or the 3x128 block "
-                                 "kernel (2 / 4 / 8 ranks)")
+                                 "kernel (2 .. 8 ranks)")
             need = self.xg_buffer_bytes(xg.world, batch)
             if xg.bytes < need:
                 raise ValueError(f"exchange buffer too small ({xg.bytes} < {need} bytes)")
@@ -200,7 +200,7 @@ class FusedMLPKernel:
     def xg_supported(self, batch: int, world: Optional[int] = None) -> bool:
         """True when training launches can average gradients INSIDE the kernel: the single-wave
         kernel's 2-layer nets (any 2..8 ranks), or the 3x128 block kernel (csrc/mlp_block5.hip:
-        reduce-scatter + all-gather with sharded Adam, 2 / 4 / 8 ranks; ``world=None`` asks whether
+        reduce-scatter + all-gather with sharded Adam or the one-hop exchange, 2 .. 8 ranks; ``world=None`` asks whether
         some world size qualifies)."""
         if len(self.dims) == 3 and self.plan.use_wave and self.xg_slab_granules() > 0:
             return 1 <= batch <= min(self.bmax, 8)

@@ -140,7 +140,7 @@ class FusedMLPEngine(_EngineBase):
             from ..parallel.xgmi import setup_grad_exchange, setup_peer_exchange, timeout_s
 
             # the persistent launch averages gradients itself when its kernel can (5-64-2 single-wave
-            # kernel; the 3x128 block kernel at 2 / 4 / 8 ranks) - the same answer on every rank, so
+            # kernel; the 3x128 block kernel at 2 .. 8 ranks) - the same answer on every rank, so
             # the collective setup below is entered by all or none
             if (self.kernel.xg_supported(self.B, ctx.world_size) and ctx.device.type == "cuda"
                     and inkernel_enabled()):

@@ -45,6 +45,25 @@ ACT_IDS = {"relu": 1, "gelu": 2}
 LOSS_IDS = {"ce": 0, "mse": 1}
 
 
+def layer_bucket_splits(numels, bucket_bytes: int, elem_bytes: int = 4):
+    """Bucket boundaries of the executor's DDP reducer at LAYER boundaries (plan_buckets
+    ``split_before``).  The executor marks a layer's weight and bias ready right after its dW GEMM,
+    so a bucket that closes mid-layer gains nothing, and what matters for overlap is the size of the
+    LAST bucket - its all-reduce runs after the whole backward.  Layers are taken from the top and
+    a bucket closes once it holds >= min(bucket_bytes, 2 MiB): for 256-1024-1024-1024-2 that is
+    {head + layer 2} (4 MB), {layer 1} (4 MB), {layer 0} (1 MB), instead of the byte-capped
+    {head} / {layer 2} / {layer 1 + layer 0} whose last 5 MB all-reduce was fully exposed."""
+    L = len(numels) // 2
+    target = min(int(bucket_bytes), 2 << 20)
+    splits, acc = [], 0
+    for layer in range(L - 1, 0, -1):
+        acc += (numels[2 * layer] + numels[2 * layer + 1]) * elem_bytes
+        if acc >= target:
+            splits.append(2 * (layer - 1) + 1)  # the next parameter down: bias of the layer below
+            acc = 0
+    return splits
+
+
 class GraphMLPEngine:
     name = "graph"
     epoch_engine = True  # runs whole epochs on device; the Trainer reads back per-step losses
@@ -109,7 +128,8 @@ class GraphMLPEngine:
             self.comm.broadcast(self.p.data_ptr(), self.P, nat.DT_F32, 0, s)  # DDP _sync_module_states
             self.p_bf16.copy_(self.p)
             plan = plan_buckets(self.numels + [1], bucket_cap_bytes=bucket_cap_bytes,
-                                first_bucket_bytes=first_bucket_bytes)
+                                first_bucket_bytes=first_bucket_bytes,
+                                split_before=layer_bucket_splits(self.numels, bucket_cap_bytes))
             self.bucket_plan = plan
             self.reducer = NativeBucketReducer(self.comm, self.g, plan,
                                                timing=reducer_timing_enabled(),

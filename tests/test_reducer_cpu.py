@@ -131,3 +131,20 @@ def test_block_group_buckets_never_split_inside_a_group():
                 assert plan.param_bucket[i] == group_of[id(p)], (d, layers, i)
         # every bucket is a contiguous slice and together they cover the flat buffer once
         assert sum(plan.counts) == sum(p.numel() for p in params)
+
+
+def test_executor_buckets_close_at_layer_boundaries():
+    """The wide-MLP executor's DDP buckets (trainer/graph_engine.py layer_bucket_splits): whole
+    layers from the top until >= 2 MiB, so the last bucket - the only all-reduce that cannot overlap
+    backward - is the input layer alone."""
+    from dct_amd.trainer.graph_engine import layer_bucket_splits
+
+    dims = [256, 1024, 1024, 1024, 2]
+    numels = []
+    for i in range(len(dims) - 1):
+        numels += [dims[i] * dims[i + 1], dims[i + 1]]
+    splits = layer_bucket_splits(numels, 8 << 20)
+    plan = plan_buckets(numels + [1], 4, 8 << 20, 1 << 20, split_before=splits)
+    # params: W0 b0 W1 b1 W2 b2 W3 b3 loss -> buckets {W2 b2 W3 b3 loss}, {W1 b1}, {W0 b0}
+    assert plan.param_bucket == [2, 2, 1, 1, 0, 0, 0, 0, 0]
+    assert plan.counts[-1] == 256 * 1024 + 1024
