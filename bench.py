@@ -111,11 +111,8 @@ def _timed(ctx, fn, device_barrier=None):
     # allocates almost nothing).  Measured on MI355X (profiles/bench_window_gc_r3.log): with it on,
     # the first window's completion wait was 0.34 ms instead of 0.10 ms in some processes; a
     # gc.collect() right before the window instead costs ~50 us of cold-cache enqueue.
-    gc_mode = os.environ.get("DCT_BENCH_GC", "pause")  # pause | on | collect
-    gc_paused = gc_mode != "on" and gc.isenabled()
+    gc_paused = gc.isenabled()
     if gc_paused:
-        if gc_mode == "collect":
-            gc.collect()
         gc.disable()
     torch.cuda.synchronize()
     ctx.barrier()
@@ -135,9 +132,6 @@ def _timed(ctx, fn, device_barrier=None):
     dt = time.perf_counter() - t0
     if gc_paused:
         gc.enable()
-    if os.environ.get("DCT_BENCH_DEBUG", "0") == "1":
-        print(f"[bench debug] window {dt * 1e6:.1f} us: enqueue {(t_enq - t0) * 1e6:.1f} us, "
-              f"wait {(t0 + dt - t_enq) * 1e6:.1f} us", flush=True)
     dt_t = torch.tensor([dt], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
     if ctx.is_distributed:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
@@ -387,8 +381,6 @@ def measure(a, ctx):
     if dbar is not None and dbar():  # first launch of the barrier kernel (code-object load) untimed
         torch.cuda.synchronize()
     dt = _timed(ctx, lambda: loop.run_steps(n_items, a.steps, loss, first_step=a.warmup), device_barrier=dbar)
-    for _ in range(int(os.environ.get("DCT_BENCH_DEBUG_REPEAT", "0"))):  # debug: the same window again
-        _timed(ctx, lambda: loop.run_steps(n_items, a.steps, loss, first_step=a.warmup), device_barrier=dbar)
 
     xg_ok = (eng.xg_verify(fallback=True) if (getattr(eng, "xg", None) is not None
                                                or getattr(eng, "gx", None) is not None) else None)

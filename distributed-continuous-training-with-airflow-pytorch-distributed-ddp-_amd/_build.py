@@ -78,7 +78,7 @@ def _flags(debug: bool = False, sanitize: bool = None):
     if debug:
         f.append("-g")
     if os.environ.get("DCT_PROF_BUILD", "0") == "1":  # in-kernel phase stamps (tools/prof_fused.py)
-        f.append("-DDCT_WAVE_PROF")
+        f.append("-DWAVE_PROF_BUILD")
     if sanitize is None:
         sanitize = os.environ.get("DCT_SANITIZE", "0") == "1"
     if sanitize:  # host-side ASan only (no GPU sanitizer on this pool)

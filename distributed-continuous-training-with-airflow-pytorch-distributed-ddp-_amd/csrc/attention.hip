@@ -476,7 +476,7 @@ static bool attn_mfma(bool bwd, const uint16_t* q, const uint16_t* k, const uint
                       const uint16_t* dout, const float* lse_in, float* lse_out, uint16_t* out0, uint16_t* dk,
                       uint16_t* dv, int Bsz, int H, int T, int D, int ldq, int ldo, float scale, hipStream_t st,
                       hipError_t* err) {
-  if (dct::knobs().attn_scalar || T % 16 || D % 16 || T > 64 || !(D == 16 || D == 32 || D == 64)) return false;
+  if (T % 16 || D % 16 || T > 64 || !(D == 16 || D == 32 || D == 64)) return false;
   if (ldq % 4 || ldo % 4 || ((((uintptr_t)q) | ((uintptr_t)k) | ((uintptr_t)v) | ((uintptr_t)dout)) & 7)) return false;
   const int BH = Bsz * H, DT = D / 16;
   switch (T / 16) {

@@ -174,15 +174,8 @@ PYBIND11_MODULE(_dct_native, m) {
   m.def("knobs", []() {
     const dct::Knobs& k = dct::knobs();
     py::dict d;
-    d["mlp_force_lds"] = k.mlp_force_lds; d["mlp_block"] = k.mlp_block; d["mlp_block_mf"] = k.mlp_block_mf;
-    d["b3_prio"] = k.b3_prio; d["mlp_rows"] = k.mlp_rows; d["gemm_v1"] = k.gemm_v1;
-    d["gemm_split_ws"] = k.gemm_split_ws; d["gemm_two_pass"] = k.gemm_two_pass; d["gemm_stages"] = k.gemm_stages;
-    d["gemm_split_wg"] = k.gemm_split_wg; d["gemm_splits"] = k.gemm_splits; d["gemm_8w"] = k.gemm_8w; d["gemm_split_8w"] = k.gemm_split_8w;
-    d["gemm_bm128"] = k.gemm_bm128; d["gemm_bm64_nk"] = k.gemm_bm64_nk; d["gemm_no_group"] = k.gemm_no_group;
-    d["gemm_dw_mink"] = k.gemm_dw_mink; d["skinny_head_rpw"] = k.skinny_head_rpw;
-    d["skinny_head_waves"] = k.skinny_head_waves; d["skinny_dw_splits"] = k.skinny_dw_splits;
-    d["tt_head_spb"] = k.tt_head_spb; d["attn_scalar"] = k.attn_scalar; d["fused_head"] = k.fused_head;
-    d["dw_into_adam"] = k.dw_into_adam; d["reducer_inline"] = k.reducer_inline;
+    d["mlp_force_lds"] = k.mlp_force_lds; d["mlp_block"] = k.mlp_block; d["fused_head"] = k.fused_head;
+    d["dw_into_adam"] = k.dw_into_adam; d["reducer_inline"] = k.reducer_inline; d["rccl_one_rank"] = k.rccl_one_rank;
     d["reducer_standin_us"] = k.reducer_standin_us; d["reducer_standin_wgs"] = k.reducer_standin_wgs;
     return d;
   });

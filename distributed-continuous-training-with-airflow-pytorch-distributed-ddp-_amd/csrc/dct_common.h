@@ -5,7 +5,7 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
-#define DCT_WAVE 64
+
 
 namespace dct {
 
@@ -19,6 +19,15 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
   return v;
+}
+
+// p[i] for a wave-uniform i, through the scalar cache: a peer buffer address loaded this way stays in
+// SGPRs, so the buffer descriptor built from it is scalar.  Loaded with a vector load instead, the
+// descriptor lands in VGPRs and every buffer op on it becomes a readfirstlane / compare / exec-mask
+// waterfall loop (~13 extra instructions per store) holding 4 VGPRs per peer.
+template <class T>
+__device__ __forceinline__ T* sload_ptr(T* const* p, int i) {
+  return (T*)((const __attribute__((address_space(4))) unsigned long long*)p)[i];
 }
 
 // bf16 <-> f32 on raw 16-bit storage (round-to-nearest-even; NaN kept NaN via the cast path)

@@ -432,77 +432,6 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
   // accumulator is the TRANSPOSED tile: lane (c = lane&15, g = lane>>4) holds row 16i + c and the
   // 4 CONSECUTIVE columns 16j + 4g .. +3 -> 8-byte bf16 / 16-byte fp32 row stores instead of
   // 2-byte scattered ones (and 4-wide bias / aux loads).
-  if (SPLIT && WM == 2 && g.split_ws) {  // (the 8-wave split kernels never get a workspace)
-    // In-launch split-K reduction (DCT_GEMM_SPLIT_WS=1; deterministic): every slice stores its
-    // partial tile with plain stores (element-major, 1 KB per store instruction across the
-    // workgroup) and publishes it with ONE agent-scope release by thread 0 before taking the tile's
-    // ticket; the slice drawing the last ticket acquires once and sums the partials in slice order
-    // (bit-reproducible) into C, so no reduce launch follows.  (A __threadfence() in every thread
-    // plus agent-scope element stores / loads measured SLOWER than fp32 atomics: tabular step 0.203
-    // -> 0.291 ms, profiles/gemm_splitk_ws_ab_r1.log.)
-    constexpr int NE = IM * 16;
-    float* slot = g.split_ws + ((size_t)tile * splits + split) * (BM * GBN);
-#pragma unroll
-    for (int i = 0; i < IM; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) slot[((i * 4 + j) * 4 + r) * GNT + tid] = acc[i][j][r];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // every wave's stores have retired; the k-loop's LDS images are free
-    volatile int* is_last = reinterpret_cast<volatile int*>(smem2);  // one __shared__ object: no second array
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int prev = __hip_atomic_fetch_add(g.split_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = prev == splits - 1;
-      if (last) __hip_atomic_store(g.split_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *is_last = last;
-    }
-    __syncthreads();
-    if (!*is_last) return;
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    float sum[NE];
-#pragma unroll
-    for (int e = 0; e < NE; ++e) sum[e] = 0.f;
-    const float* base = g.split_ws + (size_t)tile * splits * (BM * GBN);
-    for (int sp = 0; sp < splits; ++sp) {
-      if (sp == split) {
-#pragma unroll
-        for (int i = 0; i < IM; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sum[(i * 4 + j) * 4 + r] += acc[i][j][r];
-      } else {
-        const float* ps = base + (size_t)sp * (BM * GBN);
-#pragma unroll
-        for (int e = 0; e < NE; ++e) sum[e] += ps[e * GNT + tid];
-      }
-    }
-    const int col_l = lane & 15, row_l = (lane >> 4) * 4;
-#pragma unroll
-    for (int i = 0; i < IM; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = n0 + wc * 64 + j * 16 + col_l;
-        if (col >= g.N) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wr * (BM / WM) + i * 16 + row_l + r;
-          if (row < g.M) {
-            float* dst = reinterpret_cast<float*>(g.C) + (size_t)row * g.ldc + col;
-            const float v = sum[(i * 4 + j) * 4 + r] * g.alpha;
-            *dst = g.accumulate ? *dst + v : v;
-          }
-        }
-      }
-    return;
-  }
   if (SPLIT && g.split_part) {  // two-pass split-K: this slice's partial tile, plain stores
     float* part = g.split_part + (size_t)split * g.M * g.N;
     const int col_l = lane & 15, row_l = (lane >> 4) * 4;
@@ -761,7 +690,6 @@ static hipError_t launch_gemm(const dct::GemmArgs& g, hipStream_t st) {
 }
 
 static bool gemm_v2_ok(const dct::GemmArgs& g, int ta, int tb) {
-  if (dct::knobs().gemm_v1) return false;
   if (g.K % dct::GBK) return false;
   auto aligned = [](const void* p) { return (((uintptr_t)p) & 15) == 0; };
   if (!aligned(g.A) || !aligned(g.B) || g.lda % 8 || g.ldb % 8) return false;
@@ -770,58 +698,19 @@ static bool gemm_v2_ok(const dct::GemmArgs& g, int ta, int tb) {
   return true;
 }
 
-// Split-K workspace (see the SPLIT && split_ws epilogue).  Allocated once per process, outside
-// any stream capture (the graph engines run one eager warm step before capturing); a captured
-// graph keeps using the buffer it recorded, so a buffer is never freed, only superseded.
-// One compute stream per device issues the split GEMMs, so one workspace serves them in order.
-static float* g_split_ws = nullptr;
-static int* g_split_cnt = nullptr;
-static size_t g_split_ws_bytes = 0;
-static int g_split_dev = -1;
-constexpr int SPLIT_CNT_N = 4096;
-static bool split_workspace(size_t bytes, int tiles, hipStream_t st, float** ws, int** cnt) {
-  if (!dct::knobs().gemm_split_ws || tiles > SPLIT_CNT_N) return false;
-  int dev = -1;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  if (g_split_ws && g_split_dev == dev && g_split_ws_bytes >= bytes) {
-    *ws = g_split_ws; *cnt = g_split_cnt;
-    return true;
-  }
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
-  if (g_split_dev != -1 && g_split_dev != dev) return false;  // one device per process
-  const size_t want = std::max<size_t>(bytes, (size_t)64 << 20);
-  float* w = nullptr;
-  int* c = nullptr;
-  if (hipMalloc(&w, want) != hipSuccess) { (void)hipGetLastError(); return false; }
-  if (!g_split_cnt) {
-    if (hipMalloc(&c, SPLIT_CNT_N * sizeof(int)) != hipSuccess || hipMemset(c, 0, SPLIT_CNT_N * sizeof(int)) != hipSuccess) {
-      (void)hipGetLastError();
-      return false;
-    }
-    if (hipDeviceSynchronize() != hipSuccess) return false;
-    g_split_cnt = c;
-  }
-  g_split_ws = w; g_split_ws_bytes = want; g_split_dev = dev;
-  *ws = g_split_ws; *cnt = g_split_cnt;
-  return true;
-}
-
 // Two-pass split-K partials.  Auto mode takes it for <= 4 slices per tile: 1024 x 1024 x 4096 dW
 // (4 slices) 30.0 -> 23.3 us, tabular step 0.186 -> 0.1835 ms; with 16-64 slices (1024 x 256 x
 // 4096, the 32k-row transformer dW) the reduce pass costs more than the atomics it removes (15.9 ->
 // 16.7 us, 13-15 -> 28-29 us; profiles/gemm_splitk_two_pass_ab_r2.log).
-// DCT_GEMM_SPLIT_TWO_PASS=1 forces it, =0 disables it. like the workspace above, one
-// buffer per process allocated outside stream capture and only ever superseded, never freed (a
+// One buffer per process, allocated outside stream capture and only ever superseded, never freed (a
 // captured graph keeps the pointer it recorded); the split GEMMs and their reduce run in stream
-// order on one compute stream, so one buffer serves them in turn.
+// order on one compute stream, so one buffer serves them in turn.  (An in-launch reduction by the
+// last-arriving slice measured slower than this reduce launch, profiles/gemm_splitk_inlaunch_ab_r4.log.)
 static float* g_part = nullptr;
 static size_t g_part_bytes = 0;
 static int g_part_dev = -1;
 static float* split_partials(size_t bytes, int max_splits, hipStream_t st) {
-  const int tp = dct::knobs().gemm_two_pass;  // -1: auto; 1: always; 0: never
-  if (tp == 0) return nullptr;
-  if (tp != 1 && max_splits > 4) return nullptr;
+  if (max_splits > 4) return nullptr;
   int dev = -1;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   if (g_part && g_part_dev == dev && g_part_bytes >= bytes) return g_part;
@@ -848,19 +737,13 @@ static int device_cus() {
   return cus;
 }
 
-// LDS pipeline depth.  Measured on the MLP / transformer shapes (tools/bench_gemm_mlp.py,
-// profiles/gemm_pipeline_ab_r1.log): 4 stages never beat 2 - with 32 KB of operands per k-step a
-// CU's load path (~70 GB/s from L2), not the round-trip latency, bounds these one-tile-per-CU
-// grids - so 2 is the default and 4 stays selectable (DCT_GEMM_STAGES=4) for other shapes.
-static int gemm_stages(int grid, int nk_slice) {
-  if (dct::knobs().gemm_stages) return (dct::knobs().gemm_stages >= 4 && nk_slice >= 3) ? 4 : 2;
-  (void)grid;
-  return 2;
-}
+// LDS pipeline depth: 2.  Measured on the MLP / transformer shapes (tools/bench_gemm_mlp.py,
+// profiles/gemm_pipeline_ab_r1.log, profiles/gemm_probe_r4.log): 3 or 4 stages never beat 2 - with
+// 32 KB of operands per k-step a CU's global -> LDS rate, not the round-trip latency, bounds these
+// one-tile-per-CU grids.
 
 template <bool TA, bool TB>
 static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
-  const dct::Knobs& kn = dct::knobs();
   hipError_t e;
   const int tiles_n = (g.N + dct::GBN - 1) / dct::GBN;
   const int tiles = ((g.M + dct::GBM - 1) / dct::GBM) * tiles_n;
@@ -871,18 +754,14 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
     // on the 32k-row transformer dW shapes - tools/bench_dw.py)
     // workgroups to aim for: one per CU.  512 (two slices per CU) doubled the fp32 atomic traffic
     // for no extra bandwidth: 1024x1024x4096 dW 38 -> 28 us at 256 (profiles/gemm_pipeline_ab_r1.log)
-    int target = device_cus();
-    if (kn.gemm_split_wg) target = std::max(1, kn.gemm_split_wg);
+    const int target = device_cus();
     splits = std::min(nk / 8, (target + tiles - 1) / tiles);
-    if (kn.gemm_splits) splits = std::min(nk, kn.gemm_splits);  // tuning override
     if (splits < 1) splits = 1;
   }
   if (splits > 1) {
-    const size_t bytes = (size_t)tiles * splits * dct::GBM * dct::GBN * sizeof(float);
-    if (!split_workspace(bytes, tiles, st, &g.split_ws, &g.split_cnt)) g.split_ws = nullptr, g.split_cnt = nullptr;
-    if (!g.split_ws) g.split_part = split_partials((size_t)splits * g.M * g.N * sizeof(float), splits, st);
+    g.split_part = split_partials((size_t)splits * g.M * g.N * sizeof(float), splits, st);
   }
-  if (splits > 1 && !g.accumulate && !g.split_ws && !g.split_part) {  // slices accumulate atomically into a zeroed C
+  if (splits > 1 && !g.accumulate && !g.split_part) {  // slices accumulate atomically into a zeroed C
     const int64_t total = (int64_t)g.M * g.N;
     const int zgrid = (int)std::min<int64_t>(2048, (total + 255) / 256);
     hipLaunchKernelGGL(dct::zero_panel_kernel, dim3(zgrid), dim3(256), 0, st, reinterpret_cast<float*>(g.C), g.ldc,
@@ -904,8 +783,8 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
   // segments per stage raise it: 4096 x 1024 x 1024 fwd / dX 15.1 / 17.2 -> 13.4 / 14.8 us
   // (half-height tiles, two per CU, below), tabular step 176.2 -> 175.7 us; from K = 256 on (the
   // 256-feature input layer: two k stages) 166.7 -> 163.7 us (profiles/gemm_k128_ab_r4.log,
-  // tools/probes/gemm_probe.hip).  DCT_GEMM_8W=0 turns it off.
-  if (kn.gemm_8w != 0 && splits == 1 && tiles <= device_cus() && 2 * tiles > device_cus() && g.K % 128 == 0 &&
+  // tools/probes/gemm_probe.hip).
+  if (splits == 1 && tiles <= device_cus() && 2 * tiles > device_cus() && g.K % 128 == 0 &&
       g.K >= 256) {
     auto fn = dct::gemm2_kernel<TA, TB, false, 128, 2, 4, 128>;
     const size_t lds = (size_t)2 * 2 * (128 * 2 * 128);  // 2 stages x (A + B) images of 128 x 128 bf16
@@ -915,26 +794,20 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
     return hipGetLastError();
   }
   if constexpr (!TA) {
-    // small K and too few 128-row tiles to fill 256 CUs several times over: half-height tiles
-    const bool force128 = kn.gemm_bm128 != 0;
+    // small K (<= 4 k-tiles) and too few 128-row tiles to fill 256 CUs several times over: half-height tiles
     // ... and whenever 128-row tiles would give at most one workgroup per CU (the 4096 x 1024 MLP
     // layers: 256 tiles): two half-height tiles per CU overlap one's loads with the other's MFMAs,
     // 16.7 -> 14.5 us fwd / 17.4 -> 15.5 us dX at 4096x1024x1024, ahead of hipBLASLt (17.8 / 17.2;
     // profiles/gemm_bm64_ab_r1.log)
-    const int bm64_nk = kn.gemm_bm64_nk;  // A/B knob
-    if (splits == 1 && (nk <= bm64_nk || tiles <= device_cus()) && tiles < 1024 && !force128)
+    if (splits == 1 && (nk <= 4 || tiles <= device_cus()) && tiles < 1024)
       return launch(dct::gemm2_kernel<TA, TB, false, 64, 2>, ((g.M + 63) / 64) * tiles_n, 2);
   }
   if (splits > 1) {
     const int grid = tiles * splits;
     // 8 waves (two per SIMD) on the split-K dW tiles: more loads in flight per CU on these
     // load-path-bound one-tile-per-CU grids - tabular step 170.9 -> 165.9 us, the TabTransformer's
-    // grouped dW launch unchanged (profiles/gemm_split_8w_ab_r4.log); DCT_GEMM_SPLIT_8W=0 = 4 waves
-    if (kn.gemm_split_8w && !g.split_ws && gemm_stages(grid, nk_slice) != 4)
-      e = launch(dct::gemm2_kernel<TA, TB, true, 128, 2, 4>, grid, 2, 512);
-    else
-      e = gemm_stages(grid, nk_slice) == 4 ? launch(dct::gemm2_kernel<TA, TB, true, 128, 4>, grid, 4)
-                                           : launch(dct::gemm2_kernel<TA, TB, true, 128, 2>, grid, 2);
+    // grouped dW launch unchanged (profiles/gemm_split_8w_ab_r4.log)
+    e = launch(dct::gemm2_kernel<TA, TB, true, 128, 2, 4>, grid, 2, 512);
     if (e != hipSuccess || !g.split_part) return e;
     const int64_t n4 = ((int64_t)g.M * g.N + 3) / 4;
     hipLaunchKernelGGL(dct::splitk_reduce_kernel, dim3((int)std::min<int64_t>(2048, (n4 + 255) / 256)), dim3(256), 0,
@@ -942,7 +815,6 @@ static hipError_t launch_gemm2(dct::GemmArgs g, hipStream_t st) {
                        g.alpha);
     return hipGetLastError();
   }
-  if (gemm_stages(tiles, nk) == 4) return launch(dct::gemm2_kernel<TA, TB, false, 128, 4>, tiles, 4);
   return launch(dct::gemm2_kernel<TA, TB, false, 128, 2>, tiles, 2);
 }
 
@@ -964,12 +836,11 @@ extern "C" int dct_gemm_bf16_dw_partials(const uint16_t* dZ, const uint16_t* X, 
   const int tiles = ((M + dct::GBM - 1) / dct::GBM) * ((N + dct::GBN - 1) / dct::GBN);
   const int nk_slice = (nk + splits - 1) / splits;
   if ((splits - 1) * nk_slice >= nk) return (int)hipErrorInvalidValue;  // an empty slice would store zeros: fine, but keep it tight
-  const bool w8 = dct::knobs().gemm_split_8w != 0;
-  auto fn = w8 ? dct::gemm2_kernel<true, false, true, 128, 2, 4> : dct::gemm2_kernel<true, false, true, 128, 2>;
+  auto fn = dct::gemm2_kernel<true, false, true, 128, 2, 4>;
   const size_t lds = (size_t)(nk_slice > 1 ? 4 : 2) * dct::G2_BYTES;
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(fn, dim3(tiles * splits), dim3(w8 ? 512 : dct::GNT), lds, reinterpret_cast<hipStream_t>(stream),
+  hipLaunchKernelGGL(fn, dim3(tiles * splits), dim3(512), lds, reinterpret_cast<hipStream_t>(stream),
                      g, splits);
   return (int)hipGetLastError();
 }
@@ -979,10 +850,7 @@ extern "C" int dct_gemm_dw_auto_splits(int M, int N, int K) {
   const int tiles = ((M + dct::GBM - 1) / dct::GBM) * ((N + dct::GBN - 1) / dct::GBN);
   const int nk = K / dct::GBK;
   if (tiles >= 256 || nk < 8 || K % dct::GBK) return 1;
-  int target = device_cus();
-  if (dct::knobs().gemm_split_wg) target = std::max(1, dct::knobs().gemm_split_wg);
-  int splits = std::min(nk / 8, (target + tiles - 1) / tiles);
-  if (dct::knobs().gemm_splits) splits = std::min(nk, dct::knobs().gemm_splits);
+  const int splits = std::min(nk / 8, (device_cus() + tiles - 1) / tiles);
   return splits < 1 ? 1 : splits;
 }
 
@@ -1026,8 +894,7 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   dct::GemmGroup gg{};
   gg.n = n;
-  const dct::Knobs& kn = dct::knobs();
-  bool grouped = !kn.gemm_no_group;
+  bool grouped = true;
   int total = 0, max_slice = 1;
   for (int i = 0; i < n; ++i) {
     dct::GemmArgs& g = gg.g[i];
@@ -1046,11 +913,9 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
   // workgroups per CU.  One transformer block's four dW GEMMs (448 workgroups at 8) keep 8; the
   // four blocks' sixteen deferred to one launch go to 32 (448 workgroups instead of 1792: a quarter
   // of the fp32 atomics, four times the k-loop per slice): TabTransformer step 0.411 -> 0.368 ms
-  // (profiles/tt_dw_mink_ab_r2.log).  DCT_GEMM_DW_MINK pins it.
-  int target = device_cus();
-  if (kn.gemm_split_wg) target = std::max(1, kn.gemm_split_wg);
-  const bool mk_env = kn.gemm_dw_mink > 0;
-  int min_kt = mk_env ? std::max(2, kn.gemm_dw_mink) : 8;
+  // (profiles/tt_dw_mink_ab_r2.log).
+  const int target = device_cus();
+  int min_kt = 8;
   for (;;) {
     total = 0;
     max_slice = 1;
@@ -1065,7 +930,7 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
       total += tiles * splits;
       max_slice = std::max(max_slice, (nk + splits - 1) / splits);
     }
-    if (!grouped || mk_env || total <= 2 * device_cus() || min_kt >= 64) break;
+    if (!grouped || total <= 2 * device_cus() || min_kt >= 64) break;
     min_kt *= 2;
   }
   if (!grouped) {
@@ -1108,14 +973,11 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
                          st, C[i], N[i], M[i], N[i]);
     }
   }
-  const bool s4 = kn.gemm_stages >= 4 && max_slice >= 3;
-  const size_t lds = (size_t)(max_slice > 1 ? (s4 ? 8 : 4) : 2) * dct::G2_BYTES;
-  const bool w8 = kn.gemm_split_8w != 0 && !s4;
-  auto fn = s4 ? dct::gemm2_grouped_kernel<true, false, 4>
-               : (w8 ? dct::gemm2_grouped_kernel<true, false, 2, 4> : dct::gemm2_grouped_kernel<true, false, 2>);
+  const size_t lds = (size_t)(max_slice > 1 ? 4 : 2) * dct::G2_BYTES;
+  auto fn = dct::gemm2_grouped_kernel<true, false, 2, 4>;
   e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(fn, dim3(total), dim3(w8 ? 512 : dct::GNT), lds, st, gg);
+  hipLaunchKernelGGL(fn, dim3(total), dim3(512), lds, st, gg);
   e = hipGetLastError();
   if (e != hipSuccess || !part) return (int)e;
   hipLaunchKernelGGL(dct::splitk_reduce_grouped_kernel,

@@ -23,8 +23,6 @@ struct GemmArgs {
   float alpha;
   float* colsum;  // optional: colsum[m] += sum_k op(A)[m][k] (the bias gradient of a dW GEMM)
   const float* residual;  // optional (fp32 out): C = residual + op(A) op(B) + bias, ld = ldc
-  float* split_ws;        // optional split-K workspace [tiles][splits][BM*GBN]: slices store partials, the
-  int* split_cnt;         // last slice of a tile (split_cnt[tile] arrival counter) sums them in slice order
   float* split_part;      // optional two-pass split-K: slice s plain-stores its partial C into
                           // split_part[s][M][N]; splitk_reduce_kernel sums the slices into C afterwards
 };

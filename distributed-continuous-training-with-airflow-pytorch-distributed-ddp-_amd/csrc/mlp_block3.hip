@@ -589,12 +589,11 @@ hipError_t mlp_launch_block3(const MlpShape& sh, const MlpArgs& a, hipStream_t s
   const int d0 = sh.dims[0], C = sh.dims[3];
   const bool tr = a.mode == 0;
   const size_t bytes = (size_t)blk3::LDS_FLOATS * sizeof(float);
-  // weather shape (D0 <= 8, C <= 2): layer-1 forward and dW1 on the 4x4x1 fp32 MFMA (DCT_MLP_BLOCK_MF=0:
-  // VALU); train mode without weight decay drops the L2 term from every Adam update
-  const bool mf = knobs().mlp_block_mf && d0 <= 8 && C <= 2;
+  // weather shape (D0 <= 8, C <= 2): layer-1 forward and dW1 on the 4x4x1 fp32 MFMA (the VALU form
+  // for other shapes); train mode without weight decay drops the L2 term from every Adam update
+  const bool mf = d0 <= 8 && C <= 2;
   const bool wd = a.wd != 0.f;
-  MlpArgs a2 = a;
-  a2.tune = knobs().b3_prio >= 0 ? knobs().b3_prio : a.tune;
+  const MlpArgs& a2 = a;
   if (a.prof) {
     if (mf) b3_launch<2, 2, true, true, true>(bytes, st, sh, a2);
     else b3_launch<2, 2, true, true>(bytes, st, sh, a2);

@@ -441,7 +441,8 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   if constexpr (XW > 1) {
     xrr = __builtin_amdgcn_make_buffer_rsrc((void*)a.xg_recv, 0, XL::BYTES, 0x00020000);
 #pragma unroll
-    for (int q = 0; q < XW; ++q) xpr[q] = __builtin_amdgcn_make_buffer_rsrc((void*)a.xg_peers[q], 0, XL::BYTES, 0x00020000);
+    for (int q = 0; q < XW; ++q)
+      xpr[q] = __builtin_amdgcn_make_buffer_rsrc((void*)sload_ptr(a.xg_peers, q), 0, XL::BYTES, 0x00020000);
   }
   // bounded spin of one wave until sweep() (this lane's loads of one pass, true when all tags
   // match) holds in every lane; false after xg_timeout (the tag is recorded in xg_status)
@@ -797,7 +798,7 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
         if (!sown) {
 #pragma unroll
           for (int q = 0; q < XW; ++q)
-            if (q == w % XW) {
+            if (q == __builtin_amdgcn_readfirstlane(w) % XW) {  // (scalar: the descriptor stays in SGPRs)
               const int rel = (xrank - q + XW) % XW;
               b5x::put(xpr[q], XL::rs(xpar, rel, NO) + tb, g0, g1, xtag);
               b5x::put(xpr[q], XL::rs(xpar, rel, NO + 1) + tb, xg_own, xg_bx, xtag);

@@ -501,7 +501,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpShape sh, MlpArgs a) {
     a.prof[30] = __builtin_amdgcn_s_memrealtime();
     tprev = __builtin_amdgcn_s_memtime();
   }
-#define DCT_MARK(k)                                             \
+#define FMLP_MARK(k)                                             \
   if (prof) {                                                   \
     const unsigned long long tn = __builtin_amdgcn_s_memtime(); \
     atomicAdd(&a.prof[(k)], tn - tprev);                        \
@@ -549,7 +549,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpShape sh, MlpArgs a) {
         else fwd_layer<3, NT, BMAX, false>(sh, lds, Ain, B, bs, last, true, a.dropout, a.seed, gstep, lab, a.loss_kind);
       }
       lds_barrier();
-      DCT_MARK(1 + li);
+      FMLP_MARK(1 + li);
     }
     if (!fuse) {
       lo = loss_phase<BMAX>(sh, lds, B, bs, lab, a.loss_kind);
@@ -560,7 +560,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpShape sh, MlpArgs a) {
       if (a.loss_out && !a.cursor) a.loss_out[s] = bl;
       if (!adam) a.grad_out[sh.P] = bl;
     }
-    DCT_MARK(5);
+    FMLP_MARK(5);
 
     // ---- backward dX
 #pragma unroll
@@ -569,7 +569,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpShape sh, MlpArgs a) {
       else if (li == 2) dx_layer<2, NT, BMAX>(sh, lds, B, dscale);
       else dx_layer<1, NT, BMAX>(sh, lds, B, dscale);
       lds_barrier();
-      DCT_MARK(6 + li);
+      FMLP_MARK(6 + li);
     }
 
     // ---- next batch into the other half of the input tile (read after the end barrier)
@@ -656,10 +656,10 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpShape sh, MlpArgs a) {
       }
     }
     lds_barrier();
-    DCT_MARK(11);
+    FMLP_MARK(11);
     buf ^= 1;
   }
-#undef DCT_MARK
+#undef FMLP_MARK
   if (prof) a.prof[31] = __builtin_amdgcn_s_memrealtime();
   if (a.cursor && tid == 0) __hip_atomic_store(a.cursor, cur0 + a.steps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (a.step_counter && tid == 0)

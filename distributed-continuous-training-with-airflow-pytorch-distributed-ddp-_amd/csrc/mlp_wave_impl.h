@@ -283,7 +283,7 @@ __device__ __forceinline__ bool xg_exchange_wave(float (&g)[XV], const MlpArgs& 
     return false;
   };
   if ((a.xg_poll & 0xff) == 3) {
-    // Pipelined polls (DCT_XG_POLL=3, stagger = xg_poll >> 8 sleeps of 64 cycles): two sweeps in
+    // Pipelined polls (xg_poll = 3, stagger = xg_poll >> 8 sleeps of 64 cycles): two sweeps in
     // flight, issued half a round trip apart, so a granule that lands just after one sweep read
     // its slot is seen by the other half a round trip later instead of a whole one.
     xg_v4u dA[XW][P2], dB[XW][P2];
@@ -525,7 +525,7 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
   // diagnostic phase stamps (shader clock, wave-uniform branch; never set in production)
   const bool profu = a.prof != nullptr;
   unsigned long long pt[6] = {0, 0, 0, 0, 0, 0}, tprev = 0;
-#ifndef DCT_WAVE_PROF
+#ifndef WAVE_PROF_BUILD
 #define WSTAMP(k)
 #else
 #define WSTAMP(k)                                                                          \
@@ -545,7 +545,7 @@ __global__ __launch_bounds__(64) void mlp_wave_kernel(WaveShape sh, MlpArgs a) {
     rrs = __builtin_amdgcn_make_buffer_rsrc(a.xg_recv, 0, nbytes, 0x00020000);
 #pragma unroll
     for (int q = 0; q < XWN; ++q) {
-      void* pq = (q < a.xg_world) ? (void*)a.xg_peers[q] : (void*)a.xg_recv;
+      void* pq = (q < a.xg_world) ? (void*)sload_ptr(a.xg_peers, q) : (void*)a.xg_recv;
       prs[q] = __builtin_amdgcn_make_buffer_rsrc(pq, 0, nbytes, 0x00020000);
     }
   }
@@ -1023,7 +1023,7 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
     rrs = __builtin_amdgcn_make_buffer_rsrc(a.xg_recv, 0, nbytes, 0x00020000);
 #pragma unroll
     for (int q = 0; q < XWN; ++q) {
-      void* pq = (q < a.xg_world) ? (void*)a.xg_peers[q] : (void*)a.xg_recv;
+      void* pq = (q < a.xg_world) ? (void*)sload_ptr(a.xg_peers, q) : (void*)a.xg_recv;
       prs[q] = __builtin_amdgcn_make_buffer_rsrc(pq, 0, nbytes, 0x00020000);
     }
   }
@@ -1032,7 +1032,7 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
 
   // diagnostic phase stamps (profiling build, tools/prof_rows.py): shader-clock deltas of wave W
   // accumulated per phase; never compiled into production launches
-#ifdef DCT_WAVE_PROF
+#ifdef WAVE_PROF_BUILD
   unsigned long long rpt[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, rprev = 0;
 #define RSTAMP(k)                                                                            \
   if (a.prof) {                                                                              \
@@ -1268,7 +1268,7 @@ __device__ __forceinline__ void mlp_rows_wave(const WaveShape& sh, const MlpArgs
   for (int i = 0; i < PF - 1; ++i)
     if (s0 + i < a.steps && !step(s0 + i, vr_ring[i], ir_ring[i])) goto steps_done;
 steps_done:
-#ifdef DCT_WAVE_PROF
+#ifdef WAVE_PROF_BUILD
   if (a.prof && j == 0) {  // wave W's phase sums at prof[16 W + k]
 #pragma unroll
     for (int k = 0; k < 10; ++k) a.prof[16 * W + k] = rpt[k];
@@ -1351,15 +1351,14 @@ hipError_t launch_rows_d0(const WaveShape& sh, const MlpArgs& a, hipStream_t st)
   return hipErrorInvalidValue;
 }
 
-// the row-parallel kernel takes plain train-mode launches of 2-layer nets (DCT_MLP_ROWS=0: off)
+// the row-parallel kernel takes plain train-mode launches of 2-layer nets
 bool rows_eligible(int L, const MlpArgs& a) {
-  const bool enabled = dct::knobs().mlp_rows != 0;
-#ifdef DCT_WAVE_PROF
+#ifdef WAVE_PROF_BUILD
   const bool prof_ok = true;  // profiling build: the rows kernel stamps its phases into a.prof
 #else
   const bool prof_ok = !a.prof;
 #endif
-  return enabled && L == 2 && a.mode == 0 && !a.cursor && !a.pending && !a.stage && prof_ok && a.B >= 1 &&
+  return L == 2 && a.mode == 0 && !a.cursor && !a.pending && !a.stage && prof_ok && a.B >= 1 &&
          a.B <= 8 && a.m && a.v;
 }
 

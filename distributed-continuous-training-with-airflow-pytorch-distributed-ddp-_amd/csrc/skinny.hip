@@ -439,36 +439,30 @@ int dct_skinny_head(const uint16_t* H, const uint16_t* W, const float* bias, con
   // two-class heads up to K = 1024: 8 waves x 4 rows (32 rows per block, 2 waves per SIMD) once
   // that still gives >= 128 blocks; otherwise 4 waves x 4 rows
   const bool w8 = C <= 2 && K <= 1024;  // 8-wave blocks: LDS partials 8 x C x K fp32 <= 64 KB
-  int nwv = (w8 && B >= 128 * 32) ? 8 : 4, rpw = 4;
-  if (const int f = dct::knobs().skinny_head_rpw) rpw = (f == 8 && C <= 2) ? 8 : (f == 2 ? 2 : 4);
-  if (const int f = dct::knobs().skinny_head_waves) nwv = (f == 8 && w8) ? 8 : 4;  // debug / A-B
-  if (nwv == 8 && rpw == 8) rpw = 4;  // 8-wave blocks come with 2 or 4 rows per wave (the grid must match)
-  const dim3 grid((B + nwv * rpw - 1) / (nwv * rpw));
+  // 4 rows per wave (2 and 8 measured no faster: profiles/skinny_dw_split_sweep_*_r1.txt)
+  const int nwv = (w8 && B >= 128 * 32) ? 8 : 4;
+  const dim3 grid((B + nwv * 4 - 1) / (nwv * 4));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int NJ = K / 512;
-#define DCT_HEAD(CT_, NJ_, R_, W_)                                                                           \
-  hipLaunchKernelGGL((dct::skinny_head_kernel<CT_, NJ_, R_, W_>), grid, dim3(64 * W_), 0, st, H, W, bias, labels, \
+#define SKH_LAUNCH(CT_, NJ_, W_)                                                                             \
+  hipLaunchKernelGGL((dct::skinny_head_kernel<CT_, NJ_, 4, W_>), grid, dim3(64 * W_), 0, st, H, W, bias, labels, \
                      dH, dW, db, loss_sum, B, K, C, grad_scale, loss_kind, loss_scale, relu_mask)
-#define DCT_HEAD_R4(CT_, NJ_) \
-  if (rpw == 8) DCT_HEAD(CT_, NJ_, 8, 4); else if (rpw == 2) DCT_HEAD(CT_, NJ_, 2, 4); else DCT_HEAD(CT_, NJ_, 4, 4)
-#define DCT_HEAD_R(CT_, NJ_)                                                     \
-  if (nwv == 8) {                                                                \
-    if (rpw == 2) DCT_HEAD(CT_, NJ_, 2, 8); else DCT_HEAD(CT_, NJ_, 4, 8);        \
-  } else DCT_HEAD_R4(CT_, NJ_)
+#define SKH_WAVES(CT_, NJ_)                 \
+  if (nwv == 8) SKH_LAUNCH(CT_, NJ_, 8);   \
+  else SKH_LAUNCH(CT_, NJ_, 4)
   if (C == 1) {
-    switch (NJ) { case 1: DCT_HEAD_R(1, 1); break; case 2: DCT_HEAD_R(1, 2); break;
-                  case 3: DCT_HEAD_R4(1, 3); break; default: DCT_HEAD_R4(1, 4); break; }
+    switch (NJ) { case 1: SKH_WAVES(1, 1); break; case 2: SKH_WAVES(1, 2); break;
+                  case 3: SKH_LAUNCH(1, 3, 4); break; default: SKH_LAUNCH(1, 4, 4); break; }
   } else if (C == 2) {
-    switch (NJ) { case 1: DCT_HEAD_R(2, 1); break; case 2: DCT_HEAD_R(2, 2); break;
-                  case 3: DCT_HEAD_R4(2, 3); break; default: DCT_HEAD_R4(2, 4); break; }
+    switch (NJ) { case 1: SKH_WAVES(2, 1); break; case 2: SKH_WAVES(2, 2); break;
+                  case 3: SKH_LAUNCH(2, 3, 4); break; default: SKH_LAUNCH(2, 4, 4); break; }
   } else if (C <= 4) {
-    if (NJ == 1) DCT_HEAD(4, 1, 4, 4); else DCT_HEAD(4, 2, 4, 4);
+    if (NJ == 1) SKH_LAUNCH(4, 1, 4); else SKH_LAUNCH(4, 2, 4);
   } else {
-    DCT_HEAD(8, 1, 4, 4);
+    SKH_LAUNCH(8, 1, 4);
   }
-#undef DCT_HEAD_R
-#undef DCT_HEAD_R4
-#undef DCT_HEAD
+#undef SKH_WAVES
+#undef SKH_LAUNCH
   return (int)hipGetLastError();
 }
 
@@ -481,7 +475,6 @@ int dct_skinny_dw(const uint16_t* dZ, const uint16_t* X, float* dW, float* db, i
   const int max_splits = (B + 63) / 64;
   splits = splits > max_splits ? max_splits : splits;
   splits = splits < 1 ? 1 : splits;
-  if (dct::knobs().skinny_dw_splits > 0) splits = dct::knobs().skinny_dw_splits;  // debug / A-B
   const int rows_per = (B + splits - 1) / splits;
   const dim3 grid(kb, (B + rows_per - 1) / rows_per);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);

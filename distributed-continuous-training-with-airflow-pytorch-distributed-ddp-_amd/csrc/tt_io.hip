@@ -259,11 +259,8 @@ __global__ __launch_bounds__(64 * NW) void head_bwd_kernel(HeadArgs a) {
 
 // samples per workgroup (one wave each): 4.  16-sample (1024-thread) blocks quarter the
 // parameter-gradient atomics but measured no faster on the TabTransformer step (0.4195-0.4240 vs
-// 0.4184-0.4221 ms, profiles/tt_head_spb_side_dw_ab_r2.log); DCT_TT_HEAD_SPB=16 selects them.
-static inline int head_spb(int B) {
-  (void)B;
-  return knobs().tt_head_spb;
-}
+// 0.4184-0.4221 ms, profiles/tt_head_spb_side_dw_ab_r2.log), nor 2 / 1 (profiles/tt_head_spb_ab_r4.log).
+constexpr int HEAD_SPB = 4;
 
 }  // namespace ttio
 }  // namespace dct
@@ -303,10 +300,9 @@ int dct_tt_head_fwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C,
   a.W = (const float*)p[4]; a.bias = (const float*)p[5]; a.loss = (float*)p[6];
   a.partial = (float*)p[7]; a.ticket = (unsigned*)p[8];
   a.B = B; a.T = T; a.C = C; a.eps = eps;
-  const int nw = dct::ttio::head_spb(B);
+  constexpr int nw = dct::ttio::HEAD_SPB;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (nw == 16) hipLaunchKernelGGL(dct::ttio::head_fwd_kernel<16>, dim3((B + 15) / 16), dim3(1024), 0, st, a);
-  else hipLaunchKernelGGL(dct::ttio::head_fwd_kernel<4>, dim3((B + 3) / 4), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(dct::ttio::head_fwd_kernel<nw>, dim3((B + nw - 1) / nw), dim3(64 * nw), 0, st, a);
   return (int)hipGetLastError();
 }
 
@@ -321,10 +317,9 @@ int dct_tt_head_bwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C,
   a.dh = (float*)p[7]; a.dh16 = (uint16_t*)p[8]; a.dln_w = (float*)p[9]; a.dln_b = (float*)p[10];
   a.dW = (float*)p[11]; a.dbias = (float*)p[12];
   a.B = B; a.T = T; a.C = C; a.eps = eps;
-  const int nw = dct::ttio::head_spb(B);
+  constexpr int nw = dct::ttio::HEAD_SPB;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (nw == 16) hipLaunchKernelGGL(dct::ttio::head_bwd_kernel<16>, dim3((B + 15) / 16), dim3(1024), 0, st, a);
-  else hipLaunchKernelGGL(dct::ttio::head_bwd_kernel<4>, dim3((B + 3) / 4), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(dct::ttio::head_bwd_kernel<nw>, dim3((B + nw - 1) / nw), dim3(64 * nw), 0, st, a);
   return (int)hipGetLastError();
 }
 

@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void xg_allreduce_adam_kernel(XgAdamArgs a) {
 #pragma unroll
     for (int q = 0; q < XW; ++q) {
       if (q < W && q != rank) {
-        const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(a.peers[q], 0, nbytes, 0x00020000);
+        const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(sload_ptr(a.peers, q), 0, nbytes, 0x00020000);
         __builtin_amdgcn_raw_buffer_store_b128(d, pr, off, 0, XA_SYS);
       }
     }

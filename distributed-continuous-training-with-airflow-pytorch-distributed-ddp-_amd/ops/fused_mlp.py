@@ -16,6 +16,9 @@ import torch
 from ._native import native, ptr, stream_handle
 
 LOSS_KINDS = {"ce": 0, "mse": 1}
+# exchange polling of the wave kernels (csrc/mlp_fused.h xg_poll): two pipelined sweeps in flight
+# (profiles/xg_poll_pipelined_ab_r2.log; probe-then-sweep and sequential polls measured slower)
+XG_POLL = 3
 
 
 def mlp_num_params(dims: Sequence[int]) -> int:
@@ -137,8 +140,7 @@ class FusedMLPKernel:
             if xg.bytes < need:
                 raise ValueError(f"exchange buffer too small ({xg.bytes} < {need} bytes)")
             xg_args = dict(xg_recv=xg.recv, xg_peers=xg.peers, xg_world=xg.world, xg_rank=xg.rank,
-                           xg_status=xg.status, xg_timeout=int(xg_timeout_s * 1e8),
-                           xg_poll=int(os.environ.get("DCT_XG_POLL", "3")))
+                           xg_status=xg.status, xg_timeout=int(xg_timeout_s * 1e8), xg_poll=XG_POLL)
         self.plan.train(
             ptr(p), ptr(m) if need_mv else 0, ptr(v) if need_mv else 0, ptr(grad_out),
             ptr(X), X.stride(0), ptr(Y), ptr(idx), int(n_items), int(batch), int(steps), int(t0),
@@ -179,8 +181,7 @@ class FusedMLPKernel:
             if xg.bytes < need:
                 raise ValueError(f"exchange buffer too small ({xg.bytes} < {need} bytes)")
             xg_args = dict(xg_recv=xg.recv, xg_peers=xg.peers, xg_world=xg.world, xg_rank=xg.rank,
-                           xg_status=xg.status, xg_timeout=int(xg_timeout_s * 1e8),
-                           xg_poll=int(os.environ.get("DCT_XG_POLL", "3")))
+                           xg_status=xg.status, xg_timeout=int(xg_timeout_s * 1e8), xg_poll=XG_POLL)
             if xg_ticks is not None:
                 if not (xg_ticks.is_cuda and xg_ticks.dtype == torch.int64 and xg_ticks.numel() >= 1):
                     raise ValueError("xg_ticks must be a cuda int64 counter")

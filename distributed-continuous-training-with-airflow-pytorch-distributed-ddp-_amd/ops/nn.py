@@ -38,10 +38,9 @@ def _stream():
 # ----------------------------------------------------------------------------- engine binding
 class _Binding:
     def __init__(self, params: Iterable[torch.Tensor], shadows: Optional[Dict[int, torch.Tensor]],
-                 side_dw: bool = False, defer_dw: bool = False, defer_groups: Sequence[int] = ()):
+                 defer_dw: bool = False, defer_groups: Sequence[int] = ()):
         self.direct = {id(p) for p in params}
         self.shadows = shadows or {}
-        self.side_dw = side_dw
         self.defer_dw = defer_dw
         # deferred dW flush points: block counts (backward order) after which the queued dW GEMMs
         # are issued right away, e.g. (2, 2) for 4 blocks - see bound_params
@@ -58,7 +57,7 @@ _BOUND: Optional[_Binding] = None
 
 @contextlib.contextmanager
 def bound_params(params: Iterable[torch.Tensor], bf16_shadows: Optional[Dict[int, torch.Tensor]] = None,
-                 side_dw: bool = False, defer_dw: bool = False, defer_groups: Sequence[int] = ()):
+                 defer_dw: bool = False, defer_groups: Sequence[int] = ()):
     """Engine-scoped fast paths for the ops below (trainer/engines.py AutogradEngine):
 
     * gradient accumulation fusion - the weight-gradient GEMMs / LayerNorm column sums of a
@@ -68,12 +67,10 @@ def bound_params(params: Iterable[torch.Tensor], bf16_shadows: Optional[Dict[int
       fire (autograd runs them for undefined gradients too), so bucket all-reduces launch as before;
     * bf16 shadow weights - ``bf16_shadows[id(p)]`` (kept current by the fused Adam) replaces
       the per-step fp32->bf16 weight conversion;
-    * ``side_dw`` - the fused transformer block's weight-gradient GEMMs go to a side stream and
-      overlap the next (earlier) block's backward kernel; the caller joins them with
-      :func:`join_side_work` after backward.  Only for callers with no gradient hooks reading the
-      buffers during backward (no DDP bucket reducer): the grads land after the hooks fired;
-    * ``defer_dw`` - the same GEMMs are queued instead and issued by :func:`join_side_work` as
-      ONE grouped split-K launch for every block (same no-reducer condition);
+    * ``defer_dw`` - the fused transformer block's weight-gradient GEMMs are queued and issued by
+      :func:`join_side_work` as ONE grouped split-K launch for every block after backward.  (Running
+      them on a side stream under the earlier blocks' backward measured slower, 0.420 -> 0.445 ms,
+      profiles/tabular_dw_side_stream_ab_r2.log / tt_head_spb_side_dw_ab_r2.log; removed.);
     * ``defer_groups`` (with ``defer_dw``) - block counts in backward order after which the queued
       GEMMs are issued at once, INSIDE the backward of the block closing the group: with a DDP
       bucket reducer whose buckets follow the same groups (plan_buckets ``split_before``), the
@@ -84,37 +81,20 @@ def bound_params(params: Iterable[torch.Tensor], bf16_shadows: Optional[Dict[int
     # leftovers of a backward that never reached join_side_work (an aborted graph capture) belong
     # to that step: issuing them into this step's gradients would corrupt it
     _SIDE["deferred"].clear()
-    if _SIDE["pending"]:  # side-stream launches of such a step: order them before this step's work
-        torch.cuda.current_stream().wait_event(_SIDE["pending"][-1][0])
-        _SIDE["pending"].clear()
-    prev, _BOUND = _BOUND, _Binding(params, bf16_shadows, side_dw, defer_dw, defer_groups)
+    prev, _BOUND = _BOUND, _Binding(params, bf16_shadows, defer_dw, defer_groups)
     try:
         yield
     finally:
         _BOUND = prev
 
 
-# side-stream weight-gradient work (bound_params(side_dw=True)): the stream, and per launch the
-# completion event plus the operand tensors it reads (kept referenced until the join, so the
-# caching allocator cannot hand their memory to later main-stream work while the side stream
-# still reads it)
-_SIDE = {"stream": None, "pending": [], "deferred": []}
-
-
-def _side_stream(dev) -> "torch.cuda.Stream":
-    s = _SIDE["stream"]
-    if s is None or s.device != dev:
-        s = _SIDE["stream"] = torch.cuda.Stream(dev)
-    return s
+# deferred weight-gradient work (bound_params(defer_dw=True)): the queued dW GEMMs with the operand
+# tensors they read (kept referenced until they are issued)
+_SIDE = {"deferred": []}
 
 
 def join_side_work():
-    """Current stream waits for every weight-gradient launch issued on the side stream, and
-    issues the deferred ones (bound_params(defer_dw=True)) as grouped launches of up to 16."""
-    pend = _SIDE["pending"]
-    if pend:
-        torch.cuda.current_stream().wait_event(pend[-1][0])
-        pend.clear()
+    """Issue the deferred dW GEMMs (bound_params(defer_dw=True)) as grouped launches of up to 16."""
     _flush_deferred()
 
 
@@ -576,8 +556,9 @@ class _TTBlockFn(torch.autograd.Function):
         h1, out = torch.empty(M, dm, dtype=f32, device=dev), torch.empty(M, dm, dtype=f32, device=dev)
         f = torch.empty(M, FF, dtype=bf, device=dev)
         # with the fused backward the FFN pre-activation is not stored (32 KB per sample written and read
-        # back): tt_block_bwd_kernel recomputes it from a2 and W1 (DCT_TT_RECOMPUTE_PRE=0: store it)
-        recomp = _TT_FUSED_BWD and os.environ.get("DCT_TT_RECOMPUTE_PRE", "1") != "0"
+        # back): tt_block_bwd_kernel recomputes it from a2 and W1 (0.3697 -> 0.3632 ms per step,
+        # profiles/tt_recompute_pre_ab_r3.log); the unfused backward reads the stored one
+        recomp = _TT_FUSED_BWD
         pre = torch.empty(0 if recomp else M, FF, dtype=bf, device=dev)
         wT = torch.empty(2 * FF * dm + 4 * dm * dm, dtype=bf, device=dev)  # W2^T | W1^T | Wo^T | Wqkv^T
         vecs = [t.contiguous() for t in (ln1_w, ln1_b, bqkv, bo, ln2_w, ln2_b, b1, b2)]
@@ -659,16 +640,6 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
         if b.deferred_blocks in b.flush_at:  # this block closes a bucket group: issue its dW now
             _flush_deferred()
         dw2 = db2 = dw1 = db1 = dwo = dbo = dwqkv = dbqkv = None
-    elif direct and b.side_dw:
-        # the four dW GEMMs accumulate straight into the bound grads: run them on the side stream,
-        # behind this block's dX chain, while the main stream goes on to the earlier block
-        side = _side_stream(dev)
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            (dw2, db2), (dw1, db1), (dwo, dbo), (dwqkv, dbqkv) = _dw_gemm_grouped(nat, items, side.cuda_stream)
-        ev = torch.cuda.Event()
-        ev.record(side)
-        _SIDE["pending"].append((ev, items))
     else:
         (dw2, db2), (dw1, db1), (dwo, dbo), (dwqkv, dbqkv) = _dw_gemm_grouped(nat, items, st)
     _remember_bf16(dh, dh16)
@@ -700,13 +671,17 @@ def _tt_block_infer(h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w
     return out
 
 
+# whole-block TabTransformer kernels (csrc/tt_block.hip) on / off, and their fused backward (tests
+# compare them with the per-op autograd nodes by flipping these module flags)
+TT_FUSED = True
+TT_FUSED_BWD = True
+
+
 def tt_block_fusable(h: torch.Tensor, H: int, T: int, ffn: int) -> bool:
     """The whole-block fused kernels cover the TabTransformer benchmark shape exactly."""
-    import os
     global _TT_FUSED_BWD
-    _TT_FUSED_BWD = os.environ.get("DCT_TT_FUSED_BWD", "1") != "0"
-    return (h.is_cuda and h.dim() == 2 and h.shape[1] == 64 and H == 4 and T == 64 and ffn == 256
-            and os.environ.get("DCT_TT_FUSED", "1") != "0")
+    _TT_FUSED_BWD = TT_FUSED_BWD
+    return h.is_cuda and h.dim() == 2 and h.shape[1] == 64 and H == 4 and T == 64 and ffn == 256 and TT_FUSED
 
 
 def tt_block(h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, B: int, H: int, T: int,
@@ -873,9 +848,7 @@ class _TTHeadLossFn(torch.autograd.Function):
 
 
 def tt_head_fusable(h: torch.Tensor, num_classes: int) -> bool:
-    import os
-    return (h.is_cuda and h.shape[1] == 64 and 1 <= num_classes <= 8
-            and os.environ.get("DCT_TT_FUSED_HEAD", "1") != "0")
+    return h.is_cuda and h.shape[1] == 64 and 1 <= num_classes <= 8
 
 
 def tt_head_loss(h, y, B: int, T: int, ln_w, ln_b, W, bias, eps: float = 1e-5):

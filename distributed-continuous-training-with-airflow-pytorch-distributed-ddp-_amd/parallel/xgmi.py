@@ -49,7 +49,7 @@ def inkernel_enabled() -> bool:
 
 def probe_timeout_s() -> float:
     """Spin limit of the first exchange launch of a run (trainer/engines.py _probe_exchange)."""
-    return float(os.environ.get("DCT_XG_PROBE_TIMEOUT_S", "3"))
+    return 3.0
 
 
 def peer_report(ctx: DistContext):

@@ -79,6 +79,11 @@ class _EngineBase:
 class FusedMLPEngine(_EngineBase):
     name = "fused"
     epoch_engine = True  # runs whole epochs on device; the Trainer reads back per-step losses
+    # DDP step path (the RCCL / peer-exchange fallback of the in-kernel exchange): steps per captured
+    # graph chunk, and the update-then-grad single kernel where the wave kernel supports it (tests
+    # override these on the class to exercise the other paths)
+    GRAPH_CHUNK = 256
+    FUSED_UPDATE = True
 
     @staticmethod
     def applicable(model, device: torch.device, batch_size: int) -> bool:
@@ -111,14 +116,13 @@ class FusedMLPEngine(_EngineBase):
         # DDP step path; DCT_FORCE_DDP=1 drives it at world size 1 (single-GPU test of the
         # RCCL communicator + graph capture + device cursors)
         self.ddp = ctx.is_distributed or os.environ.get("DCT_FORCE_DDP", "0") == "1"
-        self.fused_update = self.kernel.fused_update_supported(self.B) and os.environ.get("DCT_FUSED_UPDATE", "1") != "0"
+        self.fused_update = self.kernel.fused_update_supported(self.B) and self.FUSED_UPDATE
         self.pending = torch.zeros(1, dtype=torch.int32, device=dev)
         self.stage = torch.zeros(64 * 4, dtype=torch.int32, device=dev)  # next-batch hand-off
-        # mlp_block5 grad-mode batch hand-off between DDP step launches (opt-in: DCT_B5_STAGE=1; the
-        # first measurement put the grad kernel 0.5 us slower with it, profiles/block5_stage_ab_r3.log)
-        self._b5_stage = os.environ.get("DCT_B5_STAGE", "0") == "1"
+        # (mlp_block5's grad mode takes no batch hand-off between DDP step launches: it measured 0.5 us
+        # slower, profiles/block5_stage_ab_r3.log; the wave kernels' fused update uses self.stage)
         self._graphs = {}
-        self.graph_chunk = int(os.environ.get("DCT_GRAPH_CHUNK", "256"))
+        self.graph_chunk = int(self.GRAPH_CHUNK)
         self.cursor = torch.zeros(1, dtype=torch.int32, device=dev)
         self.graph_used = False
         if ctx.is_distributed:
@@ -357,12 +361,10 @@ class FusedMLPEngine(_EngineBase):
                               cursor=self.cursor, loss_out=loss_out, pending=self.pending, stage=self.stage)
             self.comm.allreduce(self.gbuf.data_ptr(), self.P + 1, nat.DT_F32, nat.OP_AVG, stream)
             return
-        # DCT_B5_STAGE=1: the 3x128 grad kernel (mlp_block5) hands the next batch to the next launch
-        # through self.stage (tagged with its batch index: a mismatch after a cursor jump gathers)
         self.kernel.train(self.p, None, None, self.X, self.Y, self.idx, n_items=n_items, batch=self.B, steps=1,
                           t0=0, lr=a["lr"], dropout=self.dropout, seed=self.rank_seed, loss=self.loss,
                           grad_out=self.gbuf, step_counter=self.step_counter, cursor=self.cursor,
-                          loss_out=loss_out, stage=None if (self.kernel.plan.use_wave or not self._b5_stage) else self.stage)
+                          loss_out=loss_out)
         if self.gx is not None:
             from ..parallel.xgmi import allreduce_adam_
 
@@ -446,7 +448,7 @@ class FusedMLPEngine(_EngineBase):
         from ..parallel.xgmi import probe_timeout_s
 
         self._xg_probed = True
-        k = min(steps, int(os.environ.get("DCT_XG_PROBE_STEPS", "4")))
+        k = min(steps, 4)
         # a timed-out exchange may leave a step half applied (xg_adam: per block): every rank keeps
         # its pre-probe state to return to - replicas were identical before the probe
         snap = [t.clone() for t in (self.p, self.m, self.v, self.step_counter)]
@@ -620,7 +622,7 @@ class AutogradEngine(_EngineBase):
         # the flat bucket buffer, and bf16 shadow weights maintained by the fused Adam
         self._shadows = None
         self.flat_p16 = None
-        if dev.type == "cuda" and self.optimizer is not None and os.environ.get("DCT_FUSE_GRADS", "1") != "0":
+        if dev.type == "cuda" and self.optimizer is not None:
             self.flat_p16 = self.flat_p.to(torch.bfloat16)
             self.optimizer.p_bf16 = self.flat_p16
             self._shadows = {}
@@ -801,7 +803,7 @@ class AutogradEngine(_EngineBase):
     def device_loop_ok(self) -> bool:
         return (self.device.type == "cuda" and self.optimizer is not None and self.X.dim() == 2
                 and self.X.shape[1] % 4 == 0 and os.environ.get("DCT_GRAPH", "1") != "0"
-                and os.environ.get("DCT_DEVICE_LOOP", "1") != "0" and not getattr(self, "_graph_failed", False))
+                and not getattr(self, "_graph_failed", False))
 
     def run_device_steps(self, rows_dev: torch.Tensor, first_step: int, steps: int, loss_out: torch.Tensor):
         """Steps first_step .. first_step + steps - 1 over rows_dev (int64, device) batches of B;
@@ -902,11 +904,6 @@ class AutogradEngine(_EngineBase):
     def _bound(self):
         if self._shadows is None:
             return contextlib.nullcontext()
-        # DCT_TT_DW_SIDE=1: transformer-block dW GEMMs on a side stream (ops/nn.py), only without a
-        # bucket reducer (its grad hooks launch all-reduces that must see the finished gradients).
-        # Off by default: the overlap slowed both kernels, TabTransformer step 0.420 -> 0.445 ms
-        # (profiles/tt_head_spb_side_dw_ab_r2.log)
-        side = self.reducer is None and os.environ.get("DCT_TT_DW_SIDE", "0") == "1"
         # every transformer block's dW GEMMs as ONE grouped launch after backward (DCT_TT_DW_DEFER=0
         # keeps one launch per block): TabTransformer step 0.421-0.426 -> 0.407 ms
         # (profiles/tt_dw_defer_ab_r2.log).  With the native bucket reducer too: its hooks then only
@@ -920,7 +917,7 @@ class AutogradEngine(_EngineBase):
             # with block groups every group's dW launch is issued before its bucket's last hook
             # fires, so the hooks launch the buckets; otherwise they launch at finalize
             self.reducer.defer_launch = defer and self._has_deferrable_ops() and not groups
-        return bound_params(self.params, self._shadows, side_dw=side, defer_dw=defer, defer_groups=groups)
+        return bound_params(self.params, self._shadows, defer_dw=defer, defer_groups=groups)
 
     def _has_deferrable_ops(self) -> bool:
         """True when the model routes weight gradients through the deferred grouped dW path

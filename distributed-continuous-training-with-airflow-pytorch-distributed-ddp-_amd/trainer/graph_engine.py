@@ -8,7 +8,7 @@ gradients straight into the flat DDP bucket buffer -> RCCL ncclAvg per bucket as
 layer's dW is enqueued -> fused flat Adam with bf16 shadow weights.  The batch cursor, Adam step
 and loss slot live in device memory, so the step needs no host round trip: by default the C++
 executor simply enqueues it for every batch (11 launches from C++ stay ahead of the GPU: 171-173
-us/step), and ``DCT_MLP_GRAPH=1`` captures it once into a hipGraph replayed per full batch (175.5-
+us/step), and ``use_graph=True`` captures it once into a hipGraph replayed per full batch (175.5-
 176.9 us/step on ROCm 7: every replay starts ~8 us after the previous one ends; 8 steps per graph
 were slower still, profiles/tabular_graph_steps_ab_r2.log, profiles/mlp_graph_vs_eager_ab_r4.log).
 The partial last batch (reference ``drop_last=False``) runs with its real row count.
@@ -91,7 +91,7 @@ class GraphMLPEngine:
         self.adam = adam
         self.device = dev = ctx.device
         if use_graph is None:
-            use_graph = os.environ.get("DCT_MLP_GRAPH", "0") == "1" and os.environ.get("DCT_GRAPH", "1") != "0"
+            use_graph = False  # (the eager C++ enqueue beats the replays; use_graph=True for A/Bs)
         self.use_graph = use_graph
         L = len(self.dims) - 1
         self.L = L

@@ -24,7 +24,7 @@ def main():
     path = sys.argv[4] if len(sys.argv) > 4 else "step"
     if path == "step":
         os.environ["DCT_XG_INKERNEL"] = "0"
-    os.environ.setdefault("DCT_GRAPH_CHUNK", "16")
+    FusedMLPEngine.GRAPH_CHUNK = 16
     ctx = init_distributed("gpu", backend="gloo")
     X, Y = weather_tensors(3000, seed=1)
     rows = torch.randperm(3000, generator=torch.Generator().manual_seed(0))

@@ -16,25 +16,41 @@ def nat():
 
 
 def test_knobs_defaults_and_reload(nat, monkeypatch):
-    for k in ("DCT_GEMM_STAGES", "DCT_MLP_BLOCK", "DCT_TT_HEAD_SPB", "DCT_FUSED_HEAD", "DCT_REDUCER_INLINE"):
+    for k in ("DCT_MLP_BLOCK", "DCT_FUSED_HEAD", "DCT_REDUCER_INLINE", "DCT_REDUCER_STANDIN_US", "DCT_DW_INTO_ADAM"):
         monkeypatch.delenv(k, raising=False)
     nat.reload_knobs()
     d = nat.knobs()
-    assert d["gemm_stages"] == 0 and d["mlp_block"] == -1 and d["tt_head_spb"] == 4
-    assert d["fused_head"] == 1 and d["reducer_inline"] == -2 and d["reducer_standin_us"] == 0 and d["gemm_bm64_nk"] == 4
-    monkeypatch.setenv("DCT_GEMM_STAGES", "4")
+    assert d["mlp_block"] == -1 and d["fused_head"] == 1 and d["dw_into_adam"] == 1
+    assert d["reducer_inline"] == -2 and d["reducer_standin_us"] == 0 and d["reducer_standin_wgs"] == 16
     monkeypatch.setenv("DCT_MLP_BLOCK", "3")
-    monkeypatch.setenv("DCT_TT_HEAD_SPB", "16")
     monkeypatch.setenv("DCT_FUSED_HEAD", "0")
+    monkeypatch.setenv("DCT_REDUCER_STANDIN_US", "60")
     # the environment alone changes nothing: the struct is re-read only at plan / bind time
-    assert nat.knobs()["gemm_stages"] == 0
+    assert nat.knobs()["mlp_block"] == -1
     nat.reload_knobs()
     d = nat.knobs()
-    assert d["gemm_stages"] == 4 and d["mlp_block"] == 3 and d["tt_head_spb"] == 16 and d["fused_head"] == 0
+    assert d["mlp_block"] == 3 and d["fused_head"] == 0 and d["reducer_standin_us"] == 60
     monkeypatch.setenv("DCT_MLP_BLOCK", "0")
-    monkeypatch.setenv("DCT_TT_HEAD_SPB", "7")  # only 4 or 16
+    monkeypatch.setenv("DCT_REDUCER_INLINE", "7")  # out of range: back to auto
     nat.reload_knobs()
-    assert nat.knobs()["mlp_block"] == 0 and nat.knobs()["tt_head_spb"] == 4
+    assert nat.knobs()["mlp_block"] == 0 and nat.knobs()["reducer_inline"] == -2
+
+
+def test_knob_count_stays_small():
+    """measured-and-rejected variants are deleted with their knobs.  Every DCT_* name the
+    package, bench.py and jobs/ read (config surface, orchestration, tests' A/B hooks included)."""
+    import os
+    import re
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    names = set()
+    for base in ("distributed-continuous-training-with-airflow-pytorch-distributed-ddp-_amd", "jobs"):
+        for dp, _, fs in os.walk(os.path.join(root, base)):
+            for f in fs:
+                if f.endswith((".py", ".cpp", ".h", ".hip")):
+                    names |= set(re.findall(r"DCT_[A-Z0-9_]+", open(os.path.join(dp, f)).read()))
+    names |= set(re.findall(r"DCT_[A-Z0-9_]+", open(os.path.join(root, "bench.py")).read()))
+    assert len(names) <= 60, sorted(names)
 
 
 def test_mlp_plan_reloads_knobs(nat, monkeypatch):

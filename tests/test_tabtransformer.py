@@ -121,11 +121,11 @@ def test_device_loop_matches_host_loop(cuda, F_):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("knob", ["DCT_TT_DW_SIDE", "DCT_TT_DW_DEFER"])
-def test_side_stream_dw_matches_in_stream(cuda, monkeypatch, knob):
-    """Fused-block dW GEMMs on the side stream (DCT_TT_DW_SIDE=1, joined after backward) or deferred
-    to one grouped launch after backward (DCT_TT_DW_DEFER=1) train the same trajectory as the
-    per-block launches on the compute stream, eager steps and captured step graphs alike."""
+def test_deferred_dw_matches_in_stream(cuda, monkeypatch):
+    """Fused-block dW GEMMs deferred to one grouped launch after backward (DCT_TT_DW_DEFER=1) train
+    the same trajectory as the per-block launches on the compute stream, eager steps and captured
+    step graphs alike."""
+    knob = "DCT_TT_DW_DEFER"
     from dct_amd.parallel.dist import init_distributed
     from dct_amd.trainer.engines import AutogradEngine
     from dct_amd.trainer.trainer import seed_everything

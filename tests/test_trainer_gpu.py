@@ -94,8 +94,8 @@ def test_ddp_step_path_world1_matches_persistent(fused_update, graph, hidden, mo
     def run(force):
         monkeypatch.setenv("DCT_FORCE_DDP", force)
         monkeypatch.setenv("DCT_GRAPH", graph)
-        monkeypatch.setenv("DCT_GRAPH_CHUNK", "7")
-        monkeypatch.setenv("DCT_FUSED_UPDATE", fused_update)
+        monkeypatch.setattr(FusedMLPEngine, "GRAPH_CHUNK", 7)
+        monkeypatch.setattr(FusedMLPEngine, "FUSED_UPDATE", fused_update == "1")
         torch.manual_seed(0)
         model = MLPClassifier(5, hidden=hidden, dropout=0.0)
         ctx = init_distributed("gpu")

@@ -1,4 +1,4 @@
-"""A/B of the GEMM pipeline depth on the tabular MLP step's own shapes (interleaved rounds, one process).
+"""The bf16 MFMA GEMM on the tabular MLP step's own shapes (interleaved rounds, one process).
 
     python tools/bench_gemm_mlp.py [--rounds 5]
 
@@ -7,8 +7,7 @@ Shapes (batch 4096, 256-1024-1024-1024-2, bench.py --model tabular-mlp-4x1024):
   dX       dZ W           4096x1024x1024 (NN) x2, bf16 out
   dW       dZ^T X         1024x1024x4096 (TN, fp32 split-K) x2, 1024x256x4096
 plus the TabTransformer step's projection / FFN shapes (32768 token rows, d 64, ffn 256).
-Each variant sets DCT_GEMM_STAGES / DCT_GEMM_SPLIT_WG and re-reads the knob struct (reload_knobs).
-Prints one JSON line per (shape, variant) with the median over rounds.
+Prints one JSON line per shape with the median over rounds, next to hipBLASLt on the same operands.
 """
 import argparse
 import json
@@ -40,46 +39,15 @@ SHAPES = [  # name, M, N, K, ta, tb, out_f32
     ("tt_dw_fc2", 64, 256, 32768, 1, 0, 1),
     ("tt_dw_o", 64, 64, 32768, 1, 0, 1),
 ]
-VARIANTS = {
-    "s2": {"DCT_GEMM_STAGES": "2"},
-    "s4": {"DCT_GEMM_STAGES": "4"},
-    "s2_wg256": {"DCT_GEMM_STAGES": "2", "DCT_GEMM_SPLIT_WG": "256"},
-    "s4_wg256": {"DCT_GEMM_STAGES": "4", "DCT_GEMM_SPLIT_WG": "256"},
-    "s4_wg1024": {"DCT_GEMM_STAGES": "4", "DCT_GEMM_SPLIT_WG": "1024"},
-    "s2_splits128": {"DCT_GEMM_STAGES": "2", "DCT_GEMM_SPLITS": "128"},
-    "s4_splits128": {"DCT_GEMM_STAGES": "4", "DCT_GEMM_SPLITS": "128"},
-}
-ENV_KEYS = ("DCT_GEMM_STAGES", "DCT_GEMM_SPLIT_WG", "DCT_GEMM_SPLITS", "DCT_GEMM_BM64_NK", "DCT_GEMM_SPLIT_TWO_PASS",
-            "DCT_GEMM_8W", "DCT_GEMM_BM128", "DCT_GEMM_SPLIT_WS")
-if os.environ.get("AB_SET") == "dw":  # split-K sweep on the transformer dW shapes only
-    SHAPES = [s for s in SHAPES if s[0].startswith("tt_dw") or s[0] == "dw_l1"]
-    VARIANTS = {f"{st}_sp{sp}": {"DCT_GEMM_STAGES": st[1], "DCT_GEMM_SPLITS": str(sp)}
-                for st in ("s2", "s4") for sp in (8, 16, 32, 64)}
-
-if os.environ.get("AB_SET") == "bm64":  # half-height tiles (2 workgroups per CU) on the big MLP GEMMs
-    SHAPES = [s for s in SHAPES if not s[0].startswith(("tt_dw", "dw_"))]
-    VARIANTS = {"bm128": {}, "bm64": {"DCT_GEMM_BM64_NK": "64"}, "bm64_s4": {"DCT_GEMM_BM64_NK": "64",
-                                                                              "DCT_GEMM_STAGES": "4"}}
-if os.environ.get("AB_SET") == "tab":  # the tabular step's big GEMMs: every 4096 x 1024 x 1024 tiling
-    SHAPES = [s for s in SHAPES if s[0] in ("fwd_l1", "dx_l1")]
-    VARIANTS = {"8w_k128": {}, "bm64": {"DCT_GEMM_8W": "0"},
-                "bm128": {"DCT_GEMM_8W": "0", "DCT_GEMM_BM128": "1"},
-                "bm128_s4": {"DCT_GEMM_8W": "0", "DCT_GEMM_BM128": "1", "DCT_GEMM_STAGES": "4"}}
 if os.environ.get("AB_SET") == "layout":  # transformer dW shapes in every operand layout (what would a
     # feature-major copy of the activations buy?): (1,0) = today's dZ^T X on token-major storage
     SHAPES = [(f"{n}_ta{ta}tb{tb}", M, N, K, ta, tb, 1) for n, M, N, K, *_ in SHAPES if n.startswith("tt_dw")
               for ta, tb in ((1, 0), (0, 1), (0, 0), (1, 1))]
-    VARIANTS = {"default": {}}
-
 if os.environ.get("AB_SET") == "dwcmp":  # the tabular dW shapes: default launch vs hipBLASLt
     SHAPES = [s for s in SHAPES if s[0] in ("dw_l1", "dw_l0", "fwd_l1", "dx_l1")]
-    VARIANTS = {"default": {}}
-if os.environ.get("AB_SET") == "twopass":  # split-K dW: two-pass partials + reduce vs fp32 atomics
-    SHAPES = [s for s in SHAPES if s[0] in ("dw_l1", "dw_l0") or s[0].startswith("tt_dw")]
-    VARIANTS = {"two_pass": {"DCT_GEMM_SPLIT_TWO_PASS": "1"}, "atomics": {"DCT_GEMM_SPLIT_TWO_PASS": "0"},
-                "in_launch": {"DCT_GEMM_SPLIT_WS": "1"},
-                "two_pass_wg512": {"DCT_GEMM_SPLIT_TWO_PASS": "1", "DCT_GEMM_SPLIT_WG": "512"},
-                "two_pass_wg1024": {"DCT_GEMM_SPLIT_TWO_PASS": "1", "DCT_GEMM_SPLIT_WG": "1024"}}
+# (round 1-4 A/B variants - pipeline depths, split-K targets, tile heights, in-launch split-K - were
+# deleted with their knobs in round 5; their results are in profiles/gemm_*_r*.log)
+VARIANTS = {"default": {}}
 
 
 def main():
@@ -106,10 +74,6 @@ def main():
         bufs[name] = (sets, C)
     for _ in range(a.rounds):
         for vname, env in VARIANTS.items():
-            for k in ENV_KEYS:
-                os.environ.pop(k, None)
-            os.environ.update(env)
-            nat.reload_knobs()  # the launcher reads the knob struct, not the environment
             for name, M, N, K, ta, tb, of in SHAPES:
                 sets, C = bufs[name]
                 cyc = [0]
@@ -128,8 +92,6 @@ def main():
                 e.record()
                 torch.cuda.synchronize()
                 res.setdefault((name, vname), []).append(s.elapsed_time(e) / a.iters * 1e3)
-    for k in ENV_KEYS:
-        os.environ.pop(k, None)
     for name, M, N, K, ta, tb, of in SHAPES:  # hipBLASLt (torch.matmul) on the same operands
         (A, B), C = bufs[name][0][0], bufs[name][1]
         At = A.t() if ta else A

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Classifier head of the tabular step (B=4096 rows, K=1024, 2 classes): the fused skinny_head
-kernel in its block shapes vs the four-kernel chain it replaces (skinny_fwd -> loss -> skinny_dw
+kernel vs the four-kernel chain it replaces (skinny_fwd -> loss -> skinny_dw
 -> skinny_dx).  Times 200 back-to-back launches with HIP events; prints one JSON line per variant."""
 import json
 import os
@@ -53,12 +53,7 @@ def main():
         return e0.elapsed_time(e1) / n * 1e3
 
     print(json.dumps({"variant": "chain(4 kernels)", "us": round(timeit(chain), 2)}), flush=True)
-    for waves, rpw in ((4, 4), (4, 8), (4, 2), (8, 4), (8, 2)):
-        os.environ["DCT_SKINNY_HEAD_WAVES"], os.environ["DCT_SKINNY_HEAD_RPW"] = str(waves), str(rpw)
-        native().reload_knobs()  # the launchers read the knob struct, filled at plan / bind time
-        print(json.dumps({"variant": f"fused waves={waves} rows/wave={rpw}", "us": round(timeit(fused), 2)}),
-              flush=True)
-
+    print(json.dumps({"variant": "fused", "us": round(timeit(fused), 2)}), flush=True)
 
 if __name__ == "__main__":
     main()
