@@ -37,6 +37,9 @@ class MlpStepExecutor {
 
  private:
   bool fused_head_knob_ = true, dw_into_adam_knob_ = true;  // DCT_FUSED_HEAD / DCT_DW_INTO_ADAM at construction
+  int nzr_ = 0;                                   // gradient ranges a full-batch step zeroes (plan_partials)
+  int64_t zr_off_[4] = {}, zr_cnt_[4] = {};
+  int64_t zr_all_off_[1] = {0}, zr_all_cnt_[1] = {0};  // the whole buffer (set in the constructor)
   void forward(int rows, hipStream_t st, int layers = -1);  // layers 0 .. layers-1 (default all)
   bool fused_head() const;
   void plan_partials();

@@ -11,25 +11,37 @@ namespace dct {
 
 // Batch gather: row r (< B) of the batch is dataset row idx[(*cursor) * stride + r] (wrapping inside
 // [0, n_items) for a partial last batch). 16-byte vector copies; labels gathered alongside.
+// up to 4 ranges of the flat gradient buffer to zero (element offset / count; 16-B aligned starts)
+struct ZeroRanges {
+  int n;
+  int64_t off[4], cnt[4];
+};
+
+__device__ __forceinline__ void zero_range(float* base, int64_t n) {
+  const int64_t n4 = n >> 2;
+  const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float4* z4 = reinterpret_cast<float4*>(base);
+  for (int64_t i = t; i < n4; i += gs) z4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t < n - (n4 << 2)) base[(n4 << 2) + t] = 0.f;
+}
+
 __global__ __launch_bounds__(256) void gather_batch_kernel(const uint4* __restrict__ X, int row_vec,
                                                            const int* __restrict__ Y, const int* __restrict__ idx,
                                                            const int* __restrict__ cursor, int stride, int B,
                                                            int n_items, uint4* __restrict__ xdst,
                                                            int* __restrict__ ydst, int* __restrict__ step_counter,
-                                                           float* __restrict__ zero, int64_t zero_n) {
+                                                           float* __restrict__ zero, ZeroRanges zr) {
   const int c = cursor ? *cursor : 0;
   // the training step's prologue rides along: Adam step counter += 1 (read by adam_flat at the
-  // end of the step) and the flat gradient buffer (+ loss slot) zeroed by the whole grid.  A
-  // kernel, not hipMemsetAsync: a captured memset node was not reliably ordered after the
-  // previous replay's Adam kernel (back-to-back hipGraphLaunch, ROCm 7) and Adam read zeroed grads.
+  // end of the step) and the accumulated ranges of the flat gradient buffer (+ loss slot) zeroed by
+  // the whole grid.  A kernel, not hipMemsetAsync: a captured memset node was not reliably ordered
+  // after the previous replay's Adam kernel (back-to-back hipGraphLaunch, ROCm 7).
   if (step_counter && blockIdx.x == 0 && threadIdx.x == 0) step_counter[0] += 1;
   if (zero) {
-    const int64_t n4 = zero_n >> 2;
-    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    float4* z4 = reinterpret_cast<float4*>(zero);
-    for (int64_t i = t; i < n4; i += gs) z4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (t < zero_n - (n4 << 2)) zero[(n4 << 2) + t] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q < zr.n) zero_range(zero + zr.off[q], zr.cnt[q]);
   }
   const int total = B * row_vec;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
@@ -211,21 +223,40 @@ int dct_reducer_check(unsigned long long* s, void* stream) {
   return (int)hipGetLastError();
 }
 
-int dct_gather_batch_step(const void* X, int row_bytes, const int* Y, const int* idx, const int* cursor, int stride,
-                          int B, int n_items, void* xdst, int* ydst, int* step_counter, float* zero,
-                          int64_t zero_n, void* stream) {
+// zero: buffer base; nr ranges [off[q], off[q] + cnt[q]) of it (off[q] % 4 == 0), nr <= 4
+int dct_gather_batch_step_ranges(const void* X, int row_bytes, const int* Y, const int* idx, const int* cursor,
+                                 int stride, int B, int n_items, void* xdst, int* ydst, int* step_counter, float* zero,
+                                 int nr, const int64_t* off, const int64_t* cnt, void* stream) {
   if (B <= 0) return 0;
   if (row_bytes % 16 || (((uintptr_t)X) | ((uintptr_t)xdst)) & 15) return (int)hipErrorInvalidValue;
   if (zero && (((uintptr_t)zero) & 15)) return (int)hipErrorInvalidValue;
+  if (nr < 0 || nr > 4) return (int)hipErrorInvalidValue;
+  dct::ZeroRanges zr{};
+  zr.n = zero ? nr : 0;
+  int64_t zmax = 0;
+  for (int q = 0; q < zr.n; ++q) {
+    if (off[q] % 4 || cnt[q] < 0) return (int)hipErrorInvalidValue;
+    zr.off[q] = off[q];
+    zr.cnt[q] = cnt[q];
+    zmax = cnt[q] > zmax ? cnt[q] : zmax;
+  }
   const int rv = row_bytes / 16;
   int64_t work = (int64_t)B * rv;
-  if (zero && (zero_n + 3) / 4 > work) work = (zero_n + 3) / 4;
+  if ((zmax + 3) / 4 > work) work = (zmax + 3) / 4;
   int grid = (int)((work + 255) / 256);
   grid = grid > 2048 ? 2048 : (grid < 1 ? 1 : grid);
   hipLaunchKernelGGL(dct::gather_batch_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      (const uint4*)X, rv, Y, idx, cursor, stride, B, n_items, (uint4*)xdst, ydst, step_counter, zero,
-                     zero_n);
+                     zr);
   return (int)hipGetLastError();
+}
+
+int dct_gather_batch_step(const void* X, int row_bytes, const int* Y, const int* idx, const int* cursor, int stride,
+                          int B, int n_items, void* xdst, int* ydst, int* step_counter, float* zero,
+                          int64_t zero_n, void* stream) {
+  const int64_t off = 0;
+  return dct_gather_batch_step_ranges(X, row_bytes, Y, idx, cursor, stride, B, n_items, xdst, ydst, step_counter,
+                                      zero, zero ? 1 : 0, &off, &zero_n, stream);
 }
 
 // Zero n fp32 values with a kernel (graph-captured steps: a kernel node instead of a memset node,
@@ -235,8 +266,12 @@ int dct_zero_f32(float* p, int64_t n, void* stream) {
   if (((uintptr_t)p) & 15) return (int)hipErrorInvalidValue;
   int grid = (int)(((n + 3) / 4 + 255) / 256);
   grid = grid > 2048 ? 2048 : (grid < 1 ? 1 : grid);
+  dct::ZeroRanges zr{};
+  zr.n = 1;
+  zr.off[0] = 0;
+  zr.cnt[0] = n;
   hipLaunchKernelGGL(dct::gather_batch_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     nullptr, 0, nullptr, nullptr, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, p, n);
+                     nullptr, 0, nullptr, nullptr, nullptr, 0, 0, 0, nullptr, nullptr, nullptr, p, zr);
   return (int)hipGetLastError();
 }
 
