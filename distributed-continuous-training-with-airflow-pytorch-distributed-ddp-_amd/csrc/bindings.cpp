@@ -177,6 +177,7 @@ PYBIND11_MODULE(_dct_native, m) {
     d["mlp_force_lds"] = k.mlp_force_lds; d["mlp_block"] = k.mlp_block; d["fused_head"] = k.fused_head;
     d["dw_into_adam"] = k.dw_into_adam; d["reducer_inline"] = k.reducer_inline; d["rccl_one_rank"] = k.rccl_one_rank;
     d["reducer_standin_us"] = k.reducer_standin_us; d["reducer_standin_wgs"] = k.reducer_standin_wgs;
+    d["reducer_flag_edges"] = k.reducer_flag_edges;
     return d;
   });
   // PCI bus id of a device: identifies the physical GPU behind a rank (ranks sharing one GPU in a
@@ -550,6 +551,7 @@ PYBIND11_MODULE(_dct_native, m) {
       .def_property_readonly("num_buckets", &dct::BucketReducer::num_buckets)
       .def_property_readonly("launched", &dct::BucketReducer::launched)
       .def_property_readonly("launched_before_finalize", &dct::BucketReducer::launched_before_finalize)
+      .def("edge_timeouts", &dct::BucketReducer::edge_timeouts)
       .def_property_readonly("comm_stream", &dct::BucketReducer::comm_stream)
       .def_property_readonly("inline_mode", &dct::BucketReducer::inline_mode)
       .def("enable_timing", &dct::BucketReducer::enable_timing, py::arg("check") = false)
@@ -598,6 +600,7 @@ PYBIND11_MODULE(_dct_native, m) {
       .def("eval_batch", &dct::MlpStepExecutor::eval_batch, py::arg("X"), py::arg("row_bytes"), py::arg("Y"),
            py::arg("idx"), py::arg("n_items"), py::arg("cursor"), py::arg("rows"), py::arg("stats"),
            py::arg("stream"))
+      .def_property("adam_ride", &dct::MlpStepExecutor::adam_ride, &dct::MlpStepExecutor::set_adam_ride)
       .def_property_readonly("num_params", &dct::MlpStepExecutor::num_params)
       .def_property_readonly("part_fallbacks", &dct::MlpStepExecutor::part_fallbacks)
       .def_property_readonly("partial_layers", &dct::MlpStepExecutor::partial_layers);

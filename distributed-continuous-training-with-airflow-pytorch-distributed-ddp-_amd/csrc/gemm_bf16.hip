@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include "dct_common.h"
+#include "adam_impl.h"
 #include "kernels.h"
 #include "knobs.h"
 
@@ -842,6 +843,57 @@ extern "C" int dct_gemm_bf16_dw_partials(const uint16_t* dZ, const uint16_t* X, 
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(fn, dim3(tiles * splits), dim3(512), lds, reinterpret_cast<hipStream_t>(stream),
                      g, splits);
+  return (int)hipGetLastError();
+}
+
+// dW split-K partials with an Adam range riding along: workgroups [0, gemm_wgs) are the GEMM's
+// (XCD-aware remap over that count), the rest run adam_flat_range over the range.  The Adam
+// workgroups need no LDS but inherit the launch's dynamic LDS (64 KB), so one sits beside each
+// GEMM tile on a CU (2 x 64 KB <= 160 KB): the HBM-bound optimizer streams under the GEMM, which is
+// bound by each CU's global -> LDS rate (tabular step: the separate Adam launch was 17 us).
+template <int S_ADAM>
+__global__ __launch_bounds__(512, 2) void gemm2_dw_adam_kernel(dct::GemmArgs g, int splits, int gemm_wgs,
+                                                               dct::AdamArgs a, int64_t lo, int64_t hi) {
+  if ((int)blockIdx.x < gemm_wgs) {
+    const int orig = blockIdx.x, xcd = orig & 7;
+    const int q8 = gemm_wgs >> 3, r8 = gemm_wgs & 7;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+    dct::gemm2_body<true, false, true, 128, 2, 4>(g, splits, wgid);
+  } else {
+    dct::adam_scalar_range<true, S_ADAM>(a, lo, hi, blockIdx.x - gemm_wgs, gridDim.x - gemm_wgs);
+  }
+}
+
+extern "C" int dct_gemm_bf16_dw_partials_adam(const uint16_t* dZ, const uint16_t* X, float* part, float* colsum, int M,
+                                              int N, int K, int splits, const dct::AdamRange* r, void* stream) {
+  if (!r) return dct_gemm_bf16_dw_partials(dZ, X, part, colsum, M, N, K, splits, stream);
+  dct::GemmArgs g{};
+  g.A = dZ; g.B = X; g.C = part; g.M = M; g.N = N; g.K = K; g.lda = M; g.ldb = N; g.ldc = N;
+  g.epilogue = dct::EPI_NONE; g.out_f32 = 1; g.accumulate = 0; g.alpha = 1.0f;
+  g.vec_a = ((((uintptr_t)dZ) & 15) == 0) && (M % 8 == 0);
+  g.vec_b = ((((uintptr_t)X) & 15) == 0) && (N % 8 == 0);
+  g.colsum = colsum;
+  g.split_part = part;
+  const int nk = K / dct::GBK;
+  if (!part || M <= 0 || N <= 0 || !gemm_v2_ok(g, 1, 0) || splits < 1 || splits > nk) return (int)hipErrorInvalidValue;
+  const int tiles = ((M + dct::GBM - 1) / dct::GBM) * ((N + dct::GBN - 1) / dct::GBN);
+  const int nk_slice = (nk + splits - 1) / splits;
+  if ((splits - 1) * nk_slice >= nk) return (int)hipErrorInvalidValue;
+  dct::AdamArgs a{};
+  int max_sp = 1;
+  const int e0 = dct::adam_args_from_range(*r, a, &max_sp);
+  if (e0) return e0;
+  const int gemm_wgs = tiles * splits;
+  // one Adam workgroup (512 threads) per CU beside the GEMM tiles, fewer for a short range
+  const int64_t work = r->hi - r->lo;  // elements, one per thread and iteration
+  int adam_wgs = (int)std::min<int64_t>((work + 511) / 512, device_cus());
+  if (adam_wgs < 1) adam_wgs = 1;
+  const size_t lds = (size_t)(nk_slice > 1 ? 4 : 2) * dct::G2_BYTES;
+  auto fn = max_sp > 4 ? gemm2_dw_adam_kernel<8> : gemm2_dw_adam_kernel<4>;
+  hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(fn, dim3(gemm_wgs + adam_wgs), dim3(512), lds, reinterpret_cast<hipStream_t>(stream), g, splits,
+                     gemm_wgs, a, r->lo, r->hi);
   return (int)hipGetLastError();
 }
 

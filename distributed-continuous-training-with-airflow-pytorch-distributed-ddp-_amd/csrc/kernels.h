@@ -27,12 +27,41 @@ struct GemmArgs {
                           // split_part[s][M][N]; splitk_reduce_kernel sums the slices into C afterwards
 };
 
+// An Adam range of the flat buffers, launched on its own or riding in another launch (the wide-MLP
+// executor: each layer's Adam in the next lower layer's dW launch, csrc/mlp_executor.cpp).  Fields as
+// AdamArgs (adam_impl.h); elements [lo, hi), lo % 4 == 0, hi % 4 == 0 or hi == n.
+struct AdamRange {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  uint16_t* p_bf16;
+  int64_t n;
+  float lr, b1, b2, eps, wd, grad_scale;
+  int decoupled;
+  const int* step_counter;
+  int nparts;
+  int64_t part_off[3], part_n[3];
+  const float* part[3];
+  int part_splits[3];
+  int64_t lo, hi;
+};
+
 }  // namespace dct
 
 extern "C" {
+// dW = dZ^T X as split-K partials (dct_gemm_bf16_dw_partials) with Adam over r's range in extra
+// workgroups of the same launch, co-resident with the GEMM tiles (r == nullptr: the GEMM alone)
+int dct_gemm_bf16_dw_partials_adam(const uint16_t* dZ, const uint16_t* X, float* part, float* colsum, int M, int N,
+                                   int K, int splits, const dct::AdamRange* r, void* stream);
+// Adam over r's range as its own launch (+ the step epilogue: loss_out[*cursor] = *loss_slot, cursor += 1)
+int dct_adam_range(const dct::AdamRange* r, int* cursor, const float* loss_slot, float* loss_out, int loss_cap,
+                   void* stream);
 // reducer instrumentation (step_kernels.hip)
 int dct_reducer_stamp(unsigned long long* dst, void* stream);
 int dct_busy_spin(long long ticks, int wgs, void* stream);
+int dct_flag_signal(int* flag, void* stream);
+int dct_flag_wait(int* flag, int* consumed, int* status, void* stream);
 int dct_reducer_close(unsigned long long* s, void* stream);
 int dct_reducer_check(unsigned long long* s, void* stream);
 int dct_phase_accum(unsigned long long* b, int n, void* stream);

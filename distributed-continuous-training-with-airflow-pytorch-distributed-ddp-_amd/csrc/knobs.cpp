@@ -28,6 +28,7 @@ void knobs_reload() {
   k.rccl_one_rank = env_int("DCT_RCCL_ONE_RANK", 0) == 1;
   k.reducer_standin_us = env_int("DCT_REDUCER_STANDIN_US", 0);
   k.reducer_standin_wgs = env_int("DCT_REDUCER_STANDIN_WGS", 16);
+  k.reducer_flag_edges = env_int("DCT_REDUCER_FLAG_EDGES", 1) != 0;
   if (k.reducer_standin_us < 0) k.reducer_standin_us = 0;
   if (k.reducer_standin_wgs < 1) k.reducer_standin_wgs = 1;
   if (k.reducer_standin_wgs > 1024) k.reducer_standin_wgs = 1024;

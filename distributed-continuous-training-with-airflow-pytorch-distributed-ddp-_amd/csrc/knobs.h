@@ -21,6 +21,7 @@ struct Knobs {
   int reducer_standin_us = 0;   // DCT_REDUCER_STANDIN_US: test-only stand-in collective - a busy kernel of this many us
                                 // per step (split over the buckets by size) on the collective's stream
   int reducer_standin_wgs = 16; // DCT_REDUCER_STANDIN_WGS: its workgroups (one wave each, no LDS)
+  int reducer_flag_edges = 1;   // DCT_REDUCER_FLAG_EDGES: eager fork / join edges as device counters (1) or events (0)
   int rccl_one_rank = 0;    // DCT_RCCL_ONE_RANK=1: call RCCL for one-rank in-place collectives too
 };
 

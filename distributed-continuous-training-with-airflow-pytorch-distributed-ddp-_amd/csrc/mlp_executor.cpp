@@ -158,6 +158,28 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
                                   reinterpret_cast<const int*>(idx), cur, B_, rows, n_items, acts_[0], y_, sc, g_,
                                   skip ? nzr_ : 1, skip ? zr_off_ : zr_all_off_, skip ? zr_cnt_ : zr_all_cnt_, st),
      "gather_batch");
+  // Adam riding in the dW launches (no reducer, full batch): when layer l's dW is launched every layer
+  // above l has finished its backward (dW and dX), so Adam over those layers' range [woff[l+1], hi)
+  // runs in extra workgroups of that dW launch (dct_gemm_bf16_dw_partials_adam) instead of all of it
+  // in one HBM-bound launch at the end; only [0, woff[1]) is left for the final launch.  Same
+  // arithmetic and slice-sum order as the one launch: bit-identical parameters.
+  const bool ride = adam_ride_ && !reducer_ && rows == B_;
+  int64_t adam_hi = P_;  // [adam_hi, P) already updated by a riding range
+  auto adam_range = [&](int64_t lo, int64_t hi) {
+    AdamRange r{};
+    r.p = p_; r.g = g_; r.m = m_; r.v = v_; r.p_bf16 = pb_; r.n = P_;
+    r.lr = lr_; r.b1 = b1_; r.b2 = b2_; r.eps = eps_; r.wd = wd_; r.grad_scale = 1.0f; r.decoupled = decoupled_;
+    r.step_counter = sc;
+    for (int q = 0; q < nparts_; ++q) {
+      if (!part_used[q]) continue;
+      const int lq = part_layer_[q];
+      r.part_off[r.nparts] = woff_[lq]; r.part_n[r.nparts] = (int64_t)dims_[lq] * dims_[lq + 1];
+      r.part[r.nparts] = part_[q]; r.part_splits[r.nparts] = part_splits_[q];
+      ++r.nparts;
+    }
+    r.lo = lo; r.hi = hi;
+    return r;
+  };
   const int C = dims_[L_];
   int ci = 0;  // dz_[ci] holds dL/d(output of the current layer)
   int top = L_ - 1;  // highest layer the backward loop below still has to run
@@ -214,9 +236,13 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
     // for it leaves its split-K slices in part_[r] for the Adam kernel to sum (no reduce pass, no
     // gradient write + re-read); the weight range of g stays zero and is not read.
     const int r = part_slot(l);
-    if (r >= 0 && dct_gemm_bf16_dw_partials(dz_[ci], acts_[l], part_[r], g_ + boff_[l], dout, din, rows,
-                                            part_splits_[r], st) == 0) {
+    const bool ride_here = ride && r >= 0 && adam_hi > woff_[l + 1];
+    AdamRange rr{};
+    if (ride_here) rr = adam_range(woff_[l + 1], adam_hi);
+    if (r >= 0 && dct_gemm_bf16_dw_partials_adam(dz_[ci], acts_[l], part_[r], g_ + boff_[l], dout, din, rows,
+                                                 part_splits_[r], ride_here ? &rr : nullptr, st) == 0) {
       part_used[r] = true;
+      if (ride_here) adam_hi = woff_[l + 1];
     } else {
       if (r >= 0) {
         // the slice plan was made for a full batch; a shorter one (the epoch's partial last batch)
@@ -244,6 +270,11 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
     }
   }
   if (reducer_) reducer_->finalize(stream);
+  if (adam_hi < P_) {  // the rest of Adam ([0, woff[1]) of a ridden step) + the step epilogue
+    const AdamRange rr = adam_range(0, adam_hi);
+    ck(dct_adam_range(&rr, cur, g_ + P_, reinterpret_cast<float*>(loss_out), loss_cap, st), "adam");
+    return;
+  }
   int np = 0;
   int64_t poff[3], pn[3];
   const float* pp[3];
@@ -275,8 +306,9 @@ void MlpStepExecutor::plan_partials() {
   // up to three layers whose dW the launcher would split 2..8 ways: their slices go straight to
   // Adam (no reduce pass for 2-4 slices, no fp32 atomics into g for 5-8 - the tabular input
   // layer's 1024 x 256 x 4096 dW, 8 slices on 128 workgroups).  Only without a DDP reducer (it
-  // must all-reduce g).
-  if (reducer_) return;
+  // must all-reduce g), and not with DCT_DW_INTO_ADAM=0 (every dW then accumulates into g, which
+  // must be zeroed whole each step).
+  if (reducer_ || !dw_into_adam_knob_) return;
   for (int l = L_ - 1; l >= 0 && nparts_ < 3; --l) {
     if (skinny(l)) continue;
     const int M = dims_[l + 1], N = dims_[l];

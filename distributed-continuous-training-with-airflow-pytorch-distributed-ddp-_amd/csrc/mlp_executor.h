@@ -21,6 +21,8 @@ class MlpStepExecutor {
                   const std::vector<uintptr_t>& pre, uintptr_t dz0, uintptr_t dz1, uintptr_t ybuf, uintptr_t stats,
                   BucketReducer* reducer);
   void set_adam(float lr, float b1, float b2, float eps, float wd, int decoupled);
+  void set_adam_ride(bool on) { adam_ride_ = on; }
+  bool adam_ride() const { return adam_ride_; }
   // One optimizer step on batch *cursor of idx (rows <= batch); advances *cursor and *step_counter.
   void step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t idx, int n_items, uintptr_t cursor,
             uintptr_t step_counter, uintptr_t loss_out, int loss_cap, int rows, uintptr_t stream);
@@ -37,6 +39,7 @@ class MlpStepExecutor {
 
  private:
   bool fused_head_knob_ = true, dw_into_adam_knob_ = true;  // DCT_FUSED_HEAD / DCT_DW_INTO_ADAM at construction
+  bool adam_ride_ = true;  // Adam ranges riding in the dW launches (set_adam_ride)
   int nzr_ = 0;                                   // gradient ranges a full-batch step zeroes (plan_partials)
   int64_t zr_off_[4] = {}, zr_cnt_[4] = {};
   int64_t zr_all_off_[1] = {0}, zr_all_cnt_[1] = {0};  // the whole buffer (set in the constructor)

@@ -156,6 +156,12 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
   for (auto& e : ready_events_) hip_check(hipEventCreateWithFlags(&e, ev_flags), "hipEventCreate");
   hip_check(hipEventCreateWithFlags(&done_event_, ev_flags), "hipEventCreate");
   dsize_ = (dtype == DT_BF16 || dtype == DT_F16) ? 2 : 4;
+  // eager edges' device counters: [nb + 2] signals (buckets, done, timing tail), [nb + 2] consumed, status
+  if ((!inline_ || inline_knob_ != 1) && k.reducer_flag_edges) {
+    const size_t bytes = (2 * (nb + 2) + 1) * sizeof(int);
+    hip_check(hipMalloc(&dsync_, bytes), "hipMalloc edge counters");
+    hip_check(hipMemset(dsync_, 0, bytes), "hipMemset edge counters");
+  }
 }
 
 BucketReducer::~BucketReducer() {
@@ -163,6 +169,7 @@ BucketReducer::~BucketReducer() {
   if (done_event_) hipEventDestroy(done_event_);
   if (tail_event_) hipEventDestroy(tail_event_);
   if (stamps_) hipFree(stamps_);
+  if (dsync_) hipFree(dsync_);
   if (comm_stream_) hipStreamDestroy(comm_stream_);
 }
 
@@ -217,14 +224,38 @@ bool BucketReducer::step_inline(void* compute_stream) {
   return st == hipStreamCaptureStatusActive;
 }
 
+// One cross-stream edge (from -> to) of a step: eagerly a device counter (dct_flag_signal /
+// dct_flag_wait, csrc/step_kernels.hip - a one-wave kernel per side instead of an event record and
+// wait, which held the queues 6-13 us each); under stream capture an event (the graph's edge).
+void BucketReducer::edge(int slot, hipEvent_t ev, hipStream_t from, hipStream_t to) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(from, &cap) != hipSuccess) {
+    (void)hipGetLastError();
+    cap = hipStreamCaptureStatusNone;
+  }
+  if (cap == hipStreamCaptureStatusNone && dsync_) {
+    const int ns = (int)offsets_.size() + 2;
+    hip_check((hipError_t)dct_flag_signal(dsync_ + slot, from), "edge signal");
+    hip_check((hipError_t)dct_flag_wait(dsync_ + slot, dsync_ + ns + slot, dsync_ + 2 * ns, to), "edge wait");
+    return;
+  }
+  hip_check(hipEventRecord(ev, from), "hipEventRecord");
+  hip_check(hipStreamWaitEvent(to, ev, 0), "hipStreamWaitEvent");
+}
+
+int BucketReducer::edge_timeouts() const {
+  if (!dsync_) return 0;
+  int v = 0;
+  hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  hip_check(hipMemcpy(&v, dsync_ + 2 * ((int)offsets_.size() + 2), sizeof(int), hipMemcpyDeviceToHost), "edge status");
+  return v;
+}
+
 void BucketReducer::launch_bucket(int b, uintptr_t compute_stream) {
   hipStream_t cs = reinterpret_cast<hipStream_t>(compute_stream);
   inline_ = step_inline(cs);
   hipStream_t rs = inline_ ? cs : comm_stream_;
-  if (!inline_) {
-    hip_check(hipEventRecord(ready_events_[b], cs), "hipEventRecord");
-    hip_check(hipStreamWaitEvent(comm_stream_, ready_events_[b], 0), "hipStreamWaitEvent");
-  }
+  if (!inline_) edge(b, ready_events_[b], cs, comm_stream_);
   if (timing_ && b == 0)
     hip_check((hipError_t)dct_reducer_stamp(stamps_, reinterpret_cast<void*>(rs)), "reducer stamp");
   if (comm_) {
@@ -265,10 +296,7 @@ void BucketReducer::finalize(uintptr_t compute_stream) {
   n_before_finalize_ = n_launched_;
   if (timing_) {  // end of backward on the compute stream, ordered before the comm stream's close
     hip_check((hipError_t)dct_reducer_stamp(stamps_ + 1, reinterpret_cast<void*>(cs)), "reducer stamp");
-    if (!inline_) {
-      hip_check(hipEventRecord(tail_event_, cs), "hipEventRecord");
-      hip_check(hipStreamWaitEvent(comm_stream_, tail_event_, 0), "hipStreamWaitEvent");
-    }
+    if (!inline_) edge((int)offsets_.size() + 1, tail_event_, cs, comm_stream_);
   }
   // buckets whose params did not all receive a gradient (unused params): reduce anyway so
   // the collective sequence matches across ranks (find_unused_parameters=False semantics
@@ -278,10 +306,7 @@ void BucketReducer::finalize(uintptr_t compute_stream) {
     next_to_launch_++;
   }
   if (timing_) hip_check((hipError_t)dct_reducer_close(stamps_, reinterpret_cast<void*>(rs)), "reducer close");
-  if (!inline_) {
-    hip_check(hipEventRecord(done_event_, comm_stream_), "hipEventRecord");
-    hip_check(hipStreamWaitEvent(cs, done_event_, 0), "hipStreamWaitEvent");
-  }
+  if (!inline_) edge((int)offsets_.size(), done_event_, comm_stream_, cs);
   if (timing_ && check_) hip_check((hipError_t)dct_reducer_check(stamps_, reinterpret_cast<void*>(cs)), "reducer check");
 }
 

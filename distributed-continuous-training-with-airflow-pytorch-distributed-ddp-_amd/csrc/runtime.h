@@ -53,9 +53,12 @@ class BucketReducer {
   // {span_ms, exposed_ms, steps, ordering_violations} accumulated since the last reset
   std::vector<double> read_timing() const;
   void reset_timing();
+  // 1 if an eager cross-stream edge's wait expired (its consumer went on without the producer)
+  int edge_timeouts() const;
 
  private:
   void launch_bucket(int b, uintptr_t compute_stream);
+  void edge(int slot, hipEvent_t ev, hipStream_t from, hipStream_t to);
   Comm* comm_;
   uintptr_t flat_;
   std::vector<int64_t> offsets_, counts_;
@@ -67,6 +70,7 @@ class BucketReducer {
   std::vector<hipEvent_t> ready_events_;
   hipEvent_t done_event_ = nullptr;
   hipEvent_t tail_event_ = nullptr;
+  int* dsync_ = nullptr;  // eager edges' device counters (edge())
   unsigned long long* stamps_ = nullptr;  // [8], see step_kernels.hip reducer_close_kernel
   bool timing_ = false, check_ = false;
   int inline_knob_ = -1;  // DCT_REDUCER_INLINE resolved (1 / 0 / -1 = inline while the compute stream is capturing)

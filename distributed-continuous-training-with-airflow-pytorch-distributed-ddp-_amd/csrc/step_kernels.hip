@@ -172,6 +172,30 @@ __global__ void reducer_check_kernel(unsigned long long* s) {
   }
 }
 
+// Cross-stream edges of the bucket reducer's eager steps (runtime.cpp BucketReducer::edge): the
+// producer stream bumps a device counter, the consumer stream runs a one-wave kernel that waits
+// for it.  hipEventRecord + hipStreamWaitEvent cost 6-13 us of queue time per edge on MI355X
+// (a marker packet that held the compute queue ~6.5 us per bucket fork, ~12 us at the join: kernel
+// trace of the forced-DDP tabular step); a one-wave kernel on each side costs about a dispatch.
+// The wait is bounded (2 s): on expiry it sets *status and lets the stream go on (wrong results
+// are then reported by BucketReducer::edge_timeouts, never a hung queue).
+__global__ __launch_bounds__(64) void flag_signal_kernel(int* flag) {
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ __launch_bounds__(64) void flag_wait_kernel(int* flag, int* consumed, int* status) {
+  if (threadIdx.x != 0) return;
+  const int c = __hip_atomic_load(consumed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) <= c) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
+      __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __hip_atomic_store(consumed, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Stand-in collective (test-only, DCT_REDUCER_STANDIN_US, runtime.cpp BucketReducer): each one-wave
 // workgroup stays resident for `ticks` of s_memrealtime (100 MHz) from its own start, sleeping
 // between polls - the CU / queue footprint of an all-reduce of that duration without its traffic,
@@ -200,6 +224,16 @@ extern "C" {
 
 int dct_phase_accum(unsigned long long* b, int n, void* stream) {
   hipLaunchKernelGGL(dct::phase_accum_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), b, n);
+  return (int)hipGetLastError();
+}
+
+int dct_flag_signal(int* flag, void* stream) {
+  hipLaunchKernelGGL(dct::flag_signal_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), flag);
+  return (int)hipGetLastError();
+}
+int dct_flag_wait(int* flag, int* consumed, int* status, void* stream) {
+  hipLaunchKernelGGL(dct::flag_wait_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), flag, consumed,
+                     status);
   return (int)hipGetLastError();
 }
 

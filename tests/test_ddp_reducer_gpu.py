@@ -59,6 +59,7 @@ def test_tabular_forced_reducer_matches_no_reducer(cuda, monkeypatch):
     red = eng.reducer
     assert red is not None and red.num_buckets >= 2
     assert not red._r.inline_mode  # a real (one-rank) RCCL collective: auto placement = comm stream
+    assert red._r.edge_timeouts() == 0  # every eager fork / join edge saw its producer
     # (a) same trajectory: the reducer path reduces the split-K dW slices into g before the bucket
     # launch, the no-reducer path sums the same slices in the same order inside Adam
     assert torch.isfinite(l1).all()
@@ -171,6 +172,7 @@ def _tabular_step_us(monkeypatch, standin_us, inline, steps=64, B=4096):
     torch.cuda.synchronize()
     span, exposed, k, bad = eng.reducer.allreduce_ms()
     assert k == steps and bad == 0
+    assert eng.reducer._r.edge_timeouts() == 0  # no eager cross-stream edge expired
     return e0.elapsed_time(e1) * 1e3 / steps, span * 1e3 / k, exposed * 1e3 / k, eng.reducer._r.inline_mode
 
 

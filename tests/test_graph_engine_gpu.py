@@ -146,3 +146,29 @@ def test_dw_slices_into_adam_match_reduce_path(B, extra, cuda, monkeypatch):
     assert torch.isfinite(l1).all()
     assert torch.allclose(l1, l0, atol=1e-3), (l1 - l0).abs().max()
     assert (p1 - p0).norm() / p0.norm() < 1e-2
+
+
+@pytest.mark.parametrize("extra", [0, 300])
+def test_adam_riding_in_dw_launches_matches_one_adam_launch(extra, cuda):
+    """Without a DDP reducer the executor runs each layer's Adam in extra workgroups of the next
+    lower layer's dW launch (csrc/gemm_bf16.hip gemm2_dw_adam_kernel) and only the input layer's in
+    the final launch: the same trajectory as one Adam launch at the end of the step (the bias
+    gradients' float atomics make runs agree to rounding, not bit for bit).  ``extra``: partial last
+    batches take the one-launch path."""
+    dims, B = [256, 1024, 1024, 1024, 2], 4096
+    X, Y = _data(6 * B + extra, dims[0], seed=7)
+    rows = torch.arange(X.shape[0])
+    res = {}
+    for ride in (True, False):
+        model, eng = _engine(dims, B, loss="mse", lr=1e-3, use_graph=False)
+        eng.exe.adam_ride = ride
+        eng.attach_data(X, Y, rows, rows[:B])
+        losses = torch.cat([eng.train_epoch(ep).cpu() for ep in range(2)])
+        torch.cuda.synchronize()
+        assert eng.exe.adam_ride == ride and eng.exe.partial_layers == 3
+        res[ride] = (losses, eng.p.cpu(), eng.m.cpu(), eng.v.cpu(), int(eng.step_counter.item()))
+    (l1, p1, m1, v1, s1), (l0, p0, m0, v0, s0) = res[True], res[False]
+    assert s1 == s0
+    assert torch.isfinite(l1).all() and torch.allclose(l1, l0, atol=1e-4), (l1 - l0).abs().max()
+    assert (p1 - p0).norm() / p0.norm() < 1e-3
+    assert (m1 - m0).norm() / m0.norm() < 1e-2 and (v1 - v0).norm() / v0.norm() < 1e-2
