@@ -129,14 +129,21 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
   }
   pending_.assign(nb, 0);
   launched_.assign(nb, 0);
+  // (normal priority: a greatest-priority comm stream made the forced-DDP tabular step with the stand-in
+  // collective 0.187 -> 0.705 ms and the TabTransformer one 0.42 -> 1.16 ms, profiles/ddp_reducer_standin_ab_r5.log)
   hip_check(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking), "hipStreamCreate");
   // Where the collectives run (DCT_REDUCER_INLINE, read once here into this reducer's copy):
-  //   -2 (auto, default): on the compute stream only for a one-rank communicator (the identity: no
-  //      collective runs, and the fork / join events would cost 20-30 us per step for nothing,
-  //      profiles/ddp_reducer_inline_default_ab_r4.log), otherwise on the comm stream, so each
-  //      bucket's all-reduce overlaps the rest of backward (the DDP Reducer's point, reference
-  //      jobs/train_lightning_ddp.py:136);
-  //    1 / 0: always the compute / the comm stream; -1: inline while the step is being captured.
+  //   -2 (auto, default): on the compute stream for a one-rank communicator (the identity: no
+  //      collective runs, and fork / join edges would cost time for nothing); otherwise on the comm
+  //      stream in eager steps, so each bucket's all-reduce overlaps the rest of backward (the DDP
+  //      Reducer's point, reference jobs/train_lightning_ddp.py:136): forced-DDP tabular step with a
+  //      60 us stand-in collective 0.187 ms vs 0.235 inline (profiles/ddp_reducer_standin_ab_r5.log) -
+  //      and on the compute stream while a step is captured: the TabTransformer's replayed step lost
+  //      with the collectives beside it (0.435-0.437 vs 0.425-0.428 ms inline) - its backward kernels
+  //      fill every CU's VGPRs and LDS at exactly one workgroup round, so any co-resident comm wave
+  //      pushes a workgroup into a second round;
+  //    1 / 0: always the compute / the comm stream (0 with a captured step: the graph's event edges);
+  //   -1: inline while the compute stream is capturing.
   // The test-only stand-in collective (DCT_REDUCER_STANDIN_US) counts as a real collective.
   const Knobs& k = dct::knobs();
   standin_us_ = k.reducer_standin_us;
@@ -144,7 +151,7 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
   inline_knob_ = k.reducer_inline;
   if (inline_knob_ == -2) {
     const bool identity = comm_ == nullptr || (comm_->world() == 1 && comm_->is_identity());
-    inline_knob_ = (identity && standin_us_ == 0) ? 1 : 0;
+    inline_knob_ = (identity && standin_us_ == 0) ? 1 : -1;
   }
   inline_ = inline_knob_ == 1;
   for (int64_t c : counts_) total_count_ += c;
@@ -227,6 +234,11 @@ bool BucketReducer::step_inline(void* compute_stream) {
 // One cross-stream edge (from -> to) of a step: eagerly a device counter (dct_flag_signal /
 // dct_flag_wait, csrc/step_kernels.hip - a one-wave kernel per side instead of an event record and
 // wait, which held the queues 6-13 us each); under stream capture an event (the graph's edge).
+// The signal is always enqueued before its wait, so two streams that share one hardware queue
+// (more streams than GPU_MAX_HW_QUEUES) serialise but never deadlock.  (A captured step whose
+// graph only signalled the buckets, with the collectives enqueued eagerly on the comm stream before
+// each replay, did deadlock there until the wait bound: the replay's join sat ahead of its own
+// collectives in the shared queue - removed again, profiles/ddp_reducer_standin_ab_r5.log.)
 void BucketReducer::edge(int slot, hipEvent_t ev, hipStream_t from, hipStream_t to) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(from, &cap) != hipSuccess) {
@@ -258,6 +270,12 @@ void BucketReducer::launch_bucket(int b, uintptr_t compute_stream) {
   if (!inline_) edge(b, ready_events_[b], cs, comm_stream_);
   if (timing_ && b == 0)
     hip_check((hipError_t)dct_reducer_stamp(stamps_, reinterpret_cast<void*>(rs)), "reducer stamp");
+  collective(b, rs);
+  launched_[b] = 1;
+  n_launched_++;
+}
+
+void BucketReducer::collective(int b, hipStream_t rs) {
   if (comm_) {
     comm_->allreduce(flat_ + (uintptr_t)(offsets_[b] * dsize_), counts_[b], dtype_, op_,
                      reinterpret_cast<uintptr_t>(rs));
@@ -268,8 +286,6 @@ void BucketReducer::launch_bucket(int b, uintptr_t compute_stream) {
     hip_check((hipError_t)dct_busy_spin((long long)(us * 100.0), standin_wgs_, reinterpret_cast<void*>(rs)),
               "stand-in collective");
   }
-  launched_[b] = 1;
-  n_launched_++;
 }
 
 // Buckets are launched strictly in index order (bucket 0 = last layers, filled first by

@@ -25,6 +25,7 @@ class Comm {
   int rank() const { return rank_; }
   int world() const { return world_; }
   bool is_identity() const { return identity_; }
+  int device() const { return device_; }
 
  private:
   void* comm_ = nullptr;
@@ -59,6 +60,7 @@ class BucketReducer {
  private:
   void launch_bucket(int b, uintptr_t compute_stream);
   void edge(int slot, hipEvent_t ev, hipStream_t from, hipStream_t to);
+  void collective(int b, hipStream_t rs);
   Comm* comm_;
   uintptr_t flat_;
   std::vector<int64_t> offsets_, counts_;

@@ -14,6 +14,11 @@ the auto placement puts it on the reducer's comm stream, as at W > 1:
     on the collective's stream, the footprint of a multi-rank all-reduce): on the comm stream the
     exposed all-reduce time is a fraction of its span, on the compute stream it is all of it.
 """
+import json
+import os
+import subprocess
+import sys
+
 import pytest
 import torch
 
@@ -132,6 +137,22 @@ def test_tabtransformer_forced_reducer_matches_no_reducer(cuda, monkeypatch, def
     assert steps >= 1 and span > 0 and bad == 0, (span, exposed, steps, bad)
 
 
+def test_tabtransformer_comm_stream_in_graph_matches_no_reducer(cuda, monkeypatch):
+    """DCT_REDUCER_INLINE=0 with the graph-replayed TabTransformer step: the captured collectives sit
+    on a graph branch behind event edges (the auto placement runs them inline while capturing) -
+    the same trajectory as without a reducer, and the eager warm-up steps' device-counter edges all
+    saw their producers."""
+    monkeypatch.setenv("DCT_REDUCER_INLINE", "0")
+    ref, l0, p0 = _tt(False, monkeypatch)
+    eng, l1, p1 = _tt(True, monkeypatch)
+    red = eng.reducer
+    assert eng.graph_used and not red._r.inline_mode
+    assert red._r.edge_timeouts() == 0
+    assert torch.isfinite(l1).all() and torch.allclose(l0, l1, rtol=2e-3, atol=2e-4), (l0, l1)
+    span, exposed, steps, bad = red.allreduce_ms()
+    assert steps >= 1 and span > 0 and bad == 0, (span, exposed, steps, bad)
+
+
 def test_phase_timer_reports_step_phases(cuda, monkeypatch):
     """DCT_PHASE_TIMING=1: device timestamps of forward / backward / all-reduce / optimizer, also
     inside the captured step graphs."""
@@ -144,15 +165,15 @@ def test_phase_timer_reports_step_phases(cuda, monkeypatch):
     assert ph["bwd"] > ph["allreduce"]
 
 
-def _tabular_step_us(monkeypatch, standin_us, inline, steps=64, B=4096):
+def _tabular_step_us(standin_us, inline, out_path, steps=64, B=4096):
     """Forced-DDP tabular 4x1024 step time (us, CUDA events over `steps` eager steps) with a
-    stand-in collective of `standin_us` per step; inline: "1" compute stream, "-2" auto."""
-    monkeypatch.setenv("DCT_REDUCER_STANDIN_US", str(standin_us))
-    monkeypatch.setenv("DCT_REDUCER_INLINE", inline)
-    monkeypatch.setenv("DCT_REDUCER_TIMING", "1")
-    monkeypatch.delenv("DCT_RCCL_ONE_RANK", raising=False)
-    monkeypatch.setenv("DCT_DEBUG", "0")
-    monkeypatch.setenv("DCT_FORCE_DDP", "1")
+    stand-in collective of `standin_us` per step; inline: "1" compute stream, "-2" auto.  Run in a
+    fresh process (_spawn): a process's streams share GPU_MAX_HW_QUEUES (4) hardware queues round-
+    robin, and once earlier tests' engines hold enough streams the comm stream lands on the compute
+    stream's queue, where its collectives serialise with backward again."""
+    os.environ.update({"DCT_REDUCER_STANDIN_US": str(standin_us), "DCT_REDUCER_INLINE": inline,
+                       "DCT_REDUCER_TIMING": "1", "DCT_DEBUG": "0", "DCT_FORCE_DDP": "1"})
+    os.environ.pop("DCT_RCCL_ONE_RANK", None)
     dims = [256, 1024, 1024, 1024, 2]
     torch.manual_seed(0)
     model = MLPClassifier(dims[0], hidden=tuple(dims[1:-1]), num_classes=2, dropout=0.0, loss="mse", lr=1e-3)
@@ -171,23 +192,37 @@ def _tabular_step_us(monkeypatch, standin_us, inline, steps=64, B=4096):
     e1.record()
     torch.cuda.synchronize()
     span, exposed, k, bad = eng.reducer.allreduce_ms()
-    assert k == steps and bad == 0
-    assert eng.reducer._r.edge_timeouts() == 0  # no eager cross-stream edge expired
-    return e0.elapsed_time(e1) * 1e3 / steps, span * 1e3 / k, exposed * 1e3 / k, eng.reducer._r.inline_mode
+    res = {"step_us": e0.elapsed_time(e1) * 1e3 / steps, "span_us": span * 1e3 / max(k, 1),
+           "exposed_us": exposed * 1e3 / max(k, 1), "inline": bool(eng.reducer._r.inline_mode), "steps": k,
+           "bad": bad, "timeouts": eng.reducer._r.edge_timeouts()}
+    json.dump(res, open(out_path, "w"))
 
 
-def test_tabular_standin_collective_overlaps_backward(cuda, monkeypatch):
+def _spawn(fn, *args, timeout=300):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (f"import sys; sys.path.insert(0, {root!r}); sys.path.insert(0, {os.path.join(root, 'tests')!r}); "
+            f"import test_ddp_reducer_gpu as t; t.{fn}(*{args!r})")
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout)
+
+
+def test_tabular_standin_collective_overlaps_backward(cuda, tmp_path):
     """(d) A 60 us stand-in all-reduce per step (split over the buckets by size, 16 one-wave busy
     workgroups; about an 8-rank all-reduce of the 13.6 MB of fp32 gradients over xGMI).  With the
     auto placement (comm stream) most of it runs under the remaining backward: the step grows by
     well under the stand-in's 60 us and the exposed time (end of backward -> last bucket done) is a
     fraction of the span.  Forced onto the compute stream it serialises: the step grows by ~60 us."""
-    base, _, _, _ = _tabular_step_us(monkeypatch, 0, "-2")
-    comm, span_c, exp_c, inl_c = _tabular_step_us(monkeypatch, 60, "-2")
-    inl, span_i, exp_i, inl_i = _tabular_step_us(monkeypatch, 60, "1")
+    res = {}
+    for name, us, inline in (("base", 0, "-2"), ("comm", 60, "-2"), ("inline", 60, "1")):
+        out = tmp_path / f"{name}.json"
+        r = _spawn("_tabular_step_us", us, inline, str(out))
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        res[name] = json.loads(out.read_text())
+        assert res[name]["steps"] == 64 and res[name]["bad"] == 0 and res[name]["timeouts"] == 0, res[name]
+    base, comm, inl = res["base"]["step_us"], res["comm"]["step_us"], res["inline"]["step_us"]
+    span_c, exp_c = res["comm"]["span_us"], res["comm"]["exposed_us"]
     print(f"forced-DDP tabular step: no stand-in {base:.1f} us, 60 us stand-in on the comm stream {comm:.1f} us "
-          f"(span {span_c:.1f}, exposed {exp_c:.1f}), on the compute stream {inl:.1f} us (span {span_i:.1f})")
-    assert not inl_c and inl_i
+          f"(span {span_c:.1f}, exposed {exp_c:.1f}), on the compute stream {inl:.1f} us")
+    assert not res["comm"]["inline"] and res["inline"]["inline"]
     assert span_c >= 55.0, span_c  # the stand-in ran
     assert inl - base > 45.0, (inl, base)  # serialised on the compute stream
     assert exp_c < 0.5 * span_c, (span_c, exp_c)
