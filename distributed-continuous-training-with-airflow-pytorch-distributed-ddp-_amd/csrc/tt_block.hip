@@ -83,6 +83,7 @@ struct Args {
   float* out;
   uint16_t* wT;  // transposed bf16 weights for the backward: W2^T | W1^T | Wo^T | Wqkv^T
   uint64_t* prof;  // optional phase timestamps (wall clock), 16 per workgroup
+  float* pool;     // optional [B][DM]: the block output's mean over the sample's tokens (classifier head input)
   int save;        // 0: inference (no_grad) - only `out` is written, no saved tensors / W^T
   int B;
   float eps, scale;
@@ -395,14 +396,28 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
     }
     const int col = 16 * wv + c;
     const float bv = a.b2[col];
+    float cs = 0.f;  // this lane's 16 rows of the output column (pool)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) HS[(16 * i + 4 * g + r) * HS_LD + col] += acc[i][r] + bv;
+      for (int r = 0; r < 4; ++r) {
+        float* hp = HS + (16 * i + 4 * g + r) * HS_LD + col;
+        const float v = *hp + (acc[i][r] + bv);
+        *hp = v;
+        cs += v;
+      }
+    if (a.pool) {
+      // the last block hands the head its token mean (256 B per sample) instead of the 16-KB output
+      // tile, which the head read twice (its forward and its backward recompute): the column's four
+      // row groups (lanes c, c + 16, c + 32, c + 48) summed in registers
+      cs += __shfl_xor(cs, 16);
+      cs += __shfl_xor(cs, 32);
+      if (g == 0) a.pool[(size_t)bidx * DM + col] = cs * (1.f / T);
+    }
   }
   __syncthreads();
   TT_MARK(6);
-  store_tile<DM * 4, HS_LD * 4>(a.out + (size_t)row0 * DM, HS);
+  if (a.out) store_tile<DM * 4, HS_LD * 4>(a.out + (size_t)row0 * DM, HS);
   if (a.save) transpose_weights(a);
   TT_MARK(7);
 }
@@ -429,6 +444,8 @@ struct BwdArgs {
   const uint16_t* wT;
   const uint16_t* a2; const uint16_t* w1; const float* b1;  // the recompute's operands
   uint16_t* dpre; uint16_t* dh1_16; uint16_t* dqkv; float* dh; uint16_t* dh16;
+  const float* dpool;  // optional [B][DM]: the gradient of the token mean (pool) instead of dout rows;
+  uint16_t* dout16;    // then bf16(dout) [M][DM] is written here for the W2 gradient GEMM
   float *dln1_w, *dln1_b, *dln2_w, *dln2_b;
   uint64_t* prof;
   float scale;
@@ -581,10 +598,16 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
     // dout in row layout (lane -> row 16wv + (lane & 15), columns 16g..16g+15): 4 x 16-B loads
     // per lane issued with the pre tile's, then 16-B LDS writes (was 16 scalar loads + 32 stores)
     const int rl = 16 * wv + (lane & 15);
-    const float4* dp = reinterpret_cast<const float4*>(a.dout + (size_t)(row0 + rl) * DM + 16 * g);
+    // (with dpool: the head's gradient of the token mean, the same for every token, / T; x 1 is exact)
+    const float4* dp = reinterpret_cast<const float4*>(a.dpool ? a.dpool + (size_t)bidx * DM + 16 * g
+                                                                : a.dout + (size_t)(row0 + rl) * DM + 16 * g);
+    const float dsc = a.dpool ? 1.f / T : 1.f;
     float4 dv[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dv[q] = dp[q];
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = dp[q];
+      dv[q] = make_float4(v.x * dsc, v.y * dsc, v.z * dsc, v.w * dsc);
+    }
     if constexpr (RECOMP) load_tile<DM * 2, XB_LD * 2>(Os, a.a2 + (size_t)row0 * DM);  // Os is free until P4
     else load_tile<FF * 2, F_LD * 2>(R, a.pre + (size_t)row0 * FF);
     red[threadIdx.x] = 0.f;
@@ -602,6 +625,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
     *reinterpret_cast<bf16x8*>(X + rl * XB_LD + 16 * g + 8) = o[1];
   }
   __syncthreads();
+  if (a.dout16) store_tile<DM * 2, XB_LD * 2>(a.dout16 + (size_t)row0 * DM, X);
 
   TT_MARK(1);
   // ---- P1: dpre = (bf16(dout) W2) * gelu'(pre) for columns 64wv..64wv+63 (all rows), in place over
@@ -901,8 +925,9 @@ extern "C" {
 
 // ptrs (27, in order): h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2,
 //   a1, mean1, rstd1, qkv, o, lse, h1, a2, mean2, rstd2, f, pre, out, wT
-int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps, float scale,
-                     void* stream) {
+// pool (optional): the last block's token mean for the classifier head; `out` (p[25]) may then be null
+int dct_tt_block_fwd_pool(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps,
+                          float scale, float* pool, void* stream) {
   using namespace dct::ttb;
   if ((n_ptrs != 27 && n_ptrs != 28) || T != dct::ttb::T || DM != dct::ttb::DM || H != NH || FF != dct::ttb::FF || Bsz <= 0)
     return (int)hipErrorInvalidValue;
@@ -910,7 +935,7 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
   const bool save = p[13] != 0;
   uintptr_t any = 0;
   for (int i = 0; i < 27; ++i) {
-    const bool needed = (i < 13 || i == 25 || save) && i != 24;  // pre (24) optional: see BwdArgs::pre
+    const bool needed = (i < 13 || (i == 25 && !pool) || save) && i != 24 && !(i == 25 && pool);  // pre (24): BwdArgs::pre
     if (needed && !p[i]) return (int)hipErrorInvalidValue;
     any |= p[i];
   }
@@ -927,6 +952,8 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
   a.h1 = (float*)p[19]; a.a2 = (uint16_t*)p[20]; a.mean2 = (float*)p[21]; a.rstd2 = (float*)p[22];
   a.f = (uint16_t*)p[23]; a.pre = (uint16_t*)p[24]; a.out = (float*)p[25]; a.wT = (uint16_t*)p[26];
   a.prof = n_ptrs == 28 ? (uint64_t*)p[27] : nullptr;
+  a.pool = pool;
+  if (pool && (((uintptr_t)pool) & 15)) return (int)hipErrorInvalidValue;
   a.save = save ? 1 : 0;
   a.B = Bsz; a.eps = eps; a.scale = scale;
   static bool attr = false;
@@ -940,10 +967,17 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
   return (int)hipGetLastError();
 }
 
+int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps, float scale,
+                     void* stream) {
+  return dct_tt_block_fwd_pool(p, n_ptrs, Bsz, T, DM, H, FF, eps, scale, nullptr, stream);
+}
+
 // ptrs (22, in order): dout, h, mean1, rstd1, ln1_w, qkv, o, lse, h1, mean2, rstd2, ln2_w, pre, wT,
 //   dpre, dh1_16, dqkv, dh, dh16, dln1_w, dln1_b, dln2_w, dln2_b  (23 with the last four)
-int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
-                     void* stream) {
+// dpool (optional): the head's gradient of the last block's token mean instead of dout (p[0] may then be
+// null); bf16(dout) is then written to dout16 ([B*T][DM]) for the W2 gradient GEMM
+int dct_tt_block_bwd_pool(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
+                          const float* dpool, uint16_t* dout16, void* stream) {
   using namespace dct::ttb;
   // 23 (+1 prof) pointers; 26 (+1 prof): + a2, w1 (bf16 [FF][DM]), b1 - with pre (p[12]) null the
   // kernel recomputes the pre-activation from them
@@ -954,7 +988,7 @@ int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
   const bool recomp = ext && p[12] == 0;
   uintptr_t any = 0;
   for (int i = 0; i < (ext ? 26 : 23); ++i) {
-    if (!p[i] && !(i == 12 && recomp) && !(i >= 23 && !recomp)) return (int)hipErrorInvalidValue;
+    if (!p[i] && !(i == 12 && recomp) && !(i >= 23 && !recomp) && !(i == 0 && dpool)) return (int)hipErrorInvalidValue;
     if (i < 19 || i >= 23) any |= p[i];
   }
   if (any & 15) return (int)hipErrorInvalidValue;
@@ -971,6 +1005,9 @@ int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
   a.b1 = ext ? (const float*)p[25] : nullptr;
   a.prof = n_ptrs == 24 ? (uint64_t*)p[23] : (n_ptrs == 27 ? (uint64_t*)p[26] : nullptr);
   a.scale = scale;
+  if (dpool && (!dout16 || ((((uintptr_t)dpool) | ((uintptr_t)dout16)) & 15))) return (int)hipErrorInvalidValue;
+  a.dpool = dpool;
+  a.dout16 = dpool ? dout16 : nullptr;
   static bool attr = false;
   if (!attr) {
     for (const void* k : {(const void*)tt_block_bwd_kernel<false>, (const void*)tt_block_bwd_kernel<true>}) {
@@ -984,6 +1021,11 @@ int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
   else
     hipLaunchKernelGGL(tt_block_bwd_kernel<false>, dim3(Bsz), dim3(256), BWD_LDS, reinterpret_cast<hipStream_t>(stream), a);
   return (int)hipGetLastError();
+}
+
+int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
+                     void* stream) {
+  return dct_tt_block_bwd_pool(p, n_ptrs, Bsz, T, DM, H, FF, scale, nullptr, nullptr, stream);
 }
 
 }  // extern "C"

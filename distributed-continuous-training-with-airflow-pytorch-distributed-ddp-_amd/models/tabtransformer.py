@@ -22,6 +22,11 @@ from ..ops.nn import layer_norm, linear, tt_block, tt_embed, tt_head_loss
 from ..trainer.module import TrainModule
 
 
+# the last block hands the classifier head the token mean (ops/nn.py tt_block(pooled=True)); False: the
+# head pools the last block's full output itself (A/B: tools/tt_pooled_head_ab.py)
+POOLED_HEAD = True
+
+
 class _Block(nn.Module):
     def __init__(self, d: int, heads: int, ffn_mult: int):
         super().__init__()
@@ -33,10 +38,10 @@ class _Block(nn.Module):
         self.fc1 = nn.Linear(d, ffn_mult * d)
         self.fc2 = nn.Linear(ffn_mult * d, d)
 
-    def forward(self, h: torch.Tensor, B: int, T: int) -> torch.Tensor:
+    def forward(self, h: torch.Tensor, B: int, T: int, pooled: bool = False) -> torch.Tensor:
         return tt_block(h, self.ln1_w, self.ln1_b, self.qkv.weight, self.qkv.bias, self.proj.weight, self.proj.bias,
                         self.ln2_w, self.ln2_b, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias,
-                        B, self.heads, T)
+                        B, self.heads, T, pooled=pooled)
 
 
 class TabTransformer(TrainModule):
@@ -57,11 +62,13 @@ class TabTransformer(TrainModule):
         self.ln_w, self.ln_b = nn.Parameter(torch.ones(d_model)), nn.Parameter(torch.zeros(d_model))
         self.head = nn.Linear(d_model, num_classes)
 
-    def _trunk(self, x: torch.Tensor) -> torch.Tensor:
+    def _trunk(self, x: torch.Tensor, pooled: bool = False) -> torch.Tensor:
+        """Token embedding + the blocks: [B*F, d], or with ``pooled`` the last block's output averaged
+        over each sample's F tokens, [B, d] (on MI355X the last block kernel writes only that)."""
         B = x.shape[0]
         h = tt_embed(x, self.feat_w, self.feat_b)
-        for blk in self.blocks:
-            h = blk(h, B, self.F)
+        for i, blk in enumerate(self.blocks):
+            h = blk(h, B, self.F, pooled=pooled and i == len(self.blocks) - 1)
         return h
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -73,8 +80,13 @@ class TabTransformer(TrainModule):
     def training_step(self, batch, batch_idx):
         x, y = batch
         # pooled LN -> Linear -> mean CE as one kernel each way on MI355X (ops/nn.py tt_head_loss)
-        loss = tt_head_loss(self._trunk(x), y, x.shape[0], self.F, self.ln_w, self.ln_b, self.head.weight,
-                            self.head.bias)
+        # (the head consumes the pooled tokens: the last block hands over [B, d], not [B*F, d])
+        if POOLED_HEAD:
+            loss = tt_head_loss(self._trunk(x, pooled=True), y, x.shape[0], 1, self.ln_w, self.ln_b, self.head.weight,
+                                self.head.bias)
+        else:
+            loss = tt_head_loss(self._trunk(x), y, x.shape[0], self.F, self.ln_w, self.ln_b, self.head.weight,
+                                self.head.bias)
         self.log("train_loss", loss, sync_dist=True)
         return loss
 

@@ -539,7 +539,7 @@ class _TTBlockFn(torch.autograd.Function):
     the two unfused nodes save, so the backward is theirs, FFN first."""
 
     @staticmethod
-    def forward(ctx, h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, eps, B, H, T):
+    def forward(ctx, h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, eps, B, H, T, pooled=False):
         nat = native()
         st = _stream()
         h = h.contiguous().float()
@@ -553,7 +553,10 @@ class _TTBlockFn(torch.autograd.Function):
         qkv = torch.empty(M, 3 * dm, dtype=bf, device=dev)
         o = torch.empty(M, dm, dtype=bf, device=dev)
         lse = torch.empty(B * H * T, dtype=f32, device=dev)
-        h1, out = torch.empty(M, dm, dtype=f32, device=dev), torch.empty(M, dm, dtype=f32, device=dev)
+        # pooled (the model's last block, training): the kernel writes the token mean [B, dm] the classifier
+        # head reads instead of the [B*T, dm] output - which the head read twice (forward and backward)
+        h1 = torch.empty(M, dm, dtype=f32, device=dev)
+        out = torch.empty(B if pooled else M, dm, dtype=f32, device=dev)
         f = torch.empty(M, FF, dtype=bf, device=dev)
         # with the fused backward the FFN pre-activation is not stored (32 KB per sample written and read
         # back): tt_block_bwd_kernel recomputes it from a2 and W1 (0.3697 -> 0.3632 ms per step,
@@ -567,11 +570,15 @@ class _TTBlockFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(dm // H)
         if _TT_PROF is not None:  # tools/debug/tt_phase_prof.py
             ptrs.append(_tt_prof_buf("fwd", B, dev))
-        nat.tt_block_fwd([0 if t is pre and recomp else t.data_ptr() for t in ptrs], B, T, dm, H, FF, float(eps),
-                         scale, st)
+        addrs = [0 if (t is pre and recomp) or (t is out and pooled) else t.data_ptr() for t in ptrs]
+        if pooled:
+            nat.tt_block_fwd_pool(addrs, B, T, dm, H, FF, float(eps), scale, out.data_ptr(), st)
+        else:
+            nat.tt_block_fwd(addrs, B, T, dm, H, FF, float(eps), scale, st)
         ctx.save_for_backward(h, st4, a1, wqkvb, qkv, o, lse, wob, h1, a2, w1b, w2b, f, pre, wT, vecs[0], vecs[4])
         ctx.params = (ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2)
         ctx.dims = (B, H, T, dm // H, scale)
+        ctx.pooled = pooled
         return out
 
     @staticmethod
@@ -579,14 +586,14 @@ class _TTBlockFn(torch.autograd.Function):
         h, st4, a1, wqkvb, qkv, o, lse, wob, h1, a2, w1b, w2b, f, pre, wT, ln1w, ln2w = ctx.saved_tensors
         p = ctx.params
         B, H, T, D, scale = ctx.dims
-        if _TT_FUSED_BWD or pre.numel() == 0:  # no stored pre-activation: only the fused backward recomputes it
+        if _TT_FUSED_BWD or pre.numel() == 0 or ctx.pooled:  # no stored pre-activation: the fused backward
             return (*_tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, p, B, H, T,
-                                         scale, w1b), None, None, None, None)
+                                         scale, w1b, pooled=ctx.pooled), None, None, None, None, None)
         dh1, dl2w, dl2b, dw1, db1, dw2, db2 = _prenorm_ffn_bwd(dout, (h1, st4[2], st4[3], a2, w1b, w2b, f, pre),
                                                                p[6:])
         dh, dl1w, dl1b, dwqkv, dbqkv, dwo, dbo = _prenorm_attn_bwd(
             dh1, (h, st4[0], st4[1], a1, wqkvb, qkv, o, lse, wob), p[:6], ctx.dims)
-        return (dh, dl1w, dl1b, dwqkv, dbqkv, dwo, dbo, dl2w, dl2b, dw1, db1, dw2, db2, None, None, None, None)
+        return (dh, dl1w, dl1b, dwqkv, dbqkv, dwo, dbo, dl2w, dl2b, dw1, db1, dw2, db2, None, None, None, None, None)
 
 
 _TT_FUSED_BWD = True
@@ -600,7 +607,7 @@ def _tt_prof_buf(kind: str, B: int, dev) -> torch.Tensor:
 
 
 def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, params, B, H, T, scale,
-                        w1b=None):
+                        w1b=None, pooled=False):
     """Backward of the fused block: ONE kernel for the whole dX chain (csrc/tt_block.hip
     tt_block_bwd_kernel: dF/gelu', W1, LN2, Wo, attention, Wqkv, LN1 per sample) writing the dZ
     operands of the four dW GEMMs, which then run split-K over all rows with the bias gradients
@@ -622,14 +629,21 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
     ptrs = [dout, h, st4[0], st4[1], ln1w, qkv, o, lse, h1, st4[2], st4[3], ln2w, pre, wT,
             dpre, dh1_16, dqkv, dh, dh16] + [g for g, _ in lg]
     addrs = [t.data_ptr() for t in ptrs]
+    dout16 = None
+    if pooled:  # dout is the head's gradient of the token mean [B, dm]: the kernel broadcasts it (/ T)
+        addrs[0] = 0
+        dout16 = torch.empty(M, dm, dtype=bf, device=dev)  # bf16(dout), written by the kernel
     if recomp:  # pre-activation recomputed from a2 / W1 / b1 inside the kernel
         addrs[12] = 0
         b1c = b1.detach().contiguous()
         addrs += [a2.data_ptr(), w1b.data_ptr(), b1c.data_ptr()]
     if _TT_PROF is not None:
         addrs.append(_tt_prof_buf("bwd", B, dev).data_ptr())
-    nat.tt_block_bwd(addrs, B, T, dm, H, FF, scale, st)
-    dout16 = _bf16_of(dout)
+    if pooled:
+        nat.tt_block_bwd_pool(addrs, B, T, dm, H, FF, scale, dout.data_ptr(), dout16.data_ptr(), st)
+    else:
+        nat.tt_block_bwd(addrs, B, T, dm, H, FF, scale, st)
+        dout16 = _bf16_of(dout)
     items = [(dout16, f, w2, b2), (dpre, a2, w1, b1), (dh1_16, o, wo, bo), (dqkv, a1, wqkv, bqkv)]
     b = _BOUND
     direct = b is not None and all(_is_direct(t) for t in (w2, b2, w1, b1, wo, bo, wqkv, bqkv))
@@ -685,16 +699,21 @@ def tt_block_fusable(h: torch.Tensor, H: int, T: int, ffn: int) -> bool:
 
 
 def tt_block(h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, B: int, H: int, T: int,
-             eps: float = 1e-5):
+             eps: float = 1e-5, pooled: bool = False):
     """One pre-norm transformer block: h + MHA(LN1 h), then + FFN(LN2 .) - one fused kernel
-    forward on MI355X for the benchmark shape, two fused nodes otherwise."""
+    forward on MI355X for the benchmark shape, two fused nodes otherwise.  ``pooled``: return the
+    block output's mean over each sample's T tokens, [B, d] (the classifier head's input)."""
     vecs = (ln1_w, ln1_b, bqkv, bo, ln2_w, ln2_b, b1, b2)  # read with 16-byte vector loads
     if tt_block_fusable(h, H, T, w1.shape[0]) and all(v.is_contiguous() and v.data_ptr() % 16 == 0 for v in vecs):
         if not torch.is_grad_enabled():  # validation / serving: the kernel writes only the block output
-            return _tt_block_infer(h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, eps, B, H, T)
-        return _TTBlockFn.apply(h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, eps, B, H, T)
+            out = _tt_block_infer(h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, eps, B, H, T)
+            return out.reshape(B, T, -1).mean(1) if pooled else out
+        kp = pooled and _TT_FUSED_BWD  # the kernel pools only for its own (fused) backward
+        out = _TTBlockFn.apply(h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, eps, B, H, T, kp)
+        return out.reshape(B, T, -1).mean(1) if pooled and not kp else out
     h = prenorm_attention(h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, B, H, T, eps)
-    return prenorm_ffn(h, ln2_w, ln2_b, w1, b1, w2, b2, eps)
+    h = prenorm_ffn(h, ln2_w, ln2_b, w1, b1, w2, b2, eps)
+    return h.reshape(B, T, -1).mean(1) if pooled else h
 
 
 def prenorm_attention(h, ln_w, ln_b, wqkv, bqkv, wo, bo, B: int, H: int, T: int, eps: float = 1e-5):
