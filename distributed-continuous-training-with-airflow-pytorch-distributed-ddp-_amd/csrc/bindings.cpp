@@ -477,20 +477,22 @@ PYBIND11_MODULE(_dct_native, m) {
               "tt_block_bwd");
       });
   m.def(
-      "tt_block_fwd_pool",
+      "tt_block_fwd_ex",
       [](std::vector<uintptr_t> ptrs, int Bsz, int T, int DM, int H, int FF, float eps, float scale, uintptr_t pool,
-         uintptr_t stream) {
-        check(dct_tt_block_fwd_pool(ptrs.data(), (int)ptrs.size(), Bsz, T, DM, H, FF, eps, scale, P<float>(pool),
-                                    reinterpret_cast<void*>(stream)),
-              "tt_block_fwd_pool");
+         uintptr_t ex, uintptr_t eE, uintptr_t ec, uintptr_t stream) {
+        check(dct_tt_block_fwd_ex(ptrs.data(), (int)ptrs.size(), Bsz, T, DM, H, FF, eps, scale, P<float>(pool),
+                                  P<const float>(ex), P<const float>(eE), P<const float>(ec),
+                                  reinterpret_cast<void*>(stream)),
+              "tt_block_fwd_ex");
       });
   m.def(
-      "tt_block_bwd_pool",
+      "tt_block_bwd_ex",
       [](std::vector<uintptr_t> ptrs, int Bsz, int T, int DM, int H, int FF, float scale, uintptr_t dpool,
-         uintptr_t dout16, uintptr_t stream) {
-        check(dct_tt_block_bwd_pool(ptrs.data(), (int)ptrs.size(), Bsz, T, DM, H, FF, scale, P<const float>(dpool),
-                                    P<uint16_t>(dout16), reinterpret_cast<void*>(stream)),
-              "tt_block_bwd_pool");
+         uintptr_t dout16, uintptr_t ex, uintptr_t eE, uintptr_t ec, uintptr_t stream) {
+        check(dct_tt_block_bwd_ex(ptrs.data(), (int)ptrs.size(), Bsz, T, DM, H, FF, scale, P<const float>(dpool),
+                                  P<uint16_t>(dout16), P<const float>(ex), P<const float>(eE), P<const float>(ec),
+                                  reinterpret_cast<void*>(stream)),
+              "tt_block_bwd_ex");
       });
   m.def("tt_embed_fwd", [](uintptr_t x, uintptr_t E, uintptr_t c, uintptr_t h, int B, int F, int D, uintptr_t st) {
     check(dct_tt_embed_fwd(P<const float>(x), P<const float>(E), P<const float>(c), P<float>(h), B, F, D,

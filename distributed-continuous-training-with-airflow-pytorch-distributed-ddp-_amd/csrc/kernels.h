@@ -121,10 +121,11 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
                      void* stream);
 int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
                      void* stream);
-int dct_tt_block_fwd_pool(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps,
-                          float scale, float* pool, void* stream);
-int dct_tt_block_bwd_pool(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
-                          const float* dpool, uint16_t* dout16, void* stream);
+int dct_tt_block_fwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps,
+                        float scale, float* pool, const float* ex, const float* eE, const float* ec, void* stream);
+int dct_tt_block_bwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
+                        const float* dpool, uint16_t* dout16, const float* ex, const float* eE, const float* ec,
+                        void* stream);
 int dct_tt_embed_fwd(const float* x, const float* E, const float* c, float* h, int B, int F, int Dm, void* stream);
 int dct_tt_embed_bwd(const float* x, const float* dh, float* dE, float* dc, int B, int F, int Dm, void* stream);
 int dct_tt_head_fwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C, float eps, void* stream);

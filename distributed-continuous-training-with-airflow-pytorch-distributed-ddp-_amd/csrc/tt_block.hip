@@ -67,6 +67,16 @@ __device__ __forceinline__ bf16x4 pack4(f32x4 v) {
   return r;
 }
 
+// Optional feature-token embedding of the FIRST block (csrc/tt_io.hip embed_fwd_kernel, fused):
+// the block input row of token f of sample b is  x[b, f] * E[f, :] + c[f, :]  (same fmaf as the
+// standalone kernel, so bit-identical); computed where the kernels would read h, which is then never
+// written to or read from HBM (8 MB at batch 512 each way)
+struct Embed {
+  const float* x;  // [B][T] features (null: the block input comes from h)
+  const float* E;  // [T][DM]
+  const float* c;  // [T][DM]
+};
+
 struct Args {
   const float* h;
   const float *ln1_w, *ln1_b;
@@ -84,10 +94,49 @@ struct Args {
   uint16_t* wT;  // transposed bf16 weights for the backward: W2^T | W1^T | Wo^T | Wqkv^T
   uint64_t* prof;  // optional phase timestamps (wall clock), 16 per workgroup
   float* pool;     // optional [B][DM]: the block output's mean over the sample's tokens (classifier head input)
+  Embed em;        // optional: the first block's input computed from the features (h unused)
   int save;        // 0: inference (no_grad) - only `out` is written, no saved tensors / W^T
   int B;
   float eps, scale;
 };
+
+
+// 4 consecutive input columns 16 g + 4 q .. 16 g + 4 q + 3 of row r (token r) of the sample whose
+// first global row is row0 (a multiple of T)
+__device__ __forceinline__ float4 input_row4(const float* h, const Embed& em, int row0, int r, int g, int q) {
+  // branch-free: (x, E row, c row) or (1, h row, +0) - fmaf(1, v, 0) == v for every non-zero v, and
+  // the sign of a zero does not reach LayerNorm's (v - mean)
+  const bool e = em.x != nullptr;
+  const float xv = e ? em.x[row0 + r] : 1.f;
+  const float* p = e ? em.E + r * DM : h + (size_t)(row0 + r) * DM;
+  const float4 a = reinterpret_cast<const float4*>(p + 16 * g)[q];
+  float4 cc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e) cc = reinterpret_cast<const float4*>(em.c + r * DM + 16 * g)[q];
+  return make_float4(fmaf(xv, a.x, cc.x), fmaf(xv, a.y, cc.y), fmaf(xv, a.z, cc.z), fmaf(xv, a.w, cc.w));
+}
+
+// 16 consecutive input columns 16 g .. 16 g + 15 of row r (token r) of the sample at row0 into v
+__device__ __forceinline__ void input_row16(const float* h, const Embed& em, int row0, int r, int g, float* v) {
+  const int row = row0 + r;
+  if (em.x) {
+    const float xv = em.x[row];
+    const float4* ep = reinterpret_cast<const float4*>(em.E + r * DM + 16 * g);
+    const float4* cp = reinterpret_cast<const float4*>(em.c + r * DM + 16 * g);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 e = ep[q], cc = cp[q];
+      v[4 * q] = fmaf(xv, e.x, cc.x); v[4 * q + 1] = fmaf(xv, e.y, cc.y);
+      v[4 * q + 2] = fmaf(xv, e.z, cc.z); v[4 * q + 3] = fmaf(xv, e.w, cc.w);
+    }
+  } else {
+    const float4* p = reinterpret_cast<const float4*>(h + (size_t)row * DM + 16 * g);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 t = p[q];
+      v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+    }
+  }
+}
 
 // offsets (elements) of the transposed weights in Args::wT / BwdArgs::wT
 constexpr int WT_W2 = 0, WT_W1 = FF * DM, WT_WO = 2 * FF * DM, WT_QKV = 2 * FF * DM + DM * DM;
@@ -139,15 +188,19 @@ __device__ __forceinline__ void store_tile(void* g, const void* s) {
 // (re)written to HS, the bf16 normalised row to AS.
 __device__ __forceinline__ void layer_norm_rows(const float* src, bool from_global, float* HS, uint16_t* AS,
                                                 const float* w, const float* b, float* mean_out, float* rstd_out,
-                                                int row0, float eps) {
+                                                int row0, float eps, const Embed& em) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = 16 * wv + (lane & 15), g = lane >> 4;
   float v[16];
-  const float* p = from_global ? src + (size_t)(row0 + r) * DM + 16 * g : HS + r * HS_LD + 16 * g;
+  if (from_global) {
+    input_row16(src, em, row0, r, g, v);
+  } else {
+    const float* p = HS + r * HS_LD + 16 * g;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float4 t = reinterpret_cast<const float4*>(p)[q];
-    v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+    for (int q = 0; q < 4; ++q) {
+      const float4 t = reinterpret_cast<const float4*>(p)[q];
+      v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+    }
   }
   float s = 0.f;
 #pragma unroll
@@ -197,7 +250,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
 
   TT_MARK(0);
   // ---- P1: LN1 (rows of this wave)
-  layer_norm_rows(a.h, true, HS, AS, a.ln1_w, a.ln1_b, a.mean1, a.rstd1, row0, a.eps);
+  layer_norm_rows(a.h, true, HS, AS, a.ln1_w, a.ln1_b, a.mean1, a.rstd1, row0, a.eps, a.em);
   __syncthreads();
   TT_MARK(1);
 
@@ -324,7 +377,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
       for (int r = 0; r < 4; ++r) HS[(16 * i + 4 * g + r) * HS_LD + col] += acc[i][r] + bv;
   }
   __syncthreads();  // LN2 rows need every wave's columns
-  layer_norm_rows(nullptr, false, HS, AS, a.ln2_w, a.ln2_b, a.mean2, a.rstd2, row0, a.eps);
+  layer_norm_rows(nullptr, false, HS, AS, a.ln2_w, a.ln2_b, a.mean2, a.rstd2, row0, a.eps, Embed{});
   __syncthreads();
 
   TT_MARK(4);
@@ -444,6 +497,7 @@ struct BwdArgs {
   const uint16_t* wT;
   const uint16_t* a2; const uint16_t* w1; const float* b1;  // the recompute's operands
   uint16_t* dpre; uint16_t* dh1_16; uint16_t* dqkv; float* dh; uint16_t* dh16;
+  Embed em;            // optional: the first block's input recomputed from the features (h unused)
   const float* dpool;  // optional [B][DM]: the gradient of the token mean (pool) instead of dout rows;
   uint16_t* dout16;    // then bf16(dout) [M][DM] is written here for the W2 gradient GEMM
   float *dln1_w, *dln1_b, *dln2_w, *dln2_b;
@@ -500,25 +554,25 @@ __device__ __forceinline__ void load_tile(void* s, const void* gsrc) {
 // weight / bias partial column sums reduced over the wave's rows, then LDS atomics into red.
 __device__ __forceinline__ void ln_bwd_rows(const float* S, const float* x, const float* mean, const float* rstd,
                                             const float* w, float* G, float* red_w, float* red_b, int row0, int wv,
-                                            int lane) {
+                                            int lane, const Embed& em) {
   const int rl = 16 * wv + (lane & 15), g = lane >> 4;
   const float mu = mean[row0 + rl], rs = rstd[row0 + rl];
-  float da[16], xh[16], gw[16], s1 = 0.f, s2 = 0.f;
-  const float4* xp = reinterpret_cast<const float4*>(x + (size_t)(row0 + rl) * DM + 16 * g);
+  float da[16], xh[16], s1 = 0.f, s2 = 0.f;  // gw = da * w recomputed below (16 fewer live VGPRs)
   const float4* sp = reinterpret_cast<const float4*>(S + rl * HS_LD + 16 * g);
   const float4* wp = reinterpret_cast<const float4*>(w + 16 * g);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const float4 xv = xp[q], dv = sp[q], ww = wp[q];
-    const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ds[4] = {dv.x, dv.y, dv.z, dv.w}, ws[4] = {ww.x, ww.y, ww.z, ww.w};
+    const float4 dv = sp[q], ww = wp[q], xv = input_row4(x, em, row0, rl, g, q);
+    const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+    const float ds[4] = {dv.x, dv.y, dv.z, dv.w}, ws[4] = {ww.x, ww.y, ww.z, ww.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int k = 4 * q + e;
       da[k] = ds[e];
       xh[k] = (xs[e] - mu) * rs;
-      gw[k] = ds[e] * ws[e];
-      s1 += gw[k];
-      s2 += gw[k] * xh[k];
+      const float gw = ds[e] * ws[e];
+      s1 += gw;
+      s2 += gw * xh[k];
     }
   }
   s1 = sum4g(s1) * (1.f / DM);
@@ -527,10 +581,11 @@ __device__ __forceinline__ void ln_bwd_rows(const float* S, const float* x, cons
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     float4 v = gp[q];
-    v.x += rs * (gw[4 * q] - s1 - xh[4 * q] * s2);
-    v.y += rs * (gw[4 * q + 1] - s1 - xh[4 * q + 1] * s2);
-    v.z += rs * (gw[4 * q + 2] - s1 - xh[4 * q + 2] * s2);
-    v.w += rs * (gw[4 * q + 3] - s1 - xh[4 * q + 3] * s2);
+    const float4 ww = wp[q];
+    v.x += rs * (da[4 * q] * ww.x - s1 - xh[4 * q] * s2);
+    v.y += rs * (da[4 * q + 1] * ww.y - s1 - xh[4 * q + 1] * s2);
+    v.z += rs * (da[4 * q + 2] * ww.z - s1 - xh[4 * q + 2] * s2);
+    v.w += rs * (da[4 * q + 3] * ww.w - s1 - xh[4 * q + 3] * s2);
     gp[q] = v;
   }
   // column sums over the wave's 16 rows by recursive halving across the 16 lanes of a row group:
@@ -730,7 +785,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
       for (int r = 0; r < 4; ++r) S[(16 * i + 4 * g + r) * HS_LD + 16 * wv + c] = acc[i][r];
   }
   __syncthreads();
-  ln_bwd_rows(S, a.h1, a.mean2, a.rstd2, a.ln2_w, G, red + 2 * DM, red + 3 * DM, row0, wv, lane);
+  ln_bwd_rows(S, a.h1, a.mean2, a.rstd2, a.ln2_w, G, red + 2 * DM, red + 3 * DM, row0, wv, lane, Embed{});
   rows_to_bf16(G, X, wv, lane);
   store_rows16<DM * 2, XB_LD * 2>(a.dh1_16 + (size_t)row0 * DM, X, wv, lane);
   __syncthreads();  // do reads all rows of X; S (over Os / dOs) fully consumed
@@ -906,9 +961,11 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
   }
   __syncthreads();
   TT_MARK(7);
-  ln_bwd_rows(S, a.h, a.mean1, a.rstd1, a.ln1_w, G, red, red + DM, row0, wv, lane);
-  rows_to_bf16(G, X, wv, lane);
-  store_rows16<DM * 2, XB_LD * 2>(a.dh16 + (size_t)row0 * DM, X, wv, lane);
+  ln_bwd_rows(S, a.h, a.mean1, a.rstd1, a.ln1_w, G, red, red + DM, row0, wv, lane, a.em);
+  if (a.dh16) {  // null for the embedding block: only the fp32 dh feeds the embedding's gradient
+    rows_to_bf16(G, X, wv, lane);
+    store_rows16<DM * 2, XB_LD * 2>(a.dh16 + (size_t)row0 * DM, X, wv, lane);
+  }
   store_rows16<DM * 4, HS_LD * 4>(a.dh + (size_t)row0 * DM, G, wv, lane);
   __syncthreads();
   {  // LayerNorm parameter gradients: one atomic per column per workgroup
@@ -925,9 +982,11 @@ extern "C" {
 
 // ptrs (27, in order): h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2,
 //   a1, mean1, rstd1, qkv, o, lse, h1, a2, mean2, rstd2, f, pre, out, wT
-// pool (optional): the last block's token mean for the classifier head; `out` (p[25]) may then be null
-int dct_tt_block_fwd_pool(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps,
-                          float scale, float* pool, void* stream) {
+// pool (optional): the last block's token mean for the classifier head; `out` (p[25]) may then be null.
+// ex / eE / ec (optional): the first block's input embedded from the features x [B][T] (E, c [T][DM]);
+// h (p[0]) is then not read and may be null
+int dct_tt_block_fwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps,
+                        float scale, float* pool, const float* ex, const float* eE, const float* ec, void* stream) {
   using namespace dct::ttb;
   if ((n_ptrs != 27 && n_ptrs != 28) || T != dct::ttb::T || DM != dct::ttb::DM || H != NH || FF != dct::ttb::FF || Bsz <= 0)
     return (int)hipErrorInvalidValue;
@@ -935,7 +994,7 @@ int dct_tt_block_fwd_pool(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM
   const bool save = p[13] != 0;
   uintptr_t any = 0;
   for (int i = 0; i < 27; ++i) {
-    const bool needed = (i < 13 || (i == 25 && !pool) || save) && i != 24 && !(i == 25 && pool);  // pre (24): BwdArgs::pre
+    const bool needed = (i < 13 || (i == 25 && !pool) || save) && i != 24 && !(i == 25 && pool) && !(i == 0 && ex);
     if (needed && !p[i]) return (int)hipErrorInvalidValue;
     any |= p[i];
   }
@@ -954,6 +1013,8 @@ int dct_tt_block_fwd_pool(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM
   a.prof = n_ptrs == 28 ? (uint64_t*)p[27] : nullptr;
   a.pool = pool;
   if (pool && (((uintptr_t)pool) & 15)) return (int)hipErrorInvalidValue;
+  if (ex && (!eE || !ec || ((((uintptr_t)eE) | ((uintptr_t)ec)) & 15))) return (int)hipErrorInvalidValue;
+  a.em = Embed{ex, eE, ec};
   a.save = save ? 1 : 0;
   a.B = Bsz; a.eps = eps; a.scale = scale;
   static bool attr = false;
@@ -969,15 +1030,17 @@ int dct_tt_block_fwd_pool(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM
 
 int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps, float scale,
                      void* stream) {
-  return dct_tt_block_fwd_pool(p, n_ptrs, Bsz, T, DM, H, FF, eps, scale, nullptr, stream);
+  return dct_tt_block_fwd_ex(p, n_ptrs, Bsz, T, DM, H, FF, eps, scale, nullptr, nullptr, nullptr, nullptr, stream);
 }
 
 // ptrs (22, in order): dout, h, mean1, rstd1, ln1_w, qkv, o, lse, h1, mean2, rstd2, ln2_w, pre, wT,
 //   dpre, dh1_16, dqkv, dh, dh16, dln1_w, dln1_b, dln2_w, dln2_b  (23 with the last four)
 // dpool (optional): the head's gradient of the last block's token mean instead of dout (p[0] may then be
 // null); bf16(dout) is then written to dout16 ([B*T][DM]) for the W2 gradient GEMM
-int dct_tt_block_bwd_pool(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
-                          const float* dpool, uint16_t* dout16, void* stream) {
+// ex / eE / ec (optional): the block input is embedded from the features (h p[1] and dh16 p[18] may be null)
+int dct_tt_block_bwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
+                        const float* dpool, uint16_t* dout16, const float* ex, const float* eE, const float* ec,
+                        void* stream) {
   using namespace dct::ttb;
   // 23 (+1 prof) pointers; 26 (+1 prof): + a2, w1 (bf16 [FF][DM]), b1 - with pre (p[12]) null the
   // kernel recomputes the pre-activation from them
@@ -988,7 +1051,8 @@ int dct_tt_block_bwd_pool(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM
   const bool recomp = ext && p[12] == 0;
   uintptr_t any = 0;
   for (int i = 0; i < (ext ? 26 : 23); ++i) {
-    if (!p[i] && !(i == 12 && recomp) && !(i >= 23 && !recomp) && !(i == 0 && dpool)) return (int)hipErrorInvalidValue;
+    if (!p[i] && !(i == 12 && recomp) && !(i >= 23 && !recomp) && !(i == 0 && dpool) && !((i == 1 || i == 18) && ex))
+      return (int)hipErrorInvalidValue;
     if (i < 19 || i >= 23) any |= p[i];
   }
   if (any & 15) return (int)hipErrorInvalidValue;
@@ -1008,6 +1072,8 @@ int dct_tt_block_bwd_pool(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM
   if (dpool && (!dout16 || ((((uintptr_t)dpool) | ((uintptr_t)dout16)) & 15))) return (int)hipErrorInvalidValue;
   a.dpool = dpool;
   a.dout16 = dpool ? dout16 : nullptr;
+  if (ex && (!eE || !ec || ((((uintptr_t)eE) | ((uintptr_t)ec)) & 15))) return (int)hipErrorInvalidValue;
+  a.em = Embed{ex, eE, ec};
   static bool attr = false;
   if (!attr) {
     for (const void* k : {(const void*)tt_block_bwd_kernel<false>, (const void*)tt_block_bwd_kernel<true>}) {
@@ -1025,7 +1091,7 @@ int dct_tt_block_bwd_pool(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM
 
 int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
                      void* stream) {
-  return dct_tt_block_bwd_pool(p, n_ptrs, Bsz, T, DM, H, FF, scale, nullptr, nullptr, stream);
+  return dct_tt_block_bwd_ex(p, n_ptrs, Bsz, T, DM, H, FF, scale, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
 }
 
 }  // extern "C"

@@ -25,6 +25,9 @@ from ..trainer.module import TrainModule
 # the last block hands the classifier head the token mean (ops/nn.py tt_block(pooled=True)); False: the
 # head pools the last block's full output itself (A/B: tools/tt_pooled_head_ab.py)
 POOLED_HEAD = True
+# the first block computes the feature-token embedding where it reads its input (tt_block(embed=...));
+# False: a separate embedding kernel writes the [B*F, d] input (A/B: tools/tt_pooled_head_ab.py)
+FUSED_EMBED = True
 
 
 class _Block(nn.Module):
@@ -38,10 +41,10 @@ class _Block(nn.Module):
         self.fc1 = nn.Linear(d, ffn_mult * d)
         self.fc2 = nn.Linear(ffn_mult * d, d)
 
-    def forward(self, h: torch.Tensor, B: int, T: int, pooled: bool = False) -> torch.Tensor:
+    def forward(self, h: torch.Tensor, B: int, T: int, pooled: bool = False, embed=None) -> torch.Tensor:
         return tt_block(h, self.ln1_w, self.ln1_b, self.qkv.weight, self.qkv.bias, self.proj.weight, self.proj.bias,
                         self.ln2_w, self.ln2_b, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias,
-                        B, self.heads, T, pooled=pooled)
+                        B, self.heads, T, pooled=pooled, embed=embed)
 
 
 class TabTransformer(TrainModule):
@@ -66,9 +69,17 @@ class TabTransformer(TrainModule):
         """Token embedding + the blocks: [B*F, d], or with ``pooled`` the last block's output averaged
         over each sample's F tokens, [B, d] (on MI355X the last block kernel writes only that)."""
         B = x.shape[0]
-        h = tt_embed(x, self.feat_w, self.feat_b)
+        if not FUSED_EMBED or len(self.blocks) == 0:
+            h = tt_embed(x, self.feat_w, self.feat_b)
+            for i, blk in enumerate(self.blocks):
+                h = blk(h, B, self.F, pooled=pooled and i == len(self.blocks) - 1)
+            return h
+        # the first block embeds the features itself (ops/nn.py tt_block(embed=...)): the [B*F, d] block
+        # input is never written to or read from HBM in the fused training step
+        h = x
         for i, blk in enumerate(self.blocks):
-            h = blk(h, B, self.F, pooled=pooled and i == len(self.blocks) - 1)
+            h = blk(h, B, self.F, pooled=pooled and i == len(self.blocks) - 1,
+                    embed=(self.feat_w, self.feat_b) if i == 0 else None)
         return h
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

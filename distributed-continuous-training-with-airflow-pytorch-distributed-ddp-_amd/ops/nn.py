@@ -539,11 +539,15 @@ class _TTBlockFn(torch.autograd.Function):
     the two unfused nodes save, so the backward is theirs, FFN first."""
 
     @staticmethod
-    def forward(ctx, h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, eps, B, H, T, pooled=False):
+    def forward(ctx, h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, eps, B, H, T, pooled=False,
+                eE=None, ec=None):
         nat = native()
         st = _stream()
+        # eE / ec (the model's first block, with the fused backward): h is the feature matrix x [B, T] and
+        # the kernels embed it themselves (x * E + c per token) where they would read the block input
+        embed = eE is not None
         h = h.contiguous().float()
-        M, dm = h.shape
+        M, dm = (B * T, ln1_w.shape[0]) if embed else h.shape
         FF = w1.shape[0]
         dev = h.device
         wqkvb, wob, w1b, w2b = _w16(wqkv), _w16(wo), _w16(w1), _w16(w2)
@@ -570,12 +574,15 @@ class _TTBlockFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(dm // H)
         if _TT_PROF is not None:  # tools/debug/tt_phase_prof.py
             ptrs.append(_tt_prof_buf("fwd", B, dev))
-        addrs = [0 if (t is pre and recomp) or (t is out and pooled) else t.data_ptr() for t in ptrs]
-        if pooled:
-            nat.tt_block_fwd_pool(addrs, B, T, dm, H, FF, float(eps), scale, out.data_ptr(), st)
+        addrs = [0 if (t is pre and recomp) or (t is out and pooled) or (t is h and embed) else t.data_ptr()
+                 for t in ptrs]
+        if pooled or embed:
+            em = [t.data_ptr() for t in (h, eE, ec)] if embed else [0, 0, 0]
+            nat.tt_block_fwd_ex(addrs, B, T, dm, H, FF, float(eps), scale, out.data_ptr() if pooled else 0, *em, st)
         else:
             nat.tt_block_fwd(addrs, B, T, dm, H, FF, float(eps), scale, st)
         ctx.save_for_backward(h, st4, a1, wqkvb, qkv, o, lse, wob, h1, a2, w1b, w2b, f, pre, wT, vecs[0], vecs[4])
+        ctx.embed = (eE, ec) if embed else None
         ctx.params = (ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2)
         ctx.dims = (B, H, T, dm // H, scale)
         ctx.pooled = pooled
@@ -586,14 +593,18 @@ class _TTBlockFn(torch.autograd.Function):
         h, st4, a1, wqkvb, qkv, o, lse, wob, h1, a2, w1b, w2b, f, pre, wT, ln1w, ln2w = ctx.saved_tensors
         p = ctx.params
         B, H, T, D, scale = ctx.dims
-        if _TT_FUSED_BWD or pre.numel() == 0 or ctx.pooled:  # no stored pre-activation: the fused backward
-            return (*_tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, p, B, H, T,
-                                         scale, w1b, pooled=ctx.pooled), None, None, None, None, None)
+        if _TT_FUSED_BWD or pre.numel() == 0 or ctx.pooled or ctx.embed:  # no stored pre-activation: fused
+            grads, demb = _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, p, B, H,
+                                              T, scale, w1b, pooled=ctx.pooled, embed=ctx.embed)
+            if ctx.embed:  # h was the feature matrix: no gradient for it, the embedding's for E / c
+                grads = (None,) + tuple(grads[1:])
+            return (*grads, None, None, None, None, None, *demb)
         dh1, dl2w, dl2b, dw1, db1, dw2, db2 = _prenorm_ffn_bwd(dout, (h1, st4[2], st4[3], a2, w1b, w2b, f, pre),
                                                                p[6:])
         dh, dl1w, dl1b, dwqkv, dbqkv, dwo, dbo = _prenorm_attn_bwd(
             dh1, (h, st4[0], st4[1], a1, wqkvb, qkv, o, lse, wob), p[:6], ctx.dims)
-        return (dh, dl1w, dl1b, dwqkv, dbqkv, dwo, dbo, dl2w, dl2b, dw1, db1, dw2, db2, None, None, None, None, None)
+        return (dh, dl1w, dl1b, dwqkv, dbqkv, dwo, dbo, dl2w, dl2b, dw1, db1, dw2, db2, None, None, None, None, None,
+                None, None)
 
 
 _TT_FUSED_BWD = True
@@ -607,7 +618,7 @@ def _tt_prof_buf(kind: str, B: int, dev) -> torch.Tensor:
 
 
 def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, params, B, H, T, scale,
-                        w1b=None, pooled=False):
+                        w1b=None, pooled=False, embed=None):
     """Backward of the fused block: ONE kernel for the whole dX chain (csrc/tt_block.hip
     tt_block_bwd_kernel: dF/gelu', W1, LN2, Wo, attention, Wqkv, LN1 per sample) writing the dZ
     operands of the four dW GEMMs, which then run split-K over all rows with the bias gradients
@@ -616,7 +627,7 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
     st = _stream()
     ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2 = params
     dout = dout.contiguous().float()
-    M, dm = h.shape
+    M, dm = a1.shape  # (h is the feature matrix [B, T] when `embed` = (E, c): the first block)
     FF = w1.shape[0]
     recomp = pre.numel() == 0
     dev, bf = h.device, torch.bfloat16
@@ -624,7 +635,7 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
     dh1_16 = torch.empty(M, dm, dtype=bf, device=dev)
     dqkv = torch.empty(M, 3 * dm, dtype=bf, device=dev)
     dh = torch.empty(M, dm, dtype=torch.float32, device=dev)
-    dh16 = torch.empty(M, dm, dtype=bf, device=dev)
+    dh16 = torch.empty(0 if embed is not None else M, dm, dtype=bf, device=dev)  # embedding block: not needed
     lg = [_grad_dst(t, zero=True) for t in (ln1_w, ln1_b, ln2_w, ln2_b)]
     ptrs = [dout, h, st4[0], st4[1], ln1w, qkv, o, lse, h1, st4[2], st4[3], ln2w, pre, wT,
             dpre, dh1_16, dqkv, dh, dh16] + [g for g, _ in lg]
@@ -639,10 +650,15 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
         addrs += [a2.data_ptr(), w1b.data_ptr(), b1c.data_ptr()]
     if _TT_PROF is not None:
         addrs.append(_tt_prof_buf("bwd", B, dev).data_ptr())
-    if pooled:
-        nat.tt_block_bwd_pool(addrs, B, T, dm, H, FF, scale, dout.data_ptr(), dout16.data_ptr(), st)
+    if embed is not None:
+        addrs[1] = addrs[18] = 0  # the block input is recomputed from x, E, c; no bf16 dh consumer
+    if pooled or embed is not None:
+        em = [t.data_ptr() for t in (h, *embed)] if embed is not None else [0, 0, 0]
+        nat.tt_block_bwd_ex(addrs, B, T, dm, H, FF, scale, dout.data_ptr() if pooled else 0,
+                            dout16.data_ptr() if pooled else 0, *em, st)
     else:
         nat.tt_block_bwd(addrs, B, T, dm, H, FF, scale, st)
+    if not pooled:
         dout16 = _bf16_of(dout)
     items = [(dout16, f, w2, b2), (dpre, a2, w1, b1), (dh1_16, o, wo, bo), (dqkv, a1, wqkv, bqkv)]
     b = _BOUND
@@ -656,10 +672,18 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
         dw2 = db2 = dw1 = db1 = dwo = dbo = dwqkv = dbqkv = None
     else:
         (dw2, db2), (dw1, db1), (dwo, dbo), (dwqkv, dbqkv) = _dw_gemm_grouped(nat, items, st)
-    _remember_bf16(dh, dh16)
     (dl1w, d1), (dl1b, d2), (dl2w, d3), (dl2b, d4) = lg
-    return (dh, None if d1 else dl1w, None if d2 else dl1b, dwqkv, dbqkv, dwo, dbo, None if d3 else dl2w,
-            None if d4 else dl2b, dw1, db1, dw2, db2)
+    grads = (dh, None if d1 else dl1w, None if d2 else dl1b, dwqkv, dbqkv, dwo, dbo, None if d3 else dl2w,
+             None if d4 else dl2b, dw1, db1, dw2, db2)
+    if embed is None:
+        _remember_bf16(dh, dh16)
+        return grads, ()
+    # the fused embedding's parameter gradients: batch reductions of dh (tt_io.hip embed_bwd_kernel)
+    E, c = embed
+    dE, dE_direct = _grad_dst(E, zero=True)
+    dc, dc_direct = _grad_dst(c, zero=True)
+    nat.tt_embed_bwd(h.data_ptr(), dh.data_ptr(), dE.data_ptr(), dc.data_ptr(), B, T, dm, st)
+    return grads, (None if dE_direct else dE, None if dc_direct else dc)
 
 
 def _prenorm_ok(h: torch.Tensor) -> bool:
@@ -699,10 +723,25 @@ def tt_block_fusable(h: torch.Tensor, H: int, T: int, ffn: int) -> bool:
 
 
 def tt_block(h, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, B: int, H: int, T: int,
-             eps: float = 1e-5, pooled: bool = False):
+             eps: float = 1e-5, pooled: bool = False, embed=None):
     """One pre-norm transformer block: h + MHA(LN1 h), then + FFN(LN2 .) - one fused kernel
     forward on MI355X for the benchmark shape, two fused nodes otherwise.  ``pooled``: return the
-    block output's mean over each sample's T tokens, [B, d] (the classifier head's input)."""
+    block output's mean over each sample's T tokens, [B, d] (the classifier head's input).
+    ``embed`` = (E, c): ``h`` is the feature matrix x [B, T] and the block input is the feature-token
+    embedding x * E + c (tt_embed), which the fused kernels compute themselves (first block)."""
+    if embed is not None:
+        E, c = embed
+        x = h
+        fuse = (torch.is_grad_enabled() and x.is_cuda and x.dim() == 2 and x.shape[1] == T and E.shape == (T, 64)
+                and all(t.is_contiguous() and t.data_ptr() % 16 == 0 for t in (E, c)))
+        h = None if fuse else tt_embed(x, E, c)
+        if fuse and tt_block_fusable(torch.empty(0, 64, device=x.device), H, T, w1.shape[0]) and _TT_FUSED_BWD and \
+                all(v.is_contiguous() and v.data_ptr() % 16 == 0 for v in (ln1_w, ln1_b, bqkv, bo, ln2_w, ln2_b, b1, b2)):
+            out = _TTBlockFn.apply(x, ln1_w, ln1_b, wqkv, bqkv, wo, bo, ln2_w, ln2_b, w1, b1, w2, b2, eps, B, H, T,
+                                   False, E, c)
+            return out.reshape(B, T, -1).mean(1) if pooled else out
+        if h is None:
+            h = tt_embed(x, E, c)
     vecs = (ln1_w, ln1_b, bqkv, bo, ln2_w, ln2_b, b1, b2)  # read with 16-byte vector loads
     if tt_block_fusable(h, H, T, w1.shape[0]) and all(v.is_contiguous() and v.data_ptr() % 16 == 0 for v in vecs):
         if not torch.is_grad_enabled():  # validation / serving: the kernel writes only the block output

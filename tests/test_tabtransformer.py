@@ -155,3 +155,34 @@ def test_deferred_dw_matches_in_stream(cuda, monkeypatch):
     noise = float((p0 - ph).norm() / p0.norm())
     diff = float((p0 - p1).norm() / p0.norm())
     assert diff < max(3 * noise, 1e-4), (diff, noise)
+
+
+@pytest.mark.gpu
+def test_fused_embedding_matches_separate_kernel(cuda, monkeypatch):
+    """The first block embedding the features itself (models/tabtransformer.py FUSED_EMBED, tt_block
+    embed=(E, c)) gives the same loss bit for bit (same fmaf per element as tt_io.hip's embed kernel)
+    and the same gradients as the separate embedding kernel writing the block input; the pooled head
+    and the fused backward on both sides."""
+    from dct_amd.models import tabtransformer as ttm
+
+    torch.manual_seed(5)
+    F_, B = 64, 256
+    base = TabTransformer(num_features=F_, d_model=64, heads=4, layers=2)
+    X, Y = _data(B, F_, seed=6)
+    X, Y = X.to(cuda), Y.to(cuda)
+    res = {}
+    for fused in (True, False):
+        monkeypatch.setattr(ttm, "FUSED_EMBED", fused)
+        m = TabTransformer(num_features=F_, d_model=64, heads=4, layers=2)
+        m.load_state_dict(base.state_dict())
+        m.to(cuda)
+        loss = m.training_step((X, Y), 0)
+        loss = loss["loss"] if isinstance(loss, dict) else loss
+        loss.backward()
+        torch.cuda.synchronize()
+        res[fused] = (loss.detach().cpu(), {n: p.grad.detach().cpu().clone() for n, p in m.named_parameters()})
+    (l1, g1), (l0, g0) = res[True], res[False]
+    assert torch.equal(l1, l0), (l1, l0)
+    for n in g0:
+        rel = float((g1[n] - g0[n]).norm() / (g0[n].norm() + 1e-12))
+        assert rel < 1e-4, (n, rel)

@@ -2,7 +2,10 @@
 """A/B of the TabTransformer step (bench.py's config: batch 512, 64 tokens, d 64, 4 heads, 4 layers)
 with the last block handing the classifier head its token mean (models/tabtransformer.py POOLED_HEAD,
 default) against the head pooling the last block's full [B*64, 64] output itself.  Two engines, each
-graph-captured with its setting, timed alternately on one GPU: ms/step over 200 device-loop steps."""
+graph-captured with its setting, timed alternately on one GPU: ms/step over 200 device-loop steps.
+
+    python tools/tt_pooled_head_ab.py [FLAG]   # FLAG: a models/tabtransformer.py switch, default POOLED_HEAD
+                                               # (FUSED_EMBED: the first block embeds the features itself)"""
 import os
 import sys
 import time
@@ -19,8 +22,11 @@ from dct_amd.parallel.dist import init_distributed  # noqa: E402
 from dct_amd.trainer.engines import AutogradEngine  # noqa: E402
 
 
+FLAG = sys.argv[1] if len(sys.argv) > 1 else "POOLED_HEAD"
+
+
 def make(ctx, X, Y, pooled):
-    ttm.POOLED_HEAD = pooled
+    setattr(ttm, FLAG, pooled)
     torch.manual_seed(0)
     model = build_model("tabtransformer", 64, d_model=64, heads=4, layers=4, lr=1e-3)
     eng = AutogradEngine(model, ctx, 512, seed=42)
@@ -51,7 +57,7 @@ def main():
         for p in (True, False):
             res[p].append(timed(*engs[p]))
     for p in (True, False):
-        print(f"POOLED_HEAD={p}: ms/step {[round(v, 4) for v in res[p]]} min {min(res[p]):.4f} "
+        print(f"{FLAG}={p}: ms/step {[round(v, 4) for v in res[p]]} min {min(res[p]):.4f} "
               f"loss[229] {float(engs[p][2][229]):.5f}", flush=True)
 
 
