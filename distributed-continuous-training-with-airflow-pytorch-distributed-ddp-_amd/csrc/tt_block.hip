@@ -435,7 +435,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
 
   TT_MARK(5);
   // ---- P6: f out; out = h1 + F W2^T + b2 for column tile wv
-  if (a.save) store_tile<FF * 2, F_LD * 2>(a.f + (size_t)row0 * FF, RS);
+  if (a.save && a.f) store_tile<FF * 2, F_LD * 2>(a.f + (size_t)row0 * FF, RS);  // null: dW2 recomputes f
   {
     f32x4 acc[4];
 #pragma unroll
@@ -756,9 +756,10 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
           *pp = make_uint2(dp[0] | ((uint32_t)dp[1] << 16), dp[2] | ((uint32_t)dp[3] << 16));
         }
     }
-    // dpre out: this wave's 64-column block of all 64 rows (128 B per row, 16-byte chunks)
+    // dpre out: this wave's 64-column block of all 64 rows (128 B per row, 16-byte chunks); null: the
+    // FFN weight-gradient kernel recomputes it (tt_ffn_dw_kernel)
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < (a.dpre ? 8 : 0); ++q) {
       const int idx = q * 64 + lane, rr = idx >> 3, cc = idx & 7;
       *reinterpret_cast<uint4*>(a.dpre + (size_t)(row0 + rr) * FF + 64 * wv + cc * 8) =
           *reinterpret_cast<const uint4*>(R + rr * F_LD + 64 * wv + cc * 8);
@@ -994,7 +995,8 @@ int dct_tt_block_fwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, 
   const bool save = p[13] != 0;
   uintptr_t any = 0;
   for (int i = 0; i < 27; ++i) {
-    const bool needed = (i < 13 || (i == 25 && !pool) || save) && i != 24 && !(i == 25 && pool) && !(i == 0 && ex);
+    const bool needed = (i < 13 || (i == 25 && !pool) || save) && i != 24 && i != 23 && !(i == 25 && pool) &&
+                        !(i == 0 && ex);
     if (needed && !p[i]) return (int)hipErrorInvalidValue;
     any |= p[i];
   }
@@ -1051,7 +1053,8 @@ int dct_tt_block_bwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, 
   const bool recomp = ext && p[12] == 0;
   uintptr_t any = 0;
   for (int i = 0; i < (ext ? 26 : 23); ++i) {
-    if (!p[i] && !(i == 12 && recomp) && !(i >= 23 && !recomp) && !(i == 0 && dpool) && !((i == 1 || i == 18) && ex))
+    if (!p[i] && !(i == 12 && recomp) && !(i >= 23 && !recomp) && !(i == 0 && dpool) && !((i == 1 || i == 18) && ex) &&
+        !(i == 14 && recomp))
       return (int)hipErrorInvalidValue;
     if (i < 19 || i >= 23) any |= p[i];
   }

@@ -1,3 +1,3 @@
 set -e
 export TMPDIR=/tmp
-bash tools/gpu.sh r5_g25 "python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_tabtransformer.py tests/test_determinism_gpu.py" "python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k 'tt_ or prenorm'" "python tools/tt_pooled_head_ab.py FUSED_EMBED"
+bash tools/gpu.sh r5_g28 "python tools/probes/ffn_dw_probe.py"

@@ -26,7 +26,9 @@ FLAG = sys.argv[1] if len(sys.argv) > 1 else "POOLED_HEAD"
 
 
 def make(ctx, X, Y, pooled):
-    setattr(ttm, FLAG, pooled)
+    from dct_amd.ops import nn as nnops
+    # "nn.NAME": a switch of ops/nn.py instead (e.g. nn._WHATIF, a timing probe)
+    setattr(nnops if FLAG.startswith("nn.") else ttm, FLAG[3:] if FLAG.startswith("nn.") else FLAG, pooled)
     torch.manual_seed(0)
     model = build_model("tabtransformer", 64, d_model=64, heads=4, layers=4, lr=1e-3)
     eng = AutogradEngine(model, ctx, 512, seed=42)
