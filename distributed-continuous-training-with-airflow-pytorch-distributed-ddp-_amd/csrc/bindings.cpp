@@ -502,24 +502,6 @@ PYBIND11_MODULE(_dct_native, m) {
     check(dct_tt_embed_bwd(P<const float>(x), P<const float>(dh), P<float>(dE), P<float>(dc), B, F, D,
                            reinterpret_cast<void*>(st)), "tt_embed_bwd");
   });
-  // FFN weight gradients of n fused blocks from a2 / dout16 (csrc/tt_ffn_dw.hip); one list of
-  // 9 addresses per block: a2, dout16, w1 (bf16), w2 (bf16), b1, dw1, dw2, db1, db2
-  m.def("tt_ffn_dw", [](std::vector<std::vector<uintptr_t>> probs, int M, uintptr_t st) {
-    const size_t n = probs.size();
-    std::vector<const uint16_t*> a2(n), dout(n), w1(n), w2(n);
-    std::vector<const float*> b1(n);
-    std::vector<float*> dw1(n), dw2(n), db1(n), db2(n);
-    for (size_t i = 0; i < n; ++i) {
-      const auto& q = probs[i];
-      if (q.size() != 9) throw std::invalid_argument("tt_ffn_dw: 9 addresses per block");
-      a2[i] = P<const uint16_t>(q[0]); dout[i] = P<const uint16_t>(q[1]); w1[i] = P<const uint16_t>(q[2]);
-      w2[i] = P<const uint16_t>(q[3]); b1[i] = P<const float>(q[4]); dw1[i] = P<float>(q[5]);
-      dw2[i] = P<float>(q[6]); db1[i] = P<float>(q[7]); db2[i] = P<float>(q[8]);
-    }
-    check(dct_tt_ffn_dw((int)n, a2.data(), dout.data(), w1.data(), w2.data(), b1.data(), dw1.data(), dw2.data(),
-                        db1.data(), db2.data(), M, reinterpret_cast<void*>(st)),
-          "tt_ffn_dw");
-  });
   m.def("tt_head_fwd", [](std::vector<uintptr_t> p, int B, int T, int D, int C, float eps, uintptr_t st) {
     check(dct_tt_head_fwd(p.data(), (int)p.size(), B, T, D, C, eps, reinterpret_cast<void*>(st)), "tt_head_fwd");
   });

@@ -435,7 +435,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
 
   TT_MARK(5);
   // ---- P6: f out; out = h1 + F W2^T + b2 for column tile wv
-  if (a.save && a.f) store_tile<FF * 2, F_LD * 2>(a.f + (size_t)row0 * FF, RS);  // null: dW2 recomputes f
+  if (a.save && a.f) store_tile<FF * 2, F_LD * 2>(a.f + (size_t)row0 * FF, RS);  // null: not stored
   {
     f32x4 acc[4];
 #pragma unroll
@@ -756,8 +756,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
           *pp = make_uint2(dp[0] | ((uint32_t)dp[1] << 16), dp[2] | ((uint32_t)dp[3] << 16));
         }
     }
-    // dpre out: this wave's 64-column block of all 64 rows (128 B per row, 16-byte chunks); null: the
-    // FFN weight-gradient kernel recomputes it (tt_ffn_dw_kernel)
+    // dpre out: this wave's 64-column block of all 64 rows (128 B per row, 16-byte chunks); null: not stored
 #pragma unroll
     for (int q = 0; q < (a.dpre ? 8 : 0); ++q) {
       const int idx = q * 64 + lane, rr = idx >> 3, cc = idx & 7;

@@ -18,7 +18,7 @@ from __future__ import annotations
 import contextlib
 import math
 import os
-from typing import Dict, Iterable, List, NamedTuple, Optional, Sequence
+from typing import Dict, Iterable, List, Optional, Sequence
 
 import torch
 import torch.nn.functional as F
@@ -99,45 +99,13 @@ def join_side_work():
 
 
 def _flush_deferred():
-    """Issue the queued dW work: FFN weight gradients (tt_ffn_dw, up to 4 blocks per launch) and
-    dW GEMMs as grouped launches of up to 16 problems (stream order)."""
+    """Issue the queued dW GEMMs as grouped launches of up to 16 problems (stream order)."""
     dfr = _SIDE["deferred"]
     if dfr:
         nat, st = native(), _stream()
-        ffn = [it for it in dfr if isinstance(it, _FFNdW)]
-        gemm = [it for it in dfr if not isinstance(it, _FFNdW)]
-        for i in range(0, len(ffn), 4):
-            _ffn_dw(nat, ffn[i:i + 4], st)
-        for i in range(0, len(gemm), 16):
-            _dw_gemm_grouped(nat, gemm[i:i + 16], st)
+        for i in range(0, len(dfr), 16):
+            _dw_gemm_grouped(nat, dfr[i:i + 16], st)
         dfr.clear()
-
-
-class _FFNdW(NamedTuple):
-    """A fused block's FFN weight-gradient work for tt_ffn_dw (the operands it reads, kept alive
-    until issued, and the parameters whose gradients it accumulates)."""
-    a2: torch.Tensor
-    dout16: torch.Tensor
-    w1b: torch.Tensor
-    w2b: torch.Tensor
-    b1c: torch.Tensor
-    w1: torch.Tensor
-    b1: torch.Tensor
-    w2: torch.Tensor
-    b2: torch.Tensor
-
-
-def _ffn_dw(nat, items, st):
-    """dW1 / db1 / dW2 / db2 of up to 4 fused blocks in one launch (csrc/tt_ffn_dw.hip): f and dpre
-    rebuilt from a2 and dout16; returns [(dw1, db1, dw2, db2)] with None for direct grads."""
-    out, probs = [], []
-    for it in items:
-        (dw1, d1), (db1, d2), (dw2, d3), (db2, d4) = [_grad_dst(t, zero=True) for t in (it.w1, it.b1, it.w2, it.b2)]
-        out.append((None if d1 else dw1, None if d2 else db1, None if d3 else dw2, None if d4 else db2))
-        probs.append([t.data_ptr() for t in (it.a2, it.dout16, it.w1b, it.w2b, it.b1c, dw1, dw2, db1, db2)])
-        assert dw1.shape == (256, 64) and dw2.shape == (64, 256) and db1.shape == (256,) and db2.shape == (64,)
-    nat.tt_ffn_dw(probs, items[0].a2.shape[0], st)
-    return out
 
 
 def _w16(w: torch.Tensor) -> torch.Tensor:
@@ -594,10 +562,7 @@ class _TTBlockFn(torch.autograd.Function):
         h1 = torch.empty(M, dm, dtype=f32, device=dev)
         out = torch.empty(B if pooled else M, dm, dtype=f32, device=dev)
         recomp = _TT_FUSED_BWD
-        # with the fused backward and an even batch, f is not stored either: the FFN weight-gradient
-        # kernel rebuilds it from a2 (csrc/tt_ffn_dw.hip, _ffn_dw)
-        ffn_rec = recomp and _TT_FFN_DW and M % 128 == 0
-        f = torch.empty(0 if ffn_rec else M, FF, dtype=bf, device=dev)
+        f = torch.empty(M, FF, dtype=bf, device=dev)
         # with the fused backward the FFN pre-activation is not stored (32 KB per sample written and read
         # back): tt_block_bwd_kernel recomputes it from a2 and W1 (0.3697 -> 0.3632 ms per step,
         # profiles/tt_recompute_pre_ab_r3.log); the unfused backward reads the stored one
@@ -609,8 +574,7 @@ class _TTBlockFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(dm // H)
         if _TT_PROF is not None:  # tools/debug/tt_phase_prof.py
             ptrs.append(_tt_prof_buf("fwd", B, dev))
-        addrs = [0 if (t is pre and recomp) or (t is out and pooled) or (t is h and embed) or (t is f and ffn_rec)
-                 else t.data_ptr()
+        addrs = [0 if (t is pre and recomp) or (t is out and pooled) or (t is h and embed) else t.data_ptr()
                  for t in ptrs]
         if pooled or embed:
             em = [t.data_ptr() for t in (h, eE, ec)] if embed else [0, 0, 0]
@@ -631,7 +595,7 @@ class _TTBlockFn(torch.autograd.Function):
         B, H, T, D, scale = ctx.dims
         if _TT_FUSED_BWD or pre.numel() == 0 or ctx.pooled or ctx.embed:  # no stored pre-activation: fused
             grads, demb = _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, p, B, H,
-                                              T, scale, w1b, pooled=ctx.pooled, embed=ctx.embed, w2b=w2b)
+                                              T, scale, w1b, pooled=ctx.pooled, embed=ctx.embed)
             if ctx.embed:  # h was the feature matrix: no gradient for it, the embedding's for E / c
                 grads = (None,) + tuple(grads[1:])
             return (*grads, None, None, None, None, None, *demb)
@@ -644,9 +608,6 @@ class _TTBlockFn(torch.autograd.Function):
 
 
 _TT_FUSED_BWD = True
-# FFN weight gradients by tt_ffn_dw_kernel from a2 / dout16 (f and dpre never stored); False: the
-# block kernels write f / dpre and the split-K dW GEMMs read them back
-_TT_FFN_DW = False  # measured slower (profiles/tt_ffn_dw_recompute_ab_r5.log); removed in the next commit
 _TT_PROF = None  # {"fwd": [...], "bwd": [...]} of per-workgroup phase timestamp buffers when profiling
 
 
@@ -657,7 +618,7 @@ def _tt_prof_buf(kind: str, B: int, dev) -> torch.Tensor:
 
 
 def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, params, B, H, T, scale,
-                        w1b=None, pooled=False, embed=None, w2b=None):
+                        w1b=None, pooled=False, embed=None):
     """Backward of the fused block: ONE kernel for the whole dX chain (csrc/tt_block.hip
     tt_block_bwd_kernel: dF/gelu', W1, LN2, Wo, attention, Wqkv, LN1 per sample) writing the dZ
     operands of the four dW GEMMs, which then run split-K over all rows with the bias gradients
@@ -669,9 +630,8 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
     M, dm = a1.shape  # (h is the feature matrix [B, T] when `embed` = (E, c): the first block)
     FF = w1.shape[0]
     recomp = pre.numel() == 0
-    ffn_rec = recomp and f.numel() == 0  # the forward did not store f: tt_ffn_dw rebuilds f and dpre
     dev, bf = h.device, torch.bfloat16
-    dpre = torch.empty(0 if ffn_rec else M, FF, dtype=bf, device=dev)
+    dpre = torch.empty(M, FF, dtype=bf, device=dev)
     dh1_16 = torch.empty(M, dm, dtype=bf, device=dev)
     dqkv = torch.empty(M, 3 * dm, dtype=bf, device=dev)
     dh = torch.empty(M, dm, dtype=torch.float32, device=dev)
@@ -686,8 +646,6 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
         dout16 = torch.empty(M, dm, dtype=bf, device=dev)  # bf16(dout), written by the kernel
     if recomp:  # pre-activation recomputed from a2 / W1 / b1 inside the kernel
         addrs[12] = 0
-        if ffn_rec:
-            addrs[14] = 0
         b1c = b1.detach().contiguous()
         addrs += [a2.data_ptr(), w1b.data_ptr(), b1c.data_ptr()]
     if _TT_PROF is not None:
@@ -703,8 +661,6 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
     if not pooled:
         dout16 = _bf16_of(dout)
     items = [(dout16, f, w2, b2), (dpre, a2, w1, b1), (dh1_16, o, wo, bo), (dqkv, a1, wqkv, bqkv)]
-    if ffn_rec:
-        items[:2] = [_FFNdW(a2, dout16, w1b, w2b, b1c, w1, b1, w2, b2)]
     b = _BOUND
     direct = b is not None and all(_is_direct(t) for t in (w2, b2, w1, b1, wo, bo, wqkv, bqkv))
     if direct and b.defer_dw:
@@ -715,11 +671,7 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
             _flush_deferred()
         dw2 = db2 = dw1 = db1 = dwo = dbo = dwqkv = dbqkv = None
     else:
-        if ffn_rec:
-            [(dw1, db1, dw2, db2)] = _ffn_dw(nat, items[:1], st)
-            (dwo, dbo), (dwqkv, dbqkv) = _dw_gemm_grouped(nat, items[1:], st)
-        else:
-            (dw2, db2), (dw1, db1), (dwo, dbo), (dwqkv, dbqkv) = _dw_gemm_grouped(nat, items, st)
+        (dw2, db2), (dw1, db1), (dwo, dbo), (dwqkv, dbqkv) = _dw_gemm_grouped(nat, items, st)
     (dl1w, d1), (dl1b, d2), (dl2w, d3), (dl2b, d4) = lg
     grads = (dh, None if d1 else dl1w, None if d2 else dl1b, dwqkv, dbqkv, dwo, dbo, None if d3 else dl2w,
              None if d4 else dl2b, dw1, db1, dw2, db2)
