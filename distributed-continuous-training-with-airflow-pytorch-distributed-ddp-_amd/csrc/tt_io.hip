@@ -261,6 +261,11 @@ __global__ __launch_bounds__(64 * NW) void head_bwd_kernel(HeadArgs a) {
 // parameter-gradient atomics but measured no faster on the TabTransformer step (0.4195-0.4240 vs
 // 0.4184-0.4221 ms, profiles/tt_head_spb_side_dw_ab_r2.log), nor 2 / 1 (profiles/tt_head_spb_ab_r4.log).
 constexpr int HEAD_SPB = 4;
+// the pooled head (T = 1: the last block handed over the token means) has ~nothing to load per sample;
+// there the same-address parameter-gradient atomics of ceil(B / 4) workgroups dominate the backward:
+// 16 samples per workgroup (a quarter of the adders per address): TT step 0.3412-0.3440 -> 0.3384-0.3392 ms
+// (bench.py alternating on one box, profiles/tt_pooled_head_spb_ab_r5.log)
+constexpr int HEAD_SPB_POOLED = 16;
 
 }  // namespace ttio
 }  // namespace dct
@@ -300,9 +305,12 @@ int dct_tt_head_fwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C,
   a.W = (const float*)p[4]; a.bias = (const float*)p[5]; a.loss = (float*)p[6];
   a.partial = (float*)p[7]; a.ticket = (unsigned*)p[8];
   a.B = B; a.T = T; a.C = C; a.eps = eps;
-  constexpr int nw = dct::ttio::HEAD_SPB;
+  constexpr int nw = dct::ttio::HEAD_SPB, nwp = dct::ttio::HEAD_SPB_POOLED;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(dct::ttio::head_fwd_kernel<nw>, dim3((B + nw - 1) / nw), dim3(64 * nw), 0, st, a);
+  if (T == 1)
+    hipLaunchKernelGGL(dct::ttio::head_fwd_kernel<nwp>, dim3((B + nwp - 1) / nwp), dim3(64 * nwp), 0, st, a);
+  else
+    hipLaunchKernelGGL(dct::ttio::head_fwd_kernel<nw>, dim3((B + nw - 1) / nw), dim3(64 * nw), 0, st, a);
   return (int)hipGetLastError();
 }
 
@@ -317,9 +325,12 @@ int dct_tt_head_bwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C,
   a.dh = (float*)p[7]; a.dh16 = (uint16_t*)p[8]; a.dln_w = (float*)p[9]; a.dln_b = (float*)p[10];
   a.dW = (float*)p[11]; a.dbias = (float*)p[12];
   a.B = B; a.T = T; a.C = C; a.eps = eps;
-  constexpr int nw = dct::ttio::HEAD_SPB;
+  constexpr int nw = dct::ttio::HEAD_SPB, nwp = dct::ttio::HEAD_SPB_POOLED;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(dct::ttio::head_bwd_kernel<nw>, dim3((B + nw - 1) / nw), dim3(64 * nw), 0, st, a);
+  if (T == 1)
+    hipLaunchKernelGGL(dct::ttio::head_bwd_kernel<nwp>, dim3((B + nwp - 1) / nwp), dim3(64 * nwp), 0, st, a);
+  else
+    hipLaunchKernelGGL(dct::ttio::head_bwd_kernel<nw>, dim3((B + nw - 1) / nw), dim3(64 * nw), 0, st, a);
   return (int)hipGetLastError();
 }
 
