@@ -46,7 +46,6 @@ FILE_FLAGS = {"mlp_block3.hip": ["-fno-slp-vectorize"],
               "mlp_block5_xgprof.hip": ["-fno-slp-vectorize"],
               "tt_block.hip": MAX_ILP,
               "tt_io.hip": MAX_ILP,
-              "tt_dw.hip": MAX_ILP,
               "mlp_wave_single.hip": MAX_ILP,
               "mlp_wave_rows_x0.hip": MAX_ILP}
 

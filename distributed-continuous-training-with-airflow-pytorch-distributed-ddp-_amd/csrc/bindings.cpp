@@ -502,25 +502,6 @@ PYBIND11_MODULE(_dct_native, m) {
     check(dct_tt_embed_bwd(P<const float>(x), P<const float>(dh), P<float>(dE), P<float>(dc), B, F, D,
                            reinterpret_cast<void*>(st)), "tt_embed_bwd");
   });
-  m.def("tt_dw",
-        [](std::vector<uintptr_t> a, std::vector<uintptr_t> b, std::vector<uintptr_t> c, std::vector<uintptr_t> colsum,
-           std::vector<int> M, std::vector<int> N, int K, uintptr_t stream, int waves, int wg_per_cu) {
-          const size_t n = a.size();
-          if (b.size() != n || c.size() != n || colsum.size() != n || M.size() != n || N.size() != n)
-            throw std::invalid_argument("tt_dw: list lengths differ");
-          std::vector<const uint16_t*> pa(n), pb(n);
-          std::vector<float*> pc(n), pcs(n);
-          for (size_t i = 0; i < n; ++i) {
-            pa[i] = P<const uint16_t>(a[i]); pb[i] = P<const uint16_t>(b[i]); pc[i] = P<float>(c[i]);
-            pcs[i] = P<float>(colsum[i]);
-          }
-          check(dct_tt_dw((int)n, pa.data(), pb.data(), pc.data(), pcs.data(), M.data(), N.data(), K, waves,
-                          wg_per_cu, reinterpret_cast<void*>(stream)),
-                "tt_dw");
-        },
-        py::arg("a"), py::arg("b"), py::arg("c"), py::arg("colsum"), py::arg("M"),
-        py::arg("N"), py::arg("K"), py::arg("stream"), py::arg("waves") = 8,
-        py::arg("wg_per_cu") = 1);
   m.def("tt_head_fwd", [](std::vector<uintptr_t> p, int B, int T, int D, int C, float eps, uintptr_t st) {
     check(dct_tt_head_fwd(p.data(), (int)p.size(), B, T, D, C, eps, reinterpret_cast<void*>(st)), "tt_head_fwd");
   });

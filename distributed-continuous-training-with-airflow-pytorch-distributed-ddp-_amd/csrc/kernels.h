@@ -127,8 +127,6 @@ int dct_tt_block_bwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, 
                         const float* dpool, uint16_t* dout16, const float* ex, const float* eE, const float* ec,
                         void* stream);
 int dct_tt_embed_fwd(const float* x, const float* E, const float* c, float* h, int B, int F, int Dm, void* stream);
-int dct_tt_dw(int n, const uint16_t* const* A, const uint16_t* const* B, float* const* C, float* const* colsum,
-              const int* M, const int* N, int K, int waves, int wg_per_cu, void* stream);
 int dct_tt_embed_bwd(const float* x, const float* dh, float* dE, float* dc, int B, int F, int Dm, void* stream);
 int dct_tt_head_fwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C, float eps, void* stream);
 int dct_tt_head_bwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C, float eps, void* stream);

@@ -211,21 +211,10 @@ def _dw_gemm_grouped(nat, items, st):
         dws.append(dw)
         dbs.append(db)
         out.append((None if dw_direct else dw, None if db_direct else db))
-    Ms, Ns = [it[0].shape[1] for it in items], [it[1].shape[1] for it in items]
-    if _TT_DW and rows % 64 == 0 and all((m, n) in _TT_DW_SHAPES for m, n in zip(Ms, Ns)) and \
-            all(it[0].data_ptr() % 16 == 0 and it[1].data_ptr() % 16 == 0 for it in items):
-        # the transformer block's four products as whole-problem tiles (csrc/tt_dw.hip)
-        nat.tt_dw([it[0].data_ptr() for it in items], [it[1].data_ptr() for it in items],
-                  [d.data_ptr() for d in dws], [d.data_ptr() for d in dbs], Ms, Ns, rows, st)
-        return out
     nat.gemm_bf16_dw_grouped([it[0].data_ptr() for it in items], [it[1].data_ptr() for it in items],
-                             [d.data_ptr() for d in dws], Ms, Ns, rows, [d.data_ptr() for d in dbs], 1, st)
+                             [d.data_ptr() for d in dws], [it[0].shape[1] for it in items],
+                             [it[1].shape[1] for it in items], rows, [d.data_ptr() for d in dbs], 1, st)
     return out
-
-
-# (dZ columns, X columns) of the fused TabTransformer block's dW products tt_dw tiles whole
-_TT_DW_SHAPES = ((64, 256), (256, 64), (64, 64), (192, 64))
-_TT_DW = False  # measured slower (profiles/tt_dw_whole_tiles_ab_r5.log); removed in the next commit
 
 
 def _mm(nat, a16, b16, M, N, K, st, epi=0, aux=None, out=None):

@@ -924,31 +924,6 @@ def test_tt_block_fused_matches_fp32_reference_and_unfused(cuda, B, monkeypatch)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("K,blocks", [(64, 1), (4096, 2), (32768, 4)])
-def test_tt_dw_matches_fp32_reference(cuda, K, blocks):
-    """csrc/tt_dw.hip: the fused block's four weight-gradient products (64x256, 256x64, 64x64, 192x64)
-    of several blocks in one launch, accumulated into non-zero C with the bias column sums, against
-    fp32 torch on the same bf16 operands."""
-    nat = native()
-    st = torch.cuda.current_stream().cuda_stream
-    g = torch.Generator(device="cpu").manual_seed(K + blocks)
-    shapes = [(64, 256), (256, 64), (64, 64), (192, 64)] * blocks
-    A = [torch.randn(K, m, generator=g).to(torch.bfloat16).to(cuda) for m, _ in shapes]
-    B = [torch.randn(K, n, generator=g).to(torch.bfloat16).to(cuda) for _, n in shapes]
-    C0 = [torch.randn(m, n, generator=g).to(cuda) for m, n in shapes]
-    S0 = [torch.randn(m, generator=g).to(cuda) for m, _ in shapes]
-    C, S = [c.clone() for c in C0], [s_.clone() for s_ in S0]
-    nat.tt_dw([a.data_ptr() for a in A], [b.data_ptr() for b in B], [c.data_ptr() for c in C],
-              [s_.data_ptr() for s_ in S], [m for m, _ in shapes], [n for _, n in shapes], K, st)
-    torch.cuda.synchronize()
-    for i in range(len(shapes)):
-        ref = C0[i] + A[i].float().t() @ B[i].float()
-        assert torch.allclose(C[i], ref, rtol=1e-4, atol=1e-3 * ref.abs().max()), (i, float((C[i] - ref).abs().max()))
-        rs = S0[i] + A[i].float().sum(0)
-        assert torch.allclose(S[i], rs, rtol=1e-4, atol=1e-3 * rs.abs().max()), i
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("B,C", [(1, 2), (37, 2), (512, 2), (64, 5)])
 def test_tt_embed_and_head_loss_match_fp32_reference(cuda, B, C):
     """csrc/tt_io.hip: feature-token embedding fwd/bwd and the pooled LN -> Linear -> mean-CE head
