@@ -15,6 +15,7 @@ dispatches are counted too). Derived columns:
           bound, counter collection stretches the kernels)
   ldsc%   SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE  (extra cycles lost to bank conflicts)
   GB/s    2 * FETCH_SIZE (KB) / kernel time  (gfx950 FETCH_SIZE counts half of a wide read)
+  V/M     SQ_INSTS_VALU / SQ_INSTS_MFMA (instruction-mix pass, tools/pmc_tt_insts.sh)
 Kernel time comes from the same run's trace, which counter collection serialises, so it is an
 upper bound; use the --stats profiles in profiles/ for timing.
 """
@@ -44,7 +45,7 @@ def main():
         dur[r["Kernel_Name"]] += (float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
         calls[r["Kernel_Name"]] += 1
     names = sorted(set(ctr) | set(dur), key=lambda n: -dur.get(n, 0.0))[:top]
-    print(f"{'us/step':>9} {'calls':>6} {'mfma%':>6} {'GF/st':>7} {'TF/s':>7} {'ldsc%':>6} {'GB/s':>7}  kernel")
+    print(f"{'us/step':>9} {'calls':>6} {'mfma%':>6} {'GF/st':>7} {'TF/s':>7} {'ldsc%':>6} {'GB/s':>7} {'V/M':>6}  kernel")
     for n in names:
         c = ctr.get(n, {})
         t_ns = dur.get(n, 0.0)
@@ -57,7 +58,9 @@ def main():
         ldsc = f"{100 * bc / la:6.1f}" if bc is not None and la else "     -"
         fs = c.get("FETCH_SIZE")
         bw = f"{2 * fs * 1024 / t_ns:7.0f}" if fs is not None and t_ns else "      -"
-        print(f"{t_ns / 1e3 / steps:9.1f} {calls[n] / steps:6.1f} {mfma} {gf} {tf} {ldsc} {bw}  {n[:100]}")
+        va, mi = c.get("SQ_INSTS_VALU"), c.get("SQ_INSTS_MFMA")
+        vm = f"{va / mi:6.1f}" if va is not None and mi else "     -"
+        print(f"{t_ns / 1e3 / steps:9.1f} {calls[n] / steps:6.1f} {mfma} {gf} {tf} {ldsc} {bw} {vm}  {n[:100]}")
 
 
 if __name__ == "__main__":
