@@ -501,9 +501,18 @@ struct BwdArgs {
   const float* dpool;  // optional [B][DM]: the gradient of the token mean (pool) instead of dout rows;
   uint16_t* dout16;    // then bf16(dout) [M][DM] is written here for the W2 gradient GEMM
   float *dln1_w, *dln1_b, *dln2_w, *dln2_b;
+  // optional: LN_REP replicas of the four LayerNorm gradient vectors [LN_REP][4][DM] and a ticket, both
+  // zero between launches (the last workgroup folds the replicas into dln* and re-zeroes them)
+  float* lnrep; unsigned* ticket;
   uint64_t* prof;
   float scale;
 };
+// The LayerNorm parameter gradients are per-workgroup column sums added into the same 4 x 64 floats
+// by every workgroup: 512 adders on one 1 KB row run the memory-side float atomics ~14x below their
+// rate (MI355X_MICROARCH.md 'Global float atomics', contention) - a ~5 us tail on every backward
+// block kernel.  Workgroup b adds into replica b % LN_REP instead (32 adders per address at batch
+// 512), and the workgroup that finishes last folds the replicas.
+constexpr int LN_REP = 16;
 
 constexpr int XB_LD = DM + 8;  // bf16 rows (144 B)
 constexpr int G_BYTES = T * HS_LD * 4;
@@ -968,9 +977,27 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
   }
   store_rows16<DM * 4, HS_LD * 4>(a.dh + (size_t)row0 * DM, G, wv, lane);
   __syncthreads();
-  {  // LayerNorm parameter gradients: one atomic per column per workgroup
-    float* dsts[4] = {a.dln1_w, a.dln1_b, a.dln2_w, a.dln2_b};
+  float* dsts[4] = {a.dln1_w, a.dln1_b, a.dln2_w, a.dln2_b};
+  if (!a.lnrep) {  // LayerNorm parameter gradients: one atomic per column per workgroup
     atomicAdd(dsts[threadIdx.x >> 6] + (threadIdx.x & 63), red[threadIdx.x]);
+  } else {
+    atomicAdd(a.lnrep + (blockIdx.x % LN_REP) * 4 * DM + threadIdx.x, red[threadIdx.x]);
+    // the add has been performed (float atomics execute at the memory side, so completion is all the
+    // ordering the fold needs - an agent-scope release fence here would write back the XCD's L2 in every
+    // workgroup: 0.339 -> 0.556 ms per TabTransformer step)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // (every read of red is done: red[0] carries the verdict; no static LDS in this kernel)
+    if (threadIdx.x == 0)
+      red[0] = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1
+                   ? 1.f : 0.f;
+    __syncthreads();
+    if (red[0] != 0.f) {  // every other workgroup's adds are done: fold (read-and-zero at the memory side)
+      float v = 0.f;
+#pragma unroll
+      for (int r = 0; r < LN_REP; ++r) v += atomicExch(a.lnrep + r * 4 * DM + threadIdx.x, 0.f);
+      atomicAdd(dsts[threadIdx.x >> 6] + (threadIdx.x & 63), v);
+      if (threadIdx.x == 0) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   TT_MARK(8);
 }
@@ -1039,9 +1066,11 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
 // dpool (optional): the head's gradient of the last block's token mean instead of dout (p[0] may then be
 // null); bf16(dout) is then written to dout16 ([B*T][DM]) for the W2 gradient GEMM
 // ex / eE / ec (optional): the block input is embedded from the features (h p[1] and dh16 p[18] may be null)
+// lnrep / ticket (optional, together): zeroed [16][4][DM] floats + a zeroed uint32 the launch leaves zeroed
+// (LayerNorm gradients through replicas, see LN_REP); null: direct atomics
 int dct_tt_block_bwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
                         const float* dpool, uint16_t* dout16, const float* ex, const float* eE, const float* ec,
-                        void* stream) {
+                        float* lnrep, unsigned* ticket, void* stream) {
   using namespace dct::ttb;
   // 23 (+1 prof) pointers; 26 (+1 prof): + a2, w1 (bf16 [FF][DM]), b1 - with pre (p[12]) null the
   // kernel recomputes the pre-activation from them
@@ -1076,6 +1105,9 @@ int dct_tt_block_bwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, 
   a.dout16 = dpool ? dout16 : nullptr;
   if (ex && (!eE || !ec || ((((uintptr_t)eE) | ((uintptr_t)ec)) & 15))) return (int)hipErrorInvalidValue;
   a.em = Embed{ex, eE, ec};
+  if ((lnrep == nullptr) != (ticket == nullptr)) return (int)hipErrorInvalidValue;
+  a.lnrep = lnrep;
+  a.ticket = ticket;
   static bool attr = false;
   if (!attr) {
     for (const void* k : {(const void*)tt_block_bwd_kernel<false>, (const void*)tt_block_bwd_kernel<true>}) {
@@ -1093,7 +1125,8 @@ int dct_tt_block_bwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, 
 
 int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
                      void* stream) {
-  return dct_tt_block_bwd_ex(p, n_ptrs, Bsz, T, DM, H, FF, scale, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
+  return dct_tt_block_bwd_ex(p, n_ptrs, Bsz, T, DM, H, FF, scale, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                             nullptr, stream);
 }
 
 }  // extern "C"

@@ -617,6 +617,21 @@ def _tt_prof_buf(kind: str, B: int, dev) -> torch.Tensor:
     return buf
 
 
+_TT_LN_REP = True
+_TT_LN_WS: Dict[int, torch.Tensor] = {}
+
+
+def _tt_ln_ws(device: torch.device) -> torch.Tensor:
+    """Persistent zeroed workspace of the fused block backward's LayerNorm-gradient replicas:
+    16 x 4 x 64 floats + a uint32 ticket (element 4096), left zeroed by every launch.  One
+    per device: the block backward kernels of a step run in stream order."""
+    ws = _TT_LN_WS.get(device.index)
+    if ws is None:
+        ws = torch.zeros(16 * 4 * 64 + 4, dtype=torch.float32, device=device)
+        _TT_LN_WS[device.index] = ws
+    return ws
+
+
 def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, params, B, H, T, scale,
                         w1b=None, pooled=False, embed=None):
     """Backward of the fused block: ONE kernel for the whole dX chain (csrc/tt_block.hip
@@ -652,12 +667,11 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
         addrs.append(_tt_prof_buf("bwd", B, dev).data_ptr())
     if embed is not None:
         addrs[1] = addrs[18] = 0  # the block input is recomputed from x, E, c; no bf16 dh consumer
-    if pooled or embed is not None:
-        em = [t.data_ptr() for t in (h, *embed)] if embed is not None else [0, 0, 0]
-        nat.tt_block_bwd_ex(addrs, B, T, dm, H, FF, scale, dout.data_ptr() if pooled else 0,
-                            dout16.data_ptr() if pooled else 0, *em, st)
-    else:
-        nat.tt_block_bwd(addrs, B, T, dm, H, FF, scale, st)
+    em = [t.data_ptr() for t in (h, *embed)] if embed is not None else [0, 0, 0]
+    ws = _tt_ln_ws(dev) if _TT_LN_REP else None  # LayerNorm gradients through replicas (csrc LN_REP)
+    nat.tt_block_bwd_ex(addrs, B, T, dm, H, FF, scale, dout.data_ptr() if pooled else 0,
+                        dout16.data_ptr() if pooled else 0, *em,
+                        ws.data_ptr() if ws is not None else 0, ws[4096:].data_ptr() if ws is not None else 0, st)
     if not pooled:
         dout16 = _bf16_of(dout)
     items = [(dout16, f, w2, b2), (dpre, a2, w1, b1), (dh1_16, o, wo, bo), (dqkv, a1, wqkv, bqkv)]
