@@ -161,17 +161,20 @@ __global__ __launch_bounds__(64 * NW) void head_fwd_kernel(HeadArgs a) {
     float v = 0.f;
 #pragma unroll
     for (int i = 0; i < NW; ++i) v += lsum[i];
-    __hip_atomic_store(a.partial + blockIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    // partial and ticket as memory-side atomics, ordered by waiting for the first to complete: no
+    // agent-scope release / acquire fences (each writes back / invalidates the XCD's L2 - see the LN
+    // replicas of tt_block.hip), and the last block reads the partials by atomics too (an L2 of
+    // another XCD may hold a stale line of them)
+    atomicExch(a.partial + blockIdx.x, v);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   }
   __syncthreads();
   if (last && threadIdx.x < 64) {
     // wave 0 sums the partials: lane-strided loads all in flight at once, then the butterfly (a fixed
     // order, so the loss is bit-identical run to run); a one-thread serial sum cost ~18 us per step
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     float s = 0.f;
-    for (unsigned i = threadIdx.x; i < gridDim.x; i += 64)
-      s += __hip_atomic_load(a.partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (unsigned i = threadIdx.x; i < gridDim.x; i += 64) s += atomicAdd(a.partial + i, 0.f);
     s = wsum(s);
     if (threadIdx.x == 0) {
       a.loss[0] = s;

@@ -1,3 +1,4 @@
 set -e
 export TMPDIR=/tmp
-bash tools/gpu.sh r5_g37 "python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k 'tt_'" "python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_tabtransformer.py tests/test_determinism_gpu.py tests/test_ddp_reducer_gpu.py" "python tools/tt_pooled_head_ab.py nn._TT_LN_REP"
+B="python bench.py --model tabtransformer --steps 600 --warmup 100 --no-reference-model"
+bash tools/gpu.sh r5_g38 "python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k 'tt_embed_and_head or head_loss'" "DCT_AB_HEADFENCE=1 $B" "$B" "DCT_AB_HEADFENCE=1 $B" "$B" "DCT_AB_HEADFENCE=1 $B" "$B"
