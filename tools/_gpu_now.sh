@@ -1,4 +1,3 @@
 set -e
 export TMPDIR=/tmp
-B="python bench.py --model tabtransformer --steps 600 --warmup 100 --no-reference-model"
-bash tools/gpu.sh r5_g43 "$B" "DCT_AB_DWCAP=8 $B" "DCT_AB_DWCAP=16 $B" "$B" "DCT_AB_DWCAP=8 $B" "DCT_AB_DWCAP=16 $B"
+bash tools/gpu.sh r5_g44 "python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k 'tt_embed_and_head or head_loss'" "python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_tabtransformer.py" "python tools/tt_pooled_head_ab.py native.tt_head_pooled_mode"

@@ -27,8 +27,12 @@ FLAG = sys.argv[1] if len(sys.argv) > 1 else "POOLED_HEAD"
 
 def make(ctx, X, Y, pooled):
     from dct_amd.ops import nn as nnops
-    # "nn.NAME": a switch of ops/nn.py instead (e.g. nn._WHATIF, a timing probe)
-    setattr(nnops if FLAG.startswith("nn.") else ttm, FLAG[3:] if FLAG.startswith("nn.") else FLAG, pooled)
+    from dct_amd.ops._native import native
+    # "nn.NAME": a switch of ops/nn.py instead; "native.NAME": a native setter taking 0 / 1
+    if FLAG.startswith("native."):
+        getattr(native(), FLAG[7:])(int(pooled))
+    else:
+        setattr(nnops if FLAG.startswith("nn.") else ttm, FLAG[3:] if FLAG.startswith("nn.") else FLAG, pooled)
     torch.manual_seed(0)
     model = build_model("tabtransformer", 64, d_model=64, heads=4, layers=4, lr=1e-3)
     eng = AutogradEngine(model, ctx, 512, seed=42)
