@@ -489,10 +489,11 @@ PYBIND11_MODULE(_dct_native, m) {
       "tt_block_bwd_ex",
       [](std::vector<uintptr_t> ptrs, int Bsz, int T, int DM, int H, int FF, float scale, uintptr_t dpool,
          uintptr_t dout16, uintptr_t ex, uintptr_t eE, uintptr_t ec, uintptr_t lnrep, uintptr_t ticket,
-         uintptr_t stream) {
+         uintptr_t a1, uintptr_t wqkv, uintptr_t bqkv, uintptr_t stream) {
         check(dct_tt_block_bwd_ex(ptrs.data(), (int)ptrs.size(), Bsz, T, DM, H, FF, scale, P<const float>(dpool),
                                   P<uint16_t>(dout16), P<const float>(ex), P<const float>(eE), P<const float>(ec),
-                                  P<float>(lnrep), P<unsigned>(ticket), reinterpret_cast<void*>(stream)),
+                                  P<float>(lnrep), P<unsigned>(ticket), P<const uint16_t>(a1),
+                                  P<const uint16_t>(wqkv), P<const float>(bqkv), reinterpret_cast<void*>(stream)),
               "tt_block_bwd_ex");
       });
   m.def("tt_embed_fwd", [](uintptr_t x, uintptr_t E, uintptr_t c, uintptr_t h, int B, int F, int D, uintptr_t st) {

@@ -125,7 +125,8 @@ int dct_tt_block_fwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, 
                         float scale, float* pool, const float* ex, const float* eE, const float* ec, void* stream);
 int dct_tt_block_bwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
                         const float* dpool, uint16_t* dout16, const float* ex, const float* eE, const float* ec,
-                        float* lnrep, unsigned* ticket, void* stream);
+                        float* lnrep, unsigned* ticket, const uint16_t* a1, const uint16_t* wqkv,
+                        const float* bqkv, void* stream);
 int dct_tt_embed_fwd(const float* x, const float* E, const float* c, float* h, int B, int F, int Dm, void* stream);
 int dct_tt_embed_bwd(const float* x, const float* dh, float* dE, float* dc, int B, int F, int Dm, void* stream);
 int dct_tt_head_fwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C, float eps, void* stream);

@@ -289,7 +289,8 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
 
   TT_MARK(2);
   // ---- P3: qkv out; attention of head wv over the 64 tokens (S^T = K Q^T; P V)
-  if (a.save) store_tile<3 * DM * 2, QKV_LD * 2>(a.qkv + (size_t)row0 * 3 * DM, RS);
+  if (a.save && a.qkv)  // null: the fused backward recomputes q, k, v from a1 (BwdArgs::wqkv)
+    store_tile<3 * DM * 2, QKV_LD * 2>(a.qkv + (size_t)row0 * 3 * DM, RS);
   {
     const uint16_t* Qs = RS + DH * wv;
     const uint16_t* Ks = RS + DM + DH * wv;
@@ -504,6 +505,8 @@ struct BwdArgs {
   // optional: LN_REP replicas of the four LayerNorm gradient vectors [LN_REP][4][DM] and a ticket, both
   // zero between launches (the last workgroup folds the replicas into dln* and re-zeroes them)
   float* lnrep; unsigned* ticket;
+  // optional: with qkv null, q / k / v are recomputed from a1 by the forward's QKV MFMAs (bit-identical)
+  const uint16_t* a1; const uint16_t* wqkv; const float* bqkv;
   uint64_t* prof;
   float scale;
 };
@@ -820,10 +823,44 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
   __syncthreads();  // every wave is done with R (dpre) and has written its dO columns
 
   TT_MARK(4);
-  // ---- P5: qkv -> R, o -> Os
-  load_tile<3 * DM * 2, QKV_LD * 2>(R, a.qkv + (size_t)row0 * 3 * DM);
+  // ---- P5: qkv -> R (or a1 -> X and the forward's QKV GEMM), o -> Os
+  if (a.qkv) load_tile<3 * DM * 2, QKV_LD * 2>(R, a.qkv + (size_t)row0 * 3 * DM);
+  else load_tile<DM * 2, XB_LD * 2>(X, a.a1 + (size_t)row0 * DM);  // X is free until P7
   load_tile<DM * 2, XB_LD * 2>(Os, a.o + (size_t)row0 * DM);
   __syncthreads();
+  if (!a.qkv) {
+    // the forward's P2 for head wv - same operands (a1 as the forward staged it), k order and
+    // rounding, so q, k, v are bit-identical to the ones it no longer stores (12 MB written and 12 MB
+    // read back per block at batch 512)
+    f32x4 acc[3][4];
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[t][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < DM / 32; ++ks) {
+      bf16x8 bw[3], af[4];
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+        bw[t] = *reinterpret_cast<const bf16x8*>(a.wqkv + (size_t)(t * DM + DH * wv + c) * DM + 32 * ks + 8 * g);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(X + (16 * i + c) * XB_LD + 32 * ks + 8 * g);
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[t][i] = mfma32(af[i], bw[t], acc[t][i]);
+    }
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int col = t * DM + DH * wv + c;
+      const float bv = a.bqkv[col];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) R[(16 * i + 4 * g + r) * QKV_LD + col] = f32_to_bf16(acc[t][i][r] + bv);
+    }
+    __syncthreads();
+  }
 
   TT_MARK(5);
   // ---- P6: attention backward of head wv; dq, dk, dv overwrite q, k, v of the head in R
@@ -1021,7 +1058,7 @@ int dct_tt_block_fwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, 
   const bool save = p[13] != 0;
   uintptr_t any = 0;
   for (int i = 0; i < 27; ++i) {
-    const bool needed = (i < 13 || (i == 25 && !pool) || save) && i != 24 && i != 23 && !(i == 25 && pool) &&
+    const bool needed = (i < 13 || (i == 25 && !pool) || save) && i != 24 && i != 23 && i != 16 && !(i == 25 && pool) &&
                         !(i == 0 && ex);
     if (needed && !p[i]) return (int)hipErrorInvalidValue;
     any |= p[i];
@@ -1068,9 +1105,12 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
 // ex / eE / ec (optional): the block input is embedded from the features (h p[1] and dh16 p[18] may be null)
 // lnrep / ticket (optional, together): zeroed [16][4][DM] floats + a zeroed uint32 the launch leaves zeroed
 // (LayerNorm gradients through replicas, see LN_REP); null: direct atomics
+// a1 / wqkv / bqkv (optional): with qkv (p[5]) null, q / k / v are recomputed from a1 [B*T][DM] bf16, the
+// bf16 Wqkv [3DM][DM] and bqkv fp32, bit-identical to the forward's
 int dct_tt_block_bwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
                         const float* dpool, uint16_t* dout16, const float* ex, const float* eE, const float* ec,
-                        float* lnrep, unsigned* ticket, void* stream) {
+                        float* lnrep, unsigned* ticket, const uint16_t* a1, const uint16_t* wqkv,
+                        const float* bqkv, void* stream) {
   using namespace dct::ttb;
   // 23 (+1 prof) pointers; 26 (+1 prof): + a2, w1 (bf16 [FF][DM]), b1 - with pre (p[12]) null the
   // kernel recomputes the pre-activation from them
@@ -1082,7 +1122,7 @@ int dct_tt_block_bwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, 
   uintptr_t any = 0;
   for (int i = 0; i < (ext ? 26 : 23); ++i) {
     if (!p[i] && !(i == 12 && recomp) && !(i >= 23 && !recomp) && !(i == 0 && dpool) && !((i == 1 || i == 18) && ex) &&
-        !(i == 14 && recomp))
+        !(i == 14 && recomp) && !(i == 5 && a1))
       return (int)hipErrorInvalidValue;
     if (i < 19 || i >= 23) any |= p[i];
   }
@@ -1108,6 +1148,10 @@ int dct_tt_block_bwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, 
   if ((lnrep == nullptr) != (ticket == nullptr)) return (int)hipErrorInvalidValue;
   a.lnrep = lnrep;
   a.ticket = ticket;
+  if (!p[5] && (!a1 || !wqkv || !bqkv || ((((uintptr_t)a1) | ((uintptr_t)wqkv)) & 15))) return (int)hipErrorInvalidValue;
+  a.a1 = p[5] ? nullptr : a1;
+  a.wqkv = p[5] ? nullptr : wqkv;
+  a.bqkv = p[5] ? nullptr : bqkv;
   static bool attr = false;
   if (!attr) {
     for (const void* k : {(const void*)tt_block_bwd_kernel<false>, (const void*)tt_block_bwd_kernel<true>}) {
@@ -1126,7 +1170,7 @@ int dct_tt_block_bwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, 
 int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
                      void* stream) {
   return dct_tt_block_bwd_ex(p, n_ptrs, Bsz, T, DM, H, FF, scale, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                             nullptr, stream);
+                             nullptr, nullptr, nullptr, nullptr, stream);
 }
 
 }  // extern "C"

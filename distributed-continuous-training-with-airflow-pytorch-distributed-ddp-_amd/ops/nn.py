@@ -554,7 +554,9 @@ class _TTBlockFn(torch.autograd.Function):
         bf, f32 = torch.bfloat16, torch.float32
         a1, a2 = torch.empty(M, dm, dtype=bf, device=dev), torch.empty(M, dm, dtype=bf, device=dev)
         st4 = torch.empty(4, M, dtype=f32, device=dev)  # mean1, rstd1, mean2, rstd2
-        qkv = torch.empty(M, 3 * dm, dtype=bf, device=dev)
+        # with the fused backward q / k / v are not stored either: tt_block_bwd_kernel recomputes them
+        # from a1 with the forward's own MFMAs (bit-identical; 12 MB written and read back per block)
+        qkv = torch.empty(0 if _TT_FUSED_BWD and _TT_QKV_RECOMP else M, 3 * dm, dtype=bf, device=dev)
         o = torch.empty(M, dm, dtype=bf, device=dev)
         lse = torch.empty(B * H * T, dtype=f32, device=dev)
         # pooled (the model's last block, training): the kernel writes the token mean [B, dm] the classifier
@@ -574,8 +576,8 @@ class _TTBlockFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(dm // H)
         if _TT_PROF is not None:  # tools/debug/tt_phase_prof.py
             ptrs.append(_tt_prof_buf("fwd", B, dev))
-        addrs = [0 if (t is pre and recomp) or (t is out and pooled) or (t is h and embed) else t.data_ptr()
-                 for t in ptrs]
+        addrs = [0 if (t is pre and recomp) or (t is out and pooled) or (t is h and embed) or t.numel() == 0
+                 else t.data_ptr() for t in ptrs]
         if pooled or embed:
             em = [t.data_ptr() for t in (h, eE, ec)] if embed else [0, 0, 0]
             nat.tt_block_fwd_ex(addrs, B, T, dm, H, FF, float(eps), scale, out.data_ptr() if pooled else 0, *em, st)
@@ -595,7 +597,7 @@ class _TTBlockFn(torch.autograd.Function):
         B, H, T, D, scale = ctx.dims
         if _TT_FUSED_BWD or pre.numel() == 0 or ctx.pooled or ctx.embed:  # no stored pre-activation: fused
             grads, demb = _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, p, B, H,
-                                              T, scale, w1b, pooled=ctx.pooled, embed=ctx.embed)
+                                              T, scale, w1b, pooled=ctx.pooled, embed=ctx.embed, wqkvb=wqkvb)
             if ctx.embed:  # h was the feature matrix: no gradient for it, the embedding's for E / c
                 grads = (None,) + tuple(grads[1:])
             return (*grads, None, None, None, None, None, *demb)
@@ -618,6 +620,7 @@ def _tt_prof_buf(kind: str, B: int, dev) -> torch.Tensor:
 
 
 _TT_LN_REP = True
+_TT_QKV_RECOMP = True
 _TT_LN_WS: Dict[int, torch.Tensor] = {}
 
 
@@ -633,7 +636,7 @@ def _tt_ln_ws(device: torch.device) -> torch.Tensor:
 
 
 def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w, ln2w, params, B, H, T, scale,
-                        w1b=None, pooled=False, embed=None):
+                        w1b=None, pooled=False, embed=None, wqkvb=None):
     """Backward of the fused block: ONE kernel for the whole dX chain (csrc/tt_block.hip
     tt_block_bwd_kernel: dF/gelu', W1, LN2, Wo, attention, Wqkv, LN1 per sample) writing the dZ
     operands of the four dW GEMMs, which then run split-K over all rows with the bias gradients
@@ -669,9 +672,15 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
         addrs[1] = addrs[18] = 0  # the block input is recomputed from x, E, c; no bf16 dh consumer
     em = [t.data_ptr() for t in (h, *embed)] if embed is not None else [0, 0, 0]
     ws = _tt_ln_ws(dev) if _TT_LN_REP else None  # LayerNorm gradients through replicas (csrc LN_REP)
+    qr = [0, 0, 0]
+    if qkv.numel() == 0:  # q / k / v recomputed from a1 (the forward did not store them)
+        bq = bqkv.detach().contiguous()
+        qr = [a1.data_ptr(), wqkvb.data_ptr(), bq.data_ptr()]
+        addrs[5] = 0
     nat.tt_block_bwd_ex(addrs, B, T, dm, H, FF, scale, dout.data_ptr() if pooled else 0,
                         dout16.data_ptr() if pooled else 0, *em,
-                        ws.data_ptr() if ws is not None else 0, ws[4096:].data_ptr() if ws is not None else 0, st)
+                        ws.data_ptr() if ws is not None else 0, ws[4096:].data_ptr() if ws is not None else 0, *qr,
+                        st)
     if not pooled:
         dout16 = _bf16_of(dout)
     items = [(dout16, f, w2, b2), (dpre, a2, w1, b1), (dh1_16, o, wo, bo), (dqkv, a1, wqkv, bqkv)]
