@@ -135,7 +135,10 @@ def test_multi_process_ipc_exchange(W, tmp_path, cuda):
     the exchange width of a full MI355X node, XW = 8 kernel variant)."""
     out = tmp_path / "xg.json"
     steps, B = 80, 4
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    # one hardware queue per worker: W processes x GPU_MAX_HW_QUEUES (4) + this process's queues can exceed
+    # the device's compute queue slots at W = 8, and a spinning rank whose peer's queue is not mapped
+    # then times out (seen once at W = 8: status 2); on a real node every rank has a GPU of its own
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", GPU_MAX_HW_QUEUES="1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={W}",
                         "--master-addr=127.0.0.1", f"--master-port={29561 + W}",
                         os.path.join(ROOT, "tests", "xg_worker.py"), str(out), str(steps), str(B)],
