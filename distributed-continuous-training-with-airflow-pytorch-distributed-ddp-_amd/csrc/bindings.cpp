@@ -527,6 +527,26 @@ PYBIND11_MODULE(_dct_native, m) {
                                          reinterpret_cast<void*>(stream)),
                 "gemm_bf16_dw_grouped");
         });
+  m.def("gemm_bf16_dw_grouped_embed",
+        [](std::vector<uintptr_t> dz, std::vector<uintptr_t> x, std::vector<uintptr_t> c, std::vector<int> M,
+           std::vector<int> N, int K, std::vector<uintptr_t> colsum, int accumulate, uintptr_t ex, uintptr_t edh,
+           uintptr_t edE, uintptr_t edc, int eB, int eF, uintptr_t stream) {
+          const size_t n = dz.size();
+          if (x.size() != n || c.size() != n || M.size() != n || N.size() != n || colsum.size() != n)
+            throw std::invalid_argument("gemm_bf16_dw_grouped_embed: list lengths differ");
+          std::vector<const uint16_t*> pz(n), px(n);
+          std::vector<float*> pc(n), pcs(n);
+          for (size_t i = 0; i < n; ++i) {
+            pz[i] = P<const uint16_t>(dz[i]); px[i] = P<const uint16_t>(x[i]); pc[i] = P<float>(c[i]);
+            pcs[i] = P<float>(colsum[i]);
+          }
+          const int r = dct_gemm_bf16_dw_grouped_embed((int)n, pz.data(), px.data(), pc.data(), M.data(), N.data(), K,
+                                                       pcs.data(), accumulate, P<const float>(ex),
+                                                       P<const float>(edh), P<float>(edE), P<float>(edc), eB, eF,
+                                                       reinterpret_cast<void*>(stream));
+          if (r != 0 && r != 1) check(r, "gemm_bf16_dw_grouped_embed");
+          return r == 0;  // True: the embedding gradients rode in the launch
+        });
   m.def(
       "attention_bwd",
       [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t dout, uintptr_t lse, uintptr_t dq, uintptr_t dk,

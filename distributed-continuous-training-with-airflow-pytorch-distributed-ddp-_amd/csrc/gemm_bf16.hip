@@ -584,16 +584,54 @@ __global__ __launch_bounds__(128 * WM, WM == 4 ? 2 : (BM == 64 ? 4 : 2)) void ge
 // block, or of every block when the backward defers them to its end) in ONE grid, so the
 // per-launch fixed cost (ramp, first-load latency, tail) is paid once.
 constexpr int DW_GROUP = 16;
+// Optional work riding in a grouped dW launch: the TabTransformer feature-token embedding's parameter
+// gradients (csrc/tt_io.hip embed_bwd_kernel) - batch sums over the first block's dh, which the
+// autograd order puts right before this launch.  One extra workgroup per feature (F of them fit the
+// slots the GEMM grid leaves free: 448 of 512 at the bench shape), 8 sample slots x 64 dimensions,
+// one writer per gradient element (no atomics): the separate kernel and its boundary go away.
+struct EmbedRide {
+  const float* x;   // [B][F] features (null: no ride)
+  const float* dh;  // [B][F][64]
+  float* dE; float* dc;  // [F][64], accumulated
+  int B, F;
+};
 struct GemmGroup {
   GemmArgs g[DW_GROUP];
   int splits[DW_GROUP];
   int start[DW_GROUP + 1];  // first work id of each problem; start[n] = total
   int n;
+  EmbedRide er;
 };
+
+__device__ __forceinline__ void embed_ride(const EmbedRide& e, int f, float* sm) {
+  const int s = threadIdx.x >> 6, d = threadIdx.x & 63, ns = blockDim.x >> 6;
+  float aw = 0.f, ab = 0.f;
+  for (int b = s; b < e.B; b += ns) {
+    const size_t tok = (size_t)b * e.F + f;
+    const float g = e.dh[tok * 64 + d];
+    aw = fmaf(e.x[tok], g, aw);
+    ab += g;
+  }
+  sm[s * 64 + d] = aw;
+  sm[(ns + s) * 64 + d] = ab;
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const int which = threadIdx.x >> 6;
+    float v = 0.f;
+    for (int q = 0; q < ns; ++q) v += sm[(which * ns + q) * 64 + d];
+    float* dst = (which ? e.dc : e.dE) + (size_t)f * 64 + d;
+    *dst += v;
+  }
+}
 
 template <bool TA, bool TB, int S, int WM = 2>
 __global__ __launch_bounds__(128 * WM, 2) void gemm2_grouped_kernel(GemmGroup gg) {
   const int w = xcd_wgid();
+  if (gg.er.x && w >= gg.start[gg.n]) {  // riding embedding-gradient workgroup
+    extern __shared__ __attribute__((aligned(16))) char smem_er[];
+    embed_ride(gg.er, w - gg.start[gg.n], reinterpret_cast<float*>(smem_er));
+    return;
+  }
   int p = 0;
 #pragma unroll
   for (int i = 1; i < DW_GROUP; ++i) p += (i < gg.n && w >= gg.start[i]) ? 1 : 0;
@@ -939,9 +977,30 @@ extern "C" int dct_gemm_bf16_ex(const uint16_t* A, const uint16_t* B, void* C, c
 // Grouped dW: C_i (+)= dZ_i^T X_i (+ colsum_i += column sums of dZ_i) for i < n (n <= 4), one
 // launch.  dZ_i [K][M_i] and X_i [K][N_i] bf16 row-major (K = rows of the batch), C_i fp32 [M_i][N_i].
 // Falls back to one launch per problem when a problem does not fit the grouped split-K kernel.
+static int dw_grouped_impl(int n, const uint16_t* const* dZ, const uint16_t* const* X, float* const* C,
+                           const int* M, const int* N, int K, float* const* colsum, int accumulate,
+                           const dct::EmbedRide& er, void* stream);
+
 extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const uint16_t* const* X, float* const* C,
                                         const int* M, const int* N, int K, float* const* colsum, int accumulate,
                                         void* stream) {
+  return dw_grouped_impl(n, dZ, X, C, M, N, K, colsum, accumulate, dct::EmbedRide{}, stream);
+}
+
+// the same launch with the TabTransformer embedding gradients riding (dct::EmbedRide; ex null: none).
+// Returns 1 when the ride did NOT run (the problems took the per-problem fallback): the caller then
+// launches dct_tt_embed_bwd itself.
+extern "C" int dct_gemm_bf16_dw_grouped_embed(int n, const uint16_t* const* dZ, const uint16_t* const* X,
+                                              float* const* C, const int* M, const int* N, int K,
+                                              float* const* colsum, int accumulate, const float* ex,
+                                              const float* edh, float* edE, float* edc, int eB, int eF,
+                                              void* stream) {
+  return dw_grouped_impl(n, dZ, X, C, M, N, K, colsum, accumulate, dct::EmbedRide{ex, edh, edE, edc, eB, eF}, stream);
+}
+
+static int dw_grouped_impl(int n, const uint16_t* const* dZ, const uint16_t* const* X, float* const* C,
+                           const int* M, const int* N, int K, float* const* colsum, int accumulate,
+                           const dct::EmbedRide& er, void* stream) {
   if (n <= 0 || n > dct::DW_GROUP || K <= 0) return n == 0 ? 0 : (int)hipErrorInvalidValue;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   dct::GemmGroup gg{};
@@ -991,9 +1050,11 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
                                      accumulate, nullptr, colsum ? colsum[i] : nullptr, stream);
       if (e) return e;
     }
-    return 0;
+    return er.x ? 1 : 0;  // the ride did not run
   }
   gg.start[n] = total;
+  gg.er = er;
+  const int ride = er.x ? er.F : 0;
   hipError_t e;
   // two-pass split-K (see split_partials): partial regions back to back, one grouped reduce after
   dct::SplitRedGroup rg{};
@@ -1029,7 +1090,7 @@ extern "C" int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const 
   auto fn = dct::gemm2_grouped_kernel<true, false, 2, 4>;
   e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(fn, dim3(total), dim3(512), lds, st, gg);
+  hipLaunchKernelGGL(fn, dim3(total + ride), dim3(512), lds, st, gg);
   e = hipGetLastError();
   if (e != hipSuccess || !part) return (int)e;
   hipLaunchKernelGGL(dct::splitk_reduce_grouped_kernel,

@@ -133,6 +133,10 @@ int dct_tt_head_fwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C,
 int dct_tt_head_bwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C, float eps, void* stream);
 int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const uint16_t* const* X, float* const* C,
                              const int* M, const int* N, int K, float* const* colsum, int accumulate, void* stream);
+int dct_gemm_bf16_dw_grouped_embed(int n, const uint16_t* const* dZ, const uint16_t* const* X, float* const* C,
+                                   const int* M, const int* N, int K, float* const* colsum, int accumulate,
+                                   const float* ex, const float* edh, float* edE, float* edc, int eB, int eF,
+                                   void* stream);
 int dct_gather_rows(const void* src, const int* idx, void* dst, int64_t n_rows, int row_bytes, void* stream);
 // device-side barrier of the xGMI peer exchange (step_kernels.hip; barrier slots at byte offset off)
 int dct_xg_barrier(void* recv, void* const* peers, int64_t off, unsigned* status, int world, int rank, unsigned tag,

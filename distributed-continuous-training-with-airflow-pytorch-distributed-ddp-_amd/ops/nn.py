@@ -81,6 +81,7 @@ def bound_params(params: Iterable[torch.Tensor], bf16_shadows: Optional[Dict[int
     # leftovers of a backward that never reached join_side_work (an aborted graph capture) belong
     # to that step: issuing them into this step's gradients would corrupt it
     _SIDE["deferred"].clear()
+    _SIDE.pop("embed", None)
     prev, _BOUND = _BOUND, _Binding(params, bf16_shadows, defer_dw, defer_groups)
     try:
         yield
@@ -99,13 +100,19 @@ def join_side_work():
 
 
 def _flush_deferred():
-    """Issue the queued dW GEMMs as grouped launches of up to 16 problems (stream order)."""
+    """Issue the queued dW GEMMs as grouped launches of up to 16 problems (stream order), with a
+    queued embedding-gradient job (the fused first block's) riding in the first."""
     dfr = _SIDE["deferred"]
+    emb = _SIDE.pop("embed", None)
+    if not dfr and emb is None:
+        return
+    nat, st = native(), _stream()
     if dfr:
-        nat, st = native(), _stream()
         for i in range(0, len(dfr), 16):
-            _dw_gemm_grouped(nat, dfr[i:i + 16], st)
+            _dw_gemm_grouped(nat, dfr[i:i + 16], st, embed=emb if i == 0 else None)
         dfr.clear()
+    elif emb is not None:
+        _embed_bwd(nat, emb, st)
 
 
 def _w16(w: torch.Tensor) -> torch.Tensor:
@@ -199,7 +206,12 @@ def _dw_gemm(nat, dz16, x16, w, b, st):
     return None if dw_direct else dw, None if db_direct else db
 
 
-def _dw_gemm_grouped(nat, items, st):
+def _embed_bwd(nat, emb, st):
+    x, dh, dE, dc, B, F, dm = emb
+    nat.tt_embed_bwd(x.data_ptr(), dh.data_ptr(), dE.data_ptr(), dc.data_ptr(), B, F, dm, st)
+
+
+def _dw_gemm_grouped(nat, items, st, embed=None):
     """Several dW (+)= dZ^T X products over the same rows (bias grads fused) in ONE launch
     (csrc/gemm_bf16.hip dct_gemm_bf16_dw_grouped); returns [(dw, db)] with None for direct grads."""
     rows = items[0][0].shape[0]
@@ -211,9 +223,15 @@ def _dw_gemm_grouped(nat, items, st):
         dws.append(dw)
         dbs.append(db)
         out.append((None if dw_direct else dw, None if db_direct else db))
-    nat.gemm_bf16_dw_grouped([it[0].data_ptr() for it in items], [it[1].data_ptr() for it in items],
-                             [d.data_ptr() for d in dws], [it[0].shape[1] for it in items],
-                             [it[1].shape[1] for it in items], rows, [d.data_ptr() for d in dbs], 1, st)
+    args = ([it[0].data_ptr() for it in items], [it[1].data_ptr() for it in items], [d.data_ptr() for d in dws],
+            [it[0].shape[1] for it in items], [it[1].shape[1] for it in items], rows, [d.data_ptr() for d in dbs], 1)
+    if embed is None:
+        nat.gemm_bf16_dw_grouped(*args, st)
+    else:  # the embedding gradients ride in the launch (csrc/gemm_bf16.hip EmbedRide), else on their own
+        x, dh, dE, dc, B, F, dm = embed
+        if not nat.gemm_bf16_dw_grouped_embed(*args, x.data_ptr(), dh.data_ptr(), dE.data_ptr(), dc.data_ptr(),
+                                              B, F, st):
+            _embed_bwd(nat, embed, st)
     return out
 
 
@@ -621,6 +639,7 @@ def _tt_prof_buf(kind: str, B: int, dev) -> torch.Tensor:
 
 _TT_LN_REP = True
 _TT_QKV_RECOMP = True
+_TT_EMBED_RIDE = True
 _TT_LN_WS: Dict[int, torch.Tensor] = {}
 
 
@@ -686,6 +705,12 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
     items = [(dout16, f, w2, b2), (dpre, a2, w1, b1), (dh1_16, o, wo, bo), (dqkv, a1, wqkv, bqkv)]
     b = _BOUND
     direct = b is not None and all(_is_direct(t) for t in (w2, b2, w1, b1, wo, bo, wqkv, bqkv))
+    # the first block's embedding gradients ride in the deferred dW launch (queued BEFORE a flush this
+    # block may trigger: under DDP its bucket must be complete when the backward returns)
+    ride = (embed is not None and direct and b.defer_dw and _TT_EMBED_RIDE
+            and all(_is_direct(t) for t in embed))
+    if ride:
+        _SIDE["embed"] = (h, dh, embed[0].grad, embed[1].grad, B, T, dm)
     if direct and b.defer_dw:
         # accumulate straight into the bound grads at the end of backward, every block in one launch
         _SIDE["deferred"].extend(items)
@@ -701,6 +726,8 @@ def _tt_block_bwd_fused(dout, h, st4, a1, qkv, o, lse, h1, a2, f, pre, wT, ln1w,
     if embed is None:
         _remember_bf16(dh, dh16)
         return grads, ()
+    if ride:
+        return grads, (None, None)
     # the fused embedding's parameter gradients: batch reductions of dh (tt_io.hip embed_bwd_kernel)
     E, c = embed
     dE, dE_direct = _grad_dst(E, zero=True)
