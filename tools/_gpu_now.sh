@@ -1,3 +1,4 @@
 set -e
 export TMPDIR=/tmp
-bash tools/gpu.sh r5_g49 "python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k 'tt_ or grouped'" "python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_tabtransformer.py tests/test_determinism_gpu.py tests/test_ddp_reducer_gpu.py" "python tools/tt_pooled_head_ab.py nn._TT_EMBED_RIDE"
+export STEP_TIMEOUT=900
+bash tools/gpu.sh r5_g50 "python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests" "python -c 'import __graft_entry__ as g; g.smoke()'" "python bench.py --steps 20 --warmup 5" "python bench.py --model tabtransformer --no-reference-model" "python bench.py --model tabular-mlp-4x1024 --no-reference-model"
