@@ -565,9 +565,11 @@ class AutogradEngine(_EngineBase):
         if ctx.is_distributed:
             ctx.broadcast_(self.flat_p, 0) if ctx.backend != "nccl" else self._bcast_nccl()
         # models whose gradients become ready in block groups (the TabTransformer's grouped deferred
-        # dW, model.ddp_block_groups) get buckets aligned with the groups: each launches as its group's
-        # dW launch is issued, overlapping the earlier blocks' backward (DCT_TT_DDP_GROUPS=0: one
-        # bucket launched at finalize)
+        # dW, model.ddp_block_groups) can get buckets aligned with the groups, each launched as its
+        # group's dW launch is issued (DCT_TT_DDP_GROUPS=1).  Off by default: the step is graph-captured,
+        # where the collectives run inline (runtime.cpp BucketReducer), so the split buys no overlap and
+        # its second dW launch costs 7-14 us per step (forced-DDP TabTransformer 0.334-0.336 -> 0.322-0.327
+        # ms, with the 60 us stand-in 0.397 -> 0.383-0.390; profiles/tt_ddp_groups_ab_r5.log)
         self._dw_groups, split_before = self._block_groups(model, params)
         self.plan = plan_buckets(numels, 4, bucket_cap_bytes, first_bucket_bytes, split_before=split_before)
         self.reducer = None
@@ -640,7 +642,7 @@ class AutogradEngine(_EngineBase):
         ((), ()).  Only for data-parallel runs (a reducer to overlap with)."""
         groups = model.ddp_block_groups() if hasattr(model, "ddp_block_groups") else None
         dp = self.ctx.is_distributed or os.environ.get("DCT_FORCE_DDP", "0") == "1"
-        if not groups or len(groups) < 2 or not dp or os.environ.get("DCT_TT_DDP_GROUPS", "1") == "0":
+        if not groups or len(groups) < 2 or not dp or os.environ.get("DCT_TT_DDP_GROUPS", "0") != "1":
             return (), ()
         index = {id(p): i for i, p in enumerate(params)}
         splits = []

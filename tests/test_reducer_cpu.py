@@ -74,10 +74,10 @@ def test_plan_buckets_split_before_aligns_buckets_with_groups():
     assert plan_buckets([10, 20, 30, 40, 50], 4, 1 << 20, 1 << 20).param_bucket == [0] * 5
 
 
-def test_tabtransformer_block_groups_split_the_ddp_buckets():
-    """AutogradEngine._block_groups on the TabTransformer: the upper half of the blocks (with the
-    head) and the lower half (with the embedding) as two bucket groups; the split index is the
-    last parameter of the highest block of the lower group."""
+def test_tabtransformer_block_groups_split_the_ddp_buckets(monkeypatch):
+    """AutogradEngine._block_groups on the TabTransformer (DCT_TT_DDP_GROUPS=1; off by default): the
+    upper half of the blocks (with the head) and the lower half (with the embedding) as two bucket
+    groups; the split index is the last parameter of the highest block of the lower group."""
     from dct_amd.models.tabtransformer import TabTransformer
     from dct_amd.parallel.dist import DistContext
     from dct_amd.trainer.engines import AutogradEngine
@@ -91,6 +91,9 @@ def test_tabtransformer_block_groups_split_the_ddp_buckets():
     class _Eng:
         ctx = DistContext(rank=0, world_size=2)
 
+    monkeypatch.delenv("DCT_TT_DDP_GROUPS", raising=False)
+    assert AutogradEngine._block_groups(_Eng(), m, params) == ((), ())  # default: one group
+    monkeypatch.setenv("DCT_TT_DDP_GROUPS", "1")
     groups, splits = AutogradEngine._block_groups(_Eng(), m, params)
     assert groups == (2, 2)
     first_b2 = [i for i, p in enumerate(params) if p is next(m.blocks[2].parameters())][0]
@@ -102,7 +105,7 @@ def test_tabtransformer_block_groups_split_the_ddp_buckets():
         assert plan.param_bucket[i] == (0 if id(p) in upper or i > first_b2 else 1)
 
 
-def test_block_group_buckets_never_split_inside_a_group():
+def test_block_group_buckets_never_split_inside_a_group(monkeypatch):
     """A TabTransformer whose per-block weights exceed the first-bucket / bucket caps (d_model 192:
     one block's 12 d^2 fp32 weights are ~1.7 MB > 1 MiB) must still get exactly one bucket per
     block group: the group's dW GEMMs are issued only inside its lowest block's backward, so a
@@ -111,6 +114,7 @@ def test_block_group_buckets_never_split_inside_a_group():
     from dct_amd.parallel.dist import DistContext
     from dct_amd.trainer.engines import AutogradEngine
 
+    monkeypatch.setenv("DCT_TT_DDP_GROUPS", "1")
     for d, layers in ((192, 4), (64, 12)):
         m = TabTransformer(num_features=8, d_model=d, heads=4, layers=layers)
         params = list(m.parameters())
