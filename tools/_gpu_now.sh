@@ -1,3 +1,4 @@
 set -e
 export TMPDIR=/tmp
-bash tools/gpu.sh r5_g52 "python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_ddp_reducer_gpu.py tests/test_tabtransformer.py tests/test_multigpu.py tests/test_trainer_gpu.py"
+B="python bench.py --model tabtransformer --steps 600 --warmup 100 --no-reference-model"
+bash tools/gpu.sh r5_g53 "$B" "DCT_AB_TWOPASS=64 $B" "$B" "DCT_AB_TWOPASS=64 $B" "$B" "DCT_AB_TWOPASS=64 $B"
