@@ -592,6 +592,8 @@ PYBIND11_MODULE(_dct_native, m) {
       .def_property_readonly("launched", &dct::BucketReducer::launched)
       .def_property_readonly("launched_before_finalize", &dct::BucketReducer::launched_before_finalize)
       .def("edge_timeouts", &dct::BucketReducer::edge_timeouts)
+      .def("check_edges", &dct::BucketReducer::check_edges)
+      .def_property_readonly("peer_world", &dct::BucketReducer::peer_world)
       .def_property_readonly("comm_stream", &dct::BucketReducer::comm_stream)
       .def_property_readonly("inline_mode", &dct::BucketReducer::inline_mode)
       .def("enable_timing", &dct::BucketReducer::enable_timing, py::arg("check") = false)

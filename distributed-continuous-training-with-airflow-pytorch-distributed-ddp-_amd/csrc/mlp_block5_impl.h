@@ -270,20 +270,27 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   const int cur0 = (!ADAM && a.cursor) ? sload(a.cursor) : 0;  // grad mode: batch index from the device cursor
   const int bs0 = min(Bsz, a.n_items - cur0 * Bsz);
   const bool first_ok = tid < B * DMAX && fb < bs0;
-  const int rb_first = (first_ok && !stp) ? a.idx[cur0 * Bsz + fb] : 0;
+  // unconditional load at a clamped index, masked after: a load behind the first_ok branch compiled
+  // to a branch with `s_waitcnt vmcnt(0)` inside it - one full memory round trip at kernel start,
+  // before a single W1 load was issued
+  const int rb_raw = a.idx[max(0, min(cur0 * Bsz + (first_ok ? fb : 0), a.n_items - 1))];
+  const int rb_first = (first_ok && !stp) ? rb_raw : 0;
   int ridx_next = 0;
   if (!stp && role && (cur0 + 1) * Bsz + pb < a.n_items) ridx_next = a.idx[(cur0 + 1) * Bsz + pb];
 
   // ---- W1 + moments: coalesced, redistributed through LDS below
+  // (p and m first, v last: the first staging round waits only for the p / m loads - vmcnt counts in
+  // issue order - while v is still arriving)
   v4f sp[Stg::LD], sm[Stg::LD], sv[Stg::LD];
 #pragma unroll
   for (int i = 0; i < Stg::LD; ++i) {
     const int f = wo1 + 4 * (i * NT + tid);
     sp[i] = *reinterpret_cast<const v4f*>(a.p + f);
-    if constexpr (ADAM) {
-      sm[i] = *reinterpret_cast<const v4f*>(a.m + f);
-      sv[i] = *reinterpret_cast<const v4f*>(a.v + f);
-    }
+    if constexpr (ADAM) sm[i] = *reinterpret_cast<const v4f*>(a.m + f);
+  }
+  if constexpr (ADAM) {
+#pragma unroll
+    for (int i = 0; i < Stg::LD; ++i) sv[i] = *reinterpret_cast<const v4f*>(a.v + wo1 + 4 * (i * NT + tid));
   }
   // W0 slices of unit u (inputs d = r0 and r0 + 4), b0[u]
   float w0[2], m0[2], v0[2];

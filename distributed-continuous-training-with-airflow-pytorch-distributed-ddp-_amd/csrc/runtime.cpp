@@ -155,10 +155,15 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
   }
   inline_ = inline_knob_ == 1;
   for (int64_t c : counts_) total_count_ += c;
-  // fork / join events between two streams of ONE device: a device-scope release is all the
-  // collective (and Adam after the join) needs, not the default system-scope fence (its cache
-  // writeback / invalidate is most of an edge's cost)
-  const unsigned ev_flags = hipEventDisableTiming | hipEventReleaseToDevice;
+  // A communicator with real peers (world > 1, not the one-rank identity): RCCL transports may read
+  // the send buffer straight from a peer GPU, so the fork events keep the default system-scope
+  // release until a multi-GPU run has confirmed that the device scope suffices; the
+  // join is an event wait (unbounded, see edge()).  One-rank / stand-in communicators: fork / join
+  // between two streams of ONE device, where a device-scope release is all the collective (and
+  // Adam after the join) needs, not the system-scope fence (its cache writeback / invalidate is
+  // most of an edge's cost).
+  peer_world_ = comm_ != nullptr && comm_->world() > 1 && !comm_->is_identity();
+  const unsigned ev_flags = peer_world_ ? hipEventDisableTiming : (hipEventDisableTiming | hipEventReleaseToDevice);
   ready_events_.resize(nb);
   for (auto& e : ready_events_) hip_check(hipEventCreateWithFlags(&e, ev_flags), "hipEventCreate");
   hip_check(hipEventCreateWithFlags(&done_event_, ev_flags), "hipEventCreate");
@@ -168,6 +173,14 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
     const size_t bytes = (2 * (nb + 2) + 1) * sizeof(int);
     hip_check(hipMalloc(&dsync_, bytes), "hipMalloc edge counters");
     hip_check(hipMemset(dsync_, 0, bytes), "hipMemset edge counters");
+    // the wait kernels' timeout word in coherent host memory: prepare() reads it every step with
+    // no synchronisation and throws, so an expired edge can never go unnoticed
+    hip_check(hipHostMalloc(reinterpret_cast<void**>(&status_host_), sizeof(int),
+                            hipHostMallocMapped | hipHostMallocCoherent),
+              "hipHostMalloc edge status");
+    *status_host_ = 0;
+    hip_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&status_dev_), status_host_, 0),
+              "hipHostGetDevicePointer edge status");
   }
 }
 
@@ -177,10 +190,12 @@ BucketReducer::~BucketReducer() {
   if (tail_event_) hipEventDestroy(tail_event_);
   if (stamps_) hipFree(stamps_);
   if (dsync_) hipFree(dsync_);
+  if (status_host_) hipHostFree(status_host_);
   if (comm_stream_) hipStreamDestroy(comm_stream_);
 }
 
 void BucketReducer::prepare() {
+  check_edges();
   std::fill(pending_.begin(), pending_.end(), 0);
   std::fill(launched_.begin(), launched_.end(), 0);
   next_to_launch_ = 0;
@@ -239,16 +254,22 @@ bool BucketReducer::step_inline(void* compute_stream) {
 // graph only signalled the buckets, with the collectives enqueued eagerly on the comm stream before
 // each replay, did deadlock there until the wait bound: the replay's join sat ahead of its own
 // collectives in the shared queue - removed again, profiles/ddp_reducer_standin_ab_r5.log.)
-void BucketReducer::edge(int slot, hipEvent_t ev, hipStream_t from, hipStream_t to) {
+// The flag wait is bounded (a spinning wave must end); an expired wait is recorded in status_host_
+// and prepare() throws at the next step.  `join` = the comm -> compute edge at the end of a step:
+// with real peers its producer (the collective) waits on OTHER ranks - a peer seconds behind (rank 0
+// writing a checkpoint, a validation pass, RCCL's first connections) would expire a bounded wait -
+// so that edge is an event wait, unbounded like the reference DDP's own.  The fork
+// edges' producers are this rank's backward kernels, which never wait on a peer.
+void BucketReducer::edge(int slot, hipEvent_t ev, hipStream_t from, hipStream_t to, bool join) {
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(from, &cap) != hipSuccess) {
     (void)hipGetLastError();
     cap = hipStreamCaptureStatusNone;
   }
-  if (cap == hipStreamCaptureStatusNone && dsync_) {
+  if (cap == hipStreamCaptureStatusNone && dsync_ && !(join && peer_world_)) {
     const int ns = (int)offsets_.size() + 2;
     hip_check((hipError_t)dct_flag_signal(dsync_ + slot, from), "edge signal");
-    hip_check((hipError_t)dct_flag_wait(dsync_ + slot, dsync_ + ns + slot, dsync_ + 2 * ns, to), "edge wait");
+    hip_check((hipError_t)dct_flag_wait(dsync_ + slot, dsync_ + ns + slot, status_dev_, to), "edge wait");
     return;
   }
   hip_check(hipEventRecord(ev, from), "hipEventRecord");
@@ -256,11 +277,17 @@ void BucketReducer::edge(int slot, hipEvent_t ev, hipStream_t from, hipStream_t 
 }
 
 int BucketReducer::edge_timeouts() const {
-  if (!dsync_) return 0;
-  int v = 0;
+  if (!status_host_) return 0;
   hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-  hip_check(hipMemcpy(&v, dsync_ + 2 * ((int)offsets_.size() + 2), sizeof(int), hipMemcpyDeviceToHost), "edge status");
-  return v;
+  return *reinterpret_cast<volatile int*>(status_host_);
+}
+
+void BucketReducer::check_edges() const {
+  // no synchronisation: the word reflects every wait kernel that has run so far
+  if (status_host_ && *reinterpret_cast<volatile int*>(status_host_) != 0)
+    throw std::runtime_error(
+        "DDP bucket reducer: a cross-stream edge wait expired - a collective or the optimizer ran without "
+        "its producer, gradients / parameters of this rank are not trustworthy");
 }
 
 void BucketReducer::launch_bucket(int b, uintptr_t compute_stream) {
@@ -322,7 +349,7 @@ void BucketReducer::finalize(uintptr_t compute_stream) {
     next_to_launch_++;
   }
   if (timing_) hip_check((hipError_t)dct_reducer_close(stamps_, reinterpret_cast<void*>(rs)), "reducer close");
-  if (!inline_) edge((int)offsets_.size(), done_event_, comm_stream_, cs);
+  if (!inline_) edge((int)offsets_.size(), done_event_, comm_stream_, cs, /*join=*/true);
   if (timing_ && check_) hip_check((hipError_t)dct_reducer_check(stamps_, reinterpret_cast<void*>(cs)), "reducer check");
 }
 

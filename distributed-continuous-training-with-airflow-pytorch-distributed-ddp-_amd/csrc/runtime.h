@@ -56,10 +56,13 @@ class BucketReducer {
   void reset_timing();
   // 1 if an eager cross-stream edge's wait expired (its consumer went on without the producer)
   int edge_timeouts() const;
+  // throws if an edge wait has expired (no synchronisation; prepare() calls it every step)
+  void check_edges() const;
+  bool peer_world() const { return peer_world_; }
 
  private:
   void launch_bucket(int b, uintptr_t compute_stream);
-  void edge(int slot, hipEvent_t ev, hipStream_t from, hipStream_t to);
+  void edge(int slot, hipEvent_t ev, hipStream_t from, hipStream_t to, bool join = false);
   void collective(int b, hipStream_t rs);
   Comm* comm_;
   uintptr_t flat_;
@@ -73,6 +76,9 @@ class BucketReducer {
   hipEvent_t done_event_ = nullptr;
   hipEvent_t tail_event_ = nullptr;
   int* dsync_ = nullptr;  // eager edges' device counters (edge())
+  int* status_host_ = nullptr;  // edge-wait timeout word, coherent host memory (check_edges())
+  int* status_dev_ = nullptr;   // its device address
+  bool peer_world_ = false;     // a communicator with real peers (world > 1)
   unsigned long long* stamps_ = nullptr;  // [8], see step_kernels.hip reducer_close_kernel
   bool timing_ = false, check_ = false;
   int inline_knob_ = -1;  // DCT_REDUCER_INLINE resolved (1 / 0 / -1 = inline while the compute stream is capturing)

@@ -177,8 +177,9 @@ __global__ void reducer_check_kernel(unsigned long long* s) {
 // for it.  hipEventRecord + hipStreamWaitEvent cost 6-13 us of queue time per edge on MI355X
 // (a marker packet that held the compute queue ~6.5 us per bucket fork, ~12 us at the join: kernel
 // trace of the forced-DDP tabular step); a one-wave kernel on each side costs about a dispatch.
-// The wait is bounded (2 s): on expiry it sets *status and lets the stream go on (wrong results
-// are then reported by BucketReducer::edge_timeouts, never a hung queue).
+// The wait is bounded (2 s): on expiry it sets *status (coherent host memory) and lets the stream
+// go on - never a hung queue; BucketReducer::prepare() throws on the next step (check_edges), so the
+// expired edge is a loud failure, not a silent one.
 __global__ __launch_bounds__(64) void flag_signal_kernel(int* flag) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(64) void flag_wait_kernel(int* flag, int* consumed,
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) <= c) {
     if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
-      __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
     __builtin_amdgcn_s_sleep(2);
