@@ -40,7 +40,9 @@ def target_path() -> str:
 # 20-step window 1.65-1.70 -> 1.60-1.69; its exchange units measured no gain at 2 / 4 ranks sharing a GPU
 # (1.81 / 2.47 vs 1.80 / 2.47 us/step) and keep the default (profiles/wave_sched_strategy_ab_r4.log).
 MAX_ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
-FILE_FLAGS = {"mlp_block3.hip": ["-fno-slp-vectorize"],
+FILE_FLAGS = {"gemm_bf16.hip": ["-fno-slp-vectorize"],
+              "optim.hip": ["-fno-slp-vectorize"],
+              "mlp_block3.hip": ["-fno-slp-vectorize"],
               "mlp_block5.hip": ["-fno-slp-vectorize"] + MAX_ILP,
               "mlp_block5_xg.hip": ["-fno-slp-vectorize"],
               "mlp_block5_xgprof.hip": ["-fno-slp-vectorize"],

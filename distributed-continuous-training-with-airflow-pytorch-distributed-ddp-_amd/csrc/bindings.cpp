@@ -45,6 +45,7 @@ struct MlpPlan {
       throw std::invalid_argument("bad MLP shape");
     supported = dct_mlp_select(sh(), &nt, &maxblk);
     dct::knobs_reload();  // plan time: the DCT_* knobs of this process's launches
+    reinterpret_cast<dct::MlpShape*>(shape.data())->mlp_block = dct::knobs().mlp_block;
     const bool force_lds = dct::knobs().mlp_force_lds != 0;
     use_wave = (!force_lds && dct_mlp_wave_supported(dims.data(), (int)dims.size() - 1, 1)) ? 1 : 0;
     if (use_wave) supported = 1;
@@ -216,6 +217,7 @@ PYBIND11_MODULE(_dct_native, m) {
       .def_property_readonly("num_params", [](const MlpPlan& p) { return p.sh()->P; })
       .def_property_readonly("lds_bytes", [](const MlpPlan& p) { return p.sh()->lds_floats * 4; })
       .def_property_readonly("bmax", [](const MlpPlan& p) { return p.sh()->bmax; })
+      .def_property_readonly("mlp_block", [](const MlpPlan& p) { return p.sh()->mlp_block; })
       .def(
           "train",
           [](const MlpPlan& plan, uintptr_t p, uintptr_t mo, uintptr_t vo, uintptr_t grad_out, uintptr_t X, int ldx,
@@ -319,6 +321,26 @@ PYBIND11_MODULE(_dct_native, m) {
                                    P<int>(cursor), P<const float>(loss_slot), P<float>(loss_out), loss_cap,
                                    reinterpret_cast<void*>(stream)),
                 "adam_flat_step");
+        });
+  // Adam over [0, n) of p / g / m / v (step t read from step_counter): riding in a split-K dW launch
+  // of dZ^T X (mode 0: one element per thread - the executor's body; 1: the float4 body) or as its own
+  // launch (mode 2, dct_adam_range) - tests/test_packed_fp32_gpu.py compares them bit for bit
+  m.def("adam_ride_check",
+        [](int mode, uintptr_t dz, uintptr_t x, uintptr_t part, uintptr_t colsum, int M, int N, int K, int splits,
+           uintptr_t p, uintptr_t g, uintptr_t mo, uintptr_t vo, int64_t n, float lr, float b1, float b2, float eps,
+           uintptr_t step_counter, uintptr_t stream) {
+          dct::AdamRange r{};
+          r.p = P<float>(p); r.g = P<const float>(g); r.m = P<float>(mo); r.v = P<float>(vo); r.n = n;
+          r.lr = lr; r.b1 = b1; r.b2 = b2; r.eps = eps; r.wd = 0.f; r.grad_scale = 1.f;
+          r.step_counter = P<const int>(step_counter); r.nparts = 0; r.lo = 0; r.hi = n;
+          if (mode == 2) {
+            check(dct_adam_range(&r, nullptr, nullptr, nullptr, 0, reinterpret_cast<void*>(stream)), "adam_range");
+            return;
+          }
+          check(dct_gemm_bf16_dw_partials_adam_ex(P<const uint16_t>(dz), P<const uint16_t>(x), P<float>(part),
+                                                  P<float>(colsum), M, N, K, splits, &r, mode == 1 ? 1 : 0,
+                                                  reinterpret_cast<void*>(stream)),
+                "gemm_bf16_dw_partials_adam");
         });
   m.def("ag_step_prologue",
         [](uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t idx, uintptr_t cursor, int B, int64_t n_items,

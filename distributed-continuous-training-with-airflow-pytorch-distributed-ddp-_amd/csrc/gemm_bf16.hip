@@ -885,11 +885,15 @@ extern "C" int dct_gemm_bf16_dw_partials(const uint16_t* dZ, const uint16_t* X, 
 }
 
 // dW split-K partials with an Adam range riding along: workgroups [0, gemm_wgs) are the GEMM's
-// (XCD-aware remap over that count), the rest run adam_flat_range over the range.  The Adam
+// (XCD-aware remap over that count), the rest run Adam over the range.  The Adam
 // workgroups need no LDS but inherit the launch's dynamic LDS (64 KB), so one sits beside each
 // GEMM tile on a CU (2 x 64 KB <= 160 KB): the HBM-bound optimizer streams under the GEMM, which is
 // bound by each CU's global -> LDS rate (tabular step: the separate Adam launch was 17 us).
-template <int S_ADAM>
+// F4: the float4 body (adam_flat_range) instead of one element per thread (adam_scalar_range, the
+// executor's choice: 155.4-157.1 vs 158.0-158.6 us per tabular step, profiles/packed_fp32_lds_dma_r6.log).
+// Both are exact here because this file is compiled without packed fp32 (_build.py FILE_FLAGS):
+// compiled WITH v_pk_* the float4 body went wrong beside the GEMM tiles' LDS-DMA (same log).
+template <int S_ADAM, bool F4 = false>
 __global__ __launch_bounds__(512, 2) void gemm2_dw_adam_kernel(dct::GemmArgs g, int splits, int gemm_wgs,
                                                                dct::AdamArgs a, int64_t lo, int64_t hi) {
   if ((int)blockIdx.x < gemm_wgs) {
@@ -897,6 +901,8 @@ __global__ __launch_bounds__(512, 2) void gemm2_dw_adam_kernel(dct::GemmArgs g, 
     const int q8 = gemm_wgs >> 3, r8 = gemm_wgs & 7;
     const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
     dct::gemm2_body<true, false, true, 128, 2, 4>(g, splits, wgid);
+  } else if constexpr (F4) {
+    dct::adam_flat_range<true, S_ADAM>(a, lo, hi, blockIdx.x - gemm_wgs, gridDim.x - gemm_wgs);
   } else {
     dct::adam_scalar_range<true, S_ADAM>(a, lo, hi, blockIdx.x - gemm_wgs, gridDim.x - gemm_wgs);
   }
@@ -904,6 +910,12 @@ __global__ __launch_bounds__(512, 2) void gemm2_dw_adam_kernel(dct::GemmArgs g, 
 
 extern "C" int dct_gemm_bf16_dw_partials_adam(const uint16_t* dZ, const uint16_t* X, float* part, float* colsum, int M,
                                               int N, int K, int splits, const dct::AdamRange* r, void* stream) {
+  return dct_gemm_bf16_dw_partials_adam_ex(dZ, X, part, colsum, M, N, K, splits, r, 0, stream);
+}
+
+extern "C" int dct_gemm_bf16_dw_partials_adam_ex(const uint16_t* dZ, const uint16_t* X, float* part, float* colsum,
+                                                 int M, int N, int K, int splits, const dct::AdamRange* r, int f4,
+                                                 void* stream) {
   if (!r) return dct_gemm_bf16_dw_partials(dZ, X, part, colsum, M, N, K, splits, stream);
   dct::GemmArgs g{};
   g.A = dZ; g.B = X; g.C = part; g.M = M; g.N = N; g.K = K; g.lda = M; g.ldb = N; g.ldc = N;
@@ -927,7 +939,8 @@ extern "C" int dct_gemm_bf16_dw_partials_adam(const uint16_t* dZ, const uint16_t
   int adam_wgs = (int)std::min<int64_t>((work + 511) / 512, device_cus());
   if (adam_wgs < 1) adam_wgs = 1;
   const size_t lds = (size_t)(nk_slice > 1 ? 4 : 2) * dct::G2_BYTES;
-  auto fn = max_sp > 4 ? gemm2_dw_adam_kernel<8> : gemm2_dw_adam_kernel<4>;
+  auto fn = f4 ? (max_sp > 4 ? gemm2_dw_adam_kernel<8, true> : gemm2_dw_adam_kernel<4, true>)
+              : (max_sp > 4 ? gemm2_dw_adam_kernel<8> : gemm2_dw_adam_kernel<4>);
   hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(fn, dim3(gemm_wgs + adam_wgs), dim3(512), lds, reinterpret_cast<hipStream_t>(stream), g, splits,

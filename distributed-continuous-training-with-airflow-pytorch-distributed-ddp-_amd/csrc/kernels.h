@@ -54,6 +54,9 @@ extern "C" {
 // workgroups of the same launch, co-resident with the GEMM tiles (r == nullptr: the GEMM alone)
 int dct_gemm_bf16_dw_partials_adam(const uint16_t* dZ, const uint16_t* X, float* part, float* colsum, int M, int N,
                                    int K, int splits, const dct::AdamRange* r, void* stream);
+// the same with the Adam body picked: f4 = 0 one element per thread (the executor's), 1 float4
+int dct_gemm_bf16_dw_partials_adam_ex(const uint16_t* dZ, const uint16_t* X, float* part, float* colsum, int M, int N,
+                                      int K, int splits, const dct::AdamRange* r, int f4, void* stream);
 // Adam over r's range as its own launch (+ the step epilogue: loss_out[*cursor] = *loss_slot, cursor += 1)
 int dct_adam_range(const dct::AdamRange* r, int* cursor, const float* loss_slot, float* loss_out, int loss_cap,
                    void* stream);

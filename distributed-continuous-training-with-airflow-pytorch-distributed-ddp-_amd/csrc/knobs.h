@@ -16,8 +16,10 @@ struct Knobs {
   int fused_head = 1;       // DCT_FUSED_HEAD=0: the four-kernel head chain
   int dw_into_adam = 1;     // DCT_DW_INTO_ADAM=0: dW through g and the reduce pass
   // bucket reducer (runtime.cpp; copied into each reducer at construction)
-  int reducer_inline = -2;  // DCT_REDUCER_INLINE: -2 auto (compute stream only for a one-rank communicator without
-                            // a stand-in, else the comm stream), 1 compute stream, 0 comm stream, -1 inline under capture
+  int reducer_inline = -2;  // DCT_REDUCER_INLINE: -2 auto (compute stream for a one-rank communicator without a
+                            // stand-in and for real peers - RCCL's packed-fp32 reduce kernels must not share CUs
+                            // with LDS-DMA GEMM tiles, runtime.cpp - else the comm stream), 1 compute stream,
+                            // 0 comm stream, -1 inline under capture
   int reducer_standin_us = 0;   // DCT_REDUCER_STANDIN_US: test-only stand-in collective - a busy kernel of this many us
                                 // per step (split over the buckets by size) on the collective's stream
   int reducer_standin_wgs = 16; // DCT_REDUCER_STANDIN_WGS: its workgroups (one wave each, no LDS)

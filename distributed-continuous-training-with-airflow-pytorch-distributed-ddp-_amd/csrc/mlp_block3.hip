@@ -565,7 +565,7 @@ __global__ __launch_bounds__(blk3::NT, 1) void mlp_block3_kernel(MlpShape sh, Ml
 #undef B3STAMP
 
 bool mlp_block3_ok(const MlpShape& sh, const MlpArgs& a) {
-  if (knobs().mlp_block == 0) return false;  // DCT_MLP_BLOCK=0: the generic LDS trainer
+  if (sh.mlp_block == 0) return false;  // DCT_MLP_BLOCK=0 (plan-time copy): the generic LDS trainer
   // a profiling launch is served for the weather shape (D0 <= 8, C <= 2, train mode) only
   const bool prof_ok = a.prof == nullptr || (sh.dims[0] <= 8 && sh.dims[3] <= 2 && a.mode == 0);
   // 16-byte W1 row loads / stores

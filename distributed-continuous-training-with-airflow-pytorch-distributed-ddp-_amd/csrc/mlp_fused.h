@@ -45,6 +45,8 @@ struct MlpShape {
   int maxq;      // weight blocks per thread
   int fuse_loss; // loss computed inside the last forward layer (classes <= 4)
   int supported;
+  int mlp_block;  // plan-time copy of DCT_MLP_BLOCK (MlpPlan, bindings.cpp): the launch path reads this, never
+                  // the process-wide knob struct
 };
 
 struct MlpArgs {

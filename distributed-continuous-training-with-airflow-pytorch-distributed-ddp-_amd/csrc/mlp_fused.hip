@@ -114,6 +114,7 @@ int mlp_make_shape(MlpShape* sh, const int* dims, int L, int bmax) {
   off += r4(2 * bmax);
   sh->lds_floats = off;
   sh->supported = (nt > 0) && (nbias <= 2 * nt) && ((size_t)off * 4 <= 160 * 1024) ? 1 : 0;
+  sh->mlp_block = -1;  // auto until the plan stamps its knob copy
   return 0;
 }
 
@@ -150,7 +151,7 @@ int dct_mlp_train(const void* shape, const MlpArgs* a, void* stream) {
     if (!dct::mlp_block5_ok(sh, *a)) return (int)hipErrorInvalidValue;
     return (int)dct::mlp_launch_block5(sh, *a, st);
   }
-  const int blk = dct::knobs().mlp_block;  // -1 auto, 3 mlp_block3, 0 the generic LDS trainer
+  const int blk = sh.mlp_block;  // plan-time DCT_MLP_BLOCK: -1 auto, 3 mlp_block3, 0 the generic LDS trainer
   if (blk < 0 && dct::mlp_block5_ok(sh, *a)) return (int)dct::mlp_launch_block5(sh, *a, st);
   if (blk != 0 && dct::mlp_block3_ok(sh, *a)) return (int)dct::mlp_launch_block3(sh, *a, st);
   switch (sh.L) {

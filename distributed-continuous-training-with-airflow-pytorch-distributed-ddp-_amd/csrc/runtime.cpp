@@ -145,13 +145,24 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
   //    1 / 0: always the compute / the comm stream (0 with a captured step: the graph's event edges);
   //   -1: inline while the compute stream is capturing.
   // The test-only stand-in collective (DCT_REDUCER_STANDIN_US) counts as a real collective.
+  //   With real peers (world > 1) the auto mode keeps the collectives on the compute stream too: RCCL's
+  //   fp32 sum / average kernels (runRing / runTreeSplit / runTreeUpDown over FuncSum<float> and
+  //   FuncPreMulSum<float> in librccl's gfx950 code object) compute with v_pk_add_f32, and packed fp32
+  //   in a kernel whose waves share a CU with LDS-DMA traffic - the operand path of every gemm2 tile
+  //   this runtime launches - goes wrong now and then (tools/probes/adam_ride_probe.hip mode 8: an
+  //   Adam kernel on a second stream beside GEMM-only launches, 58 of 60 launches with wrong low
+  //   halves; profiles/packed_fp32_lds_dma_r6.log).  A collective overlapping the backward GEMMs could
+  //   therefore return a wrong gradient sum with no error; inline, nothing runs beside it.
+  //   DCT_REDUCER_INLINE=0 / -1 still selects the comm stream (stand-in measurements, or steps whose
+  //   kernels use no LDS-DMA).
   const Knobs& k = dct::knobs();
   standin_us_ = k.reducer_standin_us;
   standin_wgs_ = k.reducer_standin_wgs;
   inline_knob_ = k.reducer_inline;
+  const bool real_peers = comm_ != nullptr && comm_->world() > 1 && !comm_->is_identity();
   if (inline_knob_ == -2) {
     const bool identity = comm_ == nullptr || (comm_->world() == 1 && comm_->is_identity());
-    inline_knob_ = (identity && standin_us_ == 0) ? 1 : -1;
+    inline_knob_ = ((identity && standin_us_ == 0) || real_peers) ? 1 : -1;
   }
   inline_ = inline_knob_ == 1;
   for (int64_t c : counts_) total_count_ += c;
@@ -162,7 +173,7 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
   // between two streams of ONE device, where a device-scope release is all the collective (and
   // Adam after the join) needs, not the system-scope fence (its cache writeback / invalidate is
   // most of an edge's cost).
-  peer_world_ = comm_ != nullptr && comm_->world() > 1 && !comm_->is_identity();
+  peer_world_ = real_peers;
   const unsigned ev_flags = peer_world_ ? hipEventDisableTiming : (hipEventDisableTiming | hipEventReleaseToDevice);
   ready_events_.resize(nb);
   for (auto& e : ready_events_) hip_check(hipEventCreateWithFlags(&e, ev_flags), "hipEventCreate");

@@ -61,3 +61,18 @@ def test_mlp_plan_reloads_knobs(nat, monkeypatch):
     monkeypatch.setenv("DCT_MLP_KERNEL", "auto")
     nat.MlpPlan([5, 64, 2], 4)
     assert nat.knobs()["mlp_force_lds"] == 0
+
+
+def test_block_choice_is_a_plan_time_copy(nat, monkeypatch):
+    """the 3x128 launch path (dct_mlp_train, mlp_block3_ok) reads DCT_MLP_BLOCK from the
+    plan's own copy, stamped when the MlpPlan is built - a later reload of the process-wide knobs does not
+    change an existing plan's launches."""
+    monkeypatch.setenv("DCT_MLP_BLOCK", "3")
+    plan = nat.MlpPlan([5, 128, 128, 2], 4)
+    assert plan.mlp_block == 3
+    monkeypatch.setenv("DCT_MLP_BLOCK", "0")
+    nat.reload_knobs()
+    assert nat.knobs()["mlp_block"] == 0 and plan.mlp_block == 3
+    assert nat.MlpPlan([5, 128, 128, 2], 4).mlp_block == 0
+    monkeypatch.delenv("DCT_MLP_BLOCK")
+    assert nat.MlpPlan([5, 128, 128, 2], 4).mlp_block == -1

@@ -9,6 +9,10 @@
 //   mode 1: scalar path (adam_scalar_range) beside the GEMM tiles     (the r5 fix)
 //   mode 2: float4 path alone (no GEMM workgroups in the launch)
 //   mode 3: float4 path, GEMM workgroups exit at once (same kernel, same code object, no MFMA work)
+//   mode 4..7: float4 path beside SYNTHETIC tiles (MFMA chains; +1 LDS-DMA refills, +2 ds_read operands)
+//   mode 8: the float4 Adam as its own launch on a second stream beside GEMM-only launches (cross-kernel)
+//   mode 16 + SCAL: a copy of the float4 body with the sites in SCAL kept out of packing (adam4_probe);
+//                   SCAL 16 / 32: the denominator paired by hand with / without op_sel on src1
 // Build (tools/probes/build_adam_ride_probe.sh): once as is, once with -fno-slp-vectorize (no v_pk_*
 // in the Adam body); run: adam_ride_probe <mode> <iterations>.
 #include "gemm_bf16.hip"
@@ -23,17 +27,142 @@ extern "C" int dct_bias_act_bwd(const void*, const void*, uint16_t*, float*, int
 #include <cstring>
 #include <vector>
 
+// A copy of adam_flat_range's float4 Adam (PARTS, no slices) whose per-element steps can be taken out of
+// the compiler's packing one site at a time: each bit of SCAL computes that step for all four
+// components with scalar v_fma_f32 / v_mul_f32 in inline asm (nothing left to pair):
+//   1: m = b1 m + (1 - b1) g   2: v = b2 v + (1 - b2) g^2   4: denom = sqrt(v) rbc2 + eps   8: step_size * m
+__device__ __forceinline__ float asm_fma(float a, float b, float c) {
+  float r;
+  asm volatile("v_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float asm_mul(float a, float b) {
+  float r;
+  asm volatile("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+template <int SCAL>
+__device__ __forceinline__ void adam4_probe(float4& P, float4 G, float4& Mm, float4& V, const dct::AdamArgs& a) {
+  float p[4] = {P.x, P.y, P.z, P.w}, g[4] = {G.x, G.y, G.z, G.w}, m[4] = {Mm.x, Mm.y, Mm.z, Mm.w},
+        v[4] = {V.x, V.y, V.z, V.w}, d[4], u[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    g[i] *= a.grad_scale;
+    g[i] += a.wd * p[i];
+    m[i] = (SCAL & 1) ? asm_fma(a.b1, m[i], asm_mul(1.f - a.b1, g[i])) : a.b1 * m[i] + (1.f - a.b1) * g[i];
+    v[i] = (SCAL & 2) ? asm_fma(a.b2, v[i], asm_mul(asm_mul(1.f - a.b2, g[i]), g[i]))
+                      : a.b2 * v[i] + (1.f - a.b2) * g[i] * g[i];
+  }
+  float sq[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) sq[i] = sqrtf(v[i]);
+  if constexpr (SCAL & 48) {
+    // the denominator pairs by hand: 16 = the compiler's first-pass form (src1 = {step_size, rbc2},
+    // op_sel picks rbc2 for the LOW half), 32 = src1 = {rbc2, rbc2}, no op_sel
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 e2 = (f2){a.eps, a.eps};
+    const f2 s1 = (SCAL & 16) ? (f2){a.step_size, a.rbc2} : (f2){a.rbc2, a.rbc2};
+#pragma unroll
+    for (int i = 0; i < 4; i += 2) {
+      const f2 q = (f2){sq[i], sq[i + 1]};
+      f2 r;
+      if constexpr (SCAL & 16)
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(r) : "v"(q), "v"(s1), "v"(e2));
+      else
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(q), "v"(s1), "v"(e2));
+      d[i] = r.x;
+      d[i + 1] = r.y;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if constexpr (!(SCAL & 48)) d[i] = (SCAL & 4) ? asm_fma(sq[i], a.rbc2, a.eps) : sq[i] * a.rbc2 + a.eps;
+    u[i] = (SCAL & 8) ? asm_mul(a.step_size, m[i]) : a.step_size * m[i];
+    p[i] -= u[i] / d[i];
+  }
+  P = make_float4(p[0], p[1], p[2], p[3]);
+  Mm = make_float4(m[0], m[1], m[2], m[3]);
+  V = make_float4(v[0], v[1], v[2], v[3]);
+}
+template <int SCAL>
+__device__ __forceinline__ void adam_probe_range(dct::AdamArgs a, int64_t lo, int64_t hi, int blk, int nblk) {
+  bool pending = a.step_counter != nullptr;
+  const int64_t n4 = (hi < a.n ? hi : a.n) >> 2;
+  const int64_t stride = (int64_t)nblk * blockDim.x;
+  float4* p4 = reinterpret_cast<float4*>(a.p);
+  const float4* g4 = reinterpret_cast<const float4*>(a.g);
+  float4* m4 = reinterpret_cast<float4*>(a.m);
+  float4* v4 = reinterpret_cast<float4*>(a.v);
+  for (int64_t i = (lo >> 2) + (int64_t)blk * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 p = p4[i], m = m4[i], v = v4[i], g = g4[i];
+    if (pending) {
+      dct::adam_bias_correction(a);
+      pending = false;
+    }
+    adam4_probe<SCAL>(p, g, m, v, a);
+    p4[i] = p;
+    m4[i] = m;
+    v4[i] = v;
+  }
+}
+
+// synthetic stand-ins for the GEMM tiles (modes 4..7): 8 waves of back-to-back 16x16x32 bf16 MFMAs whose
+// operands come from LDS (ds_read_b128), refilled by 16-B LDS-DMA (global_load_lds_dwordx4, M0 set in
+// asm as the GEMM does) - ROLE bit 1: LDS-DMA refills, bit 2: ds_read operands (else registers)
+template <int ROLE>
+__device__ __forceinline__ void synth_tile(const uint16_t* src, float* sink) {
+  extern __shared__ __attribute__((aligned(16))) char dyn[];
+  typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  f4 acc[4];
+  for (int j = 0; j < 4; ++j) acc[j] = (f4){0.f, 0.f, 0.f, 0.f};
+  bf8 x = *reinterpret_cast<const bf8*>(src + (t & 1023) * 8), y = *reinterpret_cast<const bf8*>(src + ((t * 7) & 1023) * 8);
+  for (int it = 0; it < 256; ++it) {
+    if constexpr (ROLE & 1) {
+      const uint16_t* g = src + (((it * 512 + t) * 8) & ((1 << 22) - 1));
+      const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(dyn + ((it & 3) * 512 + wave * 64) * 16));
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(g), "s"(dst) : "memory");
+    }
+    if constexpr (ROLE & 2) {
+      x = *reinterpret_cast<const bf8*>(dyn + (((it + 1) & 3) * 512 + ((t * 5) & 511)) * 16);
+      y = *reinterpret_cast<const bf8*>(dyn + (((it + 2) & 3) * 512 + ((t * 3) & 511)) * 16);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, y, acc[k & 3], 0, 0, 0);
+    if constexpr (ROLE & 1) {
+      if ((it & 3) == 3) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    }
+  }
+  float r = 0.f;
+  for (int j = 0; j < 4; ++j) r += acc[j][0] + acc[j][2];
+  if (r == 1234.5f) sink[t] = r;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(512, 2) void ride_probe_kernel(dct::GemmArgs g, int splits, int gemm_wgs, dct::AdamArgs a,
                                                             int64_t lo, int64_t hi) {
   if ((int)blockIdx.x < gemm_wgs) {
     if constexpr (MODE == 3) return;
+    if constexpr (MODE >= 4 && MODE <= 7) {  // synthetic tile role (MODE - 4 = ROLE bits)
+      synth_tile<MODE - 4>(g.A, reinterpret_cast<float*>(g.C));
+      return;
+    }
     const int orig = blockIdx.x, xcd = orig & 7;
     const int q8 = gemm_wgs >> 3, r8 = gemm_wgs & 7;
     const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
     dct::gemm2_body<true, false, true, 128, 2, 4>(g, splits, wgid);
   } else if constexpr (MODE == 1) {
     dct::adam_scalar_range<true, 8>(a, lo, hi, blockIdx.x - gemm_wgs, gridDim.x - gemm_wgs);
+  } else if constexpr (MODE >= 4 && MODE <= 7) {
+    dct::adam_flat_range<true, 8>(a, lo, hi, blockIdx.x - gemm_wgs, gridDim.x - gemm_wgs);
+  } else if constexpr (MODE >= 16) {  // the probe copy, sites (MODE - 16) scalarised
+    adam_probe_range<MODE - 16>(a, lo, hi, blockIdx.x - gemm_wgs, gridDim.x - gemm_wgs);
   } else {
     dct::adam_flat_range<true, 8>(a, lo, hi, blockIdx.x - gemm_wgs, gridDim.x - gemm_wgs);
   }
@@ -41,6 +170,14 @@ __global__ __launch_bounds__(512, 2) void ride_probe_kernel(dct::GemmArgs g, int
 
 __global__ void ref_kernel(dct::AdamArgs a, int64_t lo, int64_t hi) {
   dct::adam_scalar_range<true, 8>(a, lo, hi, blockIdx.x, gridDim.x);
+}
+
+// mode 8: the float4 (packed) Adam as its OWN launch on a second stream, concurrent with GEMM-only
+// launches of the same tiles on the first stream - another kernel's packed fp32 beside the GEMM's
+// LDS-DMA (what an RCCL reduce kernel on a DDP comm stream would be: RCCL's fp32 sum kernels use
+// v_pk_add_f32)
+__global__ __launch_bounds__(512) void flat4_kernel(dct::AdamArgs a, int64_t lo, int64_t hi) {
+  dct::adam_flat_range<true, 8>(a, lo, hi, blockIdx.x, gridDim.x);
 }
 
 #define CK(x)                                                                            \
@@ -121,10 +258,41 @@ int main(int argc, char** argv) {
   const size_t lds = 4 * dct::G2_BYTES;
   void (*fn)(dct::GemmArgs, int, int, dct::AdamArgs, int64_t, int64_t) =
       mode == 0 || mode == 2 ? ride_probe_kernel<0> : (mode == 1 ? ride_probe_kernel<1> : ride_probe_kernel<3>);
+  switch (mode) {  // 16 + SCAL: the probe copy of the float4 body beside the GEMM tiles
+    case 4: fn = ride_probe_kernel<4>; break;   // float4 Adam beside synthetic MFMA tiles (register operands)
+    case 5: fn = ride_probe_kernel<5>; break;   // ... + LDS-DMA refills
+    case 6: fn = ride_probe_kernel<6>; break;   // ... operands by ds_read_b128, no LDS-DMA
+    case 7: fn = ride_probe_kernel<7>; break;   // ... LDS-DMA + ds_read_b128 (the GEMM's traffic)
+    case 16: fn = ride_probe_kernel<16>; break;
+    case 17: fn = ride_probe_kernel<17>; break;
+    case 18: fn = ride_probe_kernel<18>; break;
+    case 20: fn = ride_probe_kernel<20>; break;
+    case 24: fn = ride_probe_kernel<24>; break;
+    case 31: fn = ride_probe_kernel<31>; break;
+    case 32: fn = ride_probe_kernel<32>; break;   // 16 + 16: hand-paired denominator with op_sel
+    case 48: fn = ride_probe_kernel<48>; break;   // 16 + 32: hand-paired denominator, no op_sel
+    default: break;
+  }
   CK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  CK(hipFuncSetAttribute((const void*)ride_probe_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   long long bad_total = 0, bad_iters = 0;
+  hipStream_t sa = 0, sb = 0;
+  if (mode == 8) {
+    CK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+  }
   for (int it = 0; it < iters; ++it) {
     reset(p, m, v);
+    if (mode == 8) {
+      // GEMM tiles alone (no Adam workgroups) back to back on stream A; the packed Adam on stream B
+      // starts once the first GEMM launch is running
+      for (int k = 0; k < 4; ++k)
+        hipLaunchKernelGGL(ride_probe_kernel<1>, dim3(gemm_wgs), dim3(512), lds, sa, gg, splits, gemm_wgs, a, (int64_t)0,
+                           (int64_t)0);
+      hipLaunchKernelGGL(flat4_kernel, dim3(256), dim3(512), 0, sb, a, (int64_t)0, n);
+      CK(hipGetLastError());
+      CK(hipDeviceSynchronize());
+    } else
     hipLaunchKernelGGL(fn, dim3(gemm_wgs + adam_wgs), dim3(512), lds, 0, gg, splits, gemm_wgs, a, (int64_t)0, n);
     CK(hipGetLastError());
     CK(hipDeviceSynchronize());
@@ -133,10 +301,11 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(ov.data(), v, n * 4, hipMemcpyDeviceToHost));
     long long bp = 0, bm = 0, bv = 0;
     int64_t first = -1;
-    int comp_hist[4] = {0, 0, 0, 0};
+    int comp_hist[4] = {0, 0, 0, 0}, pass_hist[2] = {0, 0};
     for (int64_t i = 0; i < n; ++i) {
       if (std::memcmp(&op[i], &ref_p[i], 4)) {
         ++bp;
+        ++pass_hist[(i >> 2) >= 256 * 512 ? 1 : 0];
         ++comp_hist[i & 3];
         if (first < 0) first = i;
       }
@@ -149,9 +318,9 @@ int main(int argc, char** argv) {
       double ratio = 0.0;
       if (first >= 0) ratio = (op[first] - hp[first]) / (double)(ref_p[first] - hp[first]);
       std::printf("iter %d: p %lld m %lld v %lld differ; p by component x/y/z/w %d/%d/%d/%d; first %lld "
-                  "(update ratio %.1f, v %.3e)\n",
+                  "(update ratio %.1f, v %.3e); first / later loop pass %d / %d\n",
                   it, bp, bm, bv, comp_hist[0], comp_hist[1], comp_hist[2], comp_hist[3], (long long)first, ratio,
-                  first >= 0 ? ref_v[first] : 0.f);
+                  first >= 0 ? ref_v[first] : 0.f, pass_hist[0], pass_hist[1]);
     }
   }
   std::printf("mode %d: %lld of %d launches differ from the scalar one-launch Adam, %lld p elements in all\n", mode,
