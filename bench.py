@@ -73,6 +73,11 @@ def parse():
                    help="cpu: BASELINE config 1 (autograd engine, gloo) - the plumbing path")
     p.add_argument("--epoch-rows", type=int, default=None,
                    help="dataset size used for the reported epoch wall-clock (weather 100k, tabular 100M)")
+    p.add_argument("--reserve-cus", type=int, default=0,
+                   help="A/B: run the step on a stream masked to all CUs but N, the DDP bucket reducer's "
+                        "collectives on a stream masked to those N (hipExtStreamCreateWithCUMask)")
+    p.add_argument("--reserve-pattern", default="spread", choices=("spread", "low", "high"),
+                   help="which CU mask bits --reserve-cus takes: evenly spaced, the first N or the last N")
     p.add_argument("--no-epoch", action="store_true",
                    help="skip the measured epoch (weather models on GPU: one real epoch of --epoch-rows rows, "
                         "train + validation, timed after the step window)")
@@ -338,8 +343,47 @@ def setup_transformer(a, ctx):
     return eng, feats
 
 
+def _reserve_cus(a, eng):
+    """--reserve-cus N: a compute stream masked to every CU but N and, if the engine has a native
+    DDP bucket reducer, its comm stream masked to those N (the collectives then never share a CU with
+    the step's kernels).  Returns the compute stream to run the measurement on."""
+    import torch
+
+    from dct_amd.ops._native import native
+
+    nat = native()
+    ncu = nat.device_cu_count()
+    n = max(1, min(a.reserve_cus, ncu - 1))
+    if a.reserve_pattern == "spread":
+        cus = sorted({(i * ncu) // n for i in range(n)})
+    elif a.reserve_pattern == "low":
+        cus = list(range(n))
+    else:
+        cus = list(range(ncu - n, ncu))
+    words = (ncu + 31) // 32
+    comm = [0] * words
+    for c in cus:
+        comm[c // 32] |= 1 << (c % 32)
+    full = [0xFFFFFFFF if 32 * (w + 1) <= ncu else (1 << (ncu - 32 * w)) - 1 for w in range(words)]
+    compute = [f & ~c for f, c in zip(full, comm)]
+    red = getattr(eng, "reducer", None)
+    if red is not None and hasattr(red, "_r"):
+        red._r.set_comm_cu_mask(comm)
+    h = nat.cu_masked_stream(compute)
+    return torch.cuda.ExternalStream(h, device=torch.cuda.current_device()), cus
+
+
 def measure(a, ctx):
     """Set up a.model, run the W warmup steps, time exactly K steps; returns (result dict, ok)."""
+    import contextlib
+
+    import torch
+
+    with contextlib.ExitStack() as stack:
+        return _measure(a, ctx, stack)
+
+
+def _measure(a, ctx, stack):
     import torch
 
     cpu = a.device == "cpu"
@@ -356,6 +400,11 @@ def measure(a, ctx):
     else:
         eng, feats = (setup_tabular if tab else setup_weather)(a, ctx)
         loop = eng
+    reserved = None
+    if a.reserve_cus > 0 and not cpu:
+        rs, reserved = _reserve_cus(a, eng)
+        torch.cuda.synchronize()
+        stack.enter_context(torch.cuda.stream(rs))
     total_steps = a.warmup + a.steps
     n_items = loop.upload_epoch_indices(0, shuffle=True)
     if total_steps * a.batch > n_items:
@@ -454,6 +503,7 @@ def measure(a, ctx):
             "losses_finite": finite,
             "params_in_sync": in_sync,
             "xgmi_exchange_ok": xg_ok,
+            "reserved_cus": reserved,
             "device": torch.cuda.get_device_name(ctx.device) if not cpu else "cpu",
         },
     }

@@ -46,6 +46,7 @@ FILE_FLAGS = {"gemm_bf16.hip": ["-fno-slp-vectorize"],
               "mlp_block5.hip": ["-fno-slp-vectorize"] + MAX_ILP,
               "mlp_block5_xg.hip": ["-fno-slp-vectorize"],
               "mlp_block5_xgprof.hip": ["-fno-slp-vectorize"],
+              "mlp_block5_b8.hip": ["-fno-slp-vectorize"],
               "tt_block.hip": MAX_ILP,
               "tt_io.hip": MAX_ILP,
               "mlp_wave_single.hip": MAX_ILP,
@@ -88,8 +89,17 @@ def _flags(debug: bool = False, sanitize: bool = None):
     return f
 
 
+def _file_flags(base: str):
+    """FILE_FLAGS of one source, plus the A/B-build flags (tools/so_ab.sh variants): AB_HIPCC_FLAGS
+    (e.g. "-DB5_PRO=0") on the sources named in AB_HIPCC_FILES (comma-separated basenames)."""
+    extra = []
+    if base in os.environ.get("AB_HIPCC_FILES", "").split(","):
+        extra = os.environ.get("AB_HIPCC_FLAGS", "").split()
+    return FILE_FLAGS.get(base, []) + extra
+
+
 def _stamp(src: str, flags) -> str:
-    flags = list(flags) + FILE_FLAGS.get(os.path.basename(src), [])
+    flags = list(flags) + _file_flags(os.path.basename(src))
     h = hashlib.sha1()
     h.update(" ".join(flags).encode())
     for p in [src] + _headers():
@@ -107,7 +117,7 @@ def _compile(src: str, flags, verbose: bool):
         return obj, False
     lang = ["-x", "hip"] if src.endswith(".hip") else []
     tmp = f"{obj}.{os.getpid()}.tmp"  # per-process: concurrent builds never share a temp file
-    cmd = [os.path.join(ROCM, "bin", "hipcc")] + flags + FILE_FLAGS.get(base, []) + lang + ["-c", src, "-o", tmp]
+    cmd = [os.path.join(ROCM, "bin", "hipcc")] + flags + _file_flags(base) + lang + ["-c", src, "-o", tmp]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -620,7 +620,13 @@ PYBIND11_MODULE(_dct_native, m) {
       .def_property_readonly("inline_mode", &dct::BucketReducer::inline_mode)
       .def("enable_timing", &dct::BucketReducer::enable_timing, py::arg("check") = false)
       .def("read_timing", &dct::BucketReducer::read_timing)
-      .def("reset_timing", &dct::BucketReducer::reset_timing);
+      .def("reset_timing", &dct::BucketReducer::reset_timing)
+      .def("set_comm_cu_mask", &dct::BucketReducer::set_comm_cu_mask, py::arg("mask"))
+      .def_property_readonly("comm_cu_mask", &dct::BucketReducer::comm_cu_mask);
+  m.def("cu_masked_stream", &dct::cu_masked_stream, py::arg("mask"));
+  m.def("stream_destroy", &dct::stream_destroy, py::arg("stream"));
+  m.def("stream_cu_mask", &dct::stream_cu_mask, py::arg("stream"));
+  m.def("device_cu_count", &dct::device_cu_count);
   py::class_<dct::PeerExchange>(m, "PeerExchange")
       .def(py::init<int, int, int64_t>(), py::arg("world"), py::arg("rank"), py::arg("bytes"))
       .def("ipc_handle", [](const dct::PeerExchange& x) { return py::bytes(x.ipc_handle()); })

@@ -20,7 +20,7 @@ void knobs_reload() {
   Knobs k;
   const char* mk = std::getenv("DCT_MLP_KERNEL");
   k.mlp_force_lds = (mk && std::strcmp(mk, "lds") == 0) ? 1 : 0;
-  if (const char* b = std::getenv("DCT_MLP_BLOCK")) k.mlp_block = (b[0] == '0') ? 0 : (b[0] == '3' ? 3 : -1);
+  if (const char* b = std::getenv("DCT_MLP_BLOCK")) k.mlp_block = (b[0] == '0') ? 0 : (b[0] == '3' ? 3 : (b[0] == '8' ? 8 : -1));
   k.fused_head = env_int("DCT_FUSED_HEAD", 1) != 0;
   k.dw_into_adam = env_int("DCT_DW_INTO_ADAM", 1) != 0;
   k.reducer_inline = env_int("DCT_REDUCER_INLINE", -2);

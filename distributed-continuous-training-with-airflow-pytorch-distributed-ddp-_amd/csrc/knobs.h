@@ -11,7 +11,8 @@ namespace dct {
 struct Knobs {
   // fused MLP trainers (mlp_fused.hip dispatch, bindings.cpp plan)
   int mlp_force_lds = 0;    // DCT_MLP_KERNEL=lds: the LDS/block kernels even where the wave kernel fits
-  int mlp_block = -1;       // DCT_MLP_BLOCK: -1 auto, 0 generic LDS trainer, 3 force mlp_block3
+  int mlp_block = -1;       // DCT_MLP_BLOCK: -1 auto, 0 generic LDS trainer, 3 force mlp_block3, 8 mlp_block5's
+                            // two-micro-batch kernels at every batch (tests: == the one-micro-batch kernels at B <= 4)
   // wide-MLP step executor (mlp_executor.cpp; copied into each executor at construction)
   int fused_head = 1;       // DCT_FUSED_HEAD=0: the four-kernel head chain
   int dw_into_adam = 1;     // DCT_DW_INTO_ADAM=0: dW through g and the reduce pass

@@ -7,6 +7,7 @@
 namespace dct {
 
 void mlp_launch_block5_xg(int world, size_t bytes, hipStream_t st, const MlpShape& sh, const MlpArgs& a);
+void mlp_launch_block5_b8(size_t bytes, hipStream_t st, const MlpShape& sh, const MlpArgs& a);
 
 // in-kernel data-parallel launches of this kernel: 2 .. 8 ranks (one node), train mode; the profiling
 // instantiations exist for 2 / 4 / 8
@@ -18,7 +19,9 @@ bool mlp_block5_ok(const MlpShape& sh, const MlpArgs& a) {
                      (a.mode == 0 && b5_xg_world_ok(a.xg_world) && a.xg_rank >= 0 && a.xg_rank < a.xg_world &&
                       a.xg_recv != nullptr && a.xg_peers != nullptr && a.xg_status != nullptr &&
                       (a.prof == nullptr || a.xg_world == 2 || a.xg_world == 4 || a.xg_world == 8));
-  return aligned && mlp_block5_shape_ok(sh.dims, sh.L, a.B) &&
+  // per-rank batch 5..8 (two micro-batches per step, mlp_block5_b8.hip): no profiling instantiation
+  const bool b8_ok = (a.B <= blk5::B && sh.mlp_block != 8) || a.prof == nullptr;
+  return aligned && b8_ok && mlp_block5_shape_ok(sh.dims, sh.L, a.B) &&
          // train mode, or grad mode for ONE step (the DDP step path: grads + loss to grad_out, device cursor)
          ((a.mode == 0 && a.cursor == nullptr) || (a.mode == 1 && a.steps == 1 && a.grad_out != nullptr)) &&
          (a.loss_kind == 0 || a.loss_kind == 1) && a.pending == nullptr && (a.stage == nullptr || a.mode == 1) && xg_ok;
@@ -26,7 +29,7 @@ bool mlp_block5_ok(const MlpShape& sh, const MlpArgs& a) {
 
 bool mlp_block5_shape_ok(const int* dims, int L, int B) {
   return L == 3 && dims[1] == blk5::H && dims[2] == blk5::H && dims[0] >= 1 && dims[0] <= blk5::DMAX &&
-         dims[3] == blk5::C && B >= 1 && B <= blk5::B;
+         dims[3] == blk5::C && B >= 1 && B <= blk5::BMAX;
 }
 
 size_t mlp_block5_xg_bytes(int world) {
@@ -45,7 +48,9 @@ size_t mlp_block5_xg_bytes(int world) {
 hipError_t mlp_launch_block5(const MlpShape& sh, const MlpArgs& a, hipStream_t st) {
   const size_t bytes = (size_t)blk5::LDS_FLOATS * sizeof(float);
   const bool wd = a.wd != 0.f;
-  if (a.xg_world > 1) {
+  if (a.B > blk5::B || sh.mlp_block == 8) {
+    mlp_launch_block5_b8(bytes, st, sh, a);  // two micro-batches per step, every world size
+  } else if (a.xg_world > 1) {
     mlp_launch_block5_xg(a.xg_world, bytes, st, sh, a);  // mlp_block5_xg.hip
   } else if (a.mode == 1) {  // grad mode: no Adam, no moments
     if (a.loss_kind == 0) b5_launch<false, 0, false, true, false>(bytes, st, sh, a);

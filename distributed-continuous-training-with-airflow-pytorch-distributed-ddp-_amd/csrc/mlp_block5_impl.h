@@ -31,25 +31,32 @@
 namespace dct {
 
 namespace blk5 {
-constexpr int H = 128, NT = 512, NW = 8, KS = 16, DMAX = 8, B = 4, C = 2;
-constexpr int XT = 0;                     // [3][DMAX][4] input tiles, feature-major (4 rows each)
-constexpr int LAB = XT + 3 * DMAX * 4;    // [3][4] labels (int), 16 reserved
-constexpr int MSK = LAB + 16;             // [2][NW] uint64: h2 > 0 of (o = 16w + b/4, row b%4)
-constexpr int LOGP = MSK + 2 * NW * 2;    // [2][NW][C][4] logit shares (wave, class, row)
-constexpr int H1W = LOGP + 2 * NW * 8;    // [NW][KS][4] wave-private h1[k][row]
-constexpr int H1X = H1W + NW * KS * 4;    // [NW][4][KS] the same tile transposed (MFMA A operands)
+// B: rows of one micro-batch (the quad's four row lanes); a step of per-rank batch <= 4 MB runs MB of them
+constexpr int H = 128, NT = 512, NW = 8, KS = 16, DMAX = 8, B = 4, C = 2, MBMAX = 2, BMAX = B * MBMAX;
 constexpr int PSTR = 36;                  // partials: [o][wave][4] with a 36-float o stride
-constexpr int PART = H1X + NW * KS * 4;   // [2][H][PSTR]
-constexpr int W2L = PART + 2 * H * PSTR;  // [2][H][C] W2[c][o] (o-major), published by the owners
-constexpr int B2L = W2L + 2 * H * C;      // [2][4] b2
-constexpr int ABT = B2L + 8;              // [4] data-parallel launches: a wave's exchange timed out
-constexpr int TOTAL = ABT + 4;
+// LDS layout of the MB-micro-batch kernel (MB = 1: batch <= 4, the reference's; MB = 2: batch <= 8)
+template <int MB>
+struct Lds {
+  static constexpr int RB = B * MB;                        // rows of one step
+  static constexpr int XT = 0;                             // [3][DMAX][RB] input tiles, feature-major
+  static constexpr int LAB = XT + 3 * DMAX * RB;           // [3][RB] labels (int)
+  static constexpr int MSK = LAB + (MB == 1 ? 16 : 32);    // [2][NW] uint64: h2 > 0 of (o = 16w + b/4, row b%4)
+  static constexpr int LOGP = MSK + 2 * NW * 2;            // [2][NW][C][4] logit shares (wave, class, row)
+  static constexpr int H1W = LOGP + 2 * NW * 8;            // [MB][NW][KS][4] wave-private h1[k][row] per micro-batch
+  static constexpr int H1X = H1W + MB * NW * KS * 4;       // [NW][4][KS] the same tile transposed (MFMA A operands)
+  static constexpr int PART = H1X + NW * KS * 4;           // [2][H][PSTR]
+  static constexpr int W2L = PART + 2 * H * PSTR;          // [2][H][C] W2[c][o] (o-major), published by the owners
+  static constexpr int B2L = W2L + 2 * H * C;              // [2][4] b2
+  static constexpr int ABT = B2L + 8;                      // [4] data-parallel launches: a wave's exchange timed out
+  static constexpr int TOTAL = ABT + 4;
+  static_assert((H1W % 4) == 0 && (PART % 4) == 0 && (MSK % 4) == 0 && (LAB % 4) == 0 && (W2L % 4) == 0 &&
+                    (B2L % 4) == 0 && (H1X % 4) == 0 && (LOGP % 4) == 0,
+                "16-B aligned tiles");
+};
+static_assert(Lds<1>::TOTAL == 11036, "the batch <= 4 layout is round 5's");
 constexpr int STG = H * H;
-constexpr int LDS_FLOATS = TOTAL > 2 * STG ? TOTAL : 2 * STG;  // two staging tiles (prologue/epilogue)
+constexpr int LDS_FLOATS = Lds<MBMAX>::TOTAL > 2 * STG ? Lds<MBMAX>::TOTAL : 2 * STG;  // two staging tiles (prologue/epilogue)
 static_assert(LDS_FLOATS * 4 <= 160 * 1024, "fits the CU");
-static_assert((H1W % 4) == 0 && (PART % 4) == 0 && (MSK % 4) == 0 && (LAB % 4) == 0 && (W2L % 4) == 0 &&
-                  (B2L % 4) == 0 && (H1X % 4) == 0 && (LOGP % 4) == 0,
-              "16-B aligned tiles");
 using Stg = bku::Stage<H, NT>;
 constexpr float LOG2E = 1.4426950408889634f, LN2 = 0.6931471805599453f;
 }  // namespace blk5
@@ -221,17 +228,24 @@ __device__ __forceinline__ void adam_v2(v2f& p, v2f g, v2f& m, v2f& v, float b1,
   p = p - m * ((v2f){d.y, d.x} * R);
 }
 
+// MB: micro-batches of B = 4 rows per step (MB = 2: per-rank batch 5..8): every micro-batch runs the
+// forward and backward of its four rows on the same lanes (rows r0 + 4 mb), its gradients accumulate
+// in registers (dZ2 / the h1 tile stay for the one dW1 pass), the last one applies Adam to the sums.
 // LK: 0 = cross-entropy, 1 = MSE against the one-hot label; WD: L2 term in the update; ADAM = false:
 // grad mode (the DDP step: ONE step at the device batch cursor, gradients + batch loss to grad_out,
 // the previous step's all-reduced loss to loss_out[cursor - 1]; no moments read or written);
 // XW > 1: train mode of one rank of XW data-parallel ranks (b5x above); RK >= 0: that rank as a
 // compile-time constant (every ownership test folds, the all-gather loads land straight in the W1
 // registers; fewer live registers and spills than the runtime-rank kernel, RK = -1)
-template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true, int XW = 1, int RK = -1>
+template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true, int XW = 1, int RK = -1, int MB = 1>
 __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, MlpArgs a) {
   using namespace blk5;
   using namespace bku;
   static_assert(XW == 1 || (ADAM && XW >= 2 && XW <= 8), "exchange: train mode, 2..8 ranks");
+  static_assert(MB >= 1 && MB <= MBMAX, "micro-batches per step");
+  using LY = Lds<MB>;
+  constexpr int RB = LY::RB, XT = LY::XT, LAB = LY::LAB, MSK = LY::MSK, LOGP = LY::LOGP, H1W = LY::H1W;
+  constexpr int H1X = LY::H1X, PART = LY::PART, W2L = LY::W2L, B2L = LY::B2L, ABT = LY::ABT, TOTAL = LY::TOTAL;
   constexpr int PS = XW > 1 ? 32 : 16;  // PROF: stamp slots per wave (XW > 1: the exchange phases 15..20)
   using XL = b5x::Lay<XW>;
   constexpr int NO = XL::NO;
@@ -250,7 +264,7 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   // batch's prefetch element, as VECTOR loads (a scalar load's wait would stall the whole prologue
   // behind it, lgkmcnt is shared with the LDS staging); the dependent X / Y gathers follow the W1 loads
   const int Bsz = a.B;
-  const int fb = tid & 3, fd = tid >> 2;
+  const int fb = tid & (RB - 1), fd = tid / RB;  // (RB: a power of two)
   // prefetch roles: thread -> (row pb, feature pk) of the next batch, or (row pb, label)
   const int nel = Bsz * D0;
   int role = 0, pb = 0, pk = 0;
@@ -264,12 +278,12 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   uint32_t st_tag = 0u, st_x = 0u, st_lab = 0u;
   if (stp) {
     st_tag = a.stage[0];
-    if (tid < B * DMAX && fd < D0 && fb < Bsz) st_x = a.stage[64 + fb * D0 + fd];
+    if (tid < RB * DMAX && fd < D0 && fb < Bsz) st_x = a.stage[64 + fb * D0 + fd];
     if (tid < Bsz) st_lab = a.stage[64 + nel + tid];
   }
   const int cur0 = (!ADAM && a.cursor) ? sload(a.cursor) : 0;  // grad mode: batch index from the device cursor
   const int bs0 = min(Bsz, a.n_items - cur0 * Bsz);
-  const bool first_ok = tid < B * DMAX && fb < bs0;
+  const bool first_ok = tid < RB * DMAX && fb < bs0;
   // unconditional load at a clamped index, masked after: a load behind the first_ok branch compiled
   // to a branch with `s_waitcnt vmcnt(0)` inside it - one full memory round trip at kernel start,
   // before a single W1 load was issued
@@ -342,15 +356,15 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     if (role && (cur0 + 1) * Bsz + pb < a.n_items) ridx_next = a.idx[(cur0 + 1) * Bsz + pb];
     if ((int)st_tag == cur0 + 1) {  // wave-uniform: staged by the launch before, for this batch
       if (first_ok && fd < D0) x_first = __uint_as_float(st_x);
-      if (tid < B && tid < bs0) lab_first = (int)st_lab;
+      if (tid < RB && tid < bs0) lab_first = (int)st_lab;
     } else {  // first launch of a run / after a reset: the gather
       const int rb = first_ok ? a.idx[cur0 * Bsz + fb] : 0;
       if (first_ok && fd < D0) x_first = a.X[(size_t)rb * a.ldx + fd];
-      if (tid < B && tid < bs0) lab_first = a.Y[rb];
+      if (tid < RB && tid < bs0) lab_first = a.Y[rb];
     }
   } else {
     if (first_ok && fd < D0) x_first = a.X[(size_t)rb_first * a.ldx + fd];
-    if (tid < B && tid < bs0) lab_first = a.Y[rb_first];  // tid < 4: fb = tid
+    if (tid < RB && tid < bs0) lab_first = a.Y[rb_first];  // tid < RB: fb = tid
   }
 
   // ---- W1 k-slice + moments into registers through the swizzled staging tiles
@@ -381,8 +395,8 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
   // ---- LDS: first batch into input buffer 0, W2 / b2 into publish buffer 0
   for (int e = 4 * tid; e < TOTAL; e += 4 * NT) *reinterpret_cast<float4*>(lds + e) = make_float4(0.f, 0.f, 0.f, 0.f);
   lds_barrier();
-  if (tid < B * DMAX) lds[XT + (tid >> 2) * 4 + (tid & 3)] = x_first;
-  if (tid < B) reinterpret_cast<int*>(lds + LAB)[tid] = lab_first;
+  if (tid < RB * DMAX) lds[XT + fd * RB + fb] = x_first;
+  if (tid < RB) reinterpret_cast<int*>(lds + LAB)[tid] = lab_first;
   if (own_w2) lds[W2L + u * C + r0] = r0 ? pw2[1] : pw2[0];
   if (own_b2) lds[B2L + l] = pb2;
   const uint32_t* pf_base = role == 1 ? reinterpret_cast<const uint32_t*>(a.X) + pk : reinterpret_cast<const uint32_t*>(a.Y);
@@ -466,11 +480,16 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     }
   };
   const int tb = tid * 16;  // this thread's granule inside a slot
-  // dropout factors of this lane's (row r0, unit u) elements at the first step
-  const uint32_t el0 = b5_elem(0, r0, u), el1 = b5_elem(1, r0, u);
-  float f1 = b5_drop(a.seed, step_base, el0, p_drop, scale);
-  float f2 = b5_drop(a.seed, step_base, el1, p_drop, scale);
-  float* h1w = lds + H1W + w * (KS * 4);
+  // dropout factors of this lane's (row r0 + 4 mb, unit u) elements at the first step
+  uint32_t el0[MB], el1[MB];
+  float f1[MB], f2[MB];
+#pragma unroll
+  for (int hf = 0; hf < MB; ++hf) {
+    el0[hf] = b5_elem(0, r0 + B * hf, u);
+    el1[hf] = b5_elem(1, r0 + B * hf, u);
+    f1[hf] = b5_drop(a.seed, step_base, el0[hf], p_drop, scale);
+    f2[hf] = b5_drop(a.seed, step_base, el1[hf], p_drop, scale);
+  }
   float* h1x = lds + H1X + w * (KS * 4);
   float eye[4];  // one-hot of lane % 4 (B operands of the MFMA quad transposes)
 #pragma unroll
@@ -489,200 +508,45 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
     const uint32_t gstep = step_base + (uint32_t)s;
     const int xbn = xb == 2 ? 0 : xb + 1;
     const int pbuf = s & 1, nbuf = pbuf ^ 1;
-    const float* xT = lds + XT + xb * DMAX * 4;
+    const float* xT = lds + XT + xb * DMAX * RB;
     const bool have_next = (s + 1 < a.steps);
     const int bs_next = have_next ? min(Bsz, a.n_items - (sb + 1) * Bsz) : 0;
     const uint32_t raw_next = pf_base[(size_t)ridx_next * pf_stride];
     const int nx2 = min((sb + 2) * Bsz + pb, a.n_items - 1);
     const int ridx_next2 = a.idx[nx2 < 0 ? 0 : nx2];
-
-    // ---- F1: h1[u][r0] (quad reduce-scatter over the input slices); the tile stays for dW0
-    const float4 xa = *reinterpret_cast<const float4*>(xT + r0 * 4);
-    const float4 xc = *reinterpret_cast<const float4*>(xT + (r0 + 4) * 4);
-    float h1;
-    {
-      const float acc0 = w0[0] * xa.x + w0[1] * xc.x, acc1 = w0[0] * xa.y + w0[1] * xc.y;
-      const float acc2 = w0[0] * xa.z + w0[1] * xc.z, acc3 = w0[0] * xa.w + w0[1] * xc.w;
-      const bool qb1 = (r0 >> 1) & 1, qb0 = r0 & 1;
-      const float k0 = qb1 ? acc2 : acc0, k1 = qb1 ? acc3 : acc1;
-      const float s0 = qb1 ? acc0 : acc2, s1 = qb1 ? acc1 : acc3;
-      const float e0 = k0 + dpp<QP_X2>(s0), e1 = k1 + dpp<QP_X2>(s1);
-      const float kq = qb0 ? e1 : e0, sq = qb0 ? e0 : e1;
-      h1 = fmaxf(kq + dpp<QP_X1>(sq) + pb0, 0.f) * f1;
-      h1w[l] = h1;                    // [k = l / 4][row = l % 4]
-      h1x[r0 * KS + (l >> 2)] = h1;   // [row][k]
-    }
-    __builtin_amdgcn_wave_barrier();
-    B5STAMP(0)
-    // ---- F2: this wave's k-slice partials of all 128 outputs x 4 rows (4x4x1 MFMA: A = h[k][lane % 4],
-    // B = the lane's own weight; C lands as acc[j][row] of output o = l + 64 j)
-    {
-      // one accumulator per (j, q): chains of 4 dependent MFMAs (40 cycles each) instead of 16
-      f32x4_t cq[2][KS / 4];
-#pragma unroll
-      for (int q = 0; q < KS / 4; ++q) {
-        const float4 hq = *reinterpret_cast<const float4*>(h1x + r0 * KS + 4 * q);
-        const float hv[4] = {hq.x, hq.y, hq.z, hq.w};
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          cq[j][q] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) cq[j][q] = mfma4(hv[e], W[j][2 * q + (e >> 1)][e & 1], cq[j][q]);
-        }
-      }
-      f32x4_t cj[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) cj[j] = (cq[j][0] + cq[j][1]) + (cq[j][2] + cq[j][3]);
-      float* part = lds + PART + pbuf * (H * PSTR);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        *reinterpret_cast<float4*>(part + (l + 64 * j) * PSTR + w * 4) = make_float4(cj[j][0], cj[j][1], cj[j][2], cj[j][3]);
-    }
-    if (stp) {  // grad mode: hand the next batch to the next launch (tag last, 0 = nothing staged)
-      const int bs_st = min(Bsz, a.n_items - (sb + 1) * Bsz);
-      if (role) a.stage[64 + tid] = pb < bs_st ? raw_next : 0u;
-      if (tid == 0) a.stage[0] = bs_st > 0 ? (uint32_t)(sb + 2) : 0u;
-    }
-    // next batch into the next input buffer (its last readers finished before the previous barrier B)
-    if (role) {
-      const uint32_t v = (have_next && pb < bs_next) ? raw_next : 0u;
-      uint32_t* dst = (role == 1) ? reinterpret_cast<uint32_t*>(lds + XT + xbn * DMAX * 4) + pk * 4 + pb
-                                  : reinterpret_cast<uint32_t*>(lds + LAB) + xbn * 4 + pb;
-      *dst = v;
-    }
-    ridx_next = role ? ridx_next2 : 0;
-    B5STAMP(1)
-    lds_barrier();  // A: all partials of this step are in (and W2 / b2 of the previous publish)
-    B5STAMP(2)
-    if constexpr (XW > 1) {
-      // a wave's exchange of the previous step timed out (flag written before this barrier):
-      // the whole workgroup leaves together, the epilogue writes nothing back
-      if (lds[ABT] != 0.f) break;
-    }
-
-    // ---- backward operands published before A: W2 columns l, l + 64 (dZ2), b2 of class cb, the
-    // label of row r0 - issued first, consumed after barrier B
-    const float2 wv0 = *reinterpret_cast<const float2*>(lds + W2L + pbuf * (H * C) + l * C);
-    const float2 wv1 = *reinterpret_cast<const float2*>(lds + W2L + pbuf * (H * C) + (l + 64) * C);
-    const float b2c = lds[B2L + pbuf * 4 + cb];
-    const int lab = reinterpret_cast<const int*>(lds + LAB)[xb * 4 + r0];
-    // ---- h2[u][r0] of this wave's 16 outputs, its logit shares, the h2 > 0 mask
-    float h2;
-    {
-      const float* pr = lds + PART + pbuf * (H * PSTR) + u * PSTR + r0;
-      float q[NW];
-#pragma unroll
-      for (int ww = 0; ww < NW; ++ww) q[ww] = pr[4 * ww];
-      const float z = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
-      h2 = fmaxf(z + pb1, 0.f) * f2;
-      const float t0s = sum_bits2to5(pw2[0] * h2), t1s = sum_bits2to5(pw2[1] * h2);  // row r0's shares
-      const unsigned long long msk = __ballot(h2 > 0.f);
-      if (l < 8) lds[LOGP + pbuf * (NW * 8) + w * 8 + l] = cb ? t1s : t0s;  // [wave][class][row]
-      if (l == 0)
-        *reinterpret_cast<uint2*>(lds + MSK + pbuf * (NW * 2) + w * 2) = make_uint2((uint32_t)msk, (uint32_t)(msk >> 32));
-    }
-    B5STAMP(3)
-    lds_barrier();  // B: logit shares and masks of every wave are in
-    B5STAMP(4)
-
-    // ---- loss: lane (share l / 8, class cb, row r0) -> logit (r0, cb) of the batch
-    const uint2 mw0 = *reinterpret_cast<const uint2*>(lds + MSK + pbuf * (NW * 2) + 2 * (l >> 4));
-    const uint2 mw1 = *reinterpret_cast<const uint2*>(lds + MSK + pbuf * (NW * 2) + 2 * ((l >> 4) + 4));
-    float dz, lv;
-    {
-      float lg = lds[LOGP + pbuf * (NW * 8) + l];
-      lg += dpp<ROR8>(lg);          // shares w', w' ^ 1 (lane bit 3)
-      lg = swap16_sum(lg, lg);      // lane bit 4
-      lg = swap32_sum(lg, lg);      // lane bit 5
-      const float z = lg + b2c;
-      const float zo = dpp<ROR4>(z);  // the other class of the same row (lane bit 2 flipped in the
-                                      // row-replicated copies)
-      const bool live = r0 < bs;
-      const float invb = __builtin_amdgcn_rcpf((float)(bs > 0 ? bs : 1));
-      const float inv = live ? invb : 0.f;
-      const float y = (cb == lab) ? 1.f : 0.f;
-      if constexpr (LK == 0) {
-        const float t = zo - z;
-        const float e = __builtin_amdgcn_exp2f(t * LOG2E);
-        const float pc = __builtin_amdgcn_rcpf(1.f + e);  // softmax of class cb
-        dz = (pc - y) * inv;
-        // row loss (lane of the labelled class): softplus(z_other - z_label), off the dz path
-        const float sp = fmaxf(t, 0.f) + LN2 * __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-fabsf(t) * LOG2E));
-        lv = (live && cb == lab) ? sp : 0.f;
-      } else {
-        const float d = z - y;
-        dz = d * inv;               // d (2 / C) / bs
-        lv = live ? 0.5f * d * d : 0.f;  // / C
-      }
-    }
-    // dlogits of the batch, wave-uniform: dz3[r][c] lives in lane 4c + r
-    float dz3[4][C];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int c = 0; c < C; ++c) dz3[r][c] = rl(dz, 4 * c + r);
     const uint32_t xtag = gstep + 1u;  // XW > 1: this step's exchange tag and parity slab
     const int xpar = (int)(gstep & 1u);
-    float xbl = 0.f;                   // XW > 1: this rank's batch loss (wave 0)
-    if (w == 0) {  // batch loss: lanes 0..7 hold (class, row) terms
-      float t = lv + dpp<QP_X1>(lv);
-      t += dpp<QP_X2>(t);
-      t += dpp<ROR4>(t);
-      const float bl = bs > 0 ? t * __builtin_amdgcn_rcpf((float)bs) : 0.f;
-      if constexpr (ADAM && XW > 1) {
-        // sync_dist: one granule to every peer now, the rank-ordered mean after the all-gather
-        xbl = rl(bl, 0);
-        if (l == 0) {
-#pragma unroll
-          for (int q = 0; q < XW; ++q)
-            if (q != xrank) b5x::put(xpr[q], XL::ls(xpar, xrank), xbl, 0.f, xtag);
-        }
-      } else if constexpr (ADAM) {
-        if (l == 0 && a.loss_out) a.loss_out[s] = bl;
-      } else {
-        if (l == 0) a.grad_out[sh.P] = bl;
-      }
-    }
-    B5STAMP(5)
-
     const int t = t0 + s + 1;
-    const float step_size = a.lr * __builtin_amdgcn_rcpf(1.f - pow_t(l2b1, (float)t));
-    const float rbc2 = __builtin_amdgcn_rsqf(1.f - pow_t(l2b2, (float)t));
-    const float rss = __builtin_amdgcn_rcpf(step_size);
-    const float aA = sqc2 * rbc2 * rss * rc1, aE = a.eps * rss * rc1;
-    // ---- dZ2 of outputs o = l + 64 j, all rows (old W2, mask bits of the owning wave)
-    float dz2[2][4];
-    {
-      const int sh4 = 4 * (l & 15);
+    // per micro-batch state that outlives it: dZ2 (the one dW1 pass runs over every micro-batch), and
+    // the gradient sums of the small parameters (the last micro-batch applies Adam to them)
+    float dz2m[MB][2][4];
+    float dz = 0.f, xbl = 0.f, tls = 0.f;  // last micro-batch's dlogit; XW > 1: batch loss; loss sum
+    float h2 = 0.f, h1 = 0.f;
+    float gw0s = 0.f, gw1s = 0.f, gb1s = 0.f, gbs = 0.f, g0s = 0.f, g1s = 0.f, db0s = 0.f;
+    float aA = 0.f, aE = 0.f;
+    v2f GO[NO];  // XW > 1 (reduce-scatter): gradients of the W1 pairs this rank owns
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const float2 wv = j ? wv1 : wv0;
-        const uint2 mw = j ? mw1 : mw0;
-        const uint32_t nib = ((sh4 < 32 ? mw.x : mw.y) >> (sh4 & 31)) & 15u;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float g = wv.x * dz3[r][0] + wv.y * dz3[r][1];
-          dz2[j][r] = ((nib >> r) & 1u) ? g * scale : 0.f;
-        }
-      }
-    }
+    for (int t2 = 0; t2 < NO; ++t2) GO[t2] = (v2f){0.f, 0.f};
+    float xg_own = 0.f, xg_bx = 0.f;  // XW > 1: this lane's second small gradient pair
+    v2f xs_g0 = (v2f){0.f, 0.f}, xs_g1 = (v2f){0.f, 0.f};  // XW > 1: the small gradient pairs
+    bool abort_step = false;
     // ---- dW1 pass (see its call sites)
-    v2f GO[NO];     // XW > 1 (reduce-scatter): gradients of the W1 pairs this rank owns
-#pragma unroll
-    for (int t = 0; t < NO; ++t) GO[t] = (v2f){0.f, 0.f};
     auto dw1_pass = [&]() {
       // ---- dW1 (MFMA: A = h1[4q + lane % 4][r], B = this lane's dZ2, C register m = the gradient of
-      // its own w1[j][4q + m]) + packed Adam on pairs of consecutive k
+      // its own w1[j][4q + m], summed over every micro-batch's rows) + packed Adam on pairs of consecutive k
 #pragma unroll
       for (int q = 0; q < KS / 4; ++q) {
-        const float4 hq = *reinterpret_cast<const float4*>(h1w + (4 * q + r0) * 4);
-        const float hv[4] = {hq.x, hq.y, hq.z, hq.w};
         f32x4_t g[2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          g[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < 2; ++j) g[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int r = 0; r < 4; ++r) g[j] = mfma4(hv[r], dz2[j][r], g[j]);
+        for (int hf = 0; hf < MB; ++hf) {
+          const float4 hq = *reinterpret_cast<const float4*>(lds + H1W + (hf * NW + w) * (KS * 4) + (4 * q + r0) * 4);
+          const float hv[4] = {hq.x, hq.y, hq.z, hq.w};
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) g[j] = mfma4(hv[r], dz2m[hf][j][r], g[j]);
         }
 
         if constexpr (ADAM && XW > 1) {
@@ -711,118 +575,321 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
         }
       }
     };
-    if constexpr (XW > 1) {
-      dw1_pass();
-      B5STAMP(15)  // dW1 MFMA + gradient pushes
-    }
-    // ---- owners: dW2[:, u], db1[u] (quad sums), W2 / b1 / b2 Adam, W2 / b2 published
-    float xg_own = 0.f, xg_bx = 0.f;  // XW > 1: this lane's second small gradient pair
-    {
-      const float d_own = dz, d_oth = dpp<ROR4>(dz);  // dlogit (r0, cb), (r0, 1 - cb)
-      const float dr0 = cb ? d_oth : d_own, dr1 = cb ? d_own : d_oth;
-      const float gw0 = quad_sum(dr0 * h2), gw1 = quad_sum(dr1 * h2);
-      float gdz = pw2[0] * dr0 + pw2[1] * dr1;
-      gdz = h2 > 0.f ? gdz * scale : 0.f;
-      const float gb1 = quad_sum(gdz);
-      // updates run in every lane (no control flow around loop-carried registers: a conditional update
-      // costs a register copy per value at the loop back edge); only the owners' results are kept
-      // (W2[r0][u] is broadcast from quad lanes 0 / 1, b2 published by wave 0's lanes 0 / 1)
-      float pown = (r0 & 1) ? pw2[1] : pw2[0];
-      const float gown = (r0 & 1) ? gw1 : gw0;
-      const float gb = (l & 1) ? (dz3[0][1] + dz3[1][1]) + (dz3[2][1] + dz3[3][1])
-                               : (dz3[0][0] + dz3[1][0]) + (dz3[2][0] + dz3[3][0]);
-      if constexpr (ADAM && XW > 1) {  // exchanged with the W0 gradients below
-        xg_own = gown;
-        xg_bx = r0 == 1 ? gb1 : gb;  // (r0 0: db0, known after dZ1)
-      } else if constexpr (ADAM) {
-        adam_pair<WD>(pown, gown, mw2, vw2, pb1, gb1, mb1, vb1, a.b1, a.b2, a.wd, aA, aE);
-        pw2[0] = dpp<QB0>(pown);
-        pw2[1] = dpp<QB1>(pown);
-        if (own_w2) lds[W2L + nbuf * (H * C) + u * C + r0] = pown;
-        adam_scaled<WD>(pb2, gb, mb2, vb2, a.b1, a.b2, a.wd, aA, aE);
-        if (own_b2) lds[B2L + nbuf * 4 + l] = pb2;
-      } else {  // grad mode (one step): dW2[r0][u], db1[u], db2 to the flat gradient
-        if (own_w2) a.grad_out[fw2] = gown;
-        if (r0 == 0) a.grad_out[bo1 + u] = gb1;
-        if (own_b2) a.grad_out[fb2] = gb;
+
+#pragma unroll
+    for (int hf = 0; hf < MB; ++hf) {
+      const bool last = hf == MB - 1;    // (constant once unrolled)
+      const int mpar = MB == 1 ? pbuf : hf;  // PART / LOGP / MSK buffer of this micro-batch
+      float* h1w = lds + H1W + (hf * NW + w) * (KS * 4);
+
+      // ---- F1: h1[u][r0] (quad reduce-scatter over the input slices); the tile stays for dW0
+      const float4 xa = *reinterpret_cast<const float4*>(xT + r0 * RB + B * hf);
+      const float4 xc = *reinterpret_cast<const float4*>(xT + (r0 + 4) * RB + B * hf);
+      {
+        const float acc0 = w0[0] * xa.x + w0[1] * xc.x, acc1 = w0[0] * xa.y + w0[1] * xc.y;
+        const float acc2 = w0[0] * xa.z + w0[1] * xc.z, acc3 = w0[0] * xa.w + w0[1] * xc.w;
+        const bool qb1 = (r0 >> 1) & 1, qb0 = r0 & 1;
+        const float k0 = qb1 ? acc2 : acc0, k1 = qb1 ? acc3 : acc1;
+        const float s0 = qb1 ? acc0 : acc2, s1 = qb1 ? acc1 : acc3;
+        const float e0 = k0 + dpp<QP_X2>(s0), e1 = k1 + dpp<QP_X2>(s1);
+        const float kq = qb0 ? e1 : e0, sq = qb0 ? e0 : e1;
+        h1 = fmaxf(kq + dpp<QP_X1>(sq) + pb0, 0.f) * f1[hf];
+        h1w[l] = h1;                    // [k = l / 4][row = l % 4]
+        h1x[r0 * KS + (l >> 2)] = h1;   // [row][k]
       }
-    }
-    B5STAMP(6)
-    // ---- dZ1 = W1^T dZ2 over this wave's k-slice, lane l keeps its own (unit u, row r0)
-    float dz1 = 0.f;
-    if constexpr (DXM) {
-      // on the 4x4x1 MFMA: each quad's 4x4 blocks of W1 (rows o = 4b + i + 64 j, columns k = 4q + m)
-      // and of dZ2 are transposed across the quad (MFMA, exact), so the call index runs over the block's 8
-      // outputs and lane (b, n) accumulates sum_o W1[o][4q + m] dZ2[o][n] for m = 0..3; the 16
-      // blocks' partials are then reduce-scattered over lane bits 2..5 to lane (b' = k, n)
-      float dzt[2][4];
+      __builtin_amdgcn_wave_barrier();
+      B5STAMP(0)
+      // ---- F2: this wave's k-slice partials of all 128 outputs x 4 rows (4x4x1 MFMA: A = h[k][lane % 4],
+      // B = the lane's own weight; C lands as acc[j][row] of output o = l + 64 j)
+      {
+        // one accumulator per (j, q): chains of 4 dependent MFMAs (40 cycles each) instead of 16
+        f32x4_t cq[2][KS / 4];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const f32x4_t t = quad_transpose_mf(dz2[j], eye);
+        for (int q = 0; q < KS / 4; ++q) {
+          const float4 hq = *reinterpret_cast<const float4*>(h1x + r0 * KS + 4 * q);
+          const float hv[4] = {hq.x, hq.y, hq.z, hq.w};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) dzt[j][i] = t[i];
+          for (int j = 0; j < 2; ++j) {
+            cq[j][q] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) cq[j][q] = mfma4(hv[e], W[j][2 * q + (e >> 1)][e & 1], cq[j][q]);
+          }
+        }
+        f32x4_t cj[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) cj[j] = (cq[j][0] + cq[j][1]) + (cq[j][2] + cq[j][3]);
+        float* part = lds + PART + mpar * (H * PSTR);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          *reinterpret_cast<float4*>(part + (l + 64 * j) * PSTR + w * 4) = make_float4(cj[j][0], cj[j][1], cj[j][2], cj[j][3]);
       }
-      float P[16];
+      if (hf == 0) {
+        if (stp) {  // grad mode: hand the next batch to the next launch (tag last, 0 = nothing staged)
+          const int bs_st = min(Bsz, a.n_items - (sb + 1) * Bsz);
+          if (role) a.stage[64 + tid] = pb < bs_st ? raw_next : 0u;
+          if (tid == 0) a.stage[0] = bs_st > 0 ? (uint32_t)(sb + 2) : 0u;
+        }
+        // next batch into the next input buffer (its last readers finished before the previous barrier B)
+        if (role) {
+          const uint32_t v = (have_next && pb < bs_next) ? raw_next : 0u;
+          uint32_t* dst = (role == 1) ? reinterpret_cast<uint32_t*>(lds + XT + xbn * DMAX * RB) + pk * RB + pb
+                                      : reinterpret_cast<uint32_t*>(lds + LAB) + xbn * RB + pb;
+          *dst = v;
+        }
+        ridx_next = role ? ridx_next2 : 0;
+      }
+      B5STAMP(1)
+      lds_barrier();  // A: all partials of this step are in (and W2 / b2 of the previous publish)
+      B5STAMP(2)
+      if constexpr (XW > 1) {
+        // a wave's exchange of the previous step timed out (flag written before this barrier):
+        // the whole workgroup leaves together, the epilogue writes nothing back
+        if (lds[ABT] != 0.f) {
+          abort_step = true;
+          break;
+        }
+      }
+
+      // ---- backward operands published before A: W2 columns l, l + 64 (dZ2), b2 of class cb, the
+      // label of row r0 - issued first, consumed after barrier B
+      const float2 wv0 = *reinterpret_cast<const float2*>(lds + W2L + pbuf * (H * C) + l * C);
+      const float2 wv1 = *reinterpret_cast<const float2*>(lds + W2L + pbuf * (H * C) + (l + 64) * C);
+      const float b2c = lds[B2L + pbuf * 4 + cb];
+      const int lab = reinterpret_cast<const int*>(lds + LAB)[xb * RB + B * hf + r0];
+      // ---- h2[u][r0] of this wave's 16 outputs, its logit shares, the h2 > 0 mask
+      {
+        const float* pr = lds + PART + mpar * (H * PSTR) + u * PSTR + r0;
+        float q[NW];
 #pragma unroll
-      for (int q = 0; q < KS / 4; ++q) {
-        f32x4_t acc[2];  // one chain per j (4 dependent MFMAs each)
+        for (int ww = 0; ww < NW; ++ww) q[ww] = pr[4 * ww];
+        const float z = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+        h2 = fmaxf(z + pb1, 0.f) * f2[hf];
+        const float t0s = sum_bits2to5(pw2[0] * h2), t1s = sum_bits2to5(pw2[1] * h2);  // row r0's shares
+        const unsigned long long msk = __ballot(h2 > 0.f);
+        if (l < 8) lds[LOGP + mpar * (NW * 8) + w * 8 + l] = cb ? t1s : t0s;  // [wave][class][row]
+        if (l == 0)
+          *reinterpret_cast<uint2*>(lds + MSK + mpar * (NW * 2) + w * 2) = make_uint2((uint32_t)msk, (uint32_t)(msk >> 32));
+      }
+      B5STAMP(3)
+      lds_barrier();  // B: logit shares and masks of every wave are in
+      B5STAMP(4)
+
+      // ---- loss: lane (share l / 8, class cb, row r0) -> logit (r0, cb) of the micro-batch
+      const uint2 mw0 = *reinterpret_cast<const uint2*>(lds + MSK + mpar * (NW * 2) + 2 * (l >> 4));
+      const uint2 mw1 = *reinterpret_cast<const uint2*>(lds + MSK + mpar * (NW * 2) + 2 * ((l >> 4) + 4));
+      float lv;
+      {
+        float lg = lds[LOGP + mpar * (NW * 8) + l];
+        lg += dpp<ROR8>(lg);          // shares w', w' ^ 1 (lane bit 3)
+        lg = swap16_sum(lg, lg);      // lane bit 4
+        lg = swap32_sum(lg, lg);      // lane bit 5
+        const float z = lg + b2c;
+        const float zo = dpp<ROR4>(z);  // the other class of the same row (lane bit 2 flipped in the
+                                        // row-replicated copies)
+        const bool live = r0 + B * hf < bs;
+        const float invb = __builtin_amdgcn_rcpf((float)(bs > 0 ? bs : 1));
+        const float inv = live ? invb : 0.f;
+        const float y = (cb == lab) ? 1.f : 0.f;
+        if constexpr (LK == 0) {
+          const float tt = zo - z;
+          const float e = __builtin_amdgcn_exp2f(tt * LOG2E);
+          const float pc = __builtin_amdgcn_rcpf(1.f + e);  // softmax of class cb
+          dz = (pc - y) * inv;
+          // row loss (lane of the labelled class): softplus(z_other - z_label), off the dz path
+          const float sp = fmaxf(tt, 0.f) + LN2 * __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-fabsf(tt) * LOG2E));
+          lv = (live && cb == lab) ? sp : 0.f;
+        } else {
+          const float d = z - y;
+          dz = d * inv;               // d (2 / C) / bs
+          lv = live ? 0.5f * d * d : 0.f;  // / C
+        }
+      }
+      // dlogits of the micro-batch, wave-uniform: dz3[r][c] lives in lane 4c + r
+      float dz3[4][C];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < C; ++c) dz3[r][c] = rl(dz, 4 * c + r);
+      if (w == 0) {  // batch loss: lanes 0..7 hold (class, row) terms
+        float tl = lv + dpp<QP_X1>(lv);
+        tl += dpp<QP_X2>(tl);
+        tl += dpp<ROR4>(tl);
+        tls = hf == 0 ? tl : tls + tl;
+        if (last) {
+          const float bl = bs > 0 ? tls * __builtin_amdgcn_rcpf((float)bs) : 0.f;
+          if constexpr (ADAM && XW > 1) {
+            // sync_dist: one granule to every peer now, the rank-ordered mean after the all-gather
+            xbl = rl(bl, 0);
+            if (l == 0) {
+#pragma unroll
+              for (int q = 0; q < XW; ++q)
+                if (q != xrank) b5x::put(xpr[q], XL::ls(xpar, xrank), xbl, 0.f, xtag);
+            }
+          } else if constexpr (ADAM) {
+            if (l == 0 && a.loss_out) a.loss_out[s] = bl;
+          } else {
+            if (l == 0) a.grad_out[sh.P] = bl;
+          }
+        }
+      }
+      B5STAMP(5)
+
+      if (last) {
+        const float step_size = a.lr * __builtin_amdgcn_rcpf(1.f - pow_t(l2b1, (float)t));
+        const float rbc2 = __builtin_amdgcn_rsqf(1.f - pow_t(l2b2, (float)t));
+        const float rss = __builtin_amdgcn_rcpf(step_size);
+        aA = sqc2 * rbc2 * rss * rc1;
+        aE = a.eps * rss * rc1;
+      }
+      // ---- dZ2 of outputs o = l + 64 j, the micro-batch's rows (old W2, mask bits of the owning wave)
+      {
+        const int sh4 = 4 * (l & 15);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const float wq[4] = {W[j][2 * q].x, W[j][2 * q].y, W[j][2 * q + 1].x, W[j][2 * q + 1].y};
-          const f32x4_t wt = quad_transpose_mf(wq, eye);
-          acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+          const float2 wv = j ? wv1 : wv0;
+          const uint2 mw = j ? mw1 : mw0;
+          const uint32_t nib = ((sh4 < 32 ? mw.x : mw.y) >> (sh4 & 31)) & 15u;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) acc[j] = mfma4(wt[i], dzt[j][i], acc[j]);
+          for (int r = 0; r < 4; ++r) {
+            const float g = wv.x * dz3[r][0] + wv.y * dz3[r][1];
+            dz2m[hf][j][r] = ((nib >> r) & 1u) ? g * scale : 0.f;
+          }
         }
-        const f32x4_t at = acc[0] + acc[1];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) P[4 * q + m] = at[m];
       }
-      dz1 = rs_bits2to5(P, l);
-    } else {
-      // one 16-value reduce-scatter per batch row (pass p leaves unit k's sum in lanes 4k..4k+3)
+      if constexpr (XW > 1) {
+        if (last) {
+          dw1_pass();
+          B5STAMP(15)  // dW1 MFMA + gradient pushes
+        }
+      }
+      // ---- owners: dW2[:, u], db1[u] (quad sums), W2 / b1 / b2 Adam, W2 / b2 published
+      {
+        const float d_own = dz, d_oth = dpp<ROR4>(dz);  // dlogit (r0, cb), (r0, 1 - cb)
+        const float dr0 = cb ? d_oth : d_own, dr1 = cb ? d_own : d_oth;
+        const float gw0 = quad_sum(dr0 * h2), gw1 = quad_sum(dr1 * h2);
+        float gdz = pw2[0] * dr0 + pw2[1] * dr1;
+        gdz = h2 > 0.f ? gdz * scale : 0.f;
+        const float gb1 = quad_sum(gdz);
+        const float gbh = (l & 1) ? (dz3[0][1] + dz3[1][1]) + (dz3[2][1] + dz3[3][1])
+                                  : (dz3[0][0] + dz3[1][0]) + (dz3[2][0] + dz3[3][0]);
+        gw0s = hf == 0 ? gw0 : gw0s + gw0;
+        gw1s = hf == 0 ? gw1 : gw1s + gw1;
+        gb1s = hf == 0 ? gb1 : gb1s + gb1;
+        gbs = hf == 0 ? gbh : gbs + gbh;
+        if (last) {
+          // updates run in every lane (no control flow around loop-carried registers: a conditional update
+          // costs a register copy per value at the loop back edge); only the owners' results are kept
+          // (W2[r0][u] is broadcast from quad lanes 0 / 1, b2 published by wave 0's lanes 0 / 1)
+          float pown = (r0 & 1) ? pw2[1] : pw2[0];
+          const float gown = (r0 & 1) ? gw1s : gw0s;
+          const float gb = gbs;
+          if constexpr (ADAM && XW > 1) {  // exchanged with the W0 gradients below
+            xg_own = gown;
+            xg_bx = r0 == 1 ? gb1s : gb;  // (r0 0: db0, known after dZ1)
+          } else if constexpr (ADAM) {
+            adam_pair<WD>(pown, gown, mw2, vw2, pb1, gb1s, mb1, vb1, a.b1, a.b2, a.wd, aA, aE);
+            pw2[0] = dpp<QB0>(pown);
+            pw2[1] = dpp<QB1>(pown);
+            if (own_w2) lds[W2L + nbuf * (H * C) + u * C + r0] = pown;
+            adam_scaled<WD>(pb2, gb, mb2, vb2, a.b1, a.b2, a.wd, aA, aE);
+            if (own_b2) lds[B2L + nbuf * 4 + l] = pb2;
+          } else {  // grad mode (one step): dW2[r0][u], db1[u], db2 to the flat gradient
+            if (own_w2) a.grad_out[fw2] = gown;
+            if (r0 == 0) a.grad_out[bo1 + u] = gb1s;
+            if (own_b2) a.grad_out[fb2] = gb;
+          }
+        }
+      }
+      B5STAMP(6)
+      // ---- dZ1 = W1^T dZ2 over this wave's k-slice, lane l keeps its own (unit u, row r0)
+      float dz1 = 0.f;
+      if constexpr (DXM) {
+        // on the 4x4x1 MFMA: each quad's 4x4 blocks of W1 (rows o = 4b + i + 64 j, columns k = 4q + m)
+        // and of dZ2 are transposed across the quad (MFMA, exact), so the call index runs over the block's 8
+        // outputs and lane (b, n) accumulates sum_o W1[o][4q + m] dZ2[o][n] for m = 0..3; the 16
+        // blocks' partials are then reduce-scattered over lane bits 2..5 to lane (b' = k, n)
+        float dzt[2][4];
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
+        for (int j = 0; j < 2; ++j) {
+          const f32x4_t tq = quad_transpose_mf(dz2m[hf][j], eye);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dzt[j][i] = tq[i];
+        }
         float P[16];
 #pragma unroll
-        for (int kk = 0; kk < KS; ++kk) P[kk] = W[0][kk >> 1][kk & 1] * dz2[0][p] + W[1][kk >> 1][kk & 1] * dz2[1][p];
-        const float tot = rs_small<16>(P, l);
-        if (r0 == p) dz1 = tot;
+        for (int q = 0; q < KS / 4; ++q) {
+          f32x4_t acc[2];  // one chain per j (4 dependent MFMAs each)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const float wq[4] = {W[j][2 * q].x, W[j][2 * q].y, W[j][2 * q + 1].x, W[j][2 * q + 1].y};
+            const f32x4_t wt = quad_transpose_mf(wq, eye);
+            acc[j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[j] = mfma4(wt[i], dzt[j][i], acc[j]);
+          }
+          const f32x4_t at = acc[0] + acc[1];
+#pragma unroll
+          for (int m = 0; m < 4; ++m) P[4 * q + m] = at[m];
+        }
+        dz1 = rs_bits2to5(P, l);
+      } else {
+        // one 16-value reduce-scatter per batch row (pass p leaves unit k's sum in lanes 4k..4k+3)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          float P[16];
+#pragma unroll
+          for (int kk = 0; kk < KS; ++kk)
+            P[kk] = W[0][kk >> 1][kk & 1] * dz2m[hf][0][p] + W[1][kk >> 1][kk & 1] * dz2m[hf][1][p];
+          const float tot = rs_small<16>(P, l);
+          if (r0 == p) dz1 = tot;
+        }
+      }
+      dz1 = h1 > 0.f ? dz1 * scale : 0.f;
+      // ---- dW0 / db0 (the quad holds unit u's four rows; inputs from the F1 tile in registers)
+      {
+        const float dq0 = dpp<QB0>(dz1), dq1 = dpp<QB1>(dz1), dq2 = dpp<QB2>(dz1), dq3 = dpp<QB3>(dz1);
+        const float g0h = dq0 * xa.x + dq1 * xa.y + dq2 * xa.z + dq3 * xa.w;
+        const float g1h = dq0 * xc.x + dq1 * xc.y + dq2 * xc.z + dq3 * xc.w;
+        const float dbh = (dq0 + dq1) + (dq2 + dq3);
+        g0s = hf == 0 ? g0h : g0s + g0h;
+        g1s = hf == 0 ? g1h : g1s + g1h;
+        db0s = hf == 0 ? dbh : db0s + dbh;
+        if (last) {
+          const float g0 = g0s, g1 = g1s;
+          if constexpr (ADAM && XW > 1) {
+            // the two small pairs go to the wave's owner rank now (its Adam runs after the dW1 loop)
+            if (r0 == 0) xg_bx = db0s;
+            xs_g0 = (v2f){g0, g1};
+            xs_g1 = (v2f){xg_own, xg_bx};
+            if (!sown) {
+#pragma unroll
+              for (int q = 0; q < XW; ++q)
+                if (q == __builtin_amdgcn_readfirstlane(w) % XW) {  // (scalar: the descriptor stays in SGPRs)
+                  const int rel = (xrank - q + XW) % XW;
+                  b5x::put(xpr[q], XL::rs(xpar, rel, NO) + tb, g0, g1, xtag);
+                  b5x::put(xpr[q], XL::rs(xpar, rel, NO + 1) + tb, xg_own, xg_bx, xtag);
+                }
+            }
+          } else if constexpr (ADAM) {
+            adam_pair<WD>(w0[0], g0, m0[0], v0[0], w0[1], g1, m0[1], v0[1], a.b1, a.b2, a.wd, aA, aE);  // d >= D0: stays 0
+            adam_scaled<WD>(pb0, db0s, mb0, vb0, a.b1, a.b2, a.wd, aA, aE);
+          } else {
+            if (r0 < D0) a.grad_out[wo0 + u * D0 + r0] = g0;
+            if (r0 + 4 < D0) a.grad_out[wo0 + u * D0 + r0 + 4] = g1;
+            if (r0 == 0) a.grad_out[bo0 + u] = db0s;
+          }
+        }
       }
     }
-    dz1 = h1 > 0.f ? dz1 * scale : 0.f;
-    // ---- dW0 / db0 (the quad holds unit u's four rows; inputs from the F1 tile in registers)
-    v2f xs_g0 = (v2f){0.f, 0.f}, xs_g1 = (v2f){0.f, 0.f};  // XW > 1: the small gradient pairs
-    {
-      const float dq0 = dpp<QB0>(dz1), dq1 = dpp<QB1>(dz1), dq2 = dpp<QB2>(dz1), dq3 = dpp<QB3>(dz1);
-      const float g0 = dq0 * xa.x + dq1 * xa.y + dq2 * xa.z + dq3 * xa.w;
-      const float g1 = dq0 * xc.x + dq1 * xc.y + dq2 * xc.z + dq3 * xc.w;
-      if constexpr (ADAM && XW > 1) {
-        // the two small pairs go to the wave's owner rank now (its Adam runs after the dW1 loop)
-        if (r0 == 0) xg_bx = (dq0 + dq1) + (dq2 + dq3);
-        xs_g0 = (v2f){g0, g1};
-        xs_g1 = (v2f){xg_own, xg_bx};
-        if (!sown) {
-#pragma unroll
-          for (int q = 0; q < XW; ++q)
-            if (q == __builtin_amdgcn_readfirstlane(w) % XW) {  // (scalar: the descriptor stays in SGPRs)
-              const int rel = (xrank - q + XW) % XW;
-              b5x::put(xpr[q], XL::rs(xpar, rel, NO) + tb, g0, g1, xtag);
-              b5x::put(xpr[q], XL::rs(xpar, rel, NO + 1) + tb, xg_own, xg_bx, xtag);
-            }
-        }
-      } else if constexpr (ADAM) {
-        adam_pair<WD>(w0[0], g0, m0[0], v0[0], w0[1], g1, m0[1], v0[1], a.b1, a.b2, a.wd, aA, aE);  // d >= D0: stays 0
-        adam_scaled<WD>(pb0, (dq0 + dq1) + (dq2 + dq3), mb0, vb0, a.b1, a.b2, a.wd, aA, aE);
-      } else {
-        if (r0 < D0) a.grad_out[wo0 + u * D0 + r0] = g0;
-        if (r0 + 4 < D0) a.grad_out[wo0 + u * D0 + r0 + 4] = g1;
-        if (r0 == 0) a.grad_out[bo0 + u] = (dq0 + dq1) + (dq2 + dq3);
-      }
+    if constexpr (XW > 1) {
+      if (abort_step) break;
     }
     // next step's dropout factors (independent work for the Adam stream below)
-    f1 = b5_drop(a.seed, gstep + 1u, el0, p_drop, scale);  // p_drop = 0: always 1
-    f2 = b5_drop(a.seed, gstep + 1u, el1, p_drop, scale);
+#pragma unroll
+    for (int hf = 0; hf < MB; ++hf) {
+      f1[hf] = b5_drop(a.seed, gstep + 1u, el0[hf], p_drop, scale);  // p_drop = 0: always 1
+      f2[hf] = b5_drop(a.seed, gstep + 1u, el1[hf], p_drop, scale);
+    }
     B5STAMP(7)
     // dW1 + packed Adam (one rank) / + reduce-scatter pushes here, after dZ1 and dW0 (XW > 1: issued
     // earlier, right behind dZ2 - its pushes then travel while dZ1 / dW0 compute)
@@ -1118,12 +1185,12 @@ __global__ __launch_bounds__(blk5::NT, 1) void mlp_block5_kernel(MlpShape sh, Ml
 #undef B5STAMP
 
 // one launch of an instantiation; its dynamic-LDS limit (two 64-KB staging tiles) is raised once
-template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true, int XW = 1, int RK = -1>
+template <bool WD, int LK, bool PROF = false, bool DXM = true, bool ADAM = true, int XW = 1, int RK = -1, int MB = 1>
 inline void b5_launch(size_t bytes, hipStream_t st, const MlpShape& sh, const MlpArgs& a) {
-  static const hipError_t attr = hipFuncSetAttribute((const void*)mlp_block5_kernel<WD, LK, PROF, DXM, ADAM, XW, RK>,
+  static const hipError_t attr = hipFuncSetAttribute((const void*)mlp_block5_kernel<WD, LK, PROF, DXM, ADAM, XW, RK, MB>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   (void)attr;
-  hipLaunchKernelGGL((mlp_block5_kernel<WD, LK, PROF, DXM, ADAM, XW, RK>), dim3(1), dim3(blk5::NT), bytes, st, sh, a);
+  hipLaunchKernelGGL((mlp_block5_kernel<WD, LK, PROF, DXM, ADAM, XW, RK, MB>), dim3(1), dim3(blk5::NT), bytes, st, sh, a);
 }
 
 

@@ -152,7 +152,7 @@ int dct_mlp_train(const void* shape, const MlpArgs* a, void* stream) {
     return (int)dct::mlp_launch_block5(sh, *a, st);
   }
   const int blk = sh.mlp_block;  // plan-time DCT_MLP_BLOCK: -1 auto, 3 mlp_block3, 0 the generic LDS trainer
-  if (blk < 0 && dct::mlp_block5_ok(sh, *a)) return (int)dct::mlp_launch_block5(sh, *a, st);
+  if ((blk < 0 || blk == 8) && dct::mlp_block5_ok(sh, *a)) return (int)dct::mlp_launch_block5(sh, *a, st);
   if (blk != 0 && dct::mlp_block3_ok(sh, *a)) return (int)dct::mlp_launch_block3(sh, *a, st);
   switch (sh.L) {
     case 2: return (int)dct::mlp_launch_train_L2(sh, *a, st);

@@ -109,6 +109,28 @@ void Comm::all_gather(uintptr_t send, uintptr_t recv, int64_t send_count, int dt
 }
 
 // ------------------------------------------------------------------------- BucketReducer
+uintptr_t cu_masked_stream(const std::vector<uint32_t>& mask) {
+  hipStream_t s = nullptr;
+  hip_check(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()), "hipExtStreamCreateWithCUMask");
+  return reinterpret_cast<uintptr_t>(s);
+}
+
+void stream_destroy(uintptr_t stream) { hip_check(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)), "hipStreamDestroy"); }
+
+std::vector<uint32_t> stream_cu_mask(uintptr_t stream) {
+  const int n = (device_cu_count() + 31) / 32;
+  std::vector<uint32_t> m(n, 0u);
+  hip_check(hipExtStreamGetCUMask(reinterpret_cast<hipStream_t>(stream), (uint32_t)n, m.data()), "hipExtStreamGetCUMask");
+  return m;
+}
+
+int device_cu_count() {
+  int dev = 0, n = 0;
+  hip_check(hipGetDevice(&dev), "hipGetDevice");
+  hip_check(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
+  return n;
+}
+
 BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_t> bucket_offsets,
                              std::vector<int64_t> bucket_counts, std::vector<int> param_bucket, int dtype,
                              int op)
@@ -163,6 +185,7 @@ BucketReducer::BucketReducer(Comm* comm, uintptr_t flat_grad, std::vector<int64_
   if (inline_knob_ == -2) {
     const bool identity = comm_ == nullptr || (comm_->world() == 1 && comm_->is_identity());
     inline_knob_ = ((identity && standin_us_ == 0) || real_peers) ? 1 : -1;
+    auto_inline_ = true;
   }
   inline_ = inline_knob_ == 1;
   for (int64_t c : counts_) total_count_ += c;
@@ -247,8 +270,35 @@ void BucketReducer::reset_timing() {
   hip_check(hipMemcpy(stamps_, h, sizeof(h), hipMemcpyHostToDevice), "reset reducer stamps");
 }
 
+void BucketReducer::set_comm_cu_mask(const std::vector<uint32_t>& mask) {
+  hipStream_t s = nullptr;
+  hip_check(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()), "hipExtStreamCreateWithCUMask");
+  hip_check(hipStreamSynchronize(comm_stream_), "hipStreamSynchronize");
+  hip_check(hipStreamDestroy(comm_stream_), "hipStreamDestroy");
+  comm_stream_ = s;
+  comm_mask_ = mask;
+  checked_stream_ = nullptr;
+}
+
+// true when the compute stream's CU mask shares no CU with the comm stream's (reserved CUs)
+bool BucketReducer::disjoint_from_comm(hipStream_t compute) {
+  if (comm_mask_.empty()) return false;
+  if (compute == checked_stream_) return checked_disjoint_;
+  std::vector<uint32_t> cm(comm_mask_.size(), 0u);
+  bool ok = compute != nullptr &&
+            hipExtStreamGetCUMask(compute, (uint32_t)cm.size(), cm.data()) == hipSuccess;
+  if (!ok) (void)hipGetLastError();
+  for (size_t i = 0; ok && i < cm.size(); ++i) ok = (cm[i] & comm_mask_[i]) == 0u;
+  checked_stream_ = compute;
+  checked_disjoint_ = ok;
+  return ok;
+}
+
 bool BucketReducer::step_inline(void* compute_stream) {
-  if (inline_knob_ >= 0) return inline_knob_ == 1;
+  // real peers, auto placement: inline unless the collectives own CUs the compute stream cannot use
+  // (set_comm_cu_mask) - then eager steps overlap them, captured ones keep them inline (-1 below)
+  const bool reserved = peer_world_ && auto_inline_ && disjoint_from_comm(reinterpret_cast<hipStream_t>(compute_stream));
+  if (inline_knob_ >= 0 && !reserved) return inline_knob_ == 1;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(reinterpret_cast<hipStream_t>(compute_stream), &st) != hipSuccess) {
     (void)hipGetLastError();

@@ -1021,7 +1021,13 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
     atomicAdd(a.lnrep + (blockIdx.x % LN_REP) * 4 * DM + threadIdx.x, red[threadIdx.x]);
     // the add has been performed (float atomics execute at the memory side, so completion is all the
     // ordering the fold needs - an agent-scope release fence here would write back the XCD's L2 in every
-    // workgroup: 0.339 -> 0.556 ms per TabTransformer step)
+    // workgroup: 0.339 -> 0.556 ms per TabTransformer step).  Hardware assumptions of gfx950 this relies
+    // on, outside the HIP memory model: vmcnt covers a no-return atomic until the memory side
+    // has acknowledged it (gfx9: stores and atomics share vmcnt); device-scope float atomics, the ticket's
+    // and the fold's read-and-zero exchanges all execute beyond the per-XCD L2; the asm's memory clobber
+    // keeps the compiler from moving the add below the wait.  A late add would stay in its replica, so
+    // tests/test_kernels_gpu.py::test_tt_ln_replica_fold_complete_and_matches_direct_atomics checks the
+    // workspace is exactly zero after every launch at B = 512 / 1024 and the fold equals direct atomics.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // (every read of red is done: red[0] carries the verdict; no static LDS in this kernel)
     if (threadIdx.x == 0)

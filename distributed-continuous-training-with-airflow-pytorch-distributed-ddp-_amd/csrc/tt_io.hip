@@ -163,8 +163,8 @@ __global__ __launch_bounds__(64 * NW) void head_fwd_kernel(HeadArgs a) {
     for (int i = 0; i < NW; ++i) v += lsum[i];
     // partial and ticket as memory-side atomics, ordered by waiting for the first to complete: no
     // agent-scope release / acquire fences (each writes back / invalidates the XCD's L2 - see the LN
-    // replicas of tt_block.hip), and the last block reads the partials by atomics too (an L2 of
-    // another XCD may hold a stale line of them)
+    // replicas of tt_block.hip, whose gfx950 assumptions this shares), and the last block reads the
+    // partials by atomics too (an L2 of another XCD may hold a stale line of them)
     atomicExch(a.partial + blockIdx.x, v);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;

@@ -75,7 +75,10 @@ KERNELS = ["auto", "lds", "lds-noblock", "lds-b3"]
                                     ([16, 32, 48, 32, 3], 16), ([5, 128, 128, 2], 16), ([7, 20, 2], 9),
                                     ([7, 20, 2], 8), ([12, 40, 4], 6), ([16, 64, 3], 2), ([5, 64, 2], 1),
                                     # mlp_block5 below its full batch and at its input-width bounds
-                                    ([3, 128, 128, 2], 3), ([8, 128, 128, 2], 1), ([1, 128, 128, 2], 2)])
+                                    ([3, 128, 128, 2], 3), ([8, 128, 128, 2], 1), ([1, 128, 128, 2], 2),
+                                    # mlp_block5 with two micro-batches per step (batch 5..8)
+                                    ([5, 128, 128, 2], 8), ([8, 128, 128, 2], 5), ([3, 128, 128, 2], 7),
+                                    ([5, 128, 128, 2], 6)])
 def test_fused_train_matches_torch_adam(dims, B, loss, kernel, cuda, monkeypatch):
     _set_kernel_env(monkeypatch, kernel)
     torch.manual_seed(1)
@@ -146,7 +149,8 @@ def test_weather_3x128_weight_decay_matches_torch_adam(kernel, loss, cuda, monke
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("dims,B", [([5, 64, 2], 4), ([5, 128, 128, 2], 4), ([12, 40, 40, 5], 13),
                                     ([9, 48, 64, 3], 4), ([20, 128, 128, 4], 3), ([32, 128, 128, 1], 4),
-                                    ([8, 128, 128, 2], 3), ([2, 128, 128, 2], 1)])
+                                    ([8, 128, 128, 2], 3), ([2, 128, 128, 2], 1), ([5, 128, 128, 2], 8),
+                                    ([7, 128, 128, 2], 6)])
 def test_fused_grad_mode_matches_autograd(dims, B, kernel, cuda, monkeypatch):
     _set_kernel_env(monkeypatch, kernel)
     torch.manual_seed(2)
@@ -205,7 +209,37 @@ def test_block5_grad_mode_staged_batches(dims, B, n_items, cuda):
         assert tag == (b + 2 if (b + 1) * B < n_items else 0), (b, tag)
 
 
-@pytest.mark.parametrize("dims,B,D0", [([7, 128, 128, 2], 4, 7), ([30, 128, 128, 3], 3, 30)])
+@pytest.mark.parametrize("dropout,loss", [(0.0, "ce"), (0.2, "ce"), (0.2, "mse")])
+def test_block5_two_micro_batch_kernel_equals_one_at_batch4(dropout, loss, cuda, monkeypatch):
+    """mlp_block5's batch 5..8 kernels (two micro-batches of four rows per step, gradients summed in
+    registers) forced at batch <= 4 (DCT_MLP_BLOCK=8): the second micro-batch's rows are all empty
+    (zero dlogits), so every parameter, moment and loss must equal the one-micro-batch kernel's bit for
+    bit - the partial last batch included (n_items % 4 = 3)."""
+    torch.manual_seed(9)
+    dims, N, n_items, B = [5, 128, 128, 2], 400, 203, 4
+    X = torch.randn(N, 5).to(cuda)
+    Y = torch.randint(0, 2, (N,)).to(cuda, torch.int32)
+    idx = torch.randperm(N)[:n_items].to(cuda, torch.int32)
+    p0 = _flat(_ref_net(dims)).to(cuda)
+    steps = math.ceil(n_items / B)
+    out = {}
+    for blk in ("-1", "8"):
+        monkeypatch.setenv("DCT_MLP_BLOCK", blk)
+        p, m, v = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
+        losses = torch.zeros(steps, device=cuda)
+        k = FusedMLPKernel(dims, bmax=4)
+        for first, n in ((0, 17), (17, steps - 17)):  # two launches: the epilogue / prologue round trip too
+            k.train(p, m, v, X, Y, idx[first * B:], n_items=n_items - first * B, batch=B, steps=n, t0=first, lr=0.01,
+                    dropout=dropout, seed=3, step_base=first, loss=loss, loss_out=losses[first:])
+        torch.cuda.synchronize()
+        out[blk] = (p.cpu(), m.cpu(), v.cpu(), losses.cpu())
+    for a_, b_ in zip(out["-1"], out["8"]):
+        assert torch.isfinite(a_).all()
+        assert torch.equal(a_, b_), float((a_ - b_).abs().max())
+
+
+@pytest.mark.parametrize("dims,B,D0", [([7, 128, 128, 2], 4, 7), ([30, 128, 128, 3], 3, 30), ([5, 128, 128, 2], 8, 5),
+                                      ([6, 128, 128, 2], 5, 6)])
 def test_block_kernel_matches_lds_kernel_with_dropout(dims, B, D0, cuda, monkeypatch):
     """The register-resident 3-layer kernels (mlp_block5 where the shape fits, mlp_block3 with and
     without the 4x4x1 MFMA layer) vs the generic LDS kernel: same dropout hash, loss and Adam -> the
@@ -223,7 +257,7 @@ def test_block_kernel_matches_lds_kernel_with_dropout(dims, B, D0, cuda, monkeyp
         _set_kernel_env(monkeypatch, blk)
         p, m, v = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
         losses = torch.zeros(steps, device=cuda)
-        k = FusedMLPKernel(dims, bmax=4)
+        k = FusedMLPKernel(dims, bmax=4 if B <= 4 else 16)
         k.train(p, m, v, X, Y, idx, n_items=n_items, batch=B, steps=steps, t0=3, lr=0.01, dropout=0.2, seed=11,
                 step_base=5, loss_out=losses)
         torch.cuda.synchronize()
@@ -1075,3 +1109,50 @@ def test_bound_train_launch_matches_keyword_launch(dims, cuda):
     for a, b in zip(*runs):
         assert torch.equal(a, b)
     assert int(runs[1][4]) == 25 and bool((runs[1][3][:25] > 0).all()) and bool((runs[1][3][25:] == -1).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [512, 1024])
+def test_tt_ln_replica_fold_complete_and_matches_direct_atomics(cuda, B, monkeypatch):
+    """ADVICE r5 (csrc/tt_block.hip LN_REP fold): the fused block backward adds each workgroup's
+    LayerNorm parameter gradients into one of 16 replicas and the LAST workgroup (ticket) folds them
+    with memory-side read-and-zero atomics, ordered only by ``s_waitcnt vmcnt(0)`` behind the adds (no
+    release fence: an agent-scope release writes back the XCD's L2, 0.339 -> 0.556 ms per step).  A
+    replica add that landed after the fold would stay in the workspace: after every launch the
+    replicas and the ticket must be exactly zero, and the folded gradients must equal the direct-
+    atomic path's up to fp32 summation order (a lost workgroup would move a column by ~1/sqrt(B) of it)."""
+    from dct_amd.ops import nn as nnops
+
+    T, H, d, n = 64, 4, 64, 256
+    M = B * T
+    g = torch.Generator(device="cpu").manual_seed(3)
+    mk = lambda *s, scale=1.0: (scale * torch.randn(*s, generator=g)).to(cuda).requires_grad_()  # noqa: E731
+    t = dict(h=mk(M, d), ln1_w=(1 + 0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_(),
+             ln1_b=mk(d, scale=0.1), wqkv=mk(3 * d, d, scale=d ** -0.5), bqkv=mk(3 * d, scale=0.1),
+             wo=mk(d, d, scale=d ** -0.5), bo=mk(d, scale=0.1),
+             ln2_w=(1 + 0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_(), ln2_b=mk(d, scale=0.1),
+             w1=mk(n, d, scale=d ** -0.5), b1=mk(n, scale=0.1), w2=mk(d, n, scale=n ** -0.5), b2=mk(d, scale=0.1))
+    keys = ["ln1_w", "ln1_b", "wqkv", "bqkv", "wo", "bo", "ln2_w", "ln2_b", "w1", "b1", "w2", "b2"]
+    ln_keys = ["ln1_w", "ln1_b", "ln2_w", "ln2_b"]
+    dout = torch.randn(M, d, device=cuda)
+    monkeypatch.setattr(nnops, "TT_FUSED", True)
+    monkeypatch.setattr(nnops, "TT_FUSED_BWD", True)
+
+    def run(rep):
+        monkeypatch.setattr(nnops, "_TT_LN_REP", rep)
+        out = nnops.tt_block(t["h"], *[t[k] for k in keys], B, H, T)
+        out.backward(dout)
+        grads = {k: t[k].grad.clone() for k in ln_keys}
+        for v in t.values():
+            v.grad = None
+        return grads
+
+    direct = run(False)
+    for it in range(8):
+        got = run(True)
+        torch.cuda.synchronize()
+        ws = nnops._TT_LN_WS[cuda.index if cuda.index is not None else 0]
+        assert int(torch.count_nonzero(ws)) == 0, (it, int(torch.count_nonzero(ws)))  # replicas + ticket re-zeroed
+        for k in ln_keys:
+            err = (got[k] - direct[k]).abs().max()
+            assert err <= 2e-4 * direct[k].abs().max() + 1e-6, (it, k, float(err), float(direct[k].abs().max()))

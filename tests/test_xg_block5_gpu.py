@@ -67,7 +67,7 @@ def _in_process_run(W, steps, split, B, out_path, wd=0.0):
     launch's prologue."""
     nat = native()
     cuda = torch.device("cuda", 0)
-    kern = FusedMLPKernel(DIMS, bmax=4)
+    kern = FusedMLPKernel(DIMS, bmax=4 if B <= 4 else 16)
     assert not kern.plan.use_wave and kern.xg_supported(B, W)
     xs = [nat.PeerExchange(W, r, kern.xg_buffer_bytes(W, B)) for r in range(W)]
     for x in xs:
@@ -114,13 +114,14 @@ def _check_vs_reference(res, W, steps, B, seed_net, X, Y, shards, wd=0.0):
     assert torch.allclose(torch.tensor(res["losses"][0]), want_l, atol=2e-4, rtol=1e-3)
 
 
-@pytest.mark.parametrize("W,wd", [(2, 0.0), (2, 0.01)])
-def test_in_process_block5_exchange_matches_ddp_reference(tmp_path, W, wd, cuda):
+@pytest.mark.parametrize("W,wd,B", [(2, 0.0, 4), (2, 0.01, 4), (2, 0.0, 8), (2, 0.0, 6)])
+def test_in_process_block5_exchange_matches_ddp_reference(tmp_path, W, wd, B, cuda):
     """Fresh process: streams of one process share GPU_MAX_HW_QUEUES (4) hardware queues round-
     robin, so more 'ranks' than that could land on one queue and serialise; W > 2 runs as separate
     processes below.  wd = 0: the per-rank compile-time-rank kernels (the reference's
-    configuration); wd > 0: the runtime-rank kernel (L2 term in every sharded update)."""
-    B, steps, split = 4, 60, 23
+    configuration); wd > 0: the runtime-rank kernel (L2 term in every sharded update).  B 6 / 8:
+    two micro-batches per step (csrc/mlp_block5_b8.hip), the exchange unchanged."""
+    steps, split = 60, 23
     out = tmp_path / "b5x.json"
     code = (f"import sys; sys.path.insert(0, {ROOT!r}); sys.path.insert(0, {os.path.join(ROOT, 'tests')!r}); "
             f"import test_xg_block5_gpu as t; t._in_process_run({W}, {steps}, {split}, {B}, {str(out)!r}, wd={wd})")
@@ -131,6 +132,26 @@ def test_in_process_block5_exchange_matches_ddp_reference(tmp_path, W, wd, cuda)
     X, Y = weather_tensors(3000, seed=5)
     shards = [distributed_indices(3000, W, r_, shuffle=True, seed=42, epoch=0) for r_ in range(W)]
     _check_vs_reference(res, W, steps, B, 1, X, Y, shards, wd=wd)
+
+
+@pytest.mark.parametrize("wd", [0.0, 0.01])
+def test_in_process_two_micro_batch_exchange_equals_one_at_batch4(tmp_path, wd, cuda, monkeypatch):
+    """The data-parallel two-micro-batch kernels (batch 5..8) forced at batch 4 (DCT_MLP_BLOCK=8): the
+    empty second micro-batch adds exact zeros, so both ranks' parameters, moments and synced losses
+    must equal the one-micro-batch exchange kernels' bit for bit."""
+    W, B, steps, split = 2, 4, 40, 17
+    res = {}
+    for blk in ("-1", "8"):
+        out = tmp_path / f"b5x_{blk}.json"
+        code = (f"import sys; sys.path.insert(0, {ROOT!r}); sys.path.insert(0, {os.path.join(ROOT, 'tests')!r}); "
+                f"import test_xg_block5_gpu as t; t._in_process_run({W}, {steps}, {split}, {B}, {str(out)!r}, wd={wd})")
+        env = dict(os.environ, DCT_MLP_BLOCK=blk)
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        res[blk] = json.loads(out.read_text())
+        assert res[blk]["status"] == [0] * W and res[blk]["steps"] == [steps] * W
+    for key in ("params", "m", "v", "losses"):
+        assert res["8"][key] == res["-1"][key], key
 
 
 def test_block5_exchange_timeout_leaves_state_untouched(cuda):
@@ -157,16 +178,16 @@ def test_block5_exchange_timeout_leaves_state_untouched(cuda):
     assert torch.equal(p, p0) and torch.equal(m, m0) and torch.equal(v, v0)
 
 
-@pytest.mark.parametrize("W", [2, 3, 4, 5, 6, 7, 8])
-def test_engine_inkernel_exchange_3x128(W, tmp_path, cuda):
+@pytest.mark.parametrize("W,B", [(2, 4), (3, 4), (4, 4), (5, 4), (6, 4), (7, 4), (8, 4), (3, 8), (8, 7)])
+def test_engine_inkernel_exchange_3x128(W, B, tmp_path, cuda):
     """FusedMLPEngine at world size W (processes sharing the GPU, IPC-mapped buffers, gloo control
     plane): the 3x128 model trains in its persistent launch with the in-kernel reduce-scatter /
     all-gather (no per-step launch), over two launches; replicas and optimizer states are
     bit-identical and follow torch DDP + Adam.  Every world size the reference accepts on one node
     (jobs/train_lightning_ddp.py:129-136): 3 / 5 / 6 / 7 ranks own ceil(16 / W) W1 pair slots each,
-    some of them empty, through the runtime-rank kernels."""
+    some of them empty, through the runtime-rank kernels.  B 7 / 8: the two-micro-batch kernels."""
     out = tmp_path / "b5.json"
-    steps, B = 45, 4
+    steps = 45
     # one hardware queue per worker: W processes x GPU_MAX_HW_QUEUES (4) + this process's queues can exceed
     # the device's compute queue slots at W = 8, and a spinning rank whose peer's queue is not mapped
     # then times out (seen once at W = 8: status 2); on a real node every rank has a GPU of its own
