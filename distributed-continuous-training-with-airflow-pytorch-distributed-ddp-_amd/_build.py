@@ -47,6 +47,7 @@ FILE_FLAGS = {"gemm_bf16.hip": ["-fno-slp-vectorize"],
               "mlp_block5_xg.hip": ["-fno-slp-vectorize"],
               "mlp_block5_xgprof.hip": ["-fno-slp-vectorize"],
               "mlp_block5_b8.hip": ["-fno-slp-vectorize"],
+              "mlp_block5_xgs.hip": ["-fno-slp-vectorize"],
               "tt_block.hip": MAX_ILP,
               "tt_io.hip": MAX_ILP,
               "mlp_wave_single.hip": MAX_ILP,

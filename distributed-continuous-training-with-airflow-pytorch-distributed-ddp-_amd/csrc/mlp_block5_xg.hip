@@ -23,12 +23,16 @@ static void b5_launch_xg(size_t bytes, hipStream_t st, const MlpShape& sh, const
   }
 }
 
-// world sizes that do not divide the 16 W1 pairs per lane (3, 5, 6, 7 ranks): runtime-rank kernels
-// only (pair XW t + rank, the last slots of some ranks empty), with the weight-decay term compiled in
-// (wd = 0 adds fmaf(0, p, g) = g exactly) - two kernels per world size instead of one per rank
+void mlp_launch_block5_xg_static(int world, size_t bytes, hipStream_t st, const MlpShape& sh, const MlpArgs& a);
+
+// world sizes that do not divide the 16 W1 pairs per lane (3, 5, 6, 7 ranks; pair XW t + rank, the last
+// slots of some ranks empty): the reference configuration on per-rank kernels (mlp_block5_xgs.hip),
+// every other one on runtime-rank kernels with the weight-decay term compiled in (wd = 0 adds
+// fmaf(0, p, g) = g exactly) - two kernels per world size instead of one per rank
 template <int XW>
 static void b5_launch_xg_rt(size_t bytes, hipStream_t st, const MlpShape& sh, const MlpArgs& a) {
-  if (a.loss_kind == 0) b5_launch<true, 0, false, true, true, XW>(bytes, st, sh, a);
+  if (a.loss_kind == 0 && a.wd == 0.f) mlp_launch_block5_xg_static(XW, bytes, st, sh, a);
+  else if (a.loss_kind == 0) b5_launch<true, 0, false, true, true, XW>(bytes, st, sh, a);
   else b5_launch<true, 1, false, true, true, XW>(bytes, st, sh, a);
 }
 

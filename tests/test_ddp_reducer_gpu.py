@@ -81,6 +81,52 @@ def test_tabular_forced_reducer_matches_no_reducer(cuda, monkeypatch):
     assert red.allreduce_ms()[2] == 0
 
 
+def test_tabular_reducer_on_reserved_cus(cuda, monkeypatch):
+    """CU reservation (profiles/ddp_reducer_cu_reservation_r6.log): the step on a stream masked to every
+    CU but 8, the reducer's collectives on a stream masked to those 8 (no collective kernel can share a
+    CU with the backward's LDS-DMA GEMM tiles).  The masks round-trip, the reducer reports the
+    reserved set, and training follows the no-reducer trajectory as in (a)."""
+    from dct_amd.ops._native import native
+
+    nat = native()
+    ncu = nat.device_cu_count()
+    assert ncu >= 64
+    words = (ncu + 31) // 32
+    full = [0xFFFFFFFF if 32 * (w + 1) <= ncu else (1 << (ncu - 32 * w)) - 1 for w in range(words)]
+    comm = [0] * words
+    for c in range(0, ncu, ncu // 8):
+        comm[c // 32] |= 1 << (c % 32)
+    compute = [f & ~c for f, c in zip(full, comm)]
+    h = nat.cu_masked_stream(compute)
+    try:
+        assert list(nat.stream_cu_mask(h)) == compute
+        ref, l0 = _tabular(False, monkeypatch)
+        with torch.cuda.stream(torch.cuda.ExternalStream(h)):
+            monkeypatch.setenv("DCT_FORCE_DDP", "1")
+            monkeypatch.setenv("DCT_RCCL_ONE_RANK", "1")
+            monkeypatch.setenv("DCT_DEBUG", "1")
+            dims = [256, 1024, 1024, 1024, 2]
+            torch.manual_seed(0)
+            model = MLPClassifier(dims[0], hidden=tuple(dims[1:-1]), num_classes=2, dropout=0.0, loss="mse", lr=1e-3)
+            ctx = init_distributed("gpu")
+            eng = GraphMLPEngine(model, ctx, 1024, seed=42, adam=adam_hparams_from(model.configure_optimizers()))
+            eng.reducer._r.set_comm_cu_mask(comm)
+            assert list(eng.reducer._r.comm_cu_mask) == comm
+            assert list(nat.stream_cu_mask(eng.reducer._r.comm_stream)) == comm
+            X, Y = _data(8 * 1024, dims[0], seed=5)
+            rows = torch.arange(X.shape[0])
+            eng.attach_data(X, Y, rows, rows[:1024])
+            l1 = torch.cat([eng.train_epoch(ep).cpu() for ep in range(2)])
+        torch.cuda.synchronize()
+        assert eng.reducer._r.edge_timeouts() == 0
+        assert torch.isfinite(l1).all()
+        assert torch.allclose(l0, l1, atol=1e-3), (l0 - l1).abs().max()
+        assert (eng.p.cpu() - ref.p.cpu()).norm() / ref.p.cpu().norm() < 1e-2
+    finally:
+        torch.cuda.synchronize()
+        nat.stream_destroy(h)
+
+
 def _tt(forced, monkeypatch, defer="1", steps=10, B=128, groups="1"):
     monkeypatch.setenv("DCT_FORCE_DDP", "1" if forced else "0")
     monkeypatch.setenv("DCT_TT_DW_DEFER", defer)
