@@ -308,6 +308,9 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
       for (int j = 0; j < 4; ++j) st[i][j] = mfma16(kf[i], qf[j], (f32x4){0.f, 0.f, 0.f, 0.f});
     bf16x4 pf[4][4];
     float lsev[4];
+    // softmax in the exp2 domain: the scale carries log2(e), so each score is one fma + v_exp_f32
+    // (__expf is fma, multiply by log2(e), v_exp_f32); lse leaves in natural-log units
+    const float sl = a.scale * 1.4426950408889634f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float m = -3.402823466e+38f;
@@ -315,13 +318,13 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) m = fmaxf(m, st[i][j][r]);
-      m = max4g(m) * a.scale;
+      m = max4g(m) * sl;
       float l = 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = __expf(st[i][j][r] * a.scale - m);
+          const float e = __builtin_amdgcn_exp2f(fmaf(st[i][j][r], sl, -m));
           st[i][j][r] = e;
           l += e;
         }
@@ -329,7 +332,7 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
       const float inv = 1.f / l;
 #pragma unroll
       for (int i = 0; i < 4; ++i) pf[j][i] = pack4(st[i][j] * inv);
-      lsev[j] = m + __logf(l);
+      lsev[j] = (m + __builtin_amdgcn_logf(l)) * 0.6931471805599453f;
     }
     bf16x4 vf[4];
 #pragma unroll
@@ -908,15 +911,16 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
           dp[j][i] = mfma16(gf[j], vf[i], (f32x4){0.f, 0.f, 0.f, 0.f});
         }
       bf16x4 pa[4][4], dsa[4][4];
+      const float sl = a.scale * 1.4426950408889634f;  // P recomputed in the exp2 domain (one fma + v_exp_f32)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int qi = 16 * j + 4 * g + r;
-          const float lq = lb[qi], dq_ = dl[qi];
+          const float lq = lb[qi] * 1.4426950408889634f, dq_ = dl[qi];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float p = __expf(sc[j][i][r] * a.scale - lq);
+            const float p = __builtin_amdgcn_exp2f(fmaf(sc[j][i][r], sl, -lq));
             sc[j][i][r] = p;
             dp[j][i][r] = p * (dp[j][i][r] - dq_);
           }
@@ -951,15 +955,17 @@ __global__ __launch_bounds__(256, 2) void tt_block_bwd_kernel(BwdArgs a) {
           dpt[i][j] = mfma16(vf[i], gf[j], (f32x4){0.f, 0.f, 0.f, 0.f});
         }
       bf16x4 dsq[4][4];
+      const float sl = a.scale * 1.4426950408889634f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int qi = 16 * j + c;
-        const float lq = lb[qi], dq_ = dl[qi];
+        const float lq = lb[qi] * 1.4426950408889634f, dq_ = dl[qi];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           f32x4 tv;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) tv[r] = __expf(st[i][j][r] * a.scale - lq) * (dpt[i][j][r] - dq_);
+          for (int r = 0; r < 4; ++r)
+            tv[r] = __builtin_amdgcn_exp2f(fmaf(st[i][j][r], sl, -lq)) * (dpt[i][j][r] - dq_);
           dsq[j][i] = pack4(tv);
         }
       }
