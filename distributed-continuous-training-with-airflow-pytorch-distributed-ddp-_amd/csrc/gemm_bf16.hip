@@ -390,6 +390,18 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
 #pragma unroll
     for (int s = 0; s < S - 1; ++s)
       if (s < n) fill(s, kt0 + s);
+    // B^T side output (NT forward GEMMs of the wide MLP): the tiles_m workgroups of one column panel
+    // each write a k-slice of its transpose, rows [bt_lo, bt_hi), from the B image of the k-stage that
+    // holds them - 16 B per thread (8 columns of one k row), no extra global reads
+    int bt_lo = 0, bt_hi = 0;
+    if constexpr (TB && !SPLIT) {
+      if (g.bt_out) {
+        const int tiles_m = (g.M + BM - 1) / BM;
+        const int rows_per = (((g.K + tiles_m - 1) / tiles_m) + 31) & ~31;
+        bt_lo = min(g.K, tm * rows_per);
+        bt_hi = min(g.K, bt_lo + rows_per);
+      }
+    }
     for (int it = 0; it < n; ++it) {
       wait_stage<FILL_OPS, S>(min(S - 2, n - 1 - it));  // this wave's part of stage `it` has landed
       raw_barrier();  // every wave's part has; every wave finished reading stage it - 1
@@ -397,6 +409,29 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
       const int cur = it & (S - 1);
       const char* ai = img(cur, 0);
       const char* bi = img(cur, 1);
+      if constexpr (TB && !SPLIT) {
+        const int k0 = (kt0 + it) * KT;
+        const int lo = max(bt_lo, k0), hi = min(bt_hi, k0 + KT);
+        constexpr int RPP = NT / 16;  // k rows per pass (16 threads of 8 columns = one 128-wide row)
+        for (int kb = lo; kb < hi; kb += RPP) {
+          const int kl = kb + (tid >> 4), ng = tid & 15;
+          const int col = n0 + ng * 8;
+          if (kl < hi && col + 8 <= g.N) {
+            const int kk = kl - k0;
+            uint32_t w[4];
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+              const int r0 = ng * 8 + e, r1 = r0 + 1;
+              const uint16_t lo16 = *reinterpret_cast<const uint16_t*>(
+                  bi + r0 * (2 * KT) + (((kk >> 3) ^ (r0 & (KT / 8 - 1))) << 4) + (kk & 7) * 2);
+              const uint16_t hi16 = *reinterpret_cast<const uint16_t*>(
+                  bi + r1 * (2 * KT) + (((kk >> 3) ^ (r1 & (KT / 8 - 1))) << 4) + (kk & 7) * 2);
+              w[e >> 1] = (uint32_t)lo16 | ((uint32_t)hi16 << 16);
+            }
+            *reinterpret_cast<uint4*>(g.bt_out + (size_t)kl * g.bt_ld + col) = make_uint4(w[0], w[1], w[2], w[3]);
+          }
+        }
+      }
 #pragma unroll
       for (int ks = 0; ks < KT / 32; ++ks) {
         bf16x8 af[IM], bfr[4];
@@ -1123,6 +1158,25 @@ extern "C" int dct_gemm_bf16_residual(const uint16_t* A, const uint16_t* W, floa
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (gemm_v2_ok(g, 0, 1)) return (int)launch_gemm2<false, true>(g, st);  // never split-K with a residual
   return (int)launch_gemm<false, true>(g, st);
+}
+
+// dct_gemm_bf16 (below) that also writes op(B)^T = B^T [K][N] (row stride bt_ld) to bt_out: NT only, on
+// the LDS-DMA kernels without split-K (hipErrorInvalidValue otherwise, nothing launched)
+extern "C" int dct_gemm_bf16_bt(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K,
+                                int lda, int ldb, int ldc, int epilogue, int out_f32, void* aux, uint16_t* bt_out,
+                                int bt_ld, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  dct::GemmArgs g{};
+  g.A = A; g.B = B; g.C = C; g.bias = bias; g.aux = aux;
+  g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.epilogue = epilogue; g.out_f32 = out_f32; g.accumulate = 0; g.alpha = 1.0f;
+  g.vec_a = ((((uintptr_t)A) & 15) == 0) && (lda % 8 == 0);
+  g.vec_b = ((((uintptr_t)B) & 15) == 0) && (ldb % 8 == 0);
+  g.bt_out = bt_out; g.bt_ld = bt_ld;
+  const bool split_k = out_f32 && epilogue == dct::EPI_NONE;  // (launch_gemm2 splits only fp32 EPI_NONE outputs)
+  if (!gemm_v2_ok(g, 0, 1) || split_k || (((uintptr_t)bt_out) & 15) || (bt_ld % 8) || (N % 8))
+    return (int)hipErrorInvalidValue;
+  return (int)launch_gemm2<false, true>(g, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int dct_gemm_bf16(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K,

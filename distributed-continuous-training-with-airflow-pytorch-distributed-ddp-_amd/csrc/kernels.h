@@ -25,6 +25,8 @@ struct GemmArgs {
   const float* residual;  // optional (fp32 out): C = residual + op(A) op(B) + bias, ld = ldc
   float* split_part;      // optional two-pass split-K: slice s plain-stores its partial C into
                           // split_part[s][M][N]; splitk_reduce_kernel sums the slices into C afterwards
+  uint16_t* bt_out;       // optional (NT, no split-K): op(B)^T = B^T [K][N] (row stride bt_ld) written from
+  int bt_ld;              // the LDS B images as they stream by - the wide MLP's forward leaves W^T for dX
 };
 
 // An Adam range of the flat buffers, launched on its own or riding in another launch (the wide-MLP
@@ -68,6 +70,8 @@ int dct_flag_wait(int* flag, int* consumed, int* status, void* stream);
 int dct_reducer_close(unsigned long long* s, void* stream);
 int dct_reducer_check(unsigned long long* s, void* stream);
 int dct_phase_accum(unsigned long long* b, int n, void* stream);
+int dct_gemm_bf16_bt(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K, int lda,
+                     int ldb, int ldc, int epilogue, int out_f32, void* aux, uint16_t* bt_out, int bt_ld, void* stream);
 int dct_gemm_bf16(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K, int lda,
                   int ldb, int ldc, int trans_a, int trans_b, int epilogue, int out_f32, int accumulate, void* aux,
                   void* stream);

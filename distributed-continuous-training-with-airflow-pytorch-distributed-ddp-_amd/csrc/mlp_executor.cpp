@@ -39,6 +39,10 @@
 #include "mlp_fused.h"
 #include "runtime.h"
 
+#ifndef EXEC_DX_NT
+#define EXEC_DX_NT 1
+#endif
+
 extern "C" {
 int dct_gather_batch(const void* X, int row_bytes, const int* Y, const int* idx, const int* cursor, int stride,
                      int B, int n_items, void* xdst, int* ydst, void* stream);
@@ -106,6 +110,16 @@ MlpStepExecutor::MlpStepExecutor(const std::vector<int>& dims, int batch, int ac
   P_ = off;
   zr_all_cnt_[0] = P_ + 1;
   plan_partials();
+  wt_.assign(L_, nullptr);
+  wt_ok_.assign(L_, 0);
+#if EXEC_DX_NT
+  for (int l = 1; l < L_; ++l)
+    if (!skinny(l) && dims[l] % 8 == 0 && dims[l + 1] % 8 == 0)
+      if (hipMalloc(&wt_[l], (size_t)dims[l] * dims[l + 1] * sizeof(uint16_t)) != hipSuccess) {
+        (void)hipGetLastError();
+        wt_[l] = nullptr;
+      }
+#endif
 }
 
 void MlpStepExecutor::set_adam(float lr, float b1, float b2, float eps, float wd, int decoupled) {
@@ -135,6 +149,14 @@ void MlpStepExecutor::forward(int rows, hipStream_t st, int layers) {
       ck(dct_skinny_fwd(acts_[l], pb_ + woff_[l], p_ + boff_[l], acts_[l + 1], rows, din, dout, st), "skinny fwd");
       continue;
     }
+    // a hidden layer whose dX runs as a GEMM: the forward also leaves W^T for it (no extra reads)
+    wt_ok_[l] = 0;
+    if (wt_[l] && dct_gemm_bf16_bt(acts_[l], pb_ + woff_[l], acts_[l + 1], p_ + boff_[l], rows, dout, din, din, din,
+                                   dout, epi, /*out_f32*/ 0, aux, wt_[l], dout, st) == 0) {
+      wt_ok_[l] = 1;
+      continue;
+    }
+    (void)hipGetLastError();
     ck(dct_gemm_bf16(acts_[l], pb_ + woff_[l], acts_[l + 1], p_ + boff_[l], rows, dout, din, din, din, dout,
                      /*trans_a*/ 0, /*trans_b*/ 1, epi, /*out_f32*/ 0, /*accumulate*/ 0, aux, st),
        "forward gemm");
@@ -262,10 +284,18 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
       reducer_->mark_ready(2 * l, stream);
     }
     if (l > 0) {  // dZ_{l-1} = (dZ_l W_l) * act'(.)  in the epilogue
-      ck(dct_gemm_bf16(dz_[ci], pb_ + woff_[l], dz_[ci ^ 1], nullptr, rows, din, dout, dout, din, din,
-                       /*trans_a*/ 0, /*trans_b*/ 0, mask_epi, /*out_f32*/ 0, /*accumulate*/ 0,
-                       const_cast<void*>(mask_aux), st),
-         "dX gemm");
+      // NT on the forward's W^T when it wrote one this step (the NN form reads W through transposing
+      // LDS loads), otherwise NN on W
+      if (wt_ok_[l])
+        ck(dct_gemm_bf16(dz_[ci], wt_[l], dz_[ci ^ 1], nullptr, rows, din, dout, dout, dout, din,
+                         /*trans_a*/ 0, /*trans_b*/ 1, mask_epi, /*out_f32*/ 0, /*accumulate*/ 0,
+                         const_cast<void*>(mask_aux), st),
+           "dX gemm");
+      else
+        ck(dct_gemm_bf16(dz_[ci], pb_ + woff_[l], dz_[ci ^ 1], nullptr, rows, din, dout, dout, din, din,
+                         /*trans_a*/ 0, /*trans_b*/ 0, mask_epi, /*out_f32*/ 0, /*accumulate*/ 0,
+                         const_cast<void*>(mask_aux), st),
+           "dX gemm");
       ci ^= 1;
     }
   }
@@ -347,6 +377,8 @@ void MlpStepExecutor::plan_partials() {
 
 MlpStepExecutor::~MlpStepExecutor() {
   for (int q = 0; q < nparts_; ++q) (void)hipFree(part_[q]);
+  for (auto* w : wt_)
+    if (w) (void)hipFree(w);
 }
 
 void MlpStepExecutor::eval_batch(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t idx, int n_items,

@@ -70,6 +70,10 @@ class MlpStepExecutor {
   int part_layer_[3] = {-1, -1, -1}, part_splits_[3] = {1, 1, 1};
   int nparts_ = 0;
   int part_fallbacks_ = 0;  // steps whose planned split-K slices went through g instead (short batch)
+  // W^T (bf16, [din][dout]) of every hidden layer whose dX is a GEMM, written by that layer's forward
+  // GEMM from its LDS B images (dct_gemm_bf16_bt): the dX GEMM then reads it in the forward's NT layout
+  std::vector<uint16_t*> wt_;
+  std::vector<char> wt_ok_;  // this step's forward wrote wt_[l]
 };
 
 }  // namespace dct
