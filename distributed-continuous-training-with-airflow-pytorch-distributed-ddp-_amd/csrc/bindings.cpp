@@ -377,6 +377,14 @@ PYBIND11_MODULE(_dct_native, m) {
       py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("M"), py::arg("N"), py::arg("K"),
       py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("trans_a"), py::arg("trans_b"), py::arg("epilogue"),
       py::arg("out_f32"), py::arg("accumulate"), py::arg("aux"), py::arg("stream"));
+  m.def("gemm_bf16_bt",
+        [](uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias, int M, int N, int K, int lda, int ldb, int ldc,
+           int epilogue, int out_f32, uintptr_t aux, uintptr_t bt_out, int bt_ld, uintptr_t stream) {
+          check(dct_gemm_bf16_bt(P<const uint16_t>(A), P<const uint16_t>(B), P<void>(C), P<const float>(bias), M, N,
+                                 K, lda, ldb, ldc, epilogue, out_f32, P<void>(aux), P<uint16_t>(bt_out), bt_ld,
+                                 reinterpret_cast<void*>(stream)),
+                "gemm_bf16_bt");
+        });
   m.def(
       "gemm_bf16_ex",
       [](uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias, int M, int N, int K, int lda, int ldb, int ldc,
@@ -420,6 +428,10 @@ PYBIND11_MODULE(_dct_native, m) {
                           loss_kind, loss_scale, relu_mask, reinterpret_cast<void*>(stream)),
           "skinny_head");
   });
+  m.attr("EPI_NONE") = 0;
+  m.attr("EPI_BIAS") = 1;
+  m.attr("EPI_BIAS_RELU") = 2;
+  m.attr("EPI_BIAS_GELU") = 3;
   m.attr("EPI_RELU_MASK") = 4;
   m.attr("EPI_GELU_GRAD") = 5;
   m.def(

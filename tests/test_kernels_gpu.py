@@ -1156,3 +1156,41 @@ def test_tt_ln_replica_fold_complete_and_matches_direct_atomics(cuda, B, monkeyp
         for k in ln_keys:
             err = (got[k] - direct[k]).abs().max()
             assert err <= 2e-4 * direct[k].abs().max() + 1e-6, (it, k, float(err), float(direct[k].abs().max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [4096, 300])
+def test_gemm_forward_wt_side_output_and_nt_dx(cuda, M):
+    """The wide MLP's forward GEMM side output (csrc/gemm_bf16.hip dct_gemm_bf16_bt): W^T written from
+    the LDS B images (bt_out) equals W.t() bit for bit, and the dX GEMM the executor runs on it - NT on
+    W^T - equals the NN form on W (both with the bf16-activation ReLU mask, EPI_RELU_MASK) bit for bit."""
+    nat = native()
+    st = torch.cuda.current_stream().cuda_stream
+    torch.manual_seed(5)
+    N, K = 1024, 512
+    X = (torch.randn(M, K, device=cuda) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=cuda) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, device=cuda) * 0.1
+    Y = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    WT = torch.zeros(K, N, device=cuda, dtype=torch.bfloat16)
+    nat.gemm_bf16_bt(X.data_ptr(), W.data_ptr(), Y.data_ptr(), b.data_ptr(), M, N, K, K, K, N, nat.EPI_BIAS_RELU, 0,
+                     0, WT.data_ptr(), N, st)
+    torch.cuda.synchronize()
+    assert torch.equal(WT, W.t().contiguous())
+    ref = torch.relu(X.float() @ W.float().t() + b)
+    assert (Y.float() - ref).abs().max() < 2e-2 * ref.abs().max()
+    # dX of the NEXT layer: dZ [M][N2] (W2 [N2][N]) -> dX [M][N] masked by relu'(Y)
+    N2 = 1024
+    dZ = (torch.randn(M, N2, device=cuda) * 0.1).to(torch.bfloat16)
+    W2 = (torch.randn(N2, N, device=cuda) * 0.05).to(torch.bfloat16)
+    W2T = W2.t().contiguous()
+    d_nn = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    d_nt = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    nat.gemm_bf16(dZ.data_ptr(), W2.data_ptr(), d_nn.data_ptr(), 0, M, N, N2, N2, N, N, 0, 0, nat.EPI_RELU_MASK, 0, 0,
+                  Y.data_ptr(), st)
+    nat.gemm_bf16(dZ.data_ptr(), W2T.data_ptr(), d_nt.data_ptr(), 0, M, N, N2, N2, N2, N, 0, 1, nat.EPI_RELU_MASK, 0, 0,
+                  Y.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert torch.equal(d_nn, d_nt)
+    want = (dZ.float() @ W2.float()) * (Y.float() > 0)
+    assert (d_nt.float() - want).abs().max() < 2e-2 * want.abs().max()
