@@ -92,6 +92,10 @@ def parse():
     return a
 
 
+# this rank's split of its last timed window: host enqueue of the K steps, then the wait for them
+WINDOW_SPLIT = {}
+
+
 def _timed(ctx, fn, device_barrier=None):
     """Seconds for fn() (the K timed steps), max over ranks, bracketed by barrier + synchronize.
 
@@ -135,6 +139,8 @@ def _timed(ctx, fn, device_barrier=None):
         torch.cuda.synchronize()
         ctx.barrier()  # host-side (gloo) or a no-op at world size 1
     dt = time.perf_counter() - t0
+    WINDOW_SPLIT["enqueue_us"] = round((t_enq - t0) * 1e6, 1)
+    WINDOW_SPLIT["wait_us"] = round((dt - (t_enq - t0)) * 1e6, 1)
     if gc_paused:
         gc.enable()
     dt_t = torch.tensor([dt], dtype=torch.float64, device=ctx.device if ctx.backend == "nccl" else "cpu")
@@ -494,6 +500,7 @@ def _measure(a, ctx, stack):
             "ranks": ctx.world_size,
             "ranks_per_device": (round(ctx.world_size / n_dev, 3) if n_dev else None),
             "us_per_step": round(ms_step * 1e3, 3),
+            "window_rank0_us": dict(WINDOW_SPLIT),
             "epoch_wall_clock_s_train": round(steps_per_epoch * ms_step / 1e3, 6),  # derived
             "epoch_rows": a.epoch_rows,
             "loss_first": round(first_l, 4),

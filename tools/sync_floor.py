@@ -33,7 +33,10 @@ def main():
         return ts[len(ts) // 2] * 1e6, ts[0] * 1e6
 
     dev = torch.device("cuda", 0)
-    dims = [5, 64, 2]
+    # --dims 5,128,128,2 (default: the headline 3x128; 5,64,2 = the reference model)
+    dims = [5, 128, 128, 2]
+    if "--dims" in sys.argv:
+        dims = [int(x) for x in sys.argv[sys.argv.index("--dims") + 1].split(",")]
     P = mlp_num_params(dims)
     k = FusedMLPKernel(dims, bmax=4)
     p = torch.randn(P, device=dev) * 0.1
@@ -60,10 +63,15 @@ def main():
         "native_null_launch_sync": best(lambda: (nat.zero_f32(tiny.data_ptr(), 1, stream), torch.cuda.synchronize())),
         "bound_s1_launch_sync": best(lambda: (bl.run(0, 1), torch.cuda.synchronize())),
         "bound_s20_launch_sync": best(lambda: (bl.run(0, 20), torch.cuda.synchronize())),
+        "bound_s40_launch_sync": best(lambda: (bl.run(0, 40), torch.cuda.synchronize())),
     }
     tag = "spin" if spin else "env ROC_ACTIVE_WAIT_TIMEOUT=" + os.environ.get("ROC_ACTIVE_WAIT_TIMEOUT", "-")
     for name, (med, lo) in out.items():
         print(f"[{tag}] {name:26s} median {med:8.2f} us   min {lo:8.2f} us", flush=True)
+    s1, s20, s40 = (out[f"bound_s{k}_launch_sync"][0] for k in (1, 20, 40))
+    per = (s40 - s20) / 20.0
+    print(f"dims {dims}: per step {per:.3f} us, fixed per launch+sync {s20 - 20 * per:.2f} us "
+          f"(null launch+sync {out['native_null_launch_sync'][0]:.2f} us)", flush=True)
 
 
 if __name__ == "__main__":
