@@ -683,6 +683,8 @@ PYBIND11_MODULE(_dct_native, m) {
            py::arg("idx"), py::arg("n_items"), py::arg("cursor"), py::arg("rows"), py::arg("stats"),
            py::arg("stream"))
       .def_property("adam_ride", &dct::MlpStepExecutor::adam_ride, &dct::MlpStepExecutor::set_adam_ride)
+      .def("set_gather_fuse", &dct::MlpStepExecutor::set_gather_fuse)
+      .def_property_readonly("gather_fused_steps", &dct::MlpStepExecutor::gather_fused_steps)
       .def_property_readonly("num_params", &dct::MlpStepExecutor::num_params)
       .def_property_readonly("part_fallbacks", &dct::MlpStepExecutor::part_fallbacks)
       .def_property_readonly("partial_layers", &dct::MlpStepExecutor::partial_layers);

@@ -270,6 +270,36 @@ __device__ __forceinline__ void g2_fill(const uint16_t* __restrict__ G, int ld, 
   }
 }
 
+// The KC fill of g2_fill<false, ROWS, NT, KT> with a row pointer per chunk (rows[q]: the source row
+// of this thread's chunk q) - the gathered A operand of dct_gemm_bf16_gather_fwd
+template <int ROWS, int NT, int KT, int CH>
+__device__ __forceinline__ void g2_fill_rows(const uint16_t* const (&rows)[CH], int k0, char* img) {
+  constexpr int CPR = KT / 8;
+  static_assert(CH * NT == ROWS * CPR, "whole chunks per thread");
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+#pragma unroll
+  for (int q = 0; q < CH; ++q) {
+    const int L = q * NT + wave * 64 + lane;
+    const int r = L / CPR, pc = L % CPR;
+    const uint16_t* src = rows[q] + k0 + (pc ^ (r & (CPR - 1))) * 8;
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(lds_void*)(img + (q * NT + wave * 64) * 16));
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(dst)
+        : "memory");
+  }
+}
+
+__device__ __forceinline__ int gather_row(const GatherFwd& ga, int c, int m) {
+  int q = c * ga.stride + m;
+  q = q < ga.n_items ? q : (ga.n_items > 0 ? q % ga.n_items : 0);
+  return ga.idx[q];
+}
+
 // 16 x 32 operand fragment (rows rb..rb+15, k-slice ks) in the MFMA A/B layout
 template <bool MC, int KT = 64>
 __device__ __forceinline__ bf16x8 g2_frag(const char* img, int rb, int ks, int lane) {
@@ -344,8 +374,10 @@ __device__ __forceinline__ int xcd_wgid() {
 // KT: k per LDS stage.  128 (8-wave tiles only): each KC row contributes 256 contiguous bytes per
 // stage instead of 128 - the one-tile-per-CU grids are bound by the CU's global -> LDS rate, which the
 // longer row segments raise (tools/probes/gemm_probe.hip: 4096 x 1024 x 1024 NT 14.3 -> 12.7 us).
-template <bool TA, bool TB, bool SPLIT, int BM, int S, int WM = 2, int KT = 64>
-__device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wgid) {
+// GA: A is gathered dataset rows (dct_gemm_bf16_gather_fwd, ga: its GatherFwd)
+template <bool TA, bool TB, bool SPLIT, int BM, int S, int WM = 2, int KT = 64, bool GA = false>
+__device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wgid, const GatherFwd* ga = nullptr) {
+  static_assert(!GA || (!TA && TB && !SPLIT), "gathered A: the forward (NT) kernels");
   static_assert(BM == 128 || (BM == 64 && !TA), "BM = 64 needs a row-major (KC) A image");
   static_assert(WM == 2 || (WM == 4 && BM == 128), "8-wave tiles: 128 x 128");
   static_assert(KT == 64 || (KT == 128 && WM == 4 && S == 2), "128-deep k stages: 8-wave tiles, 2 stages");
@@ -376,9 +408,28 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
   const bool do_cs = g.colsum != nullptr && tn == 0 && wc == 0;
   float cs[IM] = {};
   auto img = [&](int buf, int op) -> char* { return smem2 + (buf * 2 + op) * IMG; };
+  // GA: the dataset row of each A chunk this thread loads (the same rows in every k stage)
+  constexpr int ACH = GA ? BM * (KT / 8) / NT : 1;
+  const uint16_t* arow[ACH];
+  int gcur = 0;
+  int glab = 0, glab_r = -1;  // GA: this thread's label (row glab_r), loaded before the k loop, stored after
+  if constexpr (GA) {
+    gcur = ga->cursor[0];
+    const int t = wgid * NT + tid;
+    if (ga->ydst && t < g.M) {
+      glab_r = t;
+      glab = ga->Y[gather_row(*ga, gcur, t)];
+    }
+#pragma unroll
+    for (int q = 0; q < ACH; ++q) {
+      const int r = (q * NT + tid) / (KT / 8);
+      arow[q] = g.A + (size_t)gather_row(*ga, gcur, min(m0 + r, g.M - 1)) * g.lda;
+    }
+  }
   auto fill = [&](int buf, int kt) {
     const int k0 = kt * KT;
-    if (!TA) g2_fill<false, BM, NT, KT>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
+    if constexpr (GA) g2_fill_rows<BM, NT, KT, ACH>(arow, k0, img(buf, 0));
+    else if (!TA) g2_fill<false, BM, NT, KT>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
     else g2_fill<true, 128, NT, KT>(g.A, g.lda, g.M, m0, k0, img(buf, 0));
     if (TB) g2_fill<false, 128, NT, KT>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
     else g2_fill<true, 128, NT, KT>(g.B, g.ldb, g.N, n0, k0, img(buf, 1));
@@ -387,8 +438,11 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
   constexpr int FILL_OPS = ((TA ? 16 * KT : BM * KT / 8) + 16 * KT) / NT;
   const int n = kt1 - kt0;
   if (n > 0) {
+    // GA: every LDS buffer is filled up front (gathered rows are HBM round trips, not L2 hits: one
+    // latency for all the stages that fit instead of one per stage); otherwise S - 1 stages
+    constexpr int PRE = GA ? S : S - 1;
 #pragma unroll
-    for (int s = 0; s < S - 1; ++s)
+    for (int s = 0; s < PRE; ++s)
       if (s < n) fill(s, kt0 + s);
     // B^T side output (NT forward GEMMs of the wide MLP): the tiles_m workgroups of one column panel
     // each write a k-slice of its transpose, rows [bt_lo, bt_hi), from the B image of the k-stage that
@@ -405,7 +459,7 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
     for (int it = 0; it < n; ++it) {
       wait_stage<FILL_OPS, S>(min(S - 2, n - 1 - it));  // this wave's part of stage `it` has landed
       raw_barrier();  // every wave's part has; every wave finished reading stage it - 1
-      if (it + S - 1 < n) fill((it + S - 1) & (S - 1), kt0 + it + S - 1);  // refill stage it - 1
+      if (it + S - 1 < n && it + S - 1 >= PRE) fill((it + S - 1) & (S - 1), kt0 + it + S - 1);  // refill stage it - 1
       const int cur = it & (S - 1);
       const char* ai = img(cur, 0);
       const char* bi = img(cur, 1);
@@ -432,6 +486,22 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
           }
         }
       }
+      if constexpr (GA) {
+        // the gathered rows for the dW GEMM, from the A image of this k stage: the tiles_n workgroups
+        // of a row panel each write a band of its rows, 16 B per thread
+        if (ga->a_out) {
+          constexpr int CPR = KT / 8, RPP = NT / CPR;
+          const int k0 = (kt0 + it) * KT;
+          const int band = (BM + tiles_n - 1) / tiles_n;
+          const int lo = min(BM, tn * band), hi = min(BM, lo + band);
+          for (int rb = lo; rb < hi; rb += RPP) {
+            const int rr = rb + tid / CPR, cc = tid % CPR;
+            if (rr < hi && m0 + rr < g.M)
+              *reinterpret_cast<uint4*>(ga->a_out + (size_t)(m0 + rr) * g.K + k0 + cc * 8) =
+                  *reinterpret_cast<const uint4*>(ai + rr * (2 * KT) + ((cc ^ (rr & (CPR - 1))) << 4));
+          }
+        }
+      }
 #pragma unroll
       for (int ks = 0; ks < KT / 32; ++ks) {
         bf16x8 af[IM], bfr[4];
@@ -452,6 +522,24 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
             acc[i][j] = SPLIT ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0)
                               : __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       }
+    }
+  }
+  if constexpr (GA) {
+    // the rest of the step prologue, after the k loop (its loads drained, so these waits cover only
+    // themselves), spread over the grid: labels, the Adam step counter, the gradient ranges to clear
+    const int nwg = ((g.M + BM - 1) / BM) * tiles_n;
+    const int t = wgid * NT + tid, nt = nwg * NT;
+    if (t == 0 && ga->step_counter) ga->step_counter[0] += 1;
+    if (glab_r >= 0) ga->ydst[glab_r] = glab;
+    if (ga->ydst)
+      for (int r = t + nt; r < g.M; r += nt) ga->ydst[r] = ga->Y[gather_row(*ga, gcur, r)];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // (constant indices into the kernel argument)
+      if (q >= ga->nz) break;
+      float* z = ga->zero + ga->zoff[q];
+      const int64_t n = ga->zcnt[q], n4 = n >> 2;
+      for (int64_t i = t; i < n4; i += nt) reinterpret_cast<float4*>(z)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (t < n - (n4 << 2)) z[(n4 << 2) + t] = 0.f;
     }
   }
   if (do_cs) {  // lanes l, l+16, l+32, l+48 hold partial sums of the same row
@@ -613,6 +701,12 @@ __device__ __forceinline__ void gemm2_body(const GemmArgs& g, int splits, int wg
 template <bool TA, bool TB, bool SPLIT, int BM = 128, int S = 2, int WM = 2, int KT = 64>
 __global__ __launch_bounds__(128 * WM, WM == 4 ? 2 : (BM == 64 ? 4 : 2)) void gemm2_kernel(GemmArgs g, int splits) {
   gemm2_body<TA, TB, SPLIT, BM, S, WM, KT>(g, splits, xcd_wgid());
+}
+
+// the wide-MLP step's first forward GEMM with the batch gather folded in (GatherFwd, kernels.h)
+template <int BM, int S, int WM, int KT>
+__global__ __launch_bounds__(128 * WM, WM == 4 ? 2 : 2) void gemm2_gather_kernel(GemmArgs g, GatherFwd ga) {
+  gemm2_body<false, true, false, BM, S, WM, KT, true>(g, 1, xcd_wgid(), &ga);
 }
 
 // Grouped split-K launch: up to DW_GROUP independent problems (the dW GEMMs of one transformer
@@ -1177,6 +1271,46 @@ extern "C" int dct_gemm_bf16_bt(const uint16_t* A, const uint16_t* B, void* C, c
   if (!gemm_v2_ok(g, 0, 1) || split_k || (((uintptr_t)bt_out) & 15) || (bt_ld % 8) || (N % 8))
     return (int)hipErrorInvalidValue;
   return (int)launch_gemm2<false, true>(g, reinterpret_cast<hipStream_t>(stream));
+}
+
+// The wide-MLP step's batch gather (csrc/step_kernels.hip gather_batch_kernel) folded into its first
+// forward GEMM: the A chunks are LDS-DMA loads from the dataset rows themselves, one workgroup per row band
+// writes the gathered rows out for the dW GEMM, and labels / step counter / gradient clearing ride along -
+// one launch and one kernel boundary fewer per step.  The same two kernel shapes launch_gemm2 picks for an
+// NT bf16 forward: 8-wave 128-deep stages for a grid of 1/2..1 tile per CU, else 4 waves, 64-deep stages.
+extern "C" int dct_gemm_bf16_gather_fwd(const uint16_t* X, int ldx, const uint16_t* W, uint16_t* C, const float* bias,
+                                        int M, int N, int K, int epilogue, void* aux, const dct::GatherFwd* ga,
+                                        void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (!ga || !ga->idx || !ga->cursor || ga->n_items <= 0 || ga->stride < 0 || ga->nz < 0 || ga->nz > 4 ||
+      (ga->ydst && !ga->Y) || (((uintptr_t)ga->a_out) & 15))
+    return (int)hipErrorInvalidValue;
+  for (int q = 0; q < ga->nz; ++q)
+    if (!ga->zero || (((uintptr_t)ga->zero) & 15) || ga->zoff[q] % 4 || ga->zcnt[q] < 0) return (int)hipErrorInvalidValue;
+  if (epilogue == dct::EPI_RELU_MASK || epilogue == dct::EPI_GELU_GRAD) return (int)hipErrorInvalidValue;
+  dct::GemmArgs g{};
+  g.A = X; g.B = W; g.C = C; g.bias = bias; g.aux = aux;
+  g.M = M; g.N = N; g.K = K; g.lda = ldx; g.ldb = K; g.ldc = N;
+  g.epilogue = epilogue; g.out_f32 = 0; g.accumulate = 0; g.alpha = 1.0f;
+  g.vec_a = ((((uintptr_t)X) & 15) == 0) && (ldx % 8 == 0);
+  g.vec_b = ((((uintptr_t)W) & 15) == 0) && (K % 8 == 0);
+  if (!gemm_v2_ok(g, 0, 1) || N % 8) return (int)hipErrorInvalidValue;
+  const int tiles = ((M + dct::GBM - 1) / dct::GBM) * ((N + dct::GBN - 1) / dct::GBN);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (tiles <= device_cus() && 2 * tiles > device_cus() && K % 128 == 0 && K >= 256) {
+    auto fn = dct::gemm2_gather_kernel<128, 2, 4, 128>;
+    const size_t lds = (size_t)2 * 2 * (128 * 2 * 128);
+    hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(fn, dim3(tiles), dim3(512), lds, st, g, *ga);
+    return (int)hipGetLastError();
+  }
+  auto fn = dct::gemm2_gather_kernel<128, 2, 2, 64>;
+  const size_t lds = (size_t)(K / dct::GBK > 1 ? 4 : 2) * dct::G2_BYTES;
+  hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(fn, dim3(tiles), dim3(256), lds, st, g, *ga);
+  return (int)hipGetLastError();
 }
 
 extern "C" int dct_gemm_bf16(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K,

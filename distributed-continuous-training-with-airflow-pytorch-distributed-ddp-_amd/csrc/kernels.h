@@ -29,6 +29,24 @@ struct GemmArgs {
   int bt_ld;              // the LDS B images as they stream by - the wide MLP's forward leaves W^T for dX
 };
 
+// The wide-MLP step's batch gather folded into its first forward GEMM (dct_gemm_bf16_gather_fwd): A row
+// m is dataset row idx[wrap(*cursor * stride + m)] (wrapping inside [0, n_items)), loaded straight
+// into the LDS A images; the gathered rows are written once to a_out [M][K] (the dW GEMM's operand),
+// and the rest of the step prologue rides along: labels ydst[m] = Y[row], *step_counter += 1, and
+// up to 4 ranges [zoff, zoff + zcnt) of `zero` cleared (zoff % 4 == 0).
+struct GatherFwd {
+  const int* idx;
+  const int* cursor;
+  int stride, n_items;
+  uint16_t* a_out;
+  const int* Y;
+  int* ydst;
+  int* step_counter;
+  float* zero;
+  int nz;
+  int64_t zoff[4], zcnt[4];
+};
+
 // An Adam range of the flat buffers, launched on its own or riding in another launch (the wide-MLP
 // executor: each layer's Adam in the next lower layer's dW launch, csrc/mlp_executor.cpp).  Fields as
 // AdamArgs (adam_impl.h); elements [lo, hi), lo % 4 == 0, hi % 4 == 0 or hi == n.
@@ -75,6 +93,10 @@ int dct_gemm_bf16_bt(const uint16_t* A, const uint16_t* B, void* C, const float*
 int dct_gemm_bf16(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K, int lda,
                   int ldb, int ldc, int trans_a, int trans_b, int epilogue, int out_f32, int accumulate, void* aux,
                   void* stream);
+// C [M][N] bf16 = act(gather(X) W^T + bias), X the dataset [rows][K] (row stride ldx), W [N][K]; see
+// GatherFwd.  hipErrorInvalidValue (nothing launched) when the shape does not take the LDS-DMA kernels.
+int dct_gemm_bf16_gather_fwd(const uint16_t* X, int ldx, const uint16_t* W, uint16_t* C, const float* bias, int M,
+                             int N, int K, int epilogue, void* aux, const dct::GatherFwd* ga, void* stream);
 // same, plus colsum[m] += sum over k of op(A)[m][k] (fused bias gradient; colsum accumulates)
 int dct_gemm_bf16_ex(const uint16_t* A, const uint16_t* B, void* C, const float* bias, int M, int N, int K, int lda,
                      int ldb, int ldc, int trans_a, int trans_b, int epilogue, int out_f32, int accumulate, void* aux,

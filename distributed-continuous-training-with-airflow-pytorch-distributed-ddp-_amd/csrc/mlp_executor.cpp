@@ -134,9 +134,9 @@ bool MlpStepExecutor::fused_head() const {
   return !off && act_ == ACT_RELU && skinny(l) && dct_skinny_head_supported(dims_[l], dims_[L_]);
 }
 
-void MlpStepExecutor::forward(int rows, hipStream_t st, int layers) {
+void MlpStepExecutor::forward(int rows, hipStream_t st, int layers, int first) {
   if (layers < 0) layers = L_;
-  for (int l = 0; l < layers; ++l) {
+  for (int l = first; l < layers; ++l) {
     const int din = dims_[l], dout = dims_[l + 1];
     const bool last = l == L_ - 1;
     int epi = EPI_BIAS;
@@ -176,10 +176,32 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
   // of the split-K layers handed to Adam (part_) untouched in g, so those ranges are skipped (the
   // tabular step zeroed 13.6 MB per step for 5 k accumulated values); anything else zeroes all of g.
   const bool skip = rows == B_ && nzr_ > 0;
-  ck(dct_gather_batch_step_ranges(reinterpret_cast<const void*>(X), row_bytes, reinterpret_cast<const int*>(Y),
-                                  reinterpret_cast<const int*>(idx), cur, B_, rows, n_items, acts_[0], y_, sc, g_,
-                                  skip ? nzr_ : 1, skip ? zr_off_ : zr_all_off_, skip ? zr_cnt_ : zr_all_cnt_, st),
-     "gather_batch");
+  // a full batch whose first layer is a hidden GEMM layer gathers inside that layer's forward GEMM
+  // (labels, step counter and the gradient ranges riding along); anything else, or a shape the fused
+  // kernel does not take, runs the gather launch first
+  int first = 0;
+  if (gather_fuse_ && skip && L_ > 1 && !skinny(0)) {
+    GatherFwd ga{};
+    ga.idx = reinterpret_cast<const int*>(idx); ga.cursor = cur; ga.stride = B_; ga.n_items = n_items;
+    ga.a_out = acts_[0]; ga.Y = reinterpret_cast<const int*>(Y); ga.ydst = y_; ga.step_counter = sc;
+    ga.zero = g_; ga.nz = nzr_;
+    for (int q = 0; q < nzr_; ++q) { ga.zoff[q] = zr_off_[q]; ga.zcnt[q] = zr_cnt_[q]; }
+    const int epi = act_ == ACT_GELU ? EPI_BIAS_GELU : EPI_BIAS_RELU;
+    void* aux = act_ == ACT_GELU ? pre_[1] : nullptr;
+    wt_ok_[0] = 0;
+    if (dct_gemm_bf16_gather_fwd(reinterpret_cast<const uint16_t*>(X), row_bytes / 2, pb_ + woff_[0], acts_[1],
+                                 p_ + boff_[0], rows, dims_[1], dims_[0], epi, aux, &ga, st) == 0) {
+      first = 1;
+      ++gather_fused_steps_;
+    } else {
+      (void)hipGetLastError();
+    }
+  }
+  if (first == 0)
+    ck(dct_gather_batch_step_ranges(reinterpret_cast<const void*>(X), row_bytes, reinterpret_cast<const int*>(Y),
+                                    reinterpret_cast<const int*>(idx), cur, B_, rows, n_items, acts_[0], y_, sc, g_,
+                                    skip ? nzr_ : 1, skip ? zr_off_ : zr_all_off_, skip ? zr_cnt_ : zr_all_cnt_, st),
+       "gather_batch");
   // Adam riding in the dW launches (no reducer, full batch): when layer l's dW is launched every layer
   // above l has finished its backward (dW and dX), so Adam over those layers' range [woff[l+1], hi)
   // runs in extra workgroups of that dW launch (dct_gemm_bf16_dw_partials_adam) instead of all of it
@@ -208,7 +230,7 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
   if (fused_head()) {
     // classifier head fused (csrc/skinny.hip skinny_head_kernel): logits, loss (into the loss
     // slot g[P]), dlogits, dW/db of the head and the layer below's dZ in one pass over its input
-    forward(rows, st, L_ - 1);
+    forward(rows, st, L_ - 1, first);
     const int l = L_ - 1;
     ck(dct_skinny_head(acts_[l], pb_ + woff_[l], p_ + boff_[l], y_, l > 0 ? dz_[1] : nullptr, g_ + woff_[l],
                        g_ + boff_[l], g_ + P_, rows, dims_[l], C, 1.0f / (float)rows, loss_kind_, 1.0f / (float)rows,
@@ -222,7 +244,7 @@ void MlpStepExecutor::step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t id
     ci = 1;
     top = L_ - 2;
   } else {
-    forward(rows, st);
+    forward(rows, st, -1, first);
     ck(dct_loss_fwd_bwd_ex(acts_[L_], 1, y_, dz_[ci], g_ + P_, nullptr, rows, C, 1.0f / (float)rows, loss_kind_,
                            1.0f / (float)rows, st),
        "loss");

@@ -23,6 +23,10 @@ class MlpStepExecutor {
   void set_adam(float lr, float b1, float b2, float eps, float wd, int decoupled);
   void set_adam_ride(bool on) { adam_ride_ = on; }
   bool adam_ride() const { return adam_ride_; }
+  // full-batch steps gather the batch inside the first forward GEMM (dct_gemm_bf16_gather_fwd) instead
+  // of a gather launch before it; gather_fused_steps() counts the steps that did
+  void set_gather_fuse(bool on) { gather_fuse_ = on; }
+  int64_t gather_fused_steps() const { return gather_fused_steps_; }
   // One optimizer step on batch *cursor of idx (rows <= batch); advances *cursor and *step_counter.
   void step(uintptr_t X, int row_bytes, uintptr_t Y, uintptr_t idx, int n_items, uintptr_t cursor,
             uintptr_t step_counter, uintptr_t loss_out, int loss_cap, int rows, uintptr_t stream);
@@ -40,10 +44,12 @@ class MlpStepExecutor {
  private:
   bool fused_head_knob_ = true, dw_into_adam_knob_ = true;  // DCT_FUSED_HEAD / DCT_DW_INTO_ADAM at construction
   bool adam_ride_ = true;  // Adam ranges riding in the dW launches (set_adam_ride)
+  bool gather_fuse_ = true;  // set_gather_fuse
+  int64_t gather_fused_steps_ = 0;
   int nzr_ = 0;                                   // gradient ranges a full-batch step zeroes (plan_partials)
   int64_t zr_off_[4] = {}, zr_cnt_[4] = {};
   int64_t zr_all_off_[1] = {0}, zr_all_cnt_[1] = {0};  // the whole buffer (set in the constructor)
-  void forward(int rows, hipStream_t st, int layers = -1);  // layers 0 .. layers-1 (default all)
+  void forward(int rows, hipStream_t st, int layers = -1, int first = 0);  // layers first .. layers-1 (default all)
   bool fused_head() const;
   void plan_partials();
   int part_slot(int l) const;  // partial-buffer slot of layer l's dW, or -1

@@ -172,3 +172,31 @@ def test_adam_riding_in_dw_launches_matches_one_adam_launch(extra, cuda):
     assert torch.isfinite(l1).all() and torch.allclose(l1, l0, atol=1e-4), (l1 - l0).abs().max()
     assert (p1 - p0).norm() / p0.norm() < 1e-3
     assert (m1 - m0).norm() / m0.norm() < 1e-2 and (v1 - v0).norm() / v0.norm() < 1e-2
+
+
+@pytest.mark.parametrize("extra", [0, 300])
+def test_gather_fused_into_first_forward_gemm_matches_gather_launch(extra, cuda):
+    """Full batches gather their rows inside the first forward GEMM (csrc/gemm_bf16.hip
+    dct_gemm_bf16_gather_fwd: dataset rows straight into the LDS A images, the gathered rows written
+    out for the dW GEMM, labels / step counter / gradient clearing riding along) instead of the gather
+    launch: the same trajectory as the gather launch (float-atomic bias gradients: equal to rounding).
+    ``extra``: the partial last batch of each epoch takes the gather launch."""
+    dims, B = [256, 1024, 1024, 1024, 2], 4096
+    X, Y = _data(6 * B + extra, dims[0], seed=9)
+    rows = torch.arange(X.shape[0])
+    res = {}
+    for fuse in (True, False):
+        model, eng = _engine(dims, B, loss="ce", lr=1e-3, use_graph=False)  # (eager: one host step per step)
+        eng.exe.set_gather_fuse(fuse)
+        eng.attach_data(X, Y, rows, rows[:B])
+        losses = torch.cat([eng.train_epoch(ep).cpu() for ep in range(2)])
+        torch.cuda.synchronize()
+        full = 2 * (X.shape[0] // B)
+        assert eng.exe.gather_fused_steps == (full if fuse else 0), eng.exe.gather_fused_steps
+        res[fuse] = (losses, eng.p.cpu(), eng.m.cpu(), int(eng.step_counter.item()))
+    (l1, p1, m1, s1), (l0, p0, m0, s0) = res[True], res[False]
+    assert s1 == s0 == 2 * -(-X.shape[0] // B)
+    assert torch.isfinite(l1).all() and torch.allclose(l1, l0, atol=1e-4), (l1 - l0).abs().max()
+    assert (p1 - p0).norm() / p0.norm() < 1e-3
+    assert (m1 - m0).norm() / m0.norm() < 1e-2
+
