@@ -544,6 +544,9 @@ PYBIND11_MODULE(_dct_native, m) {
   m.def("tt_head_bwd", [](std::vector<uintptr_t> p, int B, int T, int D, int C, float eps, uintptr_t st) {
     check(dct_tt_head_bwd(p.data(), (int)p.size(), B, T, D, C, eps, reinterpret_cast<void*>(st)), "tt_head_bwd");
   });
+  m.def("tt_head_fused", [](std::vector<uintptr_t> p, int B, int T, int D, int C, float eps, uintptr_t st) {
+    check(dct_tt_head_fused(p.data(), (int)p.size(), B, T, D, C, eps, reinterpret_cast<void*>(st)), "tt_head_fused");
+  });
   m.def("gemm_bf16_dw_grouped",
         [](std::vector<uintptr_t> dz, std::vector<uintptr_t> x, std::vector<uintptr_t> c, std::vector<int> M,
            std::vector<int> N, int K, std::vector<uintptr_t> colsum, int accumulate, uintptr_t stream) {

@@ -160,6 +160,7 @@ int dct_tt_embed_fwd(const float* x, const float* E, const float* c, float* h, i
 int dct_tt_embed_bwd(const float* x, const float* dh, float* dE, float* dc, int B, int F, int Dm, void* stream);
 int dct_tt_head_fwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C, float eps, void* stream);
 int dct_tt_head_bwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C, float eps, void* stream);
+int dct_tt_head_fused(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C, float eps, void* stream);
 int dct_gemm_bf16_dw_grouped(int n, const uint16_t* const* dZ, const uint16_t* const* X, float* const* C,
                              const int* M, const int* N, int K, float* const* colsum, int accumulate, void* stream);
 int dct_gemm_bf16_dw_grouped_embed(int n, const uint16_t* const* dZ, const uint16_t* const* X, float* const* C,

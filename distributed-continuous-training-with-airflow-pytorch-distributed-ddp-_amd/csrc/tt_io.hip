@@ -183,19 +183,24 @@ __global__ __launch_bounds__(64 * NW) void head_fwd_kernel(HeadArgs a) {
   }
 }
 
-template <int NW>
+// FWD: the training forward with the backward folded in (dct_tt_head_fused): the loss as head_fwd_kernel
+// stores it, and every gradient as this kernel computes it for an upstream gradient of exactly 1 - the
+// seed the autograd engine's loss.backward(ones) passes - so the training step needs no backward launch
+template <int NW, bool FWD = false>
 __global__ __launch_bounds__(64 * NW) void head_bwd_kernel(HeadArgs a) {
   __shared__ float red[NW][2 + CMAX][D];  // per wave: dln_w, dln_b, dW[C]
   __shared__ float rbias[NW][CMAX];
+  __shared__ float lsum[NW];
   const int w = threadIdx.x >> 6, d = threadIdx.x & 63;
   const int b = blockIdx.x * NW + w;
   const bool live = b < a.B;
   float gw = 0.f, gb = 0.f, gW[CMAX], gbias[CMAX];
 #pragma unroll
   for (int k = 0; k < CMAX; ++k) { gW[k] = 0.f; gbias[k] = 0.f; }
+  if (FWD && d == 0) lsum[w] = 0.f;
   if (live) {
     const int yb = (int)a.y[b];
-    const float dls = a.dloss[0];
+    const float dls = FWD ? 1.f : a.dloss[0];
     const HeadFwd r = head_chain(a, b, d);
     float m = r.logit[0];
 #pragma unroll
@@ -203,6 +208,12 @@ __global__ __launch_bounds__(64 * NW) void head_bwd_kernel(HeadArgs a) {
     float se = 0.f;
 #pragma unroll
     for (int k = 0; k < CMAX; ++k) se += (k < a.C) ? __expf(r.logit[k] - m) : 0.f;
+    if (FWD && d == 0) {  // the sample's loss, as head_fwd_kernel
+      float ly = 0.f;
+#pragma unroll
+      for (int k = 0; k < CMAX; ++k) ly = (k == yb) ? r.logit[k] : ly;
+      lsum[w] = (m + __logf(se) - ly) / a.B;
+    }
     const float scale = dls / a.B, inv = 1.f / se;
     float dz = 0.f;
 #pragma unroll
@@ -257,6 +268,27 @@ __global__ __launch_bounds__(64 * NW) void head_bwd_kernel(HeadArgs a) {
 #pragma unroll
     for (int q = 0; q < NW; ++q) v += rbias[q][threadIdx.x];
     atomicAdd(a.dbias + threadIdx.x, v);
+  }
+  if constexpr (FWD) {  // the loss: block partials and the last block's ordered sum, as head_fwd_kernel
+    __shared__ unsigned last;
+    if (threadIdx.x == 0) {
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) v += lsum[i];
+      atomicExch(a.partial + blockIdx.x, v);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      last = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x < 64) {
+      float s = 0.f;
+      for (unsigned i = threadIdx.x; i < gridDim.x; i += 64) s += atomicAdd(a.partial + i, 0.f);
+      s = wsum(s);
+      if (threadIdx.x == 0) {
+        a.loss[0] = s;
+        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
 }
 
@@ -334,6 +366,28 @@ int dct_tt_head_bwd(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C,
     hipLaunchKernelGGL(dct::ttio::head_bwd_kernel<nwp>, dim3((B + nwp - 1) / nwp), dim3(64 * nwp), 0, st, a);
   else
     hipLaunchKernelGGL(dct::ttio::head_bwd_kernel<nw>, dim3((B + nw - 1) / nw), dim3(64 * nw), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// ptrs: h, y(int64), ln_w, ln_b, W, bias, loss, partial, ticket, dh, dh16, dln_w, dln_b, dW, dbias:
+// the forward's loss and the backward's gradients for an upstream loss gradient of 1, one launch
+int dct_tt_head_fused(const uintptr_t* p, int n_ptrs, int B, int T, int Dm, int C, float eps, void* stream) {
+  if (n_ptrs != 15 || Dm != dct::ttio::D || C < 1 || C > dct::ttio::CMAX || B <= 0 || T <= 0 ||
+      ((p[0] | p[9] | p[10]) & 15))
+    return (int)hipErrorInvalidValue;
+  dct::ttio::HeadArgs a{};
+  a.h = (const float*)p[0]; a.y = (const int64_t*)p[1]; a.ln_w = (const float*)p[2]; a.ln_b = (const float*)p[3];
+  a.W = (const float*)p[4]; a.bias = (const float*)p[5]; a.loss = (float*)p[6];
+  a.partial = (float*)p[7]; a.ticket = (unsigned*)p[8];
+  a.dh = (float*)p[9]; a.dh16 = (uint16_t*)p[10]; a.dln_w = (float*)p[11]; a.dln_b = (float*)p[12];
+  a.dW = (float*)p[13]; a.dbias = (float*)p[14];
+  a.B = B; a.T = T; a.C = C; a.eps = eps;
+  constexpr int nw = dct::ttio::HEAD_SPB, nwp = dct::ttio::HEAD_SPB_POOLED;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (T == 1)
+    hipLaunchKernelGGL((dct::ttio::head_bwd_kernel<nwp, true>), dim3((B + nwp - 1) / nwp), dim3(64 * nwp), 0, st, a);
+  else
+    hipLaunchKernelGGL((dct::ttio::head_bwd_kernel<nw, true>), dim3((B + nw - 1) / nw), dim3(64 * nw), 0, st, a);
   return (int)hipGetLastError();
 }
 

@@ -922,9 +922,27 @@ def _head_scratch(device: torch.device, B: int) -> torch.Tensor:
     return buf
 
 
+# Set by the autograd engine around a training step whose loss.backward() seed is exactly 1 (its
+# persistent ones seed, trainer/engines.py _backward): the classifier head then computes its backward in
+# the forward launch (dct_tt_head_fused) and the backward only hands the results over - one launch less
+# per step.  Anywhere else (a scaled loss, a user's own backward) the head keeps its two launches.
+_UNIT_LOSS_SEED = False
+
+
+@contextlib.contextmanager
+def unit_loss_seed():
+    global _UNIT_LOSS_SEED
+    prev, _UNIT_LOSS_SEED = _UNIT_LOSS_SEED, True
+    try:
+        yield
+    finally:
+        _UNIT_LOSS_SEED = prev
+
+
 class _TTHeadLossFn(torch.autograd.Function):
     """mean_b CE(Linear(LN(mean_t h[b, t, :])), y_b) in one kernel; the backward kernel recomputes the
-    per-sample chain and writes dh (fp32 + the bf16 copy the last block's dW GEMM consumes)."""
+    per-sample chain and writes dh (fp32 + the bf16 copy the last block's dW GEMM consumes).  Under
+    unit_loss_seed() a training forward runs both in one launch (the backward returns its results)."""
 
     @staticmethod
     def forward(ctx, h, y, ln_w, ln_b, W, bias, B, T, eps):
@@ -933,16 +951,32 @@ class _TTHeadLossFn(torch.autograd.Function):
         vec = [t.contiguous() for t in (ln_w, ln_b, W, bias)]
         loss = torch.empty((), dtype=torch.float32, device=h.device)  # stored by the kernel's last block
         scratch = _head_scratch(h.device, B)
+        ctx.params = (ln_w, ln_b, W, bias)
+        ctx.dims = (B, T, eps)
+        ctx.fused = None
+        if _UNIT_LOSS_SEED and ctx.needs_input_grad[0]:
+            dh = torch.empty_like(h)
+            dh16 = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
+            gs = [_grad_dst(p, zero=True) for p in ctx.params]
+            native().tt_head_fused([h.data_ptr(), y.data_ptr()] + [t.data_ptr() for t in vec]
+                                   + [loss.data_ptr(), scratch.data_ptr() + 4, scratch.data_ptr(), dh.data_ptr(),
+                                      dh16.data_ptr()] + [g.data_ptr() for g, _ in gs], B, T,
+                                   h.shape[1], W.shape[0], float(eps), _stream())
+            ctx.fused = (dh, dh16, gs)
+            return loss
         native().tt_head_fwd([h.data_ptr(), y.data_ptr()] + [t.data_ptr() for t in vec]
                              + [loss.data_ptr(), scratch.data_ptr() + 4, scratch.data_ptr()], B, T,
                              h.shape[1], W.shape[0], float(eps), _stream())
         ctx.save_for_backward(h, y, *vec)
-        ctx.params = (ln_w, ln_b, W, bias)
-        ctx.dims = (B, T, eps)
         return loss
 
     @staticmethod
     def backward(ctx, dloss):
+        if ctx.fused is not None:  # computed by the forward launch for dloss = 1 (unit_loss_seed)
+            dh, dh16, gs = ctx.fused
+            ctx.fused = None
+            _remember_bf16(dh, dh16)
+            return (dh, None, *[None if direct else g for g, direct in gs], None, None, None)
         h, y, lw, lb, Wc, bc = ctx.saved_tensors
         B, T, eps = ctx.dims
         dh = torch.empty_like(h)

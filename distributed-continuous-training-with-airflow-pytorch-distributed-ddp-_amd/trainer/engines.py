@@ -31,7 +31,7 @@ import torch
 from ..data.sampler import distributed_indices
 from ..ops._native import reload_knobs
 from ..ops.fused_mlp import FusedMLPKernel, mlp_num_params
-from ..ops.nn import bound_params, join_side_work
+from ..ops.nn import bound_params, join_side_work, unit_loss_seed
 from ..ops.optim import FlatAdam, adam_flat_
 from ..parallel.dist import DistContext, init_native_comm
 from ..parallel.reducer import NativeBucketReducer, TorchBucketReducer, plan_buckets
@@ -699,7 +699,9 @@ class AutogradEngine(_EngineBase):
             self.reducer.prepare()
         self._pm(0)
         self.model.train()
-        with self._bound():
+        # the step's backward root is training_step's loss with a seed of exactly 1 (_backward): a fused
+        # classifier head may compute its backward inside the forward launch (ops/nn.py unit_loss_seed)
+        with self._bound(), unit_loss_seed():
             loss = self.model.training_step((x, y), batch_idx)
             if isinstance(loss, dict):
                 loss = loss["loss"]

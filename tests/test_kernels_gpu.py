@@ -958,11 +958,16 @@ def test_tt_block_fused_matches_fp32_reference_and_unfused(cuda, B, monkeypatch)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("B,C", [(1, 2), (37, 2), (512, 2), (64, 5)])
-def test_tt_embed_and_head_loss_match_fp32_reference(cuda, B, C):
+def test_tt_embed_and_head_loss_match_fp32_reference(cuda, B, C, fused):
     """csrc/tt_io.hip: feature-token embedding fwd/bwd and the pooled LN -> Linear -> mean-CE head
-    (loss forward, recomputing backward) vs fp32 torch, every gradient including dh."""
-    from dct_amd.ops.nn import tt_embed, tt_head_loss
+    (loss forward, recomputing backward) vs fp32 torch, every gradient including dh.  ``fused``: the
+    training forward under unit_loss_seed() (backward seed 1) - loss and gradients from ONE launch
+    (dct_tt_head_fused), the backward only hands them over."""
+    import contextlib
+
+    from dct_amd.ops.nn import tt_embed, tt_head_loss, unit_loss_seed
 
     F_, d = 64, 64
     g = torch.Generator(device="cpu").manual_seed(5)
@@ -973,10 +978,11 @@ def test_tt_embed_and_head_loss_match_fp32_reference(cuda, B, C):
     lw = (1 + 0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_()
     lb, W, bias = mk(d, scale=0.1), mk(C, d, scale=0.3), mk(C, scale=0.1)
     params = [E, c, lw, lb, W, bias]
-    h = tt_embed(x, E, c)
-    h2 = h * 1.5  # an op between embedding and head, so dh flows through autograd
-    loss = tt_head_loss(h2, y, B, F_, lw, lb, W, bias)
-    loss.backward()
+    with unit_loss_seed() if fused else contextlib.nullcontext():
+        h = tt_embed(x, E, c)
+        h2 = h * 1.5  # an op between embedding and head, so dh flows through autograd
+        loss = tt_head_loss(h2, y, B, F_, lw, lb, W, bias)
+        loss.backward(torch.ones_like(loss))
     got = [p.grad.clone() for p in params]
     for p in params:
         p.grad = None
@@ -997,7 +1003,7 @@ def test_tt_head_loss_repeated_launches_deterministic(cuda):
     block order and stores the loss, leaving the ticket at zero - so back-to-back launches of any batch
     size (the scratch grows past its first size) give the fp32 reference loss, bit-identical on
     repeats, without a zero-filled loss tensor."""
-    from dct_amd.ops.nn import tt_head_loss
+    from dct_amd.ops.nn import tt_head_loss, unit_loss_seed
 
     F_, d, C = 64, 64, 2
     g = torch.Generator(device="cpu").manual_seed(11)
@@ -1015,6 +1021,13 @@ def test_tt_head_loss_repeated_launches_deterministic(cuda):
         vals = [float(t) for t in losses]
         assert vals[0] == vals[1] == vals[2], (B, vals)
         assert abs(vals[0] - ref.item()) < 1e-4 * max(1.0, abs(ref.item())), (B, vals[0], ref.item())
+        # the fused training forward (loss + gradients in one launch) stores the same loss, bit for bit
+        hg = h.clone().requires_grad_()
+        with unit_loss_seed():
+            lf = tt_head_loss(hg, y, B, F_, lw.requires_grad_(), lb.requires_grad_(), W.requires_grad_(),
+                              bias.requires_grad_())
+        assert float(lf) == vals[0], (B, float(lf), vals[0])
+        lw.requires_grad_(False), lb.requires_grad_(False), W.requires_grad_(False), bias.requires_grad_(False)
 
 
 @pytest.mark.gpu

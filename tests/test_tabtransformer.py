@@ -186,3 +186,36 @@ def test_fused_embedding_matches_separate_kernel(cuda, monkeypatch):
     for n in g0:
         rel = float((g1[n] - g0[n]).norm() / (g0[n].norm() + 1e-12))
         assert rel < 1e-4, (n, rel)
+
+
+@pytest.mark.gpu
+def test_training_step_fused_head_matches_two_launch_head(cuda):
+    """training_step under unit_loss_seed() (the autograd engine's step: backward seed exactly 1) runs
+    the pooled classifier head's backward inside its forward launch (csrc/tt_io.hip dct_tt_head_fused):
+    the loss bit for bit and every parameter gradient (to float-atomic rounding) equal the head's
+    forward + backward launches."""
+    from dct_amd.ops.nn import unit_loss_seed
+
+    torch.manual_seed(3)
+    B, F_ = 128, 64
+    X, Y = _data(B, F_)
+    X, Y = X.to(cuda), Y.to(cuda)
+    res = {}
+    for fused in (False, True):
+        torch.manual_seed(4)
+        m = TabTransformer(num_features=F_, d_model=64, heads=4, layers=2).to(cuda)
+        m.train()
+        if fused:
+            with unit_loss_seed():
+                loss = m.training_step((X, Y), 0)
+                loss.backward(torch.ones_like(loss))
+        else:
+            loss = m.training_step((X, Y), 0)
+            loss.backward(torch.ones_like(loss))
+        torch.cuda.synchronize()
+        res[fused] = (float(loss), {n: p.grad.detach().clone() for n, p in m.named_parameters()})
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert l0 == l1, (l0, l1)
+    for n in g0:
+        rel = (g1[n] - g0[n]).norm() / (g0[n].norm() + 1e-12)
+        assert rel < 1e-5, (n, float(rel))
