@@ -875,7 +875,7 @@ class AutogradEngine(_EngineBase):
                     self.reducer.prepare()
                 self._pm(0)
                 self.model.train()
-                with self._bound():
+                with self._bound(), unit_loss_seed():  # (as _step_body: the backward seed is exactly 1)
                     loss = self.model.training_step((self._x_dev, self._y_dev), first)
                     if isinstance(loss, dict):
                         loss = loss["loss"]
