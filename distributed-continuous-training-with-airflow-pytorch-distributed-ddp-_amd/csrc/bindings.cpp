@@ -520,6 +520,15 @@ PYBIND11_MODULE(_dct_native, m) {
               "tt_block_fwd_ex");
       });
   m.def(
+      "tt_block_fwd_gx",
+      [](std::vector<uintptr_t> ptrs, int Bsz, int T, int DM, int H, int FF, float eps, float scale, uintptr_t pool,
+         uintptr_t ex, uintptr_t eE, uintptr_t ec, std::vector<uintptr_t> gx, uintptr_t stream) {
+        check(dct_tt_block_fwd_gx(ptrs.data(), (int)ptrs.size(), Bsz, T, DM, H, FF, eps, scale, P<float>(pool),
+                                  P<const float>(ex), P<const float>(eE), P<const float>(ec), gx.data(),
+                                  (int)gx.size(), reinterpret_cast<void*>(stream)),
+              "tt_block_fwd_gx");
+      });
+  m.def(
       "tt_block_bwd_ex",
       [](std::vector<uintptr_t> ptrs, int Bsz, int T, int DM, int H, int FF, float scale, uintptr_t dpool,
          uintptr_t dout16, uintptr_t ex, uintptr_t eE, uintptr_t ec, uintptr_t lnrep, uintptr_t ticket,

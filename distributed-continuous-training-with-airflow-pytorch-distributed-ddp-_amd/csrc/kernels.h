@@ -150,6 +150,9 @@ int dct_tt_block_fwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int
                      void* stream);
 int dct_tt_block_bwd(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,
                      void* stream);
+int dct_tt_block_fwd_gx(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps,
+                        float scale, float* pool, const float* ex, const float* eE, const float* ec,
+                        const uintptr_t* gx, int n_gx, void* stream);
 int dct_tt_block_fwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps,
                         float scale, float* pool, const float* ex, const float* eE, const float* ec, void* stream);
 int dct_tt_block_bwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float scale,

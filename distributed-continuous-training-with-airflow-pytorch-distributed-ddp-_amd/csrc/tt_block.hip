@@ -77,6 +77,25 @@ struct Embed {
   const float* c;  // [T][DM]
 };
 
+// Optional batch gather of the first block (the autograd engine's captured step, ops/nn.py
+// fold_batch_gather): sample b's features are dataset row idx[wrap(*cursor * stride + b)] of X [rows][T],
+// read where the embedding reads x; the workgroup also writes them to xdst (the backward's x) and the
+// label to ydst, and the grid runs the rest of the step prologue (csrc/step_kernels.hip
+// ag_prologue_kernel): Adam step counter += 1, zero[0, zero_n) cleared - one launch less per step
+struct Gather {
+  const float* X;
+  const int64_t* idx;
+  const int* cursor;
+  int stride;
+  int64_t n_items;
+  float* xdst;
+  const int64_t* Y;
+  int64_t* ydst;
+  int* step_counter;
+  float* zero;
+  int64_t zero_n;
+};
+
 struct Args {
   const float* h;
   const float *ln1_w, *ln1_b;
@@ -95,6 +114,7 @@ struct Args {
   uint64_t* prof;  // optional phase timestamps (wall clock), 16 per workgroup
   float* pool;     // optional [B][DM]: the block output's mean over the sample's tokens (classifier head input)
   Embed em;        // optional: the first block's input computed from the features (h unused)
+  Gather gx;       // optional (gx.X): those features gathered from the dataset (em.x is then the destination)
   int save;        // 0: inference (no_grad) - only `out` is written, no saved tensors / W^T
   int B;
   float eps, scale;
@@ -249,8 +269,26 @@ __global__ __launch_bounds__(256, 2) void tt_block_fwd_kernel(Args a) {
   const int c = lane & 15, g = lane >> 4;
 
   TT_MARK(0);
+  Embed em = a.em;
+  if (a.gx.X) {
+    // this sample's dataset row; em.x rebased so that em.x[row0 + r] is its feature r
+    int64_t q = (int64_t)a.gx.cursor[0] * a.gx.stride + bidx;
+    q = q < a.gx.n_items ? q : (a.gx.n_items > 0 ? q % a.gx.n_items : 0);
+    const int64_t drow = a.gx.idx[q];
+    const float* xr = a.gx.X + drow * T;
+    em.x = xr - row0;
+    if (threadIdx.x < T) a.gx.xdst[row0 + threadIdx.x] = xr[threadIdx.x];
+    if (threadIdx.x == 0) a.gx.ydst[bidx] = a.gx.Y[drow];
+    if (bidx == 0 && threadIdx.x == 0 && a.gx.step_counter) a.gx.step_counter[0] += 1;
+    if (a.gx.zero) {
+      const int64_t n4 = a.gx.zero_n >> 2, t = (int64_t)bidx * blockDim.x + threadIdx.x;
+      for (int64_t i = t; i < n4; i += (int64_t)gridDim.x * blockDim.x)
+        reinterpret_cast<float4*>(a.gx.zero)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (t < a.gx.zero_n - (n4 << 2)) a.gx.zero[(n4 << 2) + t] = 0.f;
+    }
+  }
   // ---- P1: LN1 (rows of this wave)
-  layer_norm_rows(a.h, true, HS, AS, a.ln1_w, a.ln1_b, a.mean1, a.rstd1, row0, a.eps, a.em);
+  layer_norm_rows(a.h, true, HS, AS, a.ln1_w, a.ln1_b, a.mean1, a.rstd1, row0, a.eps, em);
   __syncthreads();
   TT_MARK(1);
 
@@ -1061,8 +1099,33 @@ extern "C" {
 // pool (optional): the last block's token mean for the classifier head; `out` (p[25]) may then be null.
 // ex / eE / ec (optional): the first block's input embedded from the features x [B][T] (E, c [T][DM]);
 // h (p[0]) is then not read and may be null
+static int tt_block_fwd_impl(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps,
+                             float scale, float* pool, const float* ex, const float* eE, const float* ec,
+                             const dct::ttb::Gather& gx, void* stream);
+
 int dct_tt_block_fwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps,
                         float scale, float* pool, const float* ex, const float* eE, const float* ec, void* stream) {
+  return tt_block_fwd_impl(p, n_ptrs, Bsz, T, DM, H, FF, eps, scale, pool, ex, eE, ec, dct::ttb::Gather{}, stream);
+}
+
+// gx (11 values): X, idx (int64), cursor (int32), stride, n_items, xdst (= ex), Y (int64), ydst (int64),
+// step_counter (int32, may be 0), zero (fp32, may be 0), zero_n - see Gather; needs the embedding (ex, eE, ec)
+int dct_tt_block_fwd_gx(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps,
+                        float scale, float* pool, const float* ex, const float* eE, const float* ec,
+                        const uintptr_t* gx, int n_gx, void* stream) {
+  if (n_gx != 11 || !ex || !gx[0] || !gx[1] || !gx[2] || gx[5] != (uintptr_t)ex || !gx[6] || !gx[7] ||
+      (int64_t)gx[4] <= 0 || (gx[9] && (gx[9] & 15)))
+    return (int)hipErrorInvalidValue;
+  dct::ttb::Gather g{};
+  g.X = (const float*)gx[0]; g.idx = (const int64_t*)gx[1]; g.cursor = (const int*)gx[2]; g.stride = (int)gx[3];
+  g.n_items = (int64_t)gx[4]; g.xdst = (float*)gx[5]; g.Y = (const int64_t*)gx[6]; g.ydst = (int64_t*)gx[7];
+  g.step_counter = (int*)gx[8]; g.zero = (float*)gx[9]; g.zero_n = (int64_t)gx[10];
+  return tt_block_fwd_impl(p, n_ptrs, Bsz, T, DM, H, FF, eps, scale, pool, ex, eE, ec, g, stream);
+}
+
+static int tt_block_fwd_impl(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, int H, int FF, float eps,
+                             float scale, float* pool, const float* ex, const float* eE, const float* ec,
+                             const dct::ttb::Gather& gx, void* stream) {
   using namespace dct::ttb;
   if ((n_ptrs != 27 && n_ptrs != 28) || T != dct::ttb::T || DM != dct::ttb::DM || H != NH || FF != dct::ttb::FF || Bsz <= 0)
     return (int)hipErrorInvalidValue;
@@ -1092,6 +1155,7 @@ int dct_tt_block_fwd_ex(const uintptr_t* p, int n_ptrs, int Bsz, int T, int DM, 
   if (pool && (((uintptr_t)pool) & 15)) return (int)hipErrorInvalidValue;
   if (ex && (!eE || !ec || ((((uintptr_t)eE) | ((uintptr_t)ec)) & 15))) return (int)hipErrorInvalidValue;
   a.em = Embed{ex, eE, ec};
+  a.gx = gx;
   a.save = save ? 1 : 0;
   a.B = Bsz; a.eps = eps; a.scale = scale;
   static bool attr = false;

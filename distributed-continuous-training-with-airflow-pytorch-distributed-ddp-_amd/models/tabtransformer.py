@@ -65,6 +65,12 @@ class TabTransformer(TrainModule):
         self.ln_w, self.ln_b = nn.Parameter(torch.ones(d_model)), nn.Parameter(torch.zeros(d_model))
         self.head = nn.Linear(d_model, num_classes)
 
+    @property
+    def folds_batch_gather(self) -> bool:
+        """The first block embeds the features itself, so it can also gather them (ops/nn.py
+        fold_batch_gather: the autograd engine's captured step then has no prologue launch)."""
+        return FUSED_EMBED and len(self.blocks) > 0
+
     def _trunk(self, x: torch.Tensor, pooled: bool = False) -> torch.Tensor:
         """Token embedding + the blocks: [B*F, d], or with ``pooled`` the last block's output averaged
         over each sample's F tokens, [B, d] (on MI355X the last block kernel writes only that)."""

@@ -550,6 +550,34 @@ def _prenorm_attn_bwd(dout, saved, params, dims):
     return dh, dlw, dlb, dwqkv, dbqkv, dwo, dbo
 
 
+class BatchGather:
+    """The step prologue folded into the model's first fused block (csrc/tt_block.hip Gather): the
+    autograd engine's captured step hands over, instead of launching ag_step_prologue, where the batch
+    comes from (dataset X fp32 [rows][F], int64 row list at a device cursor, int64 labels) and where it
+    goes (the step's static x / y - the block writes both, x being its embedding input), plus the step
+    counter and the gradient buffer to clear.  ``consumed`` tells the engine a block took it."""
+
+    def __init__(self, X, idx, cursor, stride, n_items, xdst, Y, ydst, step_counter, zero):
+        self.values = [X.data_ptr(), idx.data_ptr(), cursor.data_ptr(), int(stride), int(n_items), xdst.data_ptr(),
+                       Y.data_ptr(), ydst.data_ptr(), step_counter.data_ptr() if step_counter is not None else 0,
+                       zero.data_ptr() if zero is not None else 0, zero.numel() if zero is not None else 0]
+        self.xdst = xdst
+        self.consumed = False
+
+
+_BATCH_GATHER: Optional[BatchGather] = None
+
+
+@contextlib.contextmanager
+def fold_batch_gather(spec: BatchGather):
+    global _BATCH_GATHER
+    prev, _BATCH_GATHER = _BATCH_GATHER, spec
+    try:
+        yield spec
+    finally:
+        _BATCH_GATHER = prev
+
+
 class _TTBlockFn(torch.autograd.Function):
     """A whole pre-norm transformer block (attention sub-block then FFN sub-block) as ONE kernel
     forward (csrc/tt_block.hip: one workgroup per sample, all intermediates in LDS) for the
@@ -596,7 +624,13 @@ class _TTBlockFn(torch.autograd.Function):
             ptrs.append(_tt_prof_buf("fwd", B, dev))
         addrs = [0 if (t is pre and recomp) or (t is out and pooled) or (t is h and embed) or t.numel() == 0
                  else t.data_ptr() for t in ptrs]
-        if pooled or embed:
+        gx = _BATCH_GATHER
+        if embed and gx is not None and not gx.consumed and h.data_ptr() == gx.xdst.data_ptr():
+            # the step prologue folded in: this launch gathers the batch into h (= the engine's static x)
+            nat.tt_block_fwd_gx(addrs, B, T, dm, H, FF, float(eps), scale, out.data_ptr() if pooled else 0,
+                                h.data_ptr(), eE.data_ptr(), ec.data_ptr(), gx.values, st)
+            gx.consumed = True
+        elif pooled or embed:
             em = [t.data_ptr() for t in (h, eE, ec)] if embed else [0, 0, 0]
             nat.tt_block_fwd_ex(addrs, B, T, dm, H, FF, float(eps), scale, out.data_ptr() if pooled else 0, *em, st)
         else:

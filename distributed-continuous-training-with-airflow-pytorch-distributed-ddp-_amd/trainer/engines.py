@@ -31,7 +31,7 @@ import torch
 from ..data.sampler import distributed_indices
 from ..ops._native import reload_knobs
 from ..ops.fused_mlp import FusedMLPKernel, mlp_num_params
-from ..ops.nn import bound_params, join_side_work, unit_loss_seed
+from ..ops.nn import BatchGather, bound_params, fold_batch_gather, join_side_work, unit_loss_seed
 from ..ops.optim import FlatAdam, adam_flat_
 from ..parallel.dist import DistContext, init_native_comm
 from ..parallel.reducer import NativeBucketReducer, TorchBucketReducer, plan_buckets
@@ -864,19 +864,40 @@ class AutogradEngine(_EngineBase):
         self._x_dev = torch.empty(self.B, self.X.shape[1], dtype=torch.float32, device=self.device)
         self._y_dev = torch.empty(self.B, dtype=torch.int64, device=self.device)
         self._dcursor = torch.full((1,), first, dtype=torch.int32, device=self.device)
+        # a model whose first fused block can gather its own batch (models/tabtransformer.py
+        # folds_batch_gather) takes the step prologue into that launch; if no block took it, the step is
+        # captured again with the prologue kernel
+        fold = bool(getattr(self.model, "folds_batch_gather", False))
+        for folded in ((True, False) if fold else (False,)):
+            spec = None
+            if folded:
+                spec = BatchGather(self.X, rows_dev, self._dcursor, self.B, rows_dev.numel(), self._x_dev, self.Y,
+                                   self._y_dev, self.optimizer._device_counter(), self.flat_g)
+            g, loss = self._capture_step(nat, rows_dev, loss_out, first, spec)
+            self.optimizer.step_count -= 1  # capture recorded without executing
+            if spec is None or spec.consumed:
+                break
+        self.gather_folded = spec is not None and spec.consumed
+        self._dgraph = g
+        self._dloss = loss
+        self.graph_used = True
+
+    def _capture_step(self, nat, rows_dev, loss_out, first, spec):
         g = torch.cuda.CUDAGraph()
         s = self._capture_stream()
         s.wait_stream(torch.cuda.current_stream())
         torch.cuda.synchronize(self.device)
         with torch.cuda.stream(s):
             with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
-                self._prologue(nat, rows_dev)
+                if spec is None:
+                    self._prologue(nat, rows_dev)
                 if self.reducer is not None:
                     self.reducer.prepare()
                 self._pm(0)
                 self.model.train()
                 with self._bound(), unit_loss_seed():  # (as _step_body: the backward seed is exactly 1)
-                    loss = self.model.training_step((self._x_dev, self._y_dev), first)
+                    with fold_batch_gather(spec) if spec is not None else contextlib.nullcontext():
+                        loss = self.model.training_step((self._x_dev, self._y_dev), first)
                     if isinstance(loss, dict):
                         loss = loss["loss"]
                     self._pm(1)
@@ -888,10 +909,7 @@ class AutogradEngine(_EngineBase):
                 self.optimizer.step(bump_counter=False, epilogue=(self._dcursor, loss.detach(), loss_out))
                 self._pm(4)
         torch.cuda.current_stream().wait_stream(s)
-        self._dgraph = g
-        self._dloss = loss
-        self.graph_used = True
-        self.optimizer.step_count -= 1  # capture recorded without executing
+        return g, loss
 
     def optimizer_state_dict(self) -> Dict:
         if self.optimizer is not None:

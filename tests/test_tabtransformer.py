@@ -82,7 +82,9 @@ def test_hip_fit_with_graph_capture(cuda, F_, min_acc):
 @pytest.mark.parametrize("F_", [32, 64])
 def test_device_loop_matches_host_loop(cuda, F_):
     """AutogradEngine.run_device_steps (one captured graph per step: device batch gather, counter,
-    grad zeroing, loss record and cursor in the Adam epilogue) trains exactly like train_step."""
+    grad zeroing, loss record and cursor in the Adam epilogue) trains exactly like train_step; at 64
+    features the gather / counter / zeroing ride in the first fused block's launch (ops/nn.py
+    fold_batch_gather)."""
     from dct_amd.parallel.dist import init_distributed
     from dct_amd.trainer.engines import AutogradEngine
     from dct_amd.trainer.trainer import seed_everything
@@ -109,6 +111,8 @@ def test_device_loop_matches_host_loop(cuda, F_):
         res.append((loss.cpu(), eng.flat_p.detach().cpu().clone(), eng.optimizer.step_count))
         if device_loop:
             assert eng.graph_used
+            # 64 features: the first fused block gathers the batch itself (no prologue launch)
+            assert eng.gather_folded == (F_ == 64), eng.gather_folded
     (l0, p0, c0), (lh, ph, _), (l1, p1, c1) = res
     assert c0 == c1 == steps
     assert torch.isfinite(l1).all() and (l1 != 0).all()
