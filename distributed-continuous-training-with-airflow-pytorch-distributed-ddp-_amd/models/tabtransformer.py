@@ -98,12 +98,13 @@ class TabTransformer(TrainModule):
         x, y = batch
         # pooled LN -> Linear -> mean CE as one kernel each way on MI355X (ops/nn.py tt_head_loss)
         # (the head consumes the pooled tokens: the last block hands over [B, d], not [B*F, d])
+        # (root: this loss is returned unscaled - the engine's backward seed reaches the head as exactly 1)
         if POOLED_HEAD:
             loss = tt_head_loss(self._trunk(x, pooled=True), y, x.shape[0], 1, self.ln_w, self.ln_b, self.head.weight,
-                                self.head.bias)
+                                self.head.bias, root=True)
         else:
             loss = tt_head_loss(self._trunk(x), y, x.shape[0], self.F, self.ln_w, self.ln_b, self.head.weight,
-                                self.head.bias)
+                                self.head.bias, root=True)
         self.log("train_loss", loss, sync_dist=True)
         return loss
 

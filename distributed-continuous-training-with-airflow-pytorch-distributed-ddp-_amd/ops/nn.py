@@ -979,7 +979,7 @@ class _TTHeadLossFn(torch.autograd.Function):
     unit_loss_seed() a training forward runs both in one launch (the backward returns its results)."""
 
     @staticmethod
-    def forward(ctx, h, y, ln_w, ln_b, W, bias, B, T, eps):
+    def forward(ctx, h, y, ln_w, ln_b, W, bias, B, T, eps, root=False):
         h = h.contiguous().float()
         y = y.contiguous().long()
         vec = [t.contiguous() for t in (ln_w, ln_b, W, bias)]
@@ -988,7 +988,7 @@ class _TTHeadLossFn(torch.autograd.Function):
         ctx.params = (ln_w, ln_b, W, bias)
         ctx.dims = (B, T, eps)
         ctx.fused = None
-        if _UNIT_LOSS_SEED and ctx.needs_input_grad[0]:
+        if root and _UNIT_LOSS_SEED and ctx.needs_input_grad[0]:
             dh = torch.empty_like(h)
             dh16 = torch.empty(h.shape, dtype=torch.bfloat16, device=h.device)
             gs = [_grad_dst(p, zero=True) for p in ctx.params]
@@ -1010,7 +1010,7 @@ class _TTHeadLossFn(torch.autograd.Function):
             dh, dh16, gs = ctx.fused
             ctx.fused = None
             _remember_bf16(dh, dh16)
-            return (dh, None, *[None if direct else g for g, direct in gs], None, None, None)
+            return (dh, None, *[None if direct else g for g, direct in gs], None, None, None, None)
         h, y, lw, lb, Wc, bc = ctx.saved_tensors
         B, T, eps = ctx.dims
         dh = torch.empty_like(h)
@@ -1020,17 +1020,19 @@ class _TTHeadLossFn(torch.autograd.Function):
         ptrs = [h, y, lw, lb, Wc, bc, dloss, dh, dh16] + [g for g, _ in gs]
         native().tt_head_bwd([t.data_ptr() for t in ptrs], B, T, h.shape[1], Wc.shape[0], float(eps), _stream())
         _remember_bf16(dh, dh16)
-        return (dh, None, *[None if direct else g for g, direct in gs], None, None, None)
+        return (dh, None, *[None if direct else g for g, direct in gs], None, None, None, None)
 
 
 def tt_head_fusable(h: torch.Tensor, num_classes: int) -> bool:
     return h.is_cuda and h.shape[1] == 64 and 1 <= num_classes <= 8
 
 
-def tt_head_loss(h, y, B: int, T: int, ln_w, ln_b, W, bias, eps: float = 1e-5):
-    """Mean cross-entropy of the pooled-token classifier head (LN -> Linear) - one kernel each way."""
+def tt_head_loss(h, y, B: int, T: int, ln_w, ln_b, W, bias, eps: float = 1e-5, root: bool = False):
+    """Mean cross-entropy of the pooled-token classifier head (LN -> Linear) - one kernel each way.
+    ``root``: the caller returns this loss unscaled as the step's backward root, so under
+    unit_loss_seed() (backward seed exactly 1) the forward launch may compute the backward as well."""
     if tt_head_fusable(h, W.shape[0]):
-        return _TTHeadLossFn.apply(h, y, ln_w, ln_b, W, bias, B, T, eps)
+        return _TTHeadLossFn.apply(h, y, ln_w, ln_b, W, bias, B, T, eps, root)
     pooled = h.reshape(B, T, h.shape[1]).mean(1)
     z = layer_norm(pooled, ln_w, ln_b, eps)
     return F.cross_entropy(linear(z, W, bias).float(), y)

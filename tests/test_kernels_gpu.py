@@ -981,7 +981,7 @@ def test_tt_embed_and_head_loss_match_fp32_reference(cuda, B, C, fused):
     with unit_loss_seed() if fused else contextlib.nullcontext():
         h = tt_embed(x, E, c)
         h2 = h * 1.5  # an op between embedding and head, so dh flows through autograd
-        loss = tt_head_loss(h2, y, B, F_, lw, lb, W, bias)
+        loss = tt_head_loss(h2, y, B, F_, lw, lb, W, bias, root=True)
         loss.backward(torch.ones_like(loss))
     got = [p.grad.clone() for p in params]
     for p in params:
@@ -1025,7 +1025,7 @@ def test_tt_head_loss_repeated_launches_deterministic(cuda):
         hg = h.clone().requires_grad_()
         with unit_loss_seed():
             lf = tt_head_loss(hg, y, B, F_, lw.requires_grad_(), lb.requires_grad_(), W.requires_grad_(),
-                              bias.requires_grad_())
+                              bias.requires_grad_(), root=True)
         assert float(lf) == vals[0], (B, float(lf), vals[0])
         lw.requires_grad_(False), lb.requires_grad_(False), W.requires_grad_(False), bias.requires_grad_(False)
 
@@ -1207,3 +1207,31 @@ def test_gemm_forward_wt_side_output_and_nt_dx(cuda, M):
     assert torch.equal(d_nn, d_nt)
     want = (dZ.float() @ W2.float()) * (Y.float() > 0)
     assert (d_nt.float() - want).abs().max() < 2e-2 * want.abs().max()
+
+
+@pytest.mark.gpu
+def test_tt_head_loss_not_root_keeps_the_backward_launch(cuda):
+    """Under unit_loss_seed() only a head loss declared the backward root (root=True) computes its
+    gradients in the forward launch: a caller that scales the loss before backward (root left False)
+    gets the scaled gradients from the backward launch."""
+    from dct_amd.ops.nn import tt_head_loss, unit_loss_seed
+
+    B, T_, d, C = 96, 1, 64, 2
+    g = torch.Generator(device="cpu").manual_seed(21)
+    h0 = torch.randn(B * T_, d, generator=g).to(cuda)
+    y = torch.randint(0, C, (B,), generator=g).to(cuda)
+    lw = (1 + 0.1 * torch.randn(d, generator=g)).to(cuda)
+    lb, W, bias = (0.1 * torch.randn(d, generator=g)).to(cuda), (0.3 * torch.randn(C, d, generator=g)).to(cuda), \
+        (0.1 * torch.randn(C, generator=g)).to(cuda)
+    grads = []
+    for scale, ctxm in ((1.0, False), (0.5, True)):
+        h = h0.clone().requires_grad_()
+        Wp = W.clone().requires_grad_()
+        with unit_loss_seed() if ctxm else torch.enable_grad():
+            loss = tt_head_loss(h, y, B, T_, lw, lb, Wp, bias) * scale
+            loss.backward(torch.ones_like(loss))
+        torch.cuda.synchronize()
+        grads.append((h.grad.clone(), Wp.grad.clone()))
+    (dh1, dW1), (dh5, dW5) = grads
+    assert torch.allclose(dh5, 0.5 * dh1, rtol=1e-5, atol=1e-8)
+    assert torch.allclose(dW5, 0.5 * dW1, rtol=1e-5, atol=1e-7)
