@@ -64,7 +64,7 @@ def main():
         res.append(dt)
     st = xgmi.check(xg, ctx)
     raw = prof.cpu().view(8, PS).double() / steps
-    per_phase = {k: float(raw[:, k].mean()) for k in PHASES}
+    per_phase = {k: float(raw[:, k].mean()) for k in list(PHASES) + [9, 10]}
     allp = ctx.all_gather_object((per_phase, res[-1] / steps * 1e6))
     same = ctx.all_gather_object(p.cpu())
     if ctx.rank == 0:
@@ -79,6 +79,11 @@ def main():
             tot += mean
             print(f"{PHASES[k]:34s}{mean:10.0f}{min(vals):8.0f}{max(vals):8.0f}")
         print(f"{'total':34s}{tot:10.0f}")
+        # per launch (not per step): the prologue (kernel start -> first step) and the epilogue (last
+        # step -> stores done, incl. the launch-end moment all-gather) - the fixed cost of every launch
+        for k, name in ((9, "prologue (per launch)"), (10, "epilogue (per launch)")):
+            vals = [pp[k] * steps for pp, _ in allp]
+            print(f"{name:34s}{sum(vals) / len(vals):10.0f}{min(vals):8.0f}{max(vals):8.0f}")
     ctx.barrier()
     del xg
     shutdown(ctx)
